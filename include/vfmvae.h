@@ -1,0 +1,120 @@
+/*
+ * vfmvae.h — C ABI of the MI355X (gfx950) VFM-VAE hot-path kernels.
+ *
+ * This is the drop-in boundary that replaces the reference's pybind11 plugins
+ * (`torch_utils/custom_ops.py:59-155` building `upfirdn2d_plugin`,
+ * `bias_act_plugin`, `filtered_lrelu_plugin`) and the torch/cuDNN calls of the
+ * decoder layers that actually run in the shipped configs
+ * (`networks/utils/convnext_utils.py:36-257`).
+ *
+ * Conventions (all entry points):
+ *   - Plain device pointers, element counts and element strides; no torch types.
+ *   - Outputs are allocated by the caller (the Python host layer allocates them
+ *     from PyTorch's caching allocator, like `torch::empty` in the reference's
+ *     host code, e.g. `upfirdn2d.cpp:38`).
+ *   - Kernels are enqueued asynchronously on `stream` (a hipStream_t; NULL is the
+ *     legacy default stream). No host synchronisation, no allocation: every entry
+ *     point is capturable into a hipGraph.
+ *   - Return value: VFM_OK (0) on success, VFM_ERR_ARGS (-2) for an invalid
+ *     argument, VFM_NO_KERNEL (-1) when no specialisation exists (only
+ *     `vfm_filtered_lrelu`, mirroring `filtered_lrelu.cpp:51-56`), or a positive
+ *     hipError_t from the launch.
+ *   - dtype codes: VFM_F32, VFM_F16, VFM_BF16, VFM_F64. Arithmetic is fp32
+ *     (fp64 for VFM_F64); filters are always fp32.
+ */
+#ifndef VFMVAE_H
+#define VFMVAE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    VFM_F32 = 0,
+    VFM_F16 = 1,
+    VFM_BF16 = 2,
+    VFM_F64 = 3,
+};
+
+enum {
+    VFM_OK = 0,
+    VFM_NO_KERNEL = -1,
+    VFM_ERR_ARGS = -2,
+};
+
+/* Library identification: returns a static string "vfmvae-hip <version> gfx950". */
+const char* vfm_version(void);
+
+/*
+ * upfirdn2d: upsample (zero insertion) -> pad/crop -> 2-D FIR -> downsample -> gain.
+ * Replaces `upfirdn2d(x, f, upx, upy, downx, downy, padx0, padx1, pady0, pady1,
+ * flip, gain)` of `torch_utils/ops/upfirdn2d.cpp:16` (kernels `upfirdn2d.cu:29-200`).
+ *   x: [N, C, inH, inW] with element strides xs[4] (N, C, H, W order); any layout.
+ *   y: [N, C, outH, outW] with element strides ys[4]; the caller computes
+ *      outW = (inW*upx + padx0 + padx1 - fw + downx) / downx (same for H).
+ *   f: fp32 filter [fh, fw] with element strides (fsh, fsw).
+ *   flip: 0 = convolution, 1 = correlation (reference `flip_filter`).
+ */
+int vfm_upfirdn2d(const void* x, void* y, const float* f, int dtype,
+                  int N, int C, int inH, int inW, const long long* xs,
+                  int outH, int outW, const long long* ys,
+                  int fh, int fw, long long fsh, long long fsw,
+                  int upx, int upy, int downx, int downy, int padx0, int pady0,
+                  int flip, float gain, void* stream);
+
+/*
+ * bias_act: y = clamp(act(x + b[(i / stepB) % sizeB]) * gain) and its 1st/2nd
+ * order gradients. Replaces `bias_act(x, b, xref, yref, dy, grad, dim, act,
+ * alpha, gain, clamp)` of `torch_utils/ops/bias_act.cpp:32` (kernel
+ * `bias_act.cu:23-147`). All tensors are dense with the same element order;
+ * NULL = absent (the reference passes empty tensors). act codes follow
+ * `bias_act.py:21-31` (1 linear, 2 relu, 3 lrelu, 4 tanh, 5 sigmoid, 6 elu,
+ * 7 selu, 8 softplus, 9 swish); clamp < 0 disables clamping.
+ */
+int vfm_bias_act(const void* x, const void* b, const void* xref, const void* yref,
+                 const void* dy, void* y, int dtype, long long numel,
+                 int grad, int act, float alpha, float gain, float clamp,
+                 long long stepB, int sizeB, void* stream);
+
+/*
+ * filtered_lrelu: bias -> upsample FIR (gain up^2) -> gain -> leaky ReLU ->
+ * clamp -> downsample FIR, fused. Replaces `filtered_lrelu(x, fu, fd, b, si, up,
+ * down, px0, px1, py0, py1, sx, sy, gain, slope, clamp, flip_filters,
+ * writeSigns)` of `torch_utils/ops/filtered_lrelu.cpp:16`.
+ *   x: [N, C, xh, xw] (strides xs), y: [N, C, yh, yw] (strides ys), both dtype.
+ *   fu: fp32 [fuh, fuw] contiguous, fd: fp32 [fdh, fdw] contiguous (separable
+ *       filters are passed as their 2-D outer product).
+ *   b: [C] dtype (may be NULL = zero bias).
+ *   s: uint8 sign tensor [N, C, sh, sw_bytes] contiguous; written when
+ *      sign_mode == 1, read (at offset sx, sy) when sign_mode == 2, unused (NULL)
+ *      when sign_mode == 0. 2 bits per element: bit0 = negative, bit1 = clamped.
+ *   clamp: use +inf for "no clamp".
+ * Returns VFM_NO_KERNEL when (up, down) is outside {1,2,4} or the tile would not
+ * fit in LDS; the host layer then takes the generic path
+ * (upfirdn2d -> vfm_filtered_lrelu_act -> upfirdn2d), as `filtered_lrelu.py:223-229`.
+ */
+int vfm_filtered_lrelu(const void* x, const float* fu, const float* fd, const void* b,
+                       unsigned char* s, void* y, int dtype,
+                       int N, int C, int xh, int xw, const long long* xs,
+                       int yh, int yw, const long long* ys,
+                       int fuh, int fuw, int fdh, int fdw,
+                       int up, int down, int px0, int py0,
+                       int sh, int sw_bytes, int sx, int sy, int sign_mode,
+                       float gain, float slope, float clamp, int flip, void* stream);
+
+/*
+ * filtered_lrelu_act_: in-place gain -> leaky ReLU -> clamp on x [N, C, H, W]
+ * (strides xs) with sign write (sign_mode 1) / read at offset (sx, sy)
+ * (sign_mode 2). Replaces `filtered_lrelu_act_` of `filtered_lrelu.cpp:213`.
+ * s: uint8 [N, C, sh, sw_bytes] contiguous.
+ */
+int vfm_filtered_lrelu_act(void* x, unsigned char* s, int dtype,
+                           int N, int C, int H, int W, const long long* xs,
+                           int sh, int sw_bytes, int sx, int sy, int sign_mode,
+                           float gain, float slope, float clamp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VFMVAE_H */

@@ -1,0 +1,60 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares.
+No compute calls (there is no GPU in the build container)."""
+import ctypes
+import glob
+import os
+import re
+
+from conftest import ROOT
+
+LIB = os.path.join(ROOT, "vfm-vae_amd", "lib", "libvfmvae_hip.so")
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        syms.update(re.findall(r"\b(vfm_\w+)\s*\(", src))
+    return sorted(syms)
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "vfm_upfirdn2d" in syms and "vfm_bias_act" in syms and "vfm_filtered_lrelu" in syms
+    assert len(syms) >= 5
+
+
+def test_library_exports_all_declared_symbols():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    lib = ctypes.CDLL(LIB)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_version_string():
+    lib = ctypes.CDLL(LIB)
+    lib.vfm_version.restype = ctypes.c_char_p
+    assert b"gfx950" in lib.vfm_version()
+
+
+def test_python_signatures_cover_header():
+    import torch_utils.custom_ops as co
+    declared = set(declared_symbols()) - {"vfm_version"}
+    assert declared == set(co.SIGNATURES), declared ^ set(co.SIGNATURES)
+
+
+def test_argument_validation_without_gpu():
+    """Invalid arguments are rejected before any device work (VFM_ERR_ARGS = -2)."""
+    import torch_utils.custom_ops as co
+    lib = co.get_native()
+    xs = (ctypes.c_longlong * 4)(1, 1, 1, 1)
+    rc = lib.vfm_upfirdn2d(None, None, None, 0, 1, 1, 1, 1, xs, 1, 1, xs, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 1.0, None)
+    assert rc == -2
+    rc = lib.vfm_bias_act(None, None, None, None, None, None, 0, 4, 0, 1, 0.0, 1.0, -1.0, 1, 1, None)
+    assert rc == -2
+    # unsupported up factor -> "no kernel" (-1), the reference's fallback signal
+    p = ctypes.c_void_p(16)
+    rc = lib.vfm_filtered_lrelu(p, p, p, None, None, p, 0, 1, 1, 4, 4, xs, 4, 4, xs, 1, 1, 1, 1, 3, 1, 0, 0,
+                                0, 0, 0, 0, 0, 1.0, 0.2, float("inf"), 0, None)
+    assert rc == -1

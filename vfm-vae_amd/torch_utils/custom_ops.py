@@ -1,0 +1,98 @@
+"""Loader for the gfx950 kernel library (`libvfmvae_hip.so`) behind `include/vfmvae.h`.
+
+Replaces the reference's JIT plugin builder `torch_utils/custom_ops.py:59-155`
+(`get_plugin`: torch.utils.cpp_extension.load of .cpp/.cu sources into an
+md5-keyed cache). Here the kernels are prebuilt in-tree by `csrc/Makefile`
+(`__graft_entry__.build()`), the binding is ctypes over the plain C ABI, and a
+missing or unloadable library is a hard error: there is no silent fallback for
+GPU tensors.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libvfmvae_hip.so")
+_lock = threading.Lock()
+_lib = None
+
+c_int, c_ll, c_float, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
+c_llp = ctypes.POINTER(ctypes.c_longlong)
+
+# name -> argtypes (restype is always int). Keep in sync with include/vfmvae.h.
+SIGNATURES = {
+    "vfm_upfirdn2d": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_int, c_int, c_llp,
+                      c_int, c_int, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_vp],
+    "vfm_bias_act": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_int, c_int, c_float, c_float, c_float,
+                     c_ll, c_int, c_vp],
+    "vfm_filtered_lrelu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp,
+                           c_int, c_int, c_llp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_int, c_vp],
+    "vfm_filtered_lrelu_act": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_int, c_int, c_int,
+                               c_int, c_int, c_float, c_float, c_float, c_vp],
+}
+
+DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}
+VFM_NO_KERNEL = -1
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def library_path():
+    return _LIB_PATH
+
+
+def get_native():
+    """Load (once) and return the ctypes handle of the kernel library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(_LIB_PATH):
+                raise NativeError(
+                    f"HIP kernel library not found at {_LIB_PATH}; run `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(or `make -C vfm-vae_amd/csrc`)")
+            lib = ctypes.CDLL(_LIB_PATH)
+            for name, argtypes in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = argtypes
+                fn.restype = c_int
+            lib.vfm_version.restype = ctypes.c_char_p
+            _lib = lib
+    return _lib
+
+
+def get_plugin(module_name=None, sources=None, headers=None, source_dir=None, **_build_kwargs):
+    """Reference-compatible entry point (`custom_ops.get_plugin`): returns the
+    prebuilt native library regardless of the source list."""
+    return get_native()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return DTYPE_CODES[t.dtype]
+    except KeyError:
+        raise NativeError(f"unsupported dtype {t.dtype}")
+
+
+def strides(t: torch.Tensor):
+    arr = (ctypes.c_longlong * t.ndim)(*t.stride())
+    return arr
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def check(rc: int, name: str, allow_no_kernel: bool = False) -> int:
+    if rc == 0 or (allow_no_kernel and rc == VFM_NO_KERNEL):
+        return rc
+    raise NativeError(f"{name} failed with code {rc}")
