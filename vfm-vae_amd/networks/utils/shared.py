@@ -1,0 +1,115 @@
+"""Shared building blocks: FC layer with learning-rate multiplier, MLP,
+fp32-upcasting GroupNorm, StyleSplit, scale-adaptive pooling.
+
+Same classes, constructor arguments and parameter names as the reference
+`networks/utils/shared.py` (:17-189) so checkpoints load unchanged.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class ResidualBlock(nn.Module):
+    """(fn(x) + x) / sqrt(2)."""
+
+    def __init__(self, fn: nn.Module):
+        super().__init__()
+        self.fn = fn
+
+    def forward(self, x):
+        return (self.fn(x) + x) * (1.0 / math.sqrt(2))
+
+
+class FullyConnectedLayer(nn.Module):
+    """y = act(x @ (W * lr/sqrt(in))^T + b * lr). Weights are stored divided by
+    the learning-rate multiplier (equalised learning rate)."""
+
+    def __init__(self, in_features, out_features, bias=True, activation='linear', lr_multiplier=1.0,
+                 weight_init=1.0, bias_init=0.0):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.activation = activation
+        self.weight = nn.Parameter(torch.randn(out_features, in_features) * (weight_init / lr_multiplier))
+        if bias:
+            init = torch.as_tensor(bias_init, dtype=torch.float32)
+            self.bias = nn.Parameter(torch.broadcast_to(init, [out_features]).clone() / lr_multiplier)
+        else:
+            self.bias = None
+        self.weight_gain = lr_multiplier / math.sqrt(in_features)
+        self.bias_gain = lr_multiplier
+
+    def forward(self, x):
+        w = self.weight.to(x.dtype) * self.weight_gain
+        b = self.bias.to(x.dtype) * self.bias_gain if self.bias is not None else None
+        if self.activation == 'linear':
+            return torch.addmm(b.unsqueeze(0), x, w.t()) if b is not None else x.matmul(w.t())
+        y = x.matmul(w.t())
+        if b is not None:
+            y = y + b
+        if self.activation == 'relu':
+            return F.relu(y)
+        if self.activation == 'lrelu':
+            return F.leaky_relu(y, negative_slope=0.2)
+        if self.activation == 'gelu':
+            return F.gelu(y)
+        raise NotImplementedError(f"Activation '{self.activation}' not implemented.")
+
+    def extra_repr(self):
+        return f'in_features={self.in_features}, out_features={self.out_features}, activation={self.activation}'
+
+
+class MLP(nn.Module):
+    """Stack of FullyConnectedLayers named fc0..fc{n-1}; accepts [B, C] or [B, K, C]."""
+
+    def __init__(self, features_list, activation='linear', lr_multiplier=1.0, linear_out=False):
+        super().__init__()
+        self.num_layers = len(features_list) - 1
+        self.out_dim = features_list[-1]
+        for i in range(self.num_layers):
+            act = 'linear' if (linear_out and i == self.num_layers - 1) else activation
+            self.add_module(f'fc{i}', FullyConnectedLayer(features_list[i], features_list[i + 1], bias=True,
+                                                          activation=act, lr_multiplier=lr_multiplier))
+
+    def forward(self, x):
+        lead = x.shape[:-1] if x.ndim == 3 else None
+        if lead is not None:
+            x = x.flatten(0, 1)
+        for i in range(self.num_layers):
+            x = getattr(self, f'fc{i}')(x)
+        if lead is not None:
+            x = x.reshape(*lead, -1)
+        return x
+
+
+class GroupNorm32(nn.GroupNorm):
+    """GroupNorm evaluated in fp32, result cast back to the input dtype."""
+
+    def forward(self, x):
+        from torch_utils.ops import decoder_ops
+        return decoder_ops.group_norm(x, self.num_groups, self.weight, self.bias, self.eps, out_dtype=x.dtype)
+
+
+class StyleSplit(nn.Module):
+    """FC to 3*C features split as m1 * m2 + m3."""
+
+    def __init__(self, in_channels, out_channels, **kwargs):
+        super().__init__()
+        self.proj = FullyConnectedLayer(in_channels, 3 * out_channels, **kwargs)
+
+    def forward(self, x):
+        m1, m2, m3 = self.proj(x).chunk(3, dim=1)
+        return m1 * m2 + m3
+
+
+class ScaleAdaptiveAvgPool2d(nn.Module):
+    def __init__(self, scale_factor: float):
+        super().__init__()
+        self.scale_factor = scale_factor
+
+    def forward(self, x):
+        h = max(1, int(x.shape[2] * self.scale_factor))
+        w = max(1, int(x.shape[3] * self.scale_factor))
+        return F.adaptive_avg_pool2d(x, (h, w))

@@ -1,0 +1,141 @@
+"""Decoder ops that actually run in the shipped configs (ConvNeXt synthesis layers,
+separable upsampling, z-conv stems), with a HIP path on ROCm devices and a
+pure-torch path elsewhere.
+
+Reference call sites: `networks/utils/convnext_utils.py:36-257`
+(modulated_pointwise_conv2d, ConvNeXtSynthesisLayer, SeparableUpsampleWithFixedBlur),
+`networks/utils/shared.py:165-167` (GroupNorm32), `networks/generator.py:839-868`.
+
+Each public function takes `impl` ('cuda' | 'ref'); 'cuda' on a ROCm tensor
+dispatches to the gfx950 kernels when they are built for that op (see
+`_HIP_OPS`), otherwise (CPU tensors or impl='ref') the torch formulation runs.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+_HIP_OPS = set()          # names of ops whose HIP path is available (filled by decoder_hip)
+_FORCE_REF = False        # global switch for A/B experiments and CPU restatement timing
+
+
+def _use_hip(name, x, impl):
+    return impl == 'cuda' and x.is_cuda and not _FORCE_REF and name in _HIP_OPS
+
+
+def set_force_ref(flag: bool):
+    global _FORCE_REF
+    _FORCE_REF = bool(flag)
+
+
+# ---------------------------------------------------------------------------
+# GroupNorm (fp32 statistics), optionally fused with a per-sample channel scale.
+
+
+def group_norm(x, num_groups, weight=None, bias=None, eps=1e-5, out_dtype=None, style=None, impl='cuda'):
+    """out = (GN(x.float()) * weight + bias) [* style[b, c]] cast to out_dtype.
+
+    `style` ([B, C]) folds the input modulation of a modulated 1x1 conv into the
+    normalisation pass (w_b = W * s_b  <=>  W @ (s_b * x))."""
+    out_dtype = out_dtype or x.dtype
+    if _use_hip('group_norm', x, impl):
+        from . import decoder_hip
+        return decoder_hip.group_norm(x, num_groups, weight, bias, eps, out_dtype, style)
+    y = F.group_norm(x.float(), num_groups, weight.float() if weight is not None else None,
+                     bias.float() if bias is not None else None, eps)
+    if style is not None:
+        y = y * style.float()[:, :, None, None]
+    return y.to(out_dtype)
+
+
+# ---------------------------------------------------------------------------
+# Depthwise k x k convolution (+bias, + optional additive [H, W] plane).
+
+
+def dwconv2d(x, weight, bias=None, padding=0, noise=None, impl='cuda'):
+    """Depthwise conv: weight [C, 1, k, k], zero padding `padding`, stride 1.
+    `noise` ([H_out, W_out], fp32) is added to every channel (legacy noise path)."""
+    if _use_hip('dwconv2d', x, impl):
+        from . import decoder_hip
+        return decoder_hip.dwconv2d(x, weight, bias, padding, noise)
+    y = F.conv2d(x, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None, padding=padding,
+                 groups=x.shape[1])
+    if noise is not None:
+        y = y + noise.to(y.dtype)
+    return y
+
+
+# ---------------------------------------------------------------------------
+# Modulated 1x1 epilogue: gelu(h * dcoef[b, o] + bias[o]).
+
+
+def scale_bias_gelu(h, scale=None, bias=None, impl='cuda'):
+    """h: [B, O, P]; scale: [B, O] fp32 (demodulation); bias: [O]. Exact (erf) GELU."""
+    if _use_hip('scale_bias_gelu', h, impl):
+        from . import decoder_hip
+        return decoder_hip.scale_bias_gelu(h, scale, bias)
+    z = h.float()
+    if scale is not None:
+        z = z * scale.float()[:, :, None]
+    if bias is not None:
+        z = z + bias.float()[None, :, None]
+    return F.gelu(z).to(h.dtype)
+
+
+# ---------------------------------------------------------------------------
+# Residual with layer scale: x_in + gamma[c] * (y + b[c]).
+
+
+def layer_scale_residual(y, bias, gamma, x_in, impl='cuda'):
+    """y: [B, C, P] (or [B, C, H, W]); bias, gamma: [C]; x_in like y. Output dtype = x_in.dtype."""
+    if _use_hip('layer_scale_residual', y, impl):
+        from . import decoder_hip
+        return decoder_hip.layer_scale_residual(y, bias, gamma, x_in)
+    shape = [1, -1] + [1] * (y.ndim - 2)
+    z = y.float()
+    if bias is not None:
+        z = z + bias.float().reshape(shape)
+    if gamma is not None:
+        z = z * gamma.float().reshape(shape)
+    return (z + x_in.float()).to(x_in.dtype)
+
+
+# ---------------------------------------------------------------------------
+# Fixed separable blur with replicate padding, fused with the pixel shuffle.
+
+
+def shuffle_blur(x, blur1d, upscale=2, impl='cuda'):
+    """PixelShuffle(upscale) followed by replicate-pad + depthwise blur with the
+    normalised outer product of `blur1d` (a python list of taps)."""
+    if _use_hip('shuffle_blur', x, impl):
+        from . import decoder_hip
+        return decoder_hip.shuffle_blur(x, blur1d, upscale)
+    y = F.pixel_shuffle(x, upscale)
+    return blur_replicate(y, blur1d, impl='ref')
+
+
+def blur_replicate(x, blur1d, impl='cuda'):
+    if _use_hip('blur_replicate', x, impl):
+        from . import decoder_hip
+        return decoder_hip.blur_replicate(x, blur1d)
+    k = torch.tensor(blur1d, dtype=torch.float32)
+    k2 = torch.outer(k, k)
+    k2 = k2 / k2.sum()
+    kh, kw = k2.shape
+    ph, pw = (kh - 1) // 2, (kw - 1) // 2
+    pad = (pw, pw + int(kw % 2 == 0), ph, ph + int(kh % 2 == 0))
+    c = x.shape[1]
+    w = k2[None, None].repeat(c, 1, 1, 1).to(device=x.device, dtype=x.dtype)
+    return F.conv2d(F.pad(x, pad, mode='replicate'), w, groups=c)
+
+
+def demod_coefficients(weight2d, style, eps=1e-8):
+    """dcoef[b, o] = rsqrt(sum_i (W[o, i] * s[b, i])^2 + eps), computed as a tiny GEMM."""
+    return torch.rsqrt(style.float().square() @ weight2d.float().square().t() + eps)
+
+
+def gelu_tanh(x):
+    return F.gelu(x, approximate='tanh')
+
+
+SQRT1_2 = 1.0 / math.sqrt(2.0)

@@ -1,0 +1,88 @@
+"""Differentiable augmentation (DiffAugment: color, translation, cutout, resize).
+
+Same policies, parameter ranges and device-RNG draw order as the reference
+`training/diffaug.py` (after Zhao et al. 2020), so seeded runs draw identical
+augmentations.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def DiffAugment(x, policy='', channels_first=True):
+    if not policy:
+        return x
+    if not channels_first:
+        x = x.permute(0, 3, 1, 2)
+    for p in policy.split(','):
+        for fn in AUGMENT_FNS[p]:
+            x = fn(x)
+    if not channels_first:
+        x = x.permute(0, 2, 3, 1)
+    return x.contiguous()
+
+
+def _u(x):
+    return torch.rand(x.size(0), 1, 1, 1, dtype=x.dtype, device=x.device)
+
+
+def rand_brightness(x):
+    return x + (_u(x) - 0.5)
+
+
+def rand_saturation(x):
+    m = x.mean(dim=1, keepdim=True)
+    return (x - m) * (_u(x) * 2) + m
+
+
+def rand_contrast(x):
+    m = x.mean(dim=[1, 2, 3], keepdim=True)
+    return (x - m) * (_u(x) + 0.5) + m
+
+
+def rand_translation(x, ratio=0.125):
+    B, C, H, W = x.shape
+    sx, sy = int(H * ratio + 0.5), int(W * ratio + 0.5)
+    tx = torch.randint(-sx, sx + 1, size=[B, 1, 1], device=x.device)
+    ty = torch.randint(-sy, sy + 1, size=[B, 1, 1], device=x.device)
+    gb, gx, gy = torch.meshgrid(torch.arange(B, device=x.device), torch.arange(H, device=x.device),
+                                torch.arange(W, device=x.device), indexing='ij')
+    gx = torch.clamp(gx + tx + 1, 0, H + 1)
+    gy = torch.clamp(gy + ty + 1, 0, W + 1)
+    xp = F.pad(x, [1, 1, 1, 1, 0, 0, 0, 0])
+    return xp.permute(0, 2, 3, 1).contiguous()[gb, gx, gy].permute(0, 3, 1, 2)
+
+
+def rand_cutout(x, ratio=0.2):
+    B, C, H, W = x.shape
+    ch, cw = int(H * ratio + 0.5), int(W * ratio + 0.5)
+    ox = torch.randint(0, H + (1 - ch % 2), size=[B, 1, 1], device=x.device)
+    oy = torch.randint(0, W + (1 - cw % 2), size=[B, 1, 1], device=x.device)
+    gb, gx, gy = torch.meshgrid(torch.arange(B, device=x.device), torch.arange(ch, device=x.device),
+                                torch.arange(cw, device=x.device), indexing='ij')
+    gx = torch.clamp(gx + ox - ch // 2, min=0, max=H - 1)
+    gy = torch.clamp(gy + oy - cw // 2, min=0, max=W - 1)
+    mask = torch.ones(B, H, W, dtype=x.dtype, device=x.device)
+    mask[gb, gx, gy] = 0
+    return x * mask.unsqueeze(1)
+
+
+def rand_resize(x, min_ratio=0.8, max_ratio=1.2):
+    r = np.random.rand() * (max_ratio - min_ratio) + min_ratio
+    size = x.shape[3]
+    new = int(r * size)
+    y = F.interpolate(x, size=new, mode='bilinear')
+    if new < size:
+        left = int((size - new) / 2.)
+        right = size - left - y.shape[3]
+        return F.pad(y, (left, right, left, right), "constant", 0.)
+    left = int((new - size) / 2.)
+    return y[:, :, left:left + size, left:left + size]
+
+
+AUGMENT_FNS = {
+    'color': [rand_brightness, rand_saturation, rand_contrast],
+    'translation': [rand_translation],
+    'resize': [rand_resize],
+    'cutout': [rand_cutout],
+}

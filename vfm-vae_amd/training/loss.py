@@ -1,0 +1,574 @@
+"""VFM-VAE training losses: the caller of the hot path.
+
+Same class, constructor arguments (the YAML `loss_kwargs` surface) and
+`accumulate_gradients(phase, real_img, real_c, cur_nimg)` contract as the
+reference `training/loss.py` (ImageTransform :39-73, TotalLoss :76-1001; D phase
+:558-719, G phase :721-1001, safe-loss :624-695/:842-946, adaptive VF weight
+:262-271, phase bookkeeping :381-492). Loss values, gradients and the
+skip/flag semantics are the reference's.
+
+Host-sync economy (same results): the nine per-microbatch `.item()` reads of the
+safe-loss check are one stacked device->host copy, and the two safe-loss
+collectives are merged into one all_reduce of a small int vector (MAX of the skip
+flag == MIN of the negated marks).
+"""
+import math
+from collections import deque
+from typing import Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from torch_utils import training_stats
+from torch_utils import distributed as dist
+from torch_utils.ops import upfirdn2d
+from training.lpips import LPIPS
+from networks.utils.vfm_utils import VFM2INTERPOLATION
+from networks.utils.dataclasses import GeneratorForwardOutput, DiscriminatorForwardOutput
+
+SAFE_MARK, UNSAFE_MARK = 1, 0
+
+
+class ImageTransform(nn.Module):
+    """Applies the generator's equivariance transform to the target image and
+    builds multiscale targets (reference loss.py:39-73)."""
+
+    def __init__(self, apply_equivariance=False, interpolation='bilinear'):
+        super().__init__()
+        self.apply_equivariance = apply_equivariance
+        self.interpolation = interpolation
+
+    def _interpolate(self, img, *, size=None, scale_factor=None):
+        kw = dict(mode=self.interpolation)
+        if self.interpolation in ("bilinear", "bicubic"):
+            kw["align_corners"] = False
+            if (scale_factor and scale_factor < 1.0) or (size and size < img.shape[-1]):
+                kw["antialias"] = True
+        return F.interpolate(img, size=size, scale_factor=scale_factor, **kw)
+
+    def forward(self, img, eq_scale_factor, eq_angle_factor):
+        if self.apply_equivariance:
+            if eq_scale_factor != 1.0:
+                img = self._interpolate(img, scale_factor=eq_scale_factor)
+            if eq_angle_factor % 4 != 0:
+                img = torch.rot90(img, k=eq_angle_factor, dims=[-1, -2])
+        return img
+
+    def multiscale_forward(self, img, targets):
+        return [self._interpolate(img, size=t.shape[-1]) for t in targets]
+
+
+def _gaussian_window(size, sigma, device, dtype):
+    x = torch.arange(size, dtype=dtype, device=device) - (size - 1) / 2
+    g = torch.exp(-(x / sigma) ** 2 / 2)
+    return g / g.sum()
+
+
+class SSIM(nn.Module):
+    """Gaussian SSIM (11x11, sigma 1.5, k1 .01, k2 .03, reflect padding, mean),
+    the torchmetrics StructuralSimilarityIndexMeasure defaults used by the
+    reference (loss.py:150) with `data_range`."""
+
+    def __init__(self, data_range=2.0, kernel_size=11, sigma=1.5, k1=0.01, k2=0.03):
+        super().__init__()
+        self.data_range, self.kernel_size, self.sigma, self.k1, self.k2 = data_range, kernel_size, sigma, k1, k2
+
+    def forward(self, preds, target):
+        c = preds.shape[1]
+        g = _gaussian_window(self.kernel_size, self.sigma, preds.device, preds.dtype)
+        win = (g[:, None] * g[None, :])[None, None].repeat(c * 5, 1, 1, 1)
+        pad = (self.kernel_size - 1) // 2
+        p = F.pad(preds, [pad] * 4, mode='reflect')
+        t = F.pad(target, [pad] * 4, mode='reflect')
+        stack = torch.cat([p, t, p * p, t * t, p * t], dim=1)
+        out = F.conv2d(stack, win, groups=c * 5)
+        mu_p, mu_t, e_pp, e_tt, e_pt = out.split(c, dim=1)
+        c1 = (self.k1 * self.data_range) ** 2
+        c2 = (self.k2 * self.data_range) ** 2
+        s_pp, s_tt, s_pt = e_pp - mu_p ** 2, e_tt - mu_t ** 2, e_pt - mu_p * mu_t
+        ssim = ((2 * mu_p * mu_t + c1) * (2 * s_pt + c2)) / ((mu_p ** 2 + mu_t ** 2 + c1) * (s_pp + s_tt + c2))
+        return ssim.mean()
+
+
+class TotalLoss:
+    def __init__(self, device, G, D, vfm_name, resume_kimg, use_equivariance_regularization, blur_init_sigma=2,
+                 blur_fade_kimg=0, l1_pixel_loss_weight=1.0, l2_pixel_loss_weight=0.0, perceptual_loss_weight=10.0,
+                 ssim_loss_weight=0.0, multiscale_pixel_loss_weights=[], multiscale_block_indices=[],
+                 multiscale_pixel_loss_start_kimg=0, multiscale_pixel_loss_end_kimg=2000, vf_loss_weight=0.0,
+                 use_adaptive_vf_loss=False, clip_loss_weight=0.0, clip_loss_start_kimg=0,
+                 matching_aware_loss_weight=0.0, matching_aware_loss_start_kimg=0, compression_mode='continuous',
+                 kl_loss_weight=1e-6, entropy_loss_weight=0.0, vq_loss_weight=1.0,
+                 stylegan_t_discriminator_loss_weight=1.0, patchgan_discriminator_loss_weight=0.0,
+                 patchgan_discriminator_loss_type='mse', feature_matching_loss_weight=1.0,
+                 use_stylegan_t_disc_warmup=False, use_patchgan_disc_warmup=False, total_kimg=0):
+        self.device = device
+        self.G = G
+        self.D = D
+        self.vfm_name = (vfm_name or '').lower()
+        self.interpolation = 'bilinear'
+        for name in VFM2INTERPOLATION:
+            if name in self.vfm_name:
+                self.interpolation = VFM2INTERPOLATION[name]
+                break
+        self.resume_kimg = resume_kimg
+        self.prev_loss_dict = None
+        self.safe_loss_checking_start_nimg = 50_000
+        self.img_transform = ImageTransform(apply_equivariance=use_equivariance_regularization,
+                                            interpolation=self.interpolation)
+        self.blur_init_sigma = blur_init_sigma
+        self.blur_curr_sigma = blur_init_sigma
+        self.blur_fade_kimg = blur_fade_kimg
+        self.l1_pixel_loss_weight = l1_pixel_loss_weight
+        self.l2_pixel_loss_weight = l2_pixel_loss_weight
+        self.perceptual_loss_weight = perceptual_loss_weight
+        self.perceptual_module = LPIPS().eval().to(device).requires_grad_(False) if perceptual_loss_weight > 0 else None
+        self.ssim_loss_weight = ssim_loss_weight
+        self.ssim_module = SSIM(data_range=2.0).to(device) if ssim_loss_weight > 0 else None
+        assert len(multiscale_pixel_loss_weights) == len(multiscale_block_indices)
+        self.multiscale_pixel_loss_weights = multiscale_pixel_loss_weights
+        self.multiscale_block_indices = multiscale_block_indices
+        self.multiscale_pixel_loss_start_kimg = multiscale_pixel_loss_start_kimg
+        self.multiscale_pixel_loss_end_kimg = multiscale_pixel_loss_end_kimg
+        self.vf_loss_weight = vf_loss_weight
+        self.use_adaptive_vf_loss = use_adaptive_vf_loss
+        self.clip_loss_weight = clip_loss_weight
+        self.clip_loss_start_kimg = clip_loss_start_kimg
+        if clip_loss_weight > 0:
+            raise NotImplementedError("CLIP loss needs open_clip pretrained weights (not in any shipped config)")
+        self.matching_aware_loss_weight = matching_aware_loss_weight
+        self.matching_aware_loss_start_kimg = matching_aware_loss_start_kimg
+        self.compression_mode = compression_mode
+        self.kl_loss_weight = kl_loss_weight
+        self.entropy_loss_weight = entropy_loss_weight
+        self.vq_loss_weight = vq_loss_weight
+        self.patchgan_discriminator_loss_type = patchgan_discriminator_loss_type
+        self.stylegan_t_discriminator_loss_weight = stylegan_t_discriminator_loss_weight
+        self.patchgan_discriminator_loss_weight = patchgan_discriminator_loss_weight
+        self.use_stylegan_t_disc_warmup = use_stylegan_t_disc_warmup
+        self.use_patchgan_disc_warmup = use_patchgan_disc_warmup
+        self.feature_matching_loss_weight = feature_matching_loss_weight
+        self._stylegan_t_on = stylegan_t_discriminator_loss_weight > 0 and not use_stylegan_t_disc_warmup
+        self._patchgan_on = patchgan_discriminator_loss_weight > 0 and not use_patchgan_disc_warmup
+        self._perceptual_loss_on = perceptual_loss_weight > 0
+        self._ssim_loss_on = ssim_loss_weight > 0
+        self._multiscale_pixel_loss_on = sum(multiscale_pixel_loss_weights) > 0
+        self._pixel_loss_on = (l1_pixel_loss_weight > 0 or l2_pixel_loss_weight > 0)
+        self._window_size = 100
+        self._pixel_loss_window_type = 'l1' if l1_pixel_loss_weight > 0 else 'l2'
+        self._pixel_window = deque(maxlen=self._window_size)
+        self._pixel_thresh, self._pixel_diff_thresh, self._pixel_patience, self._pixel_cn = 0.1, 0.01, 10, 0
+        self._d_window = deque(maxlen=self._window_size)
+        self._d_thresh, self._d_diff_thresh, self._d_patience, self._d_cn = 0.1, 0.05, 10, 0
+        self._freeze_done = False
+        self._off_done = False
+        self.total_kimg = total_kimg
+        self.grad_sync = {}        # phase name -> GradBucketer (set by the training loop / bench)
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def blur(img, blur_sigma):
+        blur_size = np.floor(blur_sigma * 3)
+        if blur_size > 0:
+            with torch.autograd.profiler.record_function('blur'):
+                f = torch.arange(-blur_size, blur_size + 1, device=img.device).div(blur_sigma).square().neg().exp2()
+                img = upfirdn2d.filter2d(img, f / f.sum())
+        return img
+
+    def set_blur_sigma(self, cur_nimg):
+        if self.blur_fade_kimg > 1:
+            self.blur_curr_sigma = max(1 - cur_nimg / (self.blur_fade_kimg * 1e3), 0) * self.blur_init_sigma
+        else:
+            self.blur_curr_sigma = 0
+
+    def run_G(self, z, c) -> GeneratorForwardOutput:
+        return self.G(z, c)
+
+    def run_D(self, img, c_enc) -> DiscriminatorForwardOutput:
+        return self.D(self.blur(img, self.blur_curr_sigma), c_enc)
+
+    def calculate_pixel_loss(self, real, gen, type='l1'):
+        return F.l1_loss(real, gen).mean() if type == 'l1' else F.mse_loss(real, gen).mean()
+
+    def calculate_perceptual_loss(self, real_img, gen_img):
+        return self.perceptual_module(real_img, gen_img).mean()
+
+    def calculate_ssim_loss(self, real_img, gen_img):
+        return 1.0 - self.ssim_module(gen_img.clamp(-1, 1), real_img.clamp(-1, 1))
+
+    def calculate_cur_vf_loss_weight(self, rec_loss, vf_loss, last_layer):
+        if not self.use_adaptive_vf_loss:
+            return self.vf_loss_weight
+        rec_grads = torch.autograd.grad(rec_loss, last_layer, retain_graph=True)[0]
+        vf_grads = torch.autograd.grad(vf_loss, last_layer, retain_graph=True)[0]
+        w = torch.norm(rec_grads) / (torch.norm(vf_grads) + 1e-4)
+        return torch.clamp(w, 0.0, 1e8).detach() * self.vf_loss_weight
+
+    @staticmethod
+    def calculate_matching_aware_loss(real_logits, gen_logits):
+        return (F.softplus(real_logits) + F.softplus(gen_logits)).mean()
+
+    @staticmethod
+    def calculate_spherical_distance(x, y):
+        return (F.normalize(x, dim=-1) * F.normalize(y, dim=-1)).sum(-1).arccos().pow(2)
+
+    def calculate_stylegan_t_disc_loss(self, logits, type):
+        return F.relu(1.0 - logits).mean() if type == 'real' else F.relu(1.0 + logits).mean()
+
+    def _patch_loss(self, pred, is_real):
+        t = self.patchgan_discriminator_loss_type
+        if t == 'bce':
+            return F.binary_cross_entropy_with_logits(pred, torch.ones_like(pred) if is_real else torch.zeros_like(pred))
+        if t == 'mse':
+            return F.mse_loss(pred, torch.ones_like(pred) if is_real else torch.zeros_like(pred))
+        if t == 'hinge':
+            return F.relu(1.0 - pred).mean() if is_real else F.relu(1.0 + pred).mean()
+        raise ValueError(f"Unsupported PatchGAN loss type: {t}")
+
+    def calculate_patchgan_disc_loss(self, logits, type):
+        assert type in ['real', 'fake']
+        if len(logits) == 0:
+            return torch.tensor(0.0, device=self.device)
+        return sum(self._patch_loss(s[-1], type == 'real') for s in logits) / len(logits)
+
+    def calculate_patchgan_gen_loss(self, logits):
+        if len(logits) == 0:
+            return torch.tensor(0.0, device=self.device)
+        loss = 0.
+        for s in logits:
+            pred = s[-1]
+            if self.patchgan_discriminator_loss_type == 'hinge':
+                loss += (-pred).mean()
+            else:
+                loss += self._patch_loss(pred, True)
+        return loss / len(logits)
+
+    def calculate_feature_matching_loss(self, real_features, fake_features):
+        loss = 0.
+        d_w = 1.0 / len(real_features)
+        for rf, ff in zip(real_features, fake_features):
+            feat_w = 4.0 / max(len(rf) - 1, 1)
+            for r, f in zip(rf[:-1], ff[:-1]):
+                loss += d_w * feat_w * F.l1_loss(f, r.detach())
+        return loss
+
+    def _safe_resize(self, img, size):
+        kw = dict(mode=self.interpolation)
+        if self.interpolation in ("bilinear", "bicubic"):
+            kw["align_corners"] = False
+            if img.size(-1) > size:
+                kw["antialias"] = True
+        return F.interpolate(img, size, **kw)
+
+    def _off_reconstruction_and_quantization_losses(self):
+        self._perceptual_loss_on = self._ssim_loss_on = self._multiscale_pixel_loss_on = self._pixel_loss_on = False
+        self.perceptual_loss_weight = self.ssim_loss_weight = 0.0
+        self.multiscale_pixel_loss_weights = [0.0] * len(self.multiscale_pixel_loss_weights)
+        self.l1_pixel_loss_weight = self.l2_pixel_loss_weight = 0.0
+        self.kl_loss_weight = self.vq_loss_weight = self.vf_loss_weight = 0.0
+        dist.print0("[Reconstruction & Quantization Losses] Off perceptual, SSIM, multiscale pixel, pixel, KL, VQ, and VF losses.")
+
+    def _sync_safety(self, skip_local: bool, marks: list):
+        """One collective: returns (skip_any_rank, marks_min_over_ranks)."""
+        vec = torch.tensor([int(skip_local)] + [-int(m) for m in marks], dtype=torch.int32, device=self.device)
+        if dist.is_initialized():
+            torch.distributed.all_reduce(vec, op=torch.distributed.ReduceOp.MAX)
+        vals = vec.tolist()
+        return bool(vals[0]), [-v for v in vals[1:]]
+
+    def _update_phase(self, cur_nimg, pixel_loss_now, d_now):
+        """Warm-up bookkeeping on rank 0, flags broadcast to all ranks (reference :381-492)."""
+        cur_kimg = cur_nimg // 1000
+        need_freeze32 = False
+        if (not dist.is_initialized()) or dist.get_rank() == 0:
+            self._d_window.append(d_now)
+            d_mean = np.mean(self._d_window)
+            if not self._stylegan_t_on and self.use_stylegan_t_disc_warmup:
+                self._pixel_window.append(pixel_loss_now)
+                if len(self._pixel_window) == self._pixel_window.maxlen and np.mean(self._pixel_window) < self._pixel_thresh:
+                    vals = list(self._pixel_window)
+                    half = len(vals) // 2
+                    diff = abs(np.mean(vals[half:]) - np.mean(vals[:half]))
+                    if diff < self._pixel_diff_thresh:
+                        self._pixel_cn += 1
+                    elif self._pixel_cn > 0:
+                        self._pixel_cn = 0
+                    self._pixel_window = deque(vals[half:], maxlen=self._pixel_window.maxlen)
+                    if self._pixel_cn >= self._pixel_patience:
+                        self._stylegan_t_on = True
+                        dist.print0(f"[WARM-UP-StyleGAN-T] enabled @ {cur_kimg} kimg")
+            if not self._patchgan_on and self.use_patchgan_disc_warmup:
+                if len(self._d_window) == self._d_window.maxlen and d_mean < self._d_thresh:
+                    vals = list(self._d_window)
+                    half = len(vals) // 2
+                    diff = abs(np.mean(vals[half:]) - np.mean(vals[:half]))
+                    if diff < self._d_diff_thresh:
+                        self._d_cn += 1
+                    elif self._d_cn > 0:
+                        self._d_cn = 0
+                    self._d_window = deque(vals[half:], maxlen=self._d_window.maxlen)
+                    if self._d_cn >= self._d_patience:
+                        need_freeze32 = True
+                        self._patchgan_on = True
+                        dist.print0(f"[WARM-UP-PatchGAN] enabled @ {cur_kimg} kimg")
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            flags = torch.tensor([int(self._stylegan_t_on), int(self._patchgan_on), int(self._perceptual_loss_on),
+                                  int(self._pixel_loss_on), int(self._ssim_loss_on),
+                                  int(self._multiscale_pixel_loss_on), int(need_freeze32)],
+                                 dtype=torch.int32, device=self.device)
+            torch.distributed.broadcast(flags, src=0)
+            f = flags.tolist()
+            (self._stylegan_t_on, self._patchgan_on, self._perceptual_loss_on, self._pixel_loss_on,
+             self._ssim_loss_on, self._multiscale_pixel_loss_on) = [bool(v) for v in f[:6]]
+            need_freeze32 = bool(f[6])
+        if need_freeze32 and not self._freeze_done:
+            self.G.set_train_mode('freeze32')
+            self._freeze_done = True
+        if self._patchgan_on and not self._off_done:
+            self._off_reconstruction_and_quantization_losses()
+            self._off_done = True
+
+    @staticmethod
+    def _agg_patchgan_per_scale(logits):
+        out = []
+        for s in logits or []:
+            pred = s[-1] if isinstance(s, list) else s
+            scores = pred.view(pred.size(0), -1).mean(dim=1)
+            out.append((scores.mean(), scores.sign().mean()))
+        return out
+
+    # ------------------------------------------------------------------ main
+    def accumulate_gradients(self, phase, real_img, real_c, cur_nimg):
+        self.set_blur_sigma(cur_nimg)
+        is_text_cond = isinstance(real_c, list) and len(real_c) > 0 and isinstance(real_c[0], str)
+        zero = lambda: torch.tensor(0.0, device=self.device)
+        check_now = cur_nimg > (self.resume_kimg * 1e3 + self.safe_loss_checking_start_nimg)
+
+        if phase == 'D':
+            d_loss = torch.zeros([], device=self.device, requires_grad=True)
+            with torch.no_grad():
+                out = self.run_G(real_img, real_c)
+            gen_img = out.gen_img.detach()
+            eq_s, eq_a, real_c_enc = out.eq_scale_factor, out.eq_angle_factor, out.global_text_tokens
+            del out
+            c_arg = real_c_enc if is_text_cond else real_c
+            gen_d = self.run_D(gen_img, c_arg)
+            real_img = self.img_transform(real_img, eq_s, eq_a) * 2 - 1.
+            real_d = self.run_D(real_img, c_arg)
+
+            st_gen = st_real = st_loss = zero()
+            if self._stylegan_t_on and self.stylegan_t_discriminator_loss_weight > 0:
+                st_gen_logits, st_real_logits = gen_d.stylegan_t_logits, real_d.stylegan_t_logits
+                st_gen = self.calculate_stylegan_t_disc_loss(st_gen_logits, 'fake')
+                st_real = self.calculate_stylegan_t_disc_loss(st_real_logits, 'real')
+                st_loss = st_gen + st_real
+            d_loss = d_loss + self.stylegan_t_discriminator_loss_weight * st_loss
+
+            pg_gen = pg_real = pg_loss = zero()
+            if self._patchgan_on and self.patchgan_discriminator_loss_weight > 0:
+                pg_gen_logits, pg_real_logits = gen_d.patchgan_logits, real_d.patchgan_logits
+                pg_gen = self.calculate_patchgan_disc_loss(pg_gen_logits, 'fake')
+                pg_real = self.calculate_patchgan_disc_loss(pg_real_logits, 'real')
+                pg_loss = pg_gen + pg_real
+            d_loss = d_loss + self.patchgan_discriminator_loss_weight * pg_loss
+
+            ma_loss = zero()
+            ma_on = (cur_nimg >= self.matching_aware_loss_start_kimg * 1e3 and self.matching_aware_loss_weight > 0
+                     and self._stylegan_t_on)
+            if ma_on:
+                if is_text_cond:
+                    perm = torch.randperm(len(real_c))
+                    c_shuf = [real_c[i] for i in perm]
+                else:
+                    c_shuf = real_c_enc[torch.randperm(len(real_c_enc), device=real_c_enc.device)]
+                ma_loss = self.calculate_matching_aware_loss(self.run_D(real_img, c_shuf).stylegan_t_logits,
+                                                             self.run_D(gen_img, c_shuf).stylegan_t_logits)
+            d_loss = d_loss + self.matching_aware_loss_weight * ma_loss
+
+            names = ['stylegan_t_gen_loss', 'stylegan_t_real_loss', 'stylegan_t_disc_loss', 'patchgan_gen_loss',
+                     'patchgan_real_loss', 'patchgan_disc_loss', 'matching_aware_loss']
+            values = [st_gen, st_real, st_loss, pg_gen, pg_real, pg_loss, ma_loss]
+            marks = [SAFE_MARK] * len(names)
+            skip = False
+            if check_now:
+                active = [self._stylegan_t_on and self.stylegan_t_discriminator_loss_weight > 0] * 3 + \
+                         [self._patchgan_on and self.patchgan_discriminator_loss_weight > 0] * 3 + [ma_on]
+                host = torch.stack([v.detach().float() for v in values]).tolist()
+                for i, (on, v) in enumerate(zip(active, host)):
+                    if on and (not math.isfinite(v) or abs(v) > 1e4):
+                        marks[i] = UNSAFE_MARK
+                        skip = True
+            skip, marks = self._sync_safety(skip, marks)
+            if skip:
+                d_loss = torch.nan_to_num(d_loss, nan=0.0, posinf=0.0, neginf=0.0) * 0.0
+            training_stats.report('Loss/D/skipped', 1.0 if skip else 0.0)
+            for k, m in zip(names, marks):
+                training_stats.report(f'Loss/D/is_safe/{k}', int(m))
+                if not m:
+                    dist.print0(f"[SafeLoss][D] Unsafe {k} at {cur_nimg // 1000} kimg - skipping.")
+            d_loss.backward()
+            if skip:
+                return
+            if self._stylegan_t_on and self.stylegan_t_discriminator_loss_weight > 0:
+                training_stats.report('Loss/D/stylegan_t/fake_scores', st_gen_logits)
+                training_stats.report('Loss/D/stylegan_t/fake_signs', st_gen_logits.sign())
+                training_stats.report('Loss/D/stylegan_t/real_scores', st_real_logits)
+                training_stats.report('Loss/D/stylegan_t/real_signs', st_real_logits.sign())
+                training_stats.report('Loss/D/stylegan_t/gen_loss', st_gen)
+                training_stats.report('Loss/D/stylegan_t/real_loss', st_real)
+                training_stats.report('Loss/D/stylegan_t/loss', st_loss)
+            if self._patchgan_on and self.patchgan_discriminator_loss_weight > 0:
+                training_stats.report('Loss/D/patchgan/gen_loss', pg_gen)
+                training_stats.report('Loss/D/patchgan/real_loss', pg_real)
+                training_stats.report('Loss/D/patchgan/loss', pg_loss)
+                for i, (s, sg) in enumerate(self._agg_patchgan_per_scale(pg_gen_logits)):
+                    training_stats.report(f'Loss/D/patchgan/fake/scale{i}/fake_scores', s)
+                    training_stats.report(f'Loss/D/patchgan/fake/scale{i}/fake_signs', sg)
+                for i, (s, sg) in enumerate(self._agg_patchgan_per_scale(pg_real_logits)):
+                    training_stats.report(f'Loss/D/patchgan/real/scale{i}/real_scores', s)
+                    training_stats.report(f'Loss/D/patchgan/real/scale{i}/real_signs', sg)
+            if ma_on:
+                training_stats.report('Loss/D/matching_aware_loss', ma_loss)
+            return
+
+        assert phase == 'G'
+        out = self.run_G(real_img, real_c)
+        gen_img, gen_ms = out.gen_img, out.gen_multiscale_imgs
+        eq_s, eq_a, real_c_enc = out.eq_scale_factor, out.eq_angle_factor, out.global_text_tokens
+        c_arg = real_c_enc if is_text_cond else real_c
+        gen_d = self.run_D(gen_img, c_arg)
+
+        st_gen_logits = None
+        st_gen = zero()
+        if self._stylegan_t_on and self.stylegan_t_discriminator_loss_weight > 0:
+            st_gen_logits = gen_d.stylegan_t_logits
+            st_gen = (-st_gen_logits).mean()
+        pg_gen_logits = None
+        pg_gen = zero()
+        if self._patchgan_on and self.patchgan_discriminator_loss_weight > 0:
+            pg_gen_logits = gen_d.patchgan_logits
+            pg_gen = self.calculate_patchgan_gen_loss(pg_gen_logits)
+
+        real_img = self.img_transform(real_img, eq_s, eq_a)
+        real_for_loss = real_img * 2 - 1.
+        fm_loss = zero()
+        if self._patchgan_on and self.feature_matching_loss_weight > 0 and self.patchgan_discriminator_loss_weight > 0:
+            real_d = self.run_D(real_for_loss, c_arg)
+            fm_loss = self.calculate_feature_matching_loss(real_d.patchgan_logits, gen_d.patchgan_logits)
+
+        l1 = self.calculate_pixel_loss(real_for_loss, gen_img, 'l1') if (self._pixel_loss_on and self.l1_pixel_loss_weight > 0) else zero()
+        l2 = self.calculate_pixel_loss(real_for_loss, gen_img, 'l2') if (self._pixel_loss_on and self.l2_pixel_loss_weight > 0) else zero()
+        perc = self.calculate_perceptual_loss(real_for_loss, gen_img) if (self._perceptual_loss_on and self.perceptual_loss_weight > 0) else zero()
+        ssim = self.calculate_ssim_loss(real_for_loss, gen_img) if (self._ssim_loss_on and self.ssim_loss_weight > 0) else zero()
+
+        ms_loss = zero()
+        ms_losses = []
+        if self._multiscale_pixel_loss_on and len(self.multiscale_pixel_loss_weights) > 0:
+            targets = [t * 2 - 1 for t in self.img_transform.multiscale_forward(real_img, gen_ms)]
+            in_window = (self.multiscale_pixel_loss_start_kimg * 1e3 <= cur_nimg < self.multiscale_pixel_loss_end_kimg * 1e3)
+            for i in range(len(gen_ms)):
+                w = self.multiscale_pixel_loss_weights[self.multiscale_block_indices.index(i)] \
+                    if i in self.multiscale_block_indices else 0.0
+                li = self.calculate_pixel_loss(targets[i], gen_ms[i], 'l1')
+                ms_loss = ms_loss + (w * li if in_window else w * li * 0.0)
+                ms_losses.append(li)
+
+        rec = zero()
+        if self._pixel_loss_on and self.l1_pixel_loss_weight > 0:
+            rec = rec + self.l1_pixel_loss_weight * l1
+        if self._pixel_loss_on and self.l2_pixel_loss_weight > 0:
+            rec = rec + self.l2_pixel_loss_weight * l2
+        if self._perceptual_loss_on and self.perceptual_loss_weight > 0:
+            rec = rec + self.perceptual_loss_weight * perc
+        if self._ssim_loss_on and self.ssim_loss_weight > 0:
+            rec = rec + self.ssim_loss_weight * ssim
+        if self._multiscale_pixel_loss_on and sum(self.multiscale_pixel_loss_weights) > 0:
+            rec = rec + ms_loss
+
+        vf_loss = zero()
+        cur_vf_w = self.vf_loss_weight
+        if self.vf_loss_weight > 0:
+            vf_loss = out.vf_loss
+            cur_vf_w = self.calculate_cur_vf_loss_weight(rec, vf_loss, out.vf_last_layer)
+        clip_loss = zero()
+
+        names = ['l1_pixel_loss', 'l2_pixel_loss', 'perceptual_loss', 'ssim_loss', 'multiscale_pixel_loss',
+                 'stylegan_t_gen_loss', 'patchgan_gen_loss', 'feature_matching_loss', 'clip_loss']
+        base = [l1, l2, perc, ssim, ms_loss, st_gen, pg_gen, fm_loss, clip_loss]
+        host = torch.stack([v.detach().float().reshape([]) for v in base]).tolist()   # one D2H copy
+        loss_dict = dict(zip(names, host))
+        marks = [SAFE_MARK] * len(names)
+        skip = False
+        if check_now and self.prev_loss_dict is not None:
+            for i, name in enumerate(names):
+                cur, prev = loss_dict[name], self.prev_loss_dict[name]
+                bad = not math.isfinite(cur)
+                if name in names[:5]:
+                    bad = bad or ((prev > 1e-6) and (cur > prev * 10))
+                if bad:
+                    marks[i] = UNSAFE_MARK
+                    skip = True
+        skip, marks = self._sync_safety(skip, marks)
+
+        if self.compression_mode == 'continuous':
+            g_loss = (rec + self.stylegan_t_discriminator_loss_weight * st_gen
+                      + self.patchgan_discriminator_loss_weight * pg_gen
+                      + self.feature_matching_loss_weight * fm_loss + cur_vf_w * vf_loss
+                      + self.clip_loss_weight * clip_loss + self.kl_loss_weight * out.kl_loss)
+        else:
+            g_loss = (rec + self.stylegan_t_discriminator_loss_weight * st_gen
+                      + self.patchgan_discriminator_loss_weight * pg_gen
+                      + self.feature_matching_loss_weight * fm_loss + cur_vf_w * vf_loss
+                      + self.clip_loss_weight * clip_loss + self.entropy_loss_weight * out.entropy_loss
+                      + self.vq_loss_weight * out.vq_loss)
+        if skip:
+            g_loss = torch.nan_to_num(g_loss, nan=0.0, posinf=0.0, neginf=0.0) * 0.0
+        training_stats.report('Loss/G/skipped', 1.0 if skip else 0.0)
+        for k, m in zip(names, marks):
+            training_stats.report(f'Loss/G/is_safe/{k}', int(m))
+            if not m:
+                dist.print0(f"[SafeLoss][G] Unsafe {k} at {cur_nimg // 1000} kimg - skipping.")
+        g_loss.backward()
+        if skip:
+            return
+        self.prev_loss_dict = loss_dict
+
+        if self.l1_pixel_loss_weight > 0:
+            training_stats.report('Loss/G/l1_pixel_loss', l1)
+        if self.l2_pixel_loss_weight > 0:
+            training_stats.report('Loss/G/l2_pixel_loss', l2)
+        if self.perceptual_loss_weight > 0:
+            training_stats.report('Loss/G/perceptual_loss', perc)
+        if self.ssim_loss_weight > 0:
+            training_stats.report('Loss/G/ssim_loss', ssim)
+        if (self.multiscale_pixel_loss_start_kimg * 1e3 <= cur_nimg < self.multiscale_pixel_loss_end_kimg * 1e3
+                and sum(self.multiscale_pixel_loss_weights) > 0):
+            training_stats.report('Loss/G/multiscale_pixel_loss', ms_loss)
+            for i in range(len(self.multiscale_pixel_loss_weights)):
+                if i < len(ms_losses):
+                    training_stats.report(f'Loss/G/multiscale_pixel_loss_block{self.multiscale_block_indices[i]:01d}', ms_losses[i])
+        if self._stylegan_t_on and self.stylegan_t_discriminator_loss_weight > 0:
+            training_stats.report('Loss/G/stylegan_t/loss', st_gen)
+            training_stats.report('Loss/G/stylegan_t/fake_scores', st_gen_logits)
+            training_stats.report('Loss/G/stylegan_t/fake_signs', st_gen_logits.sign())
+        if self._patchgan_on and self.patchgan_discriminator_loss_weight > 0:
+            training_stats.report('Loss/G/patchgan/loss', pg_gen)
+            for i, (s, sg) in enumerate(self._agg_patchgan_per_scale(pg_gen_logits)):
+                training_stats.report(f'Loss/G/patchgan/fake/scale{i}/fake_scores', s)
+                training_stats.report(f'Loss/G/patchgan/fake/scale{i}/fake_signs', sg)
+        if self._patchgan_on and self.feature_matching_loss_weight > 0:
+            training_stats.report('Loss/G/patchgan/feature_matching_loss', fm_loss)
+        if self.vf_loss_weight > 0:
+            training_stats.report('Loss/G/vf_loss', vf_loss)
+        if self.compression_mode == 'continuous' and self.kl_loss_weight > 0:
+            training_stats.report('Loss/G/kl_loss', out.kl_loss)
+        elif self.compression_mode == 'discrete':
+            if self.entropy_loss_weight > 0:
+                training_stats.report('Loss/G/entropy_loss', out.entropy_loss)
+            if self.vq_loss_weight > 0:
+                training_stats.report('Loss/G/vq_loss', out.vq_loss)
+                training_stats.report('Loss/G/codebook_usages', out.codebook_usages)
+        pixel_now = loss_dict['l1_pixel_loss'] if self._pixel_loss_window_type == 'l1' else loss_dict['l2_pixel_loss']
+        d_now = loss_dict['stylegan_t_gen_loss'] if self.stylegan_t_discriminator_loss_weight > 0 else 0.
+        self._update_phase(cur_nimg, pixel_now, d_now)
