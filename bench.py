@@ -1,0 +1,189 @@
+#!/usr/bin/env python
+"""VFM-VAE training throughput on MI355X.
+
+Metric (BASELINE.json): train images/sec at 256^2, f16d32, SigLIP2-L encoder,
+stage-0 strong-alignment loss mix (L1 + LPIPS + multiscale + adaptive VF + KL +
+StyleGAN-T D), batch 32 per GPU. One "step" = one full training iteration of
+training/training_loop.py (D phase + G phase + gradient sync + Adam + G_ema).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (value = images/sec over all ranks, max-over-rank
+step time). Extra keys: `roofline` (dominant HIP kernel, HIP-event timed during
+the timed region) and `cpu_baseline` (the pure-torch CPU restatement of the same
+iteration on the host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "vfm-vae_amd")
+for _p in (PKG, ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np
+import torch
+import yaml
+
+CONFIG = os.path.join(PKG, "configs", "vfm_vae_f16d32_siglip2_stage_0_synthetic.yaml")
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0      # dense
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--config", default=CONFIG)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
+    return ap.parse_args(argv)
+
+
+def build(cfg_path, batch_gpu, device, world):
+    """Construct G, G_ema, D, loss, optimisers and the shared TrainingIteration."""
+    import copy
+    import dnnlib
+    from train import resolve_config
+    from training.training_loop import TrainingIteration, make_optimizer
+    c = resolve_config(yaml.safe_load(open(cfg_path)))
+    torch.manual_seed(c.get("random_seed", 42))
+    random.seed(c.get("random_seed", 42))
+    np.random.seed(c.get("random_seed", 42))
+    G = dnnlib.util.construct_class_by_name(label_dim=0, **c.G_kwargs).train().requires_grad_(False).to(device)
+    G_ema = copy.deepcopy(G).eval()
+    D = dnnlib.util.construct_class_by_name(c_dim=G.c_dim, **c.D_kwargs).train().requires_grad_(False).to(device)
+    loss = dnnlib.util.construct_class_by_name(device=device, G=G, D=D, **c.loss_kwargs)
+    G_opt = make_optimizer(G.parameters(), c.G_opt_kwargs, device)
+    D_opt = make_optimizer(D.parameters(), c.D_opt_kwargs, device)
+    step = TrainingIteration(G, D, G_ema, loss, G_opt, D_opt, batch_size=batch_gpu * world, n_batch_acc=1,
+                             ema_kimg=c.ema_kimg, ema_rampup=c.ema_rampup)
+    return c, step
+
+
+def cpu_baseline(cfg_path, threads):
+    """The same iteration through the pure-torch CPU restatement, batch 1 (bounded sample)."""
+    from oracle import cpu_step
+    return cpu_step.time_iteration(cfg_path, batch=1, threads=threads)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    from torch_utils import distributed as dist
+    from torch_utils.ops import decoder_ops, kernel_timer
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1:
+        dist.init()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    assert world == args.gpus or world_env == 1, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(device)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cudnn.benchmark = True
+    if args.force_ref_ops:
+        decoder_ops.set_force_ref(True)
+
+    c, step = build(args.config, args.batch, device, world)
+    from training.data_synthetic import SyntheticDataset
+    pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=rank).make_pool(args.batch, device)
+    labels = ['a photo'] * args.batch
+
+    def one(i, cur_nimg):
+        img = pool[i % len(pool)].to(torch.float32) / 255.
+        step([img], [labels], cur_nimg)
+
+    cur = 0
+    for i in range(args.warmup):
+        one(i, cur)
+        cur += args.batch * world
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    kernel_timer.enable(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one(args.warmup + i, cur)
+        cur += args.batch * world
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kernel_timer.enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = args.batch * world * args.steps / dt
+
+    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args.config, args.cpu_threads)
+        except Exception as e:   # reported, never fatal for the GPU number
+            cpu = {"error": repr(e)[:200]}
+    if rank == 0:
+        line = {
+            "metric": "train images/sec @256^2 f16d32 (SigLIP2-L, stage-0 strong alignment)",
+            "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic uint8 256x256x3 (seeded), random-init weights of the named architectures",
+            "config": {"workload": "f16d32 SigLIP2-L stage-0 strong-alignment training iteration (D+G+sync+Adam+EMA)",
+                       "model": "VFM-VAE f16d32 (SigLIP2-L @512 + ConvNeXt decoder + DINO ViT-S D + LPIPS-VGG16)",
+                       "global_batch": args.batch * world, "batch_per_gpu": args.batch, "seq_len": 1024,
+                       "resolution": 256, "parallelism": f"dp{world}",
+                       "decoder_ops": "torch" if args.force_ref_ops else "hip"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        dist.destroy_process_group()
+
+
+def smoke_step():
+    """One tiny training iteration on cuda:0 through the native kernels (used by smoke())."""
+    import copy
+    import tempfile
+    import dnnlib
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import net_cases
+    from training.training_loop import TrainingIteration, make_optimizer
+    from networks.generator import Generator
+    from networks.discriminator import ProjectedDiscriminator
+    from training.loss import TotalLoss
+    dev = torch.device("cuda:0")
+    d = os.path.join(tempfile.mkdtemp(), net_cases.VFM_DIRNAME)
+    os.makedirs(d)
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(os.path.join(d, "config.json"), "w"))
+    torch.manual_seed(0)
+    G = Generator(label_dim=0, **net_cases.g_kwargs(d)).train().requires_grad_(False).to(dev)
+    D = ProjectedDiscriminator(c_dim=0, **net_cases.D_KWARGS).train().requires_grad_(False).to(dev)
+    loss = TotalLoss(device=dev, G=G, D=D, **net_cases.loss_kwargs(d))
+    opt = dict(class_name='torch.optim.Adam', lr=1e-4, betas=[0.0, 0.99], eps=1e-8)
+    it = TrainingIteration(G, D, copy.deepcopy(G).eval(), loss, make_optimizer(G.parameters(), opt, dev),
+                           make_optimizer(D.parameters(), opt, dev), batch_size=2)
+    img = torch.rand(2, 3, 64, 64, device=dev)
+    it([img], [['x', 'x']], 0)
+    torch.cuda.synchronize()
+    for n, p in G.named_parameters():
+        assert torch.isfinite(p).all(), n
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,359 @@
+"""Main training loop.
+
+Same entry point and keyword surface as the reference
+`training/training_loop.py:training_loop(**c)` (:462-881): phase loop D then G,
+gradient accumulation, gradient synchronisation with mean/gain/nan_to_num
+semantics (reference sync_grads :281-289), Adam per phase, G_ema update
+(:734-742), ticks, stats.jsonl, snapshots `network-snapshot-{kimg:08d}.pth`
+with keys {G, D, G_ema, training_set_kwargs} (:782-801) and auto-resume.
+
+MI355X-specific execution (`TrainingIteration`, shared with bench.py):
+  * gradients of each phase live in ONE flat fp32 buffer (parameter .grad are
+    views), so the reduction, /world, *gain and nan_to_num are single passes;
+  * with world_size > 1 the buffer is all-reduced in buckets launched from
+    post-accumulate-grad hooks on a dedicated stream, overlapping the backward
+    (RCCL over xGMI); the math equals the reference's flat sharded all-reduce;
+  * Adam runs fused (one multi-tensor kernel) when on a GPU;
+  * the EMA update is one multi-tensor lerp over the parameters that can change
+    (frozen VFM weights are bit-identical in G and G_ema, so their EMA
+    p.lerp(p_ema, beta) is the identity and is not recomputed).
+"""
+import copy
+import json
+import math
+import os
+import random
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+import dnnlib
+from torch_utils import misc
+from torch_utils import training_stats
+from torch_utils import distributed as dist
+from torch_utils.ops import conv2d_gradfix
+
+
+# ---------------------------------------------------------------------------
+# Gradient synchronisation over a flat buffer.
+
+
+class FlatGradSync:
+    """Owns the .grad storage of the trainable parameters of one phase."""
+
+    def __init__(self, module: nn.Module, bucket_mb: float = 64.0):
+        self.module = module
+        self.bucket_mb = bucket_mb
+        self.world = dist.get_world_size()
+        self.params = []
+        self.key = None
+        self.hooks = []
+        self.comm_stream = None
+
+    def _build(self, params):
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []
+        self.params = params
+        self.key = tuple(id(p) for p in params)
+        order = list(reversed(params))              # gradients of late layers arrive first
+        total = sum(p.numel() for p in order)
+        dev = params[0].device
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.offsets = {}
+        off = 0
+        for p in order:
+            self.offsets[id(p)] = (off, p.numel())
+            off += p.numel()
+        limit = max(1, int(self.bucket_mb * 2 ** 20 / 4))
+        self.buckets = []                           # (start, end, n_params)
+        start, n, cnt = 0, 0, 0
+        self.bucket_of = {}
+        for p in order:
+            self.bucket_of[id(p)] = len(self.buckets)
+            n += p.numel()
+            cnt += 1
+            if n >= limit:
+                self.buckets.append((start, start + n, cnt))
+                start, n, cnt = start + n, 0, 0
+        if cnt:
+            self.buckets.append((start, start + n, cnt))
+        if dev.type == 'cuda' and self.world > 1:
+            self.comm_stream = torch.cuda.Stream(device=dev)
+        for p in params:
+            self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def prepare(self):
+        """Call after requires_grad is set for the phase, before the first backward."""
+        params = [p for p in self.module.parameters() if p.requires_grad and p.dtype == torch.float32]
+        if not params:
+            self.params = []
+            return
+        if tuple(id(p) for p in params) != self.key:
+            self._build(params)
+        self.flat.zero_()
+        for p in self.params:
+            off, n = self.offsets[id(p)]
+            p.grad = self.flat[off:off + n].view_as(p)
+        self.seen = set()
+        self.ready = [0] * len(self.buckets)
+        self.pending = {}
+        self.last_microbatch = True
+
+    def _on_grad(self, p):
+        self.seen.add(id(p))
+        if not self.last_microbatch or self.world <= 1:
+            return
+        bi = self.bucket_of[id(p)]
+        self.ready[bi] += 1
+        if self.ready[bi] == self.buckets[bi][2]:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        s, e, _ = self.buckets[bi]
+        view = self.flat[s:e]
+        if self.comm_stream is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(self.comm_stream):
+                self.pending[bi] = torch.distributed.all_reduce(view, async_op=True)
+        else:
+            self.pending[bi] = torch.distributed.all_reduce(view, async_op=True)
+
+    def finish(self, gain: Optional[float] = None):
+        """Complete the reduction: flat = nan_to_num(sum_ranks / world * gain)."""
+        if not self.params:
+            return
+        if self.world > 1:
+            for bi in range(len(self.buckets)):
+                if bi not in self.pending:
+                    self._launch(bi)
+            for bi in sorted(self.pending):
+                self.pending[bi].wait()
+            if self.comm_stream is not None:
+                torch.cuda.current_stream(self.flat.device).wait_stream(self.comm_stream)
+            self.flat.mul_(1.0 / self.world)
+        if gain is not None and gain != 1:
+            self.flat.mul_(gain)
+        torch.nan_to_num_(self.flat, nan=0, posinf=1e5, neginf=-1e5)
+        for p in self.params:   # parameters that produced no gradient keep grad=None (Adam skips them)
+            if id(p) not in self.seen:
+                p.grad = None
+
+
+class TrainingIteration:
+    """One optimisation iteration: D phase, G phase, EMA (reference :708-742)."""
+
+    def __init__(self, G, D, G_ema, loss, G_opt, D_opt, batch_size, n_batch_acc=1, ema_kimg=10.0,
+                 ema_rampup=0.05, bucket_mb=64.0):
+        self.G, self.D, self.G_ema, self.loss = G, D, G_ema, loss
+        self.phases = [dnnlib.EasyDict(name='D', module=D, opt=D_opt, sync=FlatGradSync(D, bucket_mb)),
+                       dnnlib.EasyDict(name='G', module=G, opt=G_opt, sync=FlatGradSync(G, bucket_mb))]
+        self.batch_size = batch_size
+        self.n_batch_acc = n_batch_acc
+        self.ema_kimg = ema_kimg
+        self.ema_rampup = ema_rampup
+        self._ema_pairs = None
+
+    @staticmethod
+    def partial_freeze(phase):
+        """Reference :446-459."""
+        if phase.name == 'D':
+            if 'dino' in phase.module._modules:
+                phase.module.dino.requires_grad_(False)
+        else:
+            phase.module.requires_grad_(False)
+            layers = phase.module.trainable_layers
+            for name, layer in phase.module.named_modules():
+                layer.requires_grad_(any(t in name for t in layers))
+
+    def run_phase(self, phase, real_imgs, real_cs, cur_nimg):
+        phase.module.requires_grad_(True)
+        self.partial_freeze(phase)
+        phase.sync.prepare()
+        n = len(real_imgs)
+        for i, (img, c) in enumerate(zip(real_imgs, real_cs)):
+            phase.sync.last_microbatch = (i == n - 1)
+            self.loss.accumulate_gradients(phase=phase.name, real_img=img, real_c=c, cur_nimg=cur_nimg)
+        phase.module.requires_grad_(False)
+        if any(p.grad is not None for p in phase.module.parameters()):
+            phase.sync.finish(gain=self.n_batch_acc)
+        phase.opt.step()
+        phase.opt.zero_grad(set_to_none=True)
+
+    @torch.no_grad()
+    def update_ema(self, cur_nimg):
+        ema_nimg = self.ema_kimg * 1000
+        if self.ema_rampup is not None:
+            ema_nimg = min(ema_nimg, cur_nimg * self.ema_rampup)
+        beta = 0.5 ** (self.batch_size / max(ema_nimg, 1e-8))
+        if self._ema_pairs is None or self._ema_pairs[0] != tuple(self.G.trainable_layers):
+            names = self.G.trainable_layers
+            dst, src = [], []
+            for (n, pe), (_, p) in zip(self.G_ema.named_parameters(), self.G.named_parameters()):
+                mod = n.rsplit('.', 1)[0]
+                if any(t in mod for t in names):
+                    dst.append(pe)
+                    src.append(p)
+                elif not torch.equal(pe, p):   # a frozen tensor that differs: keep it in the update
+                    dst.append(pe)
+                    src.append(p)
+            self._ema_pairs = (tuple(names), dst, src)
+        _, dst, src = self._ema_pairs
+        if dst:
+            # p_ema <- p.lerp(p_ema, beta) == p_ema + (1 - beta) * (p - p_ema)
+            torch._foreach_lerp_(dst, src, 1.0 - beta)
+        for be, b in zip(self.G_ema.buffers(), self.G.buffers()):
+            be.copy_(b)
+
+    def __call__(self, phase_real_img, phase_real_c, cur_nimg):
+        for phase in self.phases:
+            self.run_phase(phase, phase_real_img, phase_real_c, cur_nimg)
+        self.update_ema(cur_nimg)
+
+
+# ---------------------------------------------------------------------------
+# Data helpers.
+
+
+def split(arr, chunk_size, dim=0):
+    if isinstance(arr, list):
+        return [arr[i:i + chunk_size] for i in range(0, len(arr), chunk_size)]
+    return list(torch.split(arr, chunk_size, dim)) if isinstance(arr, torch.Tensor) else \
+        np.array_split(arr, int(np.ceil(len(arr) / chunk_size)), dim)
+
+
+def preprocess_image(image, device):
+    return image.to(device, non_blocking=True).to(torch.float32) / 255.
+
+
+def fetch_data(iterator, device, batch_gpu):
+    real_img, real_cs = next(iterator)
+    real_img = preprocess_image(real_img, device)
+    real_cs = real_cs if isinstance(real_cs[0], str) else real_cs.to(device)
+    return split(real_img, batch_gpu), split(real_cs, batch_gpu)
+
+
+def load_state_dict_with_report(model, state_dict, name="model", strict=False, max_items=10):
+    res = model.load_state_dict(state_dict, strict=strict)
+    missing, unexpected = list(res.missing_keys), list(res.unexpected_keys)
+    dist.print0(f"[resume:{name}] loaded; missing={len(missing)} unexpected={len(unexpected)}")
+    for k in missing[:max_items]:
+        dist.print0(f"      missing {k}")
+    for k in unexpected[:max_items]:
+        dist.print0(f"      unexpected {k}")
+    return res
+
+
+def make_optimizer(params, opt_kwargs, device):
+    kw = dict(opt_kwargs)
+    if device.type == 'cuda' and kw.get('class_name') == 'torch.optim.Adam' and 'fused' not in kw:
+        kw['fused'] = True
+    params = [p for p in params]
+    return dnnlib.util.construct_class_by_name(params=params, **kw)
+
+
+def save_snapshot(path, G, D, G_ema, training_set_kwargs):
+    torch.save({"G": G.state_dict(), "D": D.state_dict(), "G_ema": G_ema.state_dict(),
+                "training_set_kwargs": dict(training_set_kwargs)}, path)
+
+
+# ---------------------------------------------------------------------------
+
+
+def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={}, data_loader_kwargs={},
+                  G_kwargs={}, D_kwargs={}, G_opt_kwargs={}, D_opt_kwargs={}, loss_kwargs={}, metrics=[],
+                  random_seed=0, batch_size=4, batch_gpu=4, accumulate_gradients=1, ema_kimg=10, ema_rampup=0.05,
+                  total_kimg=25000, kimg_per_tick=4, image_snapshot_ticks=50, network_snapshot_ticks=50,
+                  resume_path=None, resume_kimg=0, resume_discriminator=True, cudnn_benchmark=True, abort_fn=None,
+                  progress_fn=None, one_epoch=False, device=None, train_sample_dir=None, wandb_project_name=None,
+                  wandb_run_name=None, max_iterations=None, **_unused):
+    device = device or (torch.device('cuda') if torch.cuda.is_available() else torch.device('cpu'))
+    start_time = time.time()
+    base_seed = random_seed * dist.get_world_size() + dist.get_rank()
+    np.random.seed(base_seed)
+    torch.manual_seed(base_seed)
+    random.seed(base_seed)
+    torch.backends.cudnn.benchmark = cudnn_benchmark
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    conv2d_gradfix.enabled = True
+
+    dist.print0('Loading training set...')
+    training_set = dnnlib.util.construct_class_by_name(**training_set_kwargs)
+    iterator = iter(training_set.iterate(batch_size=batch_size // dist.get_world_size(), rank=dist.get_rank(),
+                                         world=dist.get_world_size(), seed=base_seed))
+
+    dist.print0('Constructing networks...')
+    G = dnnlib.util.construct_class_by_name(label_dim=getattr(training_set, 'label_dim', 0), **G_kwargs)
+    G = G.train().requires_grad_(False).to(device)
+    G_ema = copy.deepcopy(G).eval()
+    D = dnnlib.util.construct_class_by_name(c_dim=G.c_dim, **D_kwargs).train().requires_grad_(False).to(device)
+
+    if resume_path is not None and dist.get_rank() == 0:
+        ckpt = torch.load(resume_path, map_location=device, weights_only=True)
+        if resume_discriminator and "D" in ckpt:
+            load_state_dict_with_report(D, ckpt["D"], name="D")
+        for key, net in (("G", G), ("G_ema", G_ema)):
+            if key in ckpt:
+                load_state_dict_with_report(net, ckpt[key], name=key)
+    if dist.get_world_size() > 1:
+        for module in (G, D, G_ema):
+            for t in misc.params_and_buffers(module):
+                torch.distributed.broadcast(t, src=0)
+
+    loss = dnnlib.util.construct_class_by_name(device=device, G=G, D=D, **loss_kwargs)
+    G_opt = make_optimizer(G.parameters(), G_opt_kwargs, device)
+    D_opt = make_optimizer(D.parameters(), D_opt_kwargs, device)
+    step = TrainingIteration(G, D, G_ema, loss, G_opt, D_opt, batch_size=batch_size,
+                             n_batch_acc=accumulate_gradients, ema_kimg=ema_kimg, ema_rampup=ema_rampup)
+
+    stats_collector = training_stats.Collector(regex='.*')
+    stats_jsonl = open(os.path.join(run_dir, 'stats.jsonl'), 'at') if dist.get_rank() == 0 else None
+    cur_nimg = resume_kimg * 1000
+    cur_tick = 0
+    tick_start_nimg = cur_nimg
+    tick_start_time = time.time()
+    maintenance_time = tick_start_time - start_time
+    batch_idx = 0
+    dist.print0(f'Training started at {resume_kimg} kimg.')
+    while True:
+        phase_real_img, phase_real_c = fetch_data(iterator, device, batch_gpu)
+        step(phase_real_img, phase_real_c, cur_nimg)
+        cur_nimg += batch_size
+        batch_idx += 1
+        done = (cur_nimg >= total_kimg * 1000) or (max_iterations is not None and batch_idx >= max_iterations)
+        if not done and cur_tick != 0 and cur_nimg < tick_start_nimg + kimg_per_tick * 1000:
+            continue
+        tick_end_time = time.time()
+        if device.type == 'cuda':
+            torch.cuda.synchronize(device)
+        tick_time = time.time() - tick_start_time
+        sec_per_kimg = tick_time / max(cur_nimg - tick_start_nimg, 1) * 1e3
+        training_stats.report0('Timing/total_sec', tick_end_time - start_time)
+        training_stats.report0('Timing/sec_per_tick', tick_time)
+        training_stats.report0('Timing/sec_per_kimg', sec_per_kimg)
+        training_stats.report0('Timing/images_per_sec', 1e3 / max(sec_per_kimg, 1e-9))
+        training_stats.report0('Timing/maintenance_sec', maintenance_time)
+        dist.print0(f"tick {cur_tick:<5d} kimg {cur_nimg / 1e3:<8.1f} sec/kimg {sec_per_kimg:<7.2f} "
+                    f"img/s {1e3 / max(sec_per_kimg, 1e-9):<8.1f} maintenance {maintenance_time:<6.1f}")
+        if (network_snapshot_ticks is not None) and (done or cur_tick % network_snapshot_ticks == 0) and cur_tick > 0:
+            if dist.get_rank() == 0:
+                save_snapshot(os.path.join(run_dir, f'network-snapshot-{cur_nimg // 1000:08d}.pth'), G, D, G_ema,
+                              training_set_kwargs)
+        stats_collector.update()
+        if stats_jsonl is not None:
+            stats_jsonl.write(json.dumps(dict(stats_collector.as_dict(), timestamp=time.time())) + '\n')
+            stats_jsonl.flush()
+        cur_tick += 1
+        tick_start_nimg = cur_nimg
+        tick_start_time = time.time()
+        maintenance_time = tick_start_time - tick_end_time
+        if done:
+            break
+    if stats_jsonl is not None:
+        stats_jsonl.close()
+    dist.print0('Exiting...')
+    return dict(G=G, D=D, G_ema=G_ema, cur_nimg=cur_nimg)
