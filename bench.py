@@ -27,6 +27,10 @@ for _p in (PKG, ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+# MIOpen: immediate-mode convolution solutions (no exhaustive find on a fresh box;
+# the find-db does not survive between boxes).
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 import numpy as np
 import torch
 import yaml
@@ -45,6 +49,7 @@ def parse_args(argv=None):
     ap.add_argument("--config", default=CONFIG)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
     return ap.parse_args(argv)
 
@@ -70,6 +75,12 @@ def build(cfg_path, batch_gpu, device, world):
     return c, step
 
 
+def _log(rank, msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(cfg_path, threads):
     """The same iteration through the pure-torch CPU restatement, batch 1 (bounded sample)."""
     from oracle import cpu_step
@@ -89,11 +100,13 @@ def main(argv=None):
     torch.cuda.set_device(device)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = False
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
 
+    t_start = time.perf_counter()
     c, step = build(args.config, args.batch, device, world)
+    _log(rank, f"built in {time.perf_counter() - t_start:.1f}s")
     from training.data_synthetic import SyntheticDataset
     pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=rank).make_pool(args.batch, device)
     labels = ['a photo'] * args.batch
@@ -102,10 +115,15 @@ def main(argv=None):
         img = pool[i % len(pool)].to(torch.float32) / 255.
         step([img], [labels], cur_nimg)
 
+    step.trace = (lambda m: _log(rank, m)) if args.trace else None
     cur = 0
     for i in range(args.warmup):
+        t1 = time.perf_counter()
         one(i, cur)
         cur += args.batch * world
+        torch.cuda.synchronize()
+        _log(rank, f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t1:.2f}s")
+    step.trace = None
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -121,6 +139,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     kernel_timer.enable(False)
+    _log(rank, f"timed {args.steps} steps: {dt:.2f}s")
     if world > 1:
         t = torch.tensor([dt], device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -132,6 +151,7 @@ def main(argv=None):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
+            _log(rank, "cpu baseline ...")
             cpu = cpu_baseline(args.config, args.cpu_threads)
         except Exception as e:   # reported, never fatal for the GPU number
             cpu = {"error": repr(e)[:200]}

@@ -113,6 +113,76 @@ int vfm_filtered_lrelu_act(void* x, unsigned char* s, int dtype,
                            int sh, int sw_bytes, int sx, int sy, int sign_mode,
                            float gain, float slope, float clamp, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Decoder ops (ConvNeXt synthesis layer, separable upsampler). The reference runs
+ * these as stock torch modules; the entry points below replace the calls at
+ *   networks/utils/convnext_utils.py:121-142  (ConvNeXtSynthesisLayer.forward:
+ *       dwconv -> noise -> GroupNorm32 -> modulated pwconv1 -> GELU -> pwconv2 -> gamma -> residual)
+ *   networks/utils/convnext_utils.py:234-257  (SeparableUpsampleWithFixedBlur.forward:
+ *       GroupNorm -> depthwise 3x3 -> pointwise -> PixelShuffle -> replicate pad -> blur)
+ *   networks/utils/shared.py:165-167          (GroupNorm32.forward, fp32 statistics)
+ * All tensors are contiguous NCHW ([B, C, P] for the row ops); per-channel
+ * vectors and filters are fp32; dtype codes as above (F32/F16/BF16).
+ * ------------------------------------------------------------------------- */
+
+/* Depthwise KxK conv (K in {1,3,5,7}), stride 1, zero padding `pad`, optional
+ * fp32 bias [C] and additive plane noise [Ho, Wo]; w: fp32 [C, K, K].
+ * y: [B, C, Ho, Wo], Ho = H + 2 pad - K + 1. The data gradient is this call
+ * with dy, the flipped kernel and pad' = K - 1 - pad. */
+int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                     int dtype, int B, int C, int H, int W, int K, int pad, void* stream);
+
+/* Number of spatial tiles the weight-gradient kernel writes partials for. */
+int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, int pad);
+
+/* Weight/bias gradient partials: partial[tiles, B*C, K*K + 1] (last slot = bias).
+ * The caller sums over tiles and the batch (fixed order, deterministic). */
+int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int dtype,
+                            int B, int C, int H, int W, int K, int pad, void* stream);
+
+/* y = ((x - mean) * rstd * w[c] + b[c]) * s[b, c], statistics over each of the
+ * G groups of C/G channels x HW (fp32); w, b, s may be NULL. mean/rstd: [B*G]
+ * fp32 outputs (saved for the backward). Input and output dtypes may differ. */
+int vfm_group_norm_fwd(const void* x, const float* w, const float* b, const float* s, void* y,
+                       float* mean, float* rstd, int dtype_in, int dtype_out,
+                       int B, int C, int G, int HW, float eps, void* stream);
+
+/* GroupNorm backward: dx (dtype_x); dw_part/db_part [B, C] per-sample
+ * contributions to d_weight / d_bias; ds [B, C] (when s != NULL). */
+int vfm_group_norm_bwd(const void* x, const void* dy, const float* mean, const float* rstd,
+                       const float* w, const float* b, const float* s, void* dx,
+                       float* dw_part, float* db_part, float* ds,
+                       int dtype_x, int dtype_dy, int B, int C, int G, int HW, void* stream);
+
+/* g = gelu_erf(h * scale[b, o] + bias[o]) on h [B, O, P] (P % 8 == 0);
+ * scale / bias may be NULL. */
+int vfm_scale_bias_gelu_fwd(const void* h, const float* scale, const float* bias, void* g,
+                            int dtype, int B, int O, int P, void* stream);
+
+/* Backward: dh; d_scale_rows [B*O] = sum_p dz * h (NULL to skip), d_bias_rows [B*O] = sum_p dz. */
+int vfm_scale_bias_gelu_bwd(const void* h, const void* dg, const float* scale, const float* bias,
+                            void* dh, float* d_scale_rows, float* d_bias_rows,
+                            int dtype, int B, int O, int P, void* stream);
+
+/* out = x_in + gamma[c] * (y + bias[c]) on [B, C, P] (P % 8 == 0); out has x_in's dtype. */
+int vfm_layer_scale_residual_fwd(const void* y, const float* bias, const float* gamma, const void* x_in,
+                                 void* out, int dtype_y, int dtype_x, int B, int C, int P, void* stream);
+
+/* Backward: dy = gamma * dout; d_gamma_rows [B*C] = sum_p (y + bias) dout; d_sum_rows [B*C] = sum_p dout. */
+int vfm_layer_scale_residual_bwd(const void* y, const float* bias, const float* gamma, const void* dout,
+                                 void* dy, float* d_gamma_rows, float* d_sum_rows,
+                                 int dtype_y, int dtype_x, int B, int C, int P, void* stream);
+
+/* PixelShuffle(r) (r = 1: none) + replicate pad ((K-1)/2 before, K/2 after) + blur
+ * with the separable normalised taps[K] (K <= 8; HOST pointer, read at launch):
+ * x [B, C r^2, H, W] -> y [B, C, H r, W r]. */
+int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, int K, int dtype,
+                         int B, int C, int H, int W, int r, void* stream);
+
+/* Exact adjoint of vfm_shuffle_blur_fwd: dout [B, C, H r, W r] -> dx [B, C r^2, H, W]. */
+int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* taps, int K, int dtype,
+                         int B, int C, int H, int W, int r, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,191 @@
+"""GPU parity of the gfx950 decoder kernels (csrc/decoder.hip) against the plain
+PyTorch fp32 formulation of the same ops (decoder_ops.*(impl='ref')), forward
+and backward, on the shapes the decoder runs plus ragged edge cases.
+
+The native path is asserted to have run (kernel_timer records each native
+launch by name), so a silent torch fallback fails the test.
+
+Tolerances: fp32 I/O 2e-5 of the reference's max magnitude (different summation
+order); bf16/fp16 I/O 1.5e-2 (one output rounding of 2^-8 plus bf16-rounded
+intermediates between the ops).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from torch_utils.ops import decoder_ops, kernel_timer
+    return decoder_ops, kernel_timer
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def _tol(dt):
+    return 2e-5 if dt == torch.float32 else 1.5e-2
+
+
+def _run(fn_hip, fn_ref, inputs, dt, names, out_grad_seed=0):
+    """inputs: list of fp32 CPU tensors (None allowed); the first `len(dt_mask)` get dtype dt."""
+    _, kt = _ops()
+    hip_in = [None if t is None else t.detach().to(DEV).requires_grad_(t.requires_grad) for t in inputs]
+    kt.enable(True)
+    out = fn_hip(*hip_in)
+    torch.manual_seed(out_grad_seed)
+    g = torch.randn(out.shape, device=DEV)
+    out.backward(g.to(out.dtype))
+    torch.cuda.synchronize()
+    recorded = set(kt.summary())
+    kt.enable(False)
+    for n in names:
+        assert n in recorded, (n, recorded)
+    ref_in = [None if t is None else t.detach().to(DEV).double().float().requires_grad_(t.requires_grad)
+              for t in hip_in]
+    ref = fn_ref(*ref_in)
+    ref.backward(g.float())
+    tol = _tol(dt)
+    assert _rel(out.float(), ref) < tol
+    for a, b in zip(hip_in, ref_in):
+        if a is not None and a.requires_grad:
+            assert a.grad is not None
+            assert _rel(a.grad.float(), b.grad) < 4 * tol, (a.shape, _rel(a.grad.float(), b.grad))
+
+
+DW_CASES = [(2, 8, 16, 16, 3), (2, 8, 16, 16, 5), (2, 6, 16, 16, 7), (1, 4, 64, 70, 3), (2, 5, 13, 9, 3),
+            (1, 3, 33, 130, 7), (3, 2, 4, 4, 3), (1, 2, 1, 5, 3)]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", DW_CASES)
+def test_dwconv2d(case, dt):
+    ops, _ = _ops()
+    B, C, H, W, K = case
+    torch.manual_seed(1)
+    x = torch.randn(B, C, H, W).to(dt).float().requires_grad_(True)
+    w = (torch.randn(C, 1, K, K) * 0.2).requires_grad_(True)
+    b = (torch.randn(C) * 0.1).requires_grad_(True)
+    noise = torch.randn(H, W).requires_grad_(True)
+    hip = lambda x, w, b, n: ops.dwconv2d(x.to(dt), w, b, K // 2, noise=n)
+    ref = lambda x, w, b, n: ops.dwconv2d(x, w, b, K // 2, noise=n, impl='ref')
+    _run(hip, ref, [x, w, b, noise], dt, ["dwconv2d_fwd", "dwconv2d_bwd_data", "dwconv2d_bwd_weight"])
+
+
+def test_dwconv2d_no_bias_valid_padding():
+    ops, _ = _ops()
+    torch.manual_seed(2)
+    x = torch.randn(2, 4, 12, 20).requires_grad_(True)
+    w = torch.randn(4, 1, 3, 3).requires_grad_(True)
+    _run(lambda x, w: ops.dwconv2d(x, w, None, 0), lambda x, w: ops.dwconv2d(x, w, None, 0, impl='ref'),
+         [x, w], torch.float32, ["dwconv2d_fwd"])
+
+
+GN_CASES = [(2, 64, 16, 16, 16), (2, 12, 5, 7, 3), (3, 32, 8, 8, 32), (1, 256, 32, 32, 32), (2, 8, 1, 1, 2)]
+
+
+@pytest.mark.parametrize("dt_in,dt_out", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                          (torch.bfloat16, torch.bfloat16), (torch.float16, torch.float16)])
+@pytest.mark.parametrize("case", GN_CASES)
+@pytest.mark.parametrize("with_style", [False, True])
+def test_group_norm(case, dt_in, dt_out, with_style):
+    ops, _ = _ops()
+    B, C, H, W, G = case
+    torch.manual_seed(3)
+    x = (torch.randn(B, C, H, W) * 3 + 1.5).to(dt_in).float().requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(C)).requires_grad_(True)
+    b = (0.1 * torch.randn(C)).requires_grad_(True)
+    s = (1 + 0.3 * torch.randn(B, C)).requires_grad_(True) if with_style else None
+    hip = lambda x, w, b, s: ops.group_norm(x.to(dt_in), G, w, b, 1e-5, out_dtype=dt_out, style=s)
+    ref = lambda x, w, b, s: ops.group_norm(x, G, w, b, 1e-5, out_dtype=torch.float32, style=s, impl='ref')
+    worst = dt_out if dt_out != torch.float32 else dt_in
+    _run(hip, ref, [x, w, b, s], worst, ["group_norm_fwd", "group_norm_bwd"])
+
+
+def test_group_norm_large_mean_is_stable():
+    """Shifted sums: a group with |mean| >> std still normalises accurately."""
+    ops, _ = _ops()
+    torch.manual_seed(4)
+    x = torch.randn(2, 16, 16, 16) * 0.01 + 300.0
+    y = ops.group_norm(x.to(DEV), 4, None, None, 1e-5)
+    r = ops.group_norm(x.double(), 4, None, None, 1e-5, impl='ref')
+    assert _rel(y.cpu(), r) < 5e-3
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 32, 64), (4, 256, 256), (1, 8, 8), (3, 40, 1000)])
+@pytest.mark.parametrize("with_scale", [True, False])
+def test_scale_bias_gelu(shape, dt, with_scale):
+    ops, _ = _ops()
+    B, O, P = shape
+    torch.manual_seed(5)
+    h = (torch.randn(B, O, P) * 2).to(dt).float().requires_grad_(True)
+    s = (torch.rand(B, O) + 0.5).requires_grad_(True) if with_scale else None
+    b = (torch.randn(O) * 0.3).requires_grad_(True)
+    hip = lambda h, s, b: ops.scale_bias_gelu(h.to(dt), s, b)
+    ref = lambda h, s, b: ops.scale_bias_gelu(h, s, b, impl='ref')
+    _run(hip, ref, [h, s, b], dt, ["scale_bias_gelu_fwd", "scale_bias_gelu_bwd"])
+
+
+@pytest.mark.parametrize("dt_y,dt_x", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                       (torch.bfloat16, torch.bfloat16), (torch.float16, torch.float16)])
+@pytest.mark.parametrize("shape", [(2, 16, 64), (4, 128, 256), (1, 3, 8)])
+def test_layer_scale_residual(shape, dt_y, dt_x):
+    ops, _ = _ops()
+    B, C, P = shape
+    torch.manual_seed(6)
+    y = torch.randn(B, C, P).to(dt_y).float().requires_grad_(True)
+    b = (0.1 * torch.randn(C)).requires_grad_(True)
+    g = (0.5 + 0.2 * torch.randn(C)).requires_grad_(True)
+    x = torch.randn(B, C, P).to(dt_x).float().requires_grad_(True)
+    hip = lambda y, b, g, x: ops.layer_scale_residual(y.to(dt_y), b, g, x.to(dt_x))
+    ref = lambda y, b, g, x: ops.layer_scale_residual(y, b, g, x, impl='ref')
+    worst = dt_y if dt_y != torch.float32 else dt_x
+    _run(hip, ref, [y, b, g, x], worst, ["layer_scale_residual_fwd", "layer_scale_residual_bwd"])
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("taps", [[1, 2, 1], [1, 3, 3, 1], [1, 4, 6, 4, 1]])
+@pytest.mark.parametrize("shape,r", [((2, 16, 8, 8), 2), ((1, 12, 5, 7), 2), ((2, 4, 9, 6), 1), ((1, 4, 1, 1), 2),
+                                     ((1, 2, 16, 32), 1)])
+def test_shuffle_blur(shape, r, taps, dt):
+    ops, _ = _ops()
+    torch.manual_seed(7)
+    x = torch.randn(*shape).to(dt).float().requires_grad_(True)
+    if r == 1:
+        hip = lambda x: ops.blur_replicate(x.to(dt), taps)
+        ref = lambda x: ops.blur_replicate(x, taps, impl='ref')
+    else:
+        hip = lambda x: ops.shuffle_blur(x.to(dt), taps, r)
+        ref = lambda x: ops.shuffle_blur(x, taps, r, impl='ref')
+    _run(hip, ref, [x], dt, ["shuffle_blur_fwd", "shuffle_blur_bwd"])
+
+
+def test_convnext_layer_hip_matches_torch_formulation():
+    """One ConvNeXt synthesis layer end to end (fwd + grads of every parameter),
+    HIP decoder ops vs the torch formulation, fp32."""
+    from networks.utils.convnext_utils import ConvNeXtSynthesisLayer
+    ops, _ = _ops()
+    torch.manual_seed(8)
+    layer = ConvNeXtSynthesisLayer(64, 32, 7, layer_scale_init=0.5).to(DEV)
+    x = torch.randn(2, 64, 16, 16, device=DEV)
+    w = torch.randn(2, 32, device=DEV)
+    outs, grads = [], []
+    for force in (False, True):
+        ops.set_force_ref(force)
+        try:
+            layer.zero_grad(set_to_none=True)
+            y = layer(x, w)
+            (y * torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)).sum().backward()
+        finally:
+            ops.set_force_ref(False)
+        outs.append(y.detach())
+        grads.append({n: p.grad.detach().clone() for n, p in layer.named_parameters() if p.grad is not None})
+    assert _rel(outs[0], outs[1]) < 2e-5
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        assert _rel(grads[0][n], grads[1][n]) < 1e-4, n

@@ -16,6 +16,9 @@ for s in "$@"; do
     benchref) timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline --force-ref-ops > $out/bench_ref.log 2>&1 ;;
     prof)    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 ;;
     opbench) timeout -k 10 300 python tools_dev/opbench.py > $out/opbench.log 2>&1 ;;
+    dtests)  timeout -k 10 600 python -m pytest tests/test_decoder_gpu.py -q -x > $out/dtests.log 2>&1 ;;
+    bsmall)  timeout -k 10 900 python bench.py --batch 8 --steps 2 --warmup 2 --trace --no-cpu-baseline > $out/bsmall.log 2>&1 ;;
+    btrace)  timeout -k 10 900 python bench.py --steps 3 --warmup 2 --trace --no-cpu-baseline > $out/btrace.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -1,0 +1,920 @@
+// Decoder kernels for gfx950: the ops the shipped ConvNeXt decoder actually runs
+// (reference networks/utils/convnext_utils.py:36-257, networks/utils/shared.py:165-167).
+//
+//  * dwconv2d fwd / bwd-weight: depthwise KxK conv (K = 3, 5, 7), stride 1, zero padding,
+//    fused bias and legacy additive noise plane. LDS-staged input tile with halo; every lane
+//    owns one column and an 8-row strip (sliding K-row register window), so an output costs
+//    K*K FMAs but only ~(K+8)/8 LDS row reads. Narrow planes (W < 64) pack several planes
+//    side by side in one wave. bwd-data is the forward with the flipped kernel.
+//  * group_norm fwd / bwd: one workgroup per (sample, group); the group is one contiguous
+//    [C/G x HW] chunk in NCHW, read with 16-B vector loads; fp32 statistics (shifted sums);
+//    optional per-(sample, channel) scale folded in (modulated-conv input modulation).
+//  * scale_bias_gelu fwd / bwd: gelu(h * s[b,o] + b[o]) (exact erf GELU) on [B, O, P], one
+//    wave per (b, o) row so the backward's d_scale / d_bias row sums need no atomics.
+//  * layer_scale_residual fwd / bwd: x_in + gamma[c] * (y + b[c]), same row structure.
+//  * shuffle_blur fwd / bwd: PixelShuffle(r) + replicate padding + fixed normalised separable
+//    blur, fused (the shuffled tensor is never materialised); the backward is the exact
+//    gather-form adjoint including the replicate-padding edge folding.
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+constexpr int NT = 256;
+constexpr int RPT = 8;   // output rows per lane in the depthwise conv
+
+// -------------------------------------------------------------------------------------------
+// Depthwise conv.
+
+struct DwArgs {
+    const void* x;
+    const float* w;       // [C, K, K] fp32
+    const float* bias;    // [C] or null
+    const float* noise;   // [Ho, Wo] or null
+    void* y;
+    int B, C, H, W, Ho, Wo, pad;
+    int TW, TH;           // tile width (pow2, <= 64), tile height (multiple of RPT)
+    int ppw;              // planes side by side in one wave row (64 / TW)
+    int spp;              // row strips per plane tile (TH / RPT)
+    int ppb;              // planes per block = ppw * (4 / spp)
+    int tilesX, tilesY, planeGroups;
+};
+
+template <class T, int K>
+__global__ __launch_bounds__(NT) void dw_fwd(DwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int LW = a.TW + K - 1, LH = a.TH + K - 1;
+    int bid = blockIdx.x;
+    const int tx = bid % a.tilesX; bid /= a.tilesX;
+    const int ty = bid % a.tilesY; bid /= a.tilesY;
+    const int pg = bid;                                  // plane group
+    const int ox0 = tx * a.TW, oy0 = ty * a.TH;
+    const int nplanes = a.B * a.C;
+
+    // Stage ppb input tiles with halo.
+    const int per = LW * LH;
+    for (int i = threadIdx.x; i < a.ppb * per; i += NT) {
+        const int pl = i / per, r = i - pl * per;
+        const int ry = r / LW, rx = r - ry * LW;
+        const int plane = pg * a.ppb + pl;
+        const int iy = oy0 + ry - a.pad, ix = ox0 + rx - a.pad;
+        float v = 0.f;
+        if (plane < nplanes && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+            v = ld(reinterpret_cast<const T*>(a.x) + (long long)plane * a.H * a.W + (long long)iy * a.W + ix);
+        lds[i] = v;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane % a.TW, psub = lane / a.TW;
+    const int strip = wave % a.spp, pgrp = wave / a.spp;
+    const int pl = pgrp * a.ppw + psub;
+    const int plane = pg * a.ppb + pl;
+    if (pl >= a.ppb || plane >= nplanes) return;
+    const int c = plane % a.C;
+    const int ox = ox0 + col;
+    const int r0 = strip * RPT;
+    if (ox >= a.Wo) return;
+
+    float wk[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + i];
+    float acc[RPT];
+    const float b = a.bias ? a.bias[c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) acc[i] = b;
+
+    const float* tile = lds + pl * per + col;
+    // Input row (r0 + j) contributes to output rows r0 + j - ky for ky in [0, K).
+#pragma unroll
+    for (int j = 0; j < RPT + K - 1; ++j) {
+        float row[K];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) row[kx] = tile[(r0 + j) * LW + kx];
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky) {
+            const int o = j - ky;
+            if (o >= 0 && o < RPT) {
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) acc[o] = fmaf(row[kx], wk[ky * K + kx], acc[o]);
+            }
+        }
+    }
+    T* yp = reinterpret_cast<T*>(a.y) + (long long)plane * a.Ho * a.Wo + ox;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int oy = oy0 + r0 + i;
+        if (oy < a.Ho) {
+            float v = acc[i];
+            if (a.noise) v += a.noise[oy * a.Wo + ox];
+            st(yp + (long long)oy * a.Wo, v);
+        }
+    }
+}
+
+// dW[plane][ky][kx] = sum_{y,x} dy[y][x] * x[y+ky-pad][x+kx-pad]; db[plane] = sum dy.
+// Same tiling as dw_fwd; the grid walks (plane group, tile); each lane accumulates K*K+1
+// partial sums for its strip; a workgroup reduction writes per-(tile, plane) partials that
+// the host sums (fixed order -> deterministic).
+template <class T, int K>
+__global__ __launch_bounds__(NT) void dw_bwd_w(DwArgs a, const void* dy, float* partial) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int LW = a.TW + K - 1, LH = a.TH + K - 1;
+    int bid = blockIdx.x;
+    const int tx = bid % a.tilesX; bid /= a.tilesX;
+    const int ty = bid % a.tilesY; bid /= a.tilesY;
+    const int pg = bid;
+    const int tile_id = ty * a.tilesX + tx;
+    const int ox0 = tx * a.TW, oy0 = ty * a.TH;
+    const int nplanes = a.B * a.C;
+    const int per = LW * LH;
+    for (int i = threadIdx.x; i < a.ppb * per; i += NT) {
+        const int pl = i / per, r = i - pl * per;
+        const int ry = r / LW, rx = r - ry * LW;
+        const int plane = pg * a.ppb + pl;
+        const int iy = oy0 + ry - a.pad, ix = ox0 + rx - a.pad;
+        float v = 0.f;
+        if (plane < nplanes && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+            v = ld(reinterpret_cast<const T*>(a.x) + (long long)plane * a.H * a.W + (long long)iy * a.W + ix);
+        lds[i] = v;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane % a.TW, psub = lane / a.TW;
+    const int strip = wave % a.spp, pgrp = wave / a.spp;
+    const int pl = pgrp * a.ppw + psub;
+    const int plane = pg * a.ppb + pl;
+    const int ox = ox0 + col;
+    const int r0 = strip * RPT;
+    const bool live = pl < a.ppb && plane < nplanes && ox < a.Wo;
+
+    float acc[K * K + 1];
+#pragma unroll
+    for (int i = 0; i < K * K + 1; ++i) acc[i] = 0.f;
+    if (live) {
+        const T* dyp = reinterpret_cast<const T*>(dy) + (long long)plane * a.Ho * a.Wo + ox;
+        const float* tile = lds + pl * per + col;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int oy = oy0 + r0 + i;
+            if (oy >= a.Ho) break;
+            const float g = ld(dyp + (long long)oy * a.Wo);
+            acc[K * K] += g;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx)
+                    acc[ky * K + kx] = fmaf(g, tile[(r0 + i + ky) * LW + kx], acc[ky * K + kx]);
+        }
+    }
+    // Reduce over the lanes that belong to the same plane: first within the wave (lanes
+    // with equal psub are TW apart), then across waves through LDS.
+    __syncthreads();
+    float* red = lds;   // reuse: [4 waves][ppw][K*K+1]
+#pragma unroll
+    for (int i = 0; i < K * K + 1; ++i) {
+        float v = acc[i];
+        for (int off = a.TW / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        if (col == 0) red[(wave * a.ppw + psub) * (K * K + 1) + i] = v;
+    }
+    __syncthreads();
+    // Planes of this block: pl in [0, ppb); plane pl lives in waves {pgrp*spp .. pgrp*spp+spp-1}, slot psub.
+    for (int i = threadIdx.x; i < a.ppb * (K * K + 1); i += NT) {
+        const int p = i / (K * K + 1), k = i - p * (K * K + 1);
+        const int plane_g = pg * a.ppb + p;
+        if (plane_g >= nplanes) continue;
+        const int grp = p / a.ppw, sub = p - grp * a.ppw;
+        float s = 0.f;
+        for (int st_ = 0; st_ < a.spp; ++st_) s += red[((grp * a.spp + st_) * a.ppw + sub) * (K * K + 1) + k];
+        partial[((long long)tile_id * nplanes + plane_g) * (K * K + 1) + k] = s;
+    }
+}
+
+template <class T, int K>
+int dw_launch(DwArgs& a, int mode, const void* dy, float* partial, hipStream_t st) {
+    const size_t lds = sizeof(float) * (size_t)a.ppb * (a.TW + K - 1) * (a.TH + K - 1);
+    const size_t red = sizeof(float) * 4 * a.ppw * (K * K + 1);
+    const long long blocks = (long long)a.tilesX * a.tilesY * a.planeGroups;
+    if (mode == 0)
+        hipLaunchKernelGGL((dw_fwd<T, K>), dim3((unsigned)blocks), dim3(NT), lds, st, a);
+    else
+        hipLaunchKernelGGL((dw_bwd_w<T, K>), dim3((unsigned)blocks), dim3(NT), lds > red ? lds : red, st, a, dy,
+                           partial);
+    return launch_status();
+}
+
+int next_pow2(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+void dw_plan(DwArgs& a) {
+    a.TW = next_pow2(a.Wo) < 64 ? next_pow2(a.Wo) : 64;
+    if (a.TW < 1) a.TW = 1;
+    a.ppw = 64 / a.TW;
+    const int rows_needed = (a.Ho + RPT - 1) / RPT;           // strips to cover the plane height
+    a.spp = rows_needed >= 4 ? 4 : (rows_needed >= 2 ? 2 : 1);
+    a.TH = a.spp * RPT;
+    a.ppb = a.ppw * (4 / a.spp);
+    a.tilesX = (a.Wo + a.TW - 1) / a.TW;
+    a.tilesY = (a.Ho + a.TH - 1) / a.TH;
+    a.planeGroups = (a.B * a.C + a.ppb - 1) / a.ppb;
+}
+
+template <class T>
+int dw_dispatch(DwArgs& a, int K, int mode, const void* dy, float* partial, hipStream_t st) {
+    switch (K) {
+    case 1: return dw_launch<T, 1>(a, mode, dy, partial, st);
+    case 3: return dw_launch<T, 3>(a, mode, dy, partial, st);
+    case 5: return dw_launch<T, 5>(a, mode, dy, partial, st);
+    case 7: return dw_launch<T, 7>(a, mode, dy, partial, st);
+    }
+    return VFM_NO_KERNEL;
+}
+
+// -------------------------------------------------------------------------------------------
+// Block reductions.
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Sum over the 256 threads; result broadcast to all. `scratch` needs 4 floats + a barrier-safe slot.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) scratch[w] = v;
+    __syncthreads();
+    return scratch[0] + scratch[1] + scratch[2] + scratch[3];
+}
+
+// Vector loads of 8 elements (16 B for 16-bit types, 2 x 16 B for fp32).
+template <class T>
+__device__ __forceinline__ void load8(const T* p, float* v) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ld(p + i);
+}
+template <>
+__device__ __forceinline__ void load8<__hip_bfloat16>(const __hip_bfloat16* p, float* v) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+template <>
+__device__ __forceinline__ void load8<__half>(const __half* p, float* v) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const __half2* h = reinterpret_cast<const __half2*>(&u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float2 f = __half22float2(h[i]);
+        v[2 * i] = f.x;
+        v[2 * i + 1] = f.y;
+    }
+}
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+template <class T>
+__device__ __forceinline__ void store8(T* p, const float* v) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st(p + i, v[i]);
+}
+template <>
+__device__ __forceinline__ void store8<__hip_bfloat16>(__hip_bfloat16* p, const float* v) {
+    __hip_bfloat16 t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = __float2bfloat16(v[i]);
+    *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(t);
+}
+template <>
+__device__ __forceinline__ void store8<__half>(__half* p, const float* v) {
+    __half t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = __float2half(v[i]);
+    *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(t);
+}
+template <>
+__device__ __forceinline__ void store8<float>(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// -------------------------------------------------------------------------------------------
+// GroupNorm.
+
+struct GnArgs {
+    const void* x;
+    const float* w;      // [C] or null
+    const float* b;      // [C] or null
+    const float* s;      // [B, C] or null (style)
+    void* y;
+    float* mean;         // [B*G]
+    float* rstd;         // [B*G]
+    int B, C, G, HW;
+    float eps;
+};
+
+template <class TI, class TO>
+__global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
+    __shared__ float scratch[8];
+    const int bg = blockIdx.x;
+    const int bidx = bg / a.G, g = bg - bidx * a.G;
+    const int cpg = a.C / a.G;
+    const long long n = (long long)cpg * a.HW;
+    const bool vec = (a.HW % 8) == 0;
+    const TI* xp = reinterpret_cast<const TI*>(a.x) + (long long)bg * n;
+    // Shifted sums (shift = first element of the group) keep the one-pass variance accurate.
+    const float shift = ld(xp);
+    float s1 = 0.f, s2 = 0.f;
+    const long long nv = vec ? n / 8 : 0;
+    for (long long i = threadIdx.x; i < nv; i += NT) {
+        float v[8];
+        load8(xp + i * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float d = v[k] - shift;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+        }
+    }
+    for (long long i = nv * 8 + threadIdx.x; i < n; i += NT) {
+        const float d = ld(xp + i) - shift;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+    }
+    s1 = block_sum(s1, scratch);
+    s2 = block_sum(s2, scratch + 4);
+    const float m1 = s1 / (float)n;
+    const float var = fmaxf(s2 / (float)n - m1 * m1, 0.f);
+    const float mean = shift + m1;
+    const float rstd = rsqrtf(var + a.eps);
+    if (threadIdx.x == 0) {
+        a.mean[bg] = mean;
+        a.rstd[bg] = rstd;
+    }
+    TO* yp = reinterpret_cast<TO*>(a.y) + (long long)bg * n;
+    for (int cl = 0; cl < cpg; ++cl) {
+        const int c = g * cpg + cl;
+        float sc = rstd * (a.w ? a.w[c] : 1.f);
+        float sh = (a.b ? a.b[c] : 0.f) - mean * sc;
+        if (a.s) {
+            const float m = a.s[bidx * a.C + c];
+            sc *= m;
+            sh *= m;
+        }
+        const TI* xc = xp + (long long)cl * a.HW;
+        TO* yc = yp + (long long)cl * a.HW;
+        if (vec) {
+            for (int i = threadIdx.x; i < a.HW / 8; i += NT) {
+                float v[8];
+                load8(xc + i * 8, v);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sc, sh);
+                store8(yc + i * 8, v);
+            }
+        } else {
+            for (int i = threadIdx.x; i < a.HW; i += NT) st(yc + i, fmaf(ld(xc + i), sc, sh));
+        }
+    }
+}
+
+struct GnBwdArgs {
+    const void* x;
+    const void* dy;
+    const float* mean;
+    const float* rstd;
+    const float* w;
+    const float* b;
+    const float* s;
+    void* dx;
+    float* dw_part;   // [B, C]  sum_p dy*s*xhat
+    float* db_part;   // [B, C]  sum_p dy*s
+    float* ds;        // [B, C]  (if s)
+    int B, C, G, HW;
+};
+
+// Per (sample, group) workgroup. Pass 1: per-channel sums A_c = sum dy*xhat, B_c = sum dy
+// (channel loop, one workgroup reduction per channel). Pass 2: dx.
+template <class TX, class TY>
+__global__ __launch_bounds__(NT) void gn_bwd(GnBwdArgs a) {
+    __shared__ float scratch[8];
+    const int bg = blockIdx.x;
+    const int bidx = bg / a.G, g = bg - bidx * a.G;
+    const int cpg = a.C / a.G;
+    const long long n = (long long)cpg * a.HW;
+    const TX* xp = reinterpret_cast<const TX*>(a.x) + (long long)bg * n;
+    const TY* gp = reinterpret_cast<const TY*>(a.dy) + (long long)bg * n;
+    const float mean = a.mean[bg], rstd = a.rstd[bg];
+    const bool vec = (a.HW % 8) == 0;
+    float sum_dxhat = 0.f, sum_dxhat_xhat = 0.f;   // group sums (block-uniform)
+    for (int cl = 0; cl < cpg; ++cl) {
+        const TX* xc = xp + (long long)cl * a.HW;
+        const TY* gc = gp + (long long)cl * a.HW;
+        float sa = 0.f, sb = 0.f;
+        if (vec) {
+            for (int i = threadIdx.x; i < a.HW / 8; i += NT) {
+                float xv[8], gv[8];
+                load8(xc + i * 8, xv);
+                load8(gc + i * 8, gv);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    sa = fmaf(gv[k], (xv[k] - mean) * rstd, sa);
+                    sb += gv[k];
+                }
+            }
+        } else {
+            for (int i = threadIdx.x; i < a.HW; i += NT) {
+                const float gv = ld(gc + i);
+                sa = fmaf(gv, (ld(xc + i) - mean) * rstd, sa);
+                sb += gv;
+            }
+        }
+        sa = block_sum(sa, scratch);
+        sb = block_sum(sb, scratch + 4);
+        const int c = g * cpg + cl;
+        const float wc = a.w ? a.w[c] : 1.f;
+        const float sc = a.s ? a.s[bidx * a.C + c] : 1.f;
+        sum_dxhat += sc * wc * sb;
+        sum_dxhat_xhat += sc * wc * sa;
+        if (threadIdx.x == 0) {
+            a.dw_part[bidx * a.C + c] = sc * sa;
+            a.db_part[bidx * a.C + c] = sc * sb;
+            if (a.ds) a.ds[bidx * a.C + c] = wc * sa + (a.b ? a.b[c] : 0.f) * sb;
+        }
+    }
+    const float m1 = sum_dxhat / (float)n, m2 = sum_dxhat_xhat / (float)n;
+    TX* dxp = reinterpret_cast<TX*>(a.dx) + (long long)bg * n;
+    for (int cl = 0; cl < cpg; ++cl) {
+        const int c = g * cpg + cl;
+        const float k = (a.w ? a.w[c] : 1.f) * (a.s ? a.s[bidx * a.C + c] : 1.f);
+        const TX* xc = xp + (long long)cl * a.HW;
+        const TY* gc = gp + (long long)cl * a.HW;
+        TX* dc = dxp + (long long)cl * a.HW;
+        if (vec) {
+            for (int i = threadIdx.x; i < a.HW / 8; i += NT) {
+                float xv[8], gv[8], o[8];
+                load8(xc + i * 8, xv);
+                load8(gc + i * 8, gv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float xh = (xv[j] - mean) * rstd;
+                    o[j] = rstd * (gv[j] * k - m1 - xh * m2);
+                }
+                store8(dc + i * 8, o);
+            }
+        } else {
+            for (int i = threadIdx.x; i < a.HW; i += NT) {
+                const float xh = (ld(xc + i) - mean) * rstd;
+                st(dc + i, rstd * (ld(gc + i) * k - m1 - xh * m2));
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------
+// Row kernels on [R rows, P] with one wave per row (P % 8 == 0 required by the host).
+
+__device__ __forceinline__ float gelu_erf(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float z) {
+    return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+}
+
+struct RowArgs {
+    const void* in0;      // h (gelu) | y (residual)
+    const void* in1;      // -      | x_in
+    const void* dout;
+    void* out0;           // g | out | dh | dy
+    const float* rscale;  // per-row [R] (gelu: s[b,o]) or null
+    const float* cvec0;   // per-channel [O]: bias / b2
+    const float* cvec1;   // per-channel [O]: - / gamma
+    float* rsum0;         // per-row partial sums [R]
+    float* rsum1;         // per-row partial sums [R]
+    int R, O, P;
+};
+
+template <class T>
+__global__ __launch_bounds__(NT) void gelu_fwd(RowArgs a) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= a.R) return;
+    const int lane = threadIdx.x & 63;
+    const int o = row % a.O;
+    const float sc = a.rscale ? a.rscale[row] : 1.f;
+    const float bi = a.cvec0 ? a.cvec0[o] : 0.f;
+    const T* hp = reinterpret_cast<const T*>(a.in0) + (long long)row * a.P;
+    T* gp = reinterpret_cast<T*>(a.out0) + (long long)row * a.P;
+    for (int i = lane; i < a.P / 8; i += 64) {
+        float v[8];
+        load8(hp + i * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = gelu_erf(fmaf(v[k], sc, bi));
+        store8(gp + i * 8, v);
+    }
+}
+
+// dz = dg * gelu'(h*s+b); dh = dz * s; rsum0[row] = sum dz*h (-> d_scale); rsum1[row] = sum dz (-> d_bias)
+template <class T>
+__global__ __launch_bounds__(NT) void gelu_bwd(RowArgs a) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= a.R) return;
+    const int lane = threadIdx.x & 63;
+    const int o = row % a.O;
+    const float sc = a.rscale ? a.rscale[row] : 1.f;
+    const float bi = a.cvec0 ? a.cvec0[o] : 0.f;
+    const T* hp = reinterpret_cast<const T*>(a.in0) + (long long)row * a.P;
+    const T* gp = reinterpret_cast<const T*>(a.dout) + (long long)row * a.P;
+    T* dp = reinterpret_cast<T*>(a.out0) + (long long)row * a.P;
+    float s0 = 0.f, s1 = 0.f;
+    for (int i = lane; i < a.P / 8; i += 64) {
+        float h[8], g[8], d[8];
+        load8(hp + i * 8, h);
+        load8(gp + i * 8, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float dz = g[k] * gelu_erf_grad(fmaf(h[k], sc, bi));
+            s0 = fmaf(dz, h[k], s0);
+            s1 += dz;
+            d[k] = dz * sc;
+        }
+        store8(dp + i * 8, d);
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+        if (a.rsum0) a.rsum0[row] = s0;
+        a.rsum1[row] = s1;
+    }
+}
+
+// out = x_in + gamma[c] * (y + b[c]);  TY = dtype of y, TX = dtype of x_in / out
+template <class TY, class TX>
+__global__ __launch_bounds__(NT) void lsr_fwd(RowArgs a) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= a.R) return;
+    const int lane = threadIdx.x & 63;
+    const int c = row % a.O;
+    const float b = a.cvec0 ? a.cvec0[c] : 0.f;
+    const float gm = a.cvec1 ? a.cvec1[c] : 1.f;
+    const TY* yp = reinterpret_cast<const TY*>(a.in0) + (long long)row * a.P;
+    const TX* xp = reinterpret_cast<const TX*>(a.in1) + (long long)row * a.P;
+    TX* op = reinterpret_cast<TX*>(a.out0) + (long long)row * a.P;
+    for (int i = lane; i < a.P / 8; i += 64) {
+        float y[8], x[8];
+        load8(yp + i * 8, y);
+        load8(xp + i * 8, x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = fmaf(gm, y[k] + b, x[k]);
+        store8(op + i * 8, x);
+    }
+}
+
+// dy = gamma*dout (dtype TY); rsum0[row] = sum (y+b)*dout (-> d_gamma); rsum1[row] = sum dout (-> d_b / gamma)
+template <class TY, class TX>
+__global__ __launch_bounds__(NT) void lsr_bwd(RowArgs a) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= a.R) return;
+    const int lane = threadIdx.x & 63;
+    const int c = row % a.O;
+    const float b = a.cvec0 ? a.cvec0[c] : 0.f;
+    const float gm = a.cvec1 ? a.cvec1[c] : 1.f;
+    const TY* yp = reinterpret_cast<const TY*>(a.in0) + (long long)row * a.P;
+    const TX* gp = reinterpret_cast<const TX*>(a.dout) + (long long)row * a.P;
+    TY* dp = reinterpret_cast<TY*>(a.out0) + (long long)row * a.P;
+    float s0 = 0.f, s1 = 0.f;
+    for (int i = lane; i < a.P / 8; i += 64) {
+        float y[8], g[8], d[8];
+        load8(yp + i * 8, y);
+        load8(gp + i * 8, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s0 = fmaf(y[k] + b, g[k], s0);
+            s1 += g[k];
+            d[k] = gm * g[k];
+        }
+        store8(dp + i * 8, d);
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+        a.rsum0[row] = s0;
+        a.rsum1[row] = s1;
+    }
+}
+
+// -------------------------------------------------------------------------------------------
+// PixelShuffle(r) + replicate pad + separable normalised blur (taps k, 1 <= K <= 7).
+
+struct BlurArgs {
+    const void* x;     // [B, C*r*r, H, W]  (pre-shuffle); r == 1: plain blur of [B, C, H, W]
+    void* y;           // [B, C, H*r, W*r]
+    int B, C, H, W, r, K, pad0;
+    float k[8];        // normalised 1-D taps (2-D kernel = k x k)
+};
+
+template <class T>
+__device__ __forceinline__ float shuffled(const BlurArgs& a, const T* xb, int c, int Y, int X) {
+    // xb points at sample b; (Y, X) already clamped into [0, H*r) x [0, W*r).
+    const int sy = Y % a.r, sx = X % a.r;
+    const int cin = c * a.r * a.r + sy * a.r + sx;
+    return ld(xb + ((long long)cin * a.H + Y / a.r) * a.W + X / a.r);
+}
+
+template <class T>
+__global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
+    const int Ho = a.H * a.r, Wo = a.W * a.r;
+    const long long total = (long long)a.B * a.C * Ho * Wo;
+    for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+        long long t = i;
+        const int X = (int)(t % Wo); t /= Wo;
+        const int Y = (int)(t % Ho); t /= Ho;
+        const int c = (int)(t % a.C);
+        const int b = (int)(t / a.C);
+        const T* xb = reinterpret_cast<const T*>(a.x) + (long long)b * a.C * a.r * a.r * a.H * a.W;
+        float acc = 0.f;
+        for (int ty = 0; ty < a.K; ++ty) {
+            const int yy = min(max(Y + ty - a.pad0, 0), Ho - 1);
+            float rowacc = 0.f;
+            for (int tx = 0; tx < a.K; ++tx) {
+                const int xx = min(max(X + tx - a.pad0, 0), Wo - 1);
+                rowacc = fmaf(a.k[tx], shuffled(a, xb, c, yy, xx), rowacc);
+            }
+            acc = fmaf(a.k[ty], rowacc, acc);
+        }
+        st(reinterpret_cast<T*>(a.y) + i, acc);
+    }
+}
+
+// Weight with which output coordinate o contributes to source coordinate s along one axis:
+// sum over taps t with clamp(o + t - pad, 0, n-1) == s of k[t].
+__device__ __forceinline__ float axis_weight(const BlurArgs& a, int o, int s, int n) {
+    float w = 0.f;
+    for (int t = 0; t < a.K; ++t) {
+        const int q = min(max(o + t - a.pad0, 0), n - 1);
+        if (q == s) w += a.k[t];
+    }
+    return w;
+}
+
+// d_x at pre-shuffle element (cin, iy, ix) = d_S(Y, X) with Y = iy*r + sy, X = ix*r + sx,
+// d_S(Y, X) = sum_{y, x} wy(y, Y) wx(x, X) dout(y, x), y in [Y - (K-1-pad0), Y + pad0] plus the
+// folded edge range when Y is 0 or n-1.
+template <class T>
+__global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
+    const int Ho = a.H * a.r, Wo = a.W * a.r;
+    const int C_in = a.C * a.r * a.r;
+    const long long total = (long long)a.B * C_in * a.H * a.W;
+    const int reach_lo = a.K - 1 - a.pad0, reach_hi = a.pad0;
+    for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+        long long t = i;
+        const int ix = (int)(t % a.W); t /= a.W;
+        const int iy = (int)(t % a.H); t /= a.H;
+        const int cin = (int)(t % C_in);
+        const int b = (int)(t / C_in);
+        const int c = cin / (a.r * a.r), sub = cin % (a.r * a.r);
+        const int Y = iy * a.r + sub / a.r, X = ix * a.r + sub % a.r;
+        const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
+        int ylo = Y - reach_hi, yhi = Y + reach_lo;
+        int xlo = X - reach_hi, xhi = X + reach_lo;
+        if (Y == 0) ylo = 0;
+        if (Y == Ho - 1) yhi = Ho - 1;
+        if (X == 0) xlo = 0;
+        if (X == Wo - 1) xhi = Wo - 1;
+        // Edge folding reaches at most K-1 positions inward.
+        if (Y == 0) yhi = min(yhi + a.K, Ho - 1);
+        if (Y == Ho - 1) ylo = max(ylo - a.K, 0);
+        if (X == 0) xhi = min(xhi + a.K, Wo - 1);
+        if (X == Wo - 1) xlo = max(xlo - a.K, 0);
+        ylo = max(ylo, 0); yhi = min(yhi, Ho - 1);
+        xlo = max(xlo, 0); xhi = min(xhi, Wo - 1);
+        float acc = 0.f;
+        for (int y = ylo; y <= yhi; ++y) {
+            const float wy = axis_weight(a, y, Y, Ho);
+            if (wy == 0.f) continue;
+            float racc = 0.f;
+            for (int x = xlo; x <= xhi; ++x) {
+                const float wx = axis_weight(a, x, X, Wo);
+                if (wx != 0.f) racc = fmaf(wx, ld(gp + (long long)y * Wo + x), racc);
+            }
+            acc = fmaf(wy, racc, acc);
+        }
+        st(reinterpret_cast<T*>(dx) + i, acc);
+    }
+}
+
+int grid_for(long long total) {
+    long long b = (total + NT - 1) / NT;
+    if (b > 16384) b = 16384;
+    return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+// ============================== C ABI ==========================================================
+
+extern "C" int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                                int dtype, int B, int C, int H, int W, int K, int pad, void* stream) {
+    if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0 || pad < 0) return VFM_ERR_ARGS;
+    DwArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.noise = noise; a.y = y;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
+    a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
+    if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
+    dw_plan(a);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (dtype) {
+    case VFM_F32: return dw_dispatch<float>(a, K, 0, nullptr, nullptr, st);
+    case VFM_F16: return dw_dispatch<__half>(a, K, 0, nullptr, nullptr, st);
+    case VFM_BF16: return dw_dispatch<__hip_bfloat16>(a, K, 0, nullptr, nullptr, st);
+    }
+    return VFM_ERR_ARGS;
+}
+
+extern "C" int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, int pad) {
+    DwArgs a{};
+    a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
+    a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
+    if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
+    dw_plan(a);
+    return a.tilesX * a.tilesY;
+}
+
+extern "C" int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int dtype, int B, int C, int H,
+                                       int W, int K, int pad, void* stream) {
+    if (!x || !dy || !partial || B <= 0 || C <= 0 || H <= 0 || W <= 0 || pad < 0) return VFM_ERR_ARGS;
+    DwArgs a{};
+    a.x = x; a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
+    a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
+    if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
+    dw_plan(a);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (dtype) {
+    case VFM_F32: return dw_dispatch<float>(a, K, 1, dy, partial, st);
+    case VFM_F16: return dw_dispatch<__half>(a, K, 1, dy, partial, st);
+    case VFM_BF16: return dw_dispatch<__hip_bfloat16>(a, K, 1, dy, partial, st);
+    }
+    return VFM_ERR_ARGS;
+}
+
+template <class TI, class TO>
+static int gn_fwd_launch(GnArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL((gn_fwd<TI, TO>), dim3(a.B * a.G), dim3(NT), 0, st, a);
+    return launch_status();
+}
+
+extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b, const float* s, void* y,
+                                  float* mean, float* rstd, int dtype_in, int dtype_out, int B, int C, int G, int HW,
+                                  float eps, void* stream) {
+    if (!x || !y || !mean || !rstd || B <= 0 || C <= 0 || G <= 0 || C % G || HW <= 0) return VFM_ERR_ARGS;
+    GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define GN_CASE(DI, TI)                                                        \
+    if (dtype_in == DI) {                                                      \
+        if (dtype_out == VFM_F32) return gn_fwd_launch<TI, float>(a, st);      \
+        if (dtype_out == VFM_BF16) return gn_fwd_launch<TI, __hip_bfloat16>(a, st); \
+        if (dtype_out == VFM_F16) return gn_fwd_launch<TI, __half>(a, st);     \
+    }
+    GN_CASE(VFM_F32, float)
+    GN_CASE(VFM_BF16, __hip_bfloat16)
+    GN_CASE(VFM_F16, __half)
+#undef GN_CASE
+    return VFM_ERR_ARGS;
+}
+
+template <class TX, class TY>
+static int gn_bwd_launch(GnBwdArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL((gn_bwd<TX, TY>), dim3(a.B * a.G), dim3(NT), 0, st, a);
+    return launch_status();
+}
+
+extern "C" int vfm_group_norm_bwd(const void* x, const void* dy, const float* mean, const float* rstd, const float* w,
+                                  const float* b, const float* s, void* dx, float* dw_part, float* db_part, float* ds,
+                                  int dtype_x, int dtype_dy, int B, int C, int G, int HW, void* stream) {
+    if (!x || !dy || !mean || !rstd || !dx || !dw_part || !db_part || B <= 0 || C % G || HW <= 0) return VFM_ERR_ARGS;
+    GnBwdArgs a{x, dy, mean, rstd, w, b, s, dx, dw_part, db_part, ds, B, C, G, HW};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define GNB_CASE(DX, TX)                                                         \
+    if (dtype_x == DX) {                                                         \
+        if (dtype_dy == VFM_F32) return gn_bwd_launch<TX, float>(a, st);         \
+        if (dtype_dy == VFM_BF16) return gn_bwd_launch<TX, __hip_bfloat16>(a, st); \
+        if (dtype_dy == VFM_F16) return gn_bwd_launch<TX, __half>(a, st);        \
+    }
+    GNB_CASE(VFM_F32, float)
+    GNB_CASE(VFM_BF16, __hip_bfloat16)
+    GNB_CASE(VFM_F16, __half)
+#undef GNB_CASE
+    return VFM_ERR_ARGS;
+}
+
+extern "C" int vfm_scale_bias_gelu_fwd(const void* h, const float* scale, const float* bias, void* g, int dtype,
+                                       int B, int O, int P, void* stream) {
+    if (!h || !g || B <= 0 || O <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    RowArgs a{};
+    a.in0 = h; a.out0 = g; a.rscale = scale; a.cvec0 = bias; a.R = B * O; a.O = O; a.P = P;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid((a.R + 3) / 4);
+    switch (dtype) {
+    case VFM_F32: hipLaunchKernelGGL((gelu_fwd<float>), grid, dim3(NT), 0, st, a); break;
+    case VFM_BF16: hipLaunchKernelGGL((gelu_fwd<__hip_bfloat16>), grid, dim3(NT), 0, st, a); break;
+    case VFM_F16: hipLaunchKernelGGL((gelu_fwd<__half>), grid, dim3(NT), 0, st, a); break;
+    default: return VFM_ERR_ARGS;
+    }
+    return launch_status();
+}
+
+extern "C" int vfm_scale_bias_gelu_bwd(const void* h, const void* dg, const float* scale, const float* bias, void* dh,
+                                       float* d_scale_rows, float* d_bias_rows, int dtype, int B, int O, int P,
+                                       void* stream) {
+    if (!h || !dg || !dh || !d_bias_rows || B <= 0 || O <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    RowArgs a{};
+    a.in0 = h; a.dout = dg; a.out0 = dh; a.rscale = scale; a.cvec0 = bias; a.rsum0 = d_scale_rows;
+    a.rsum1 = d_bias_rows; a.R = B * O; a.O = O; a.P = P;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid((a.R + 3) / 4);
+    switch (dtype) {
+    case VFM_F32: hipLaunchKernelGGL((gelu_bwd<float>), grid, dim3(NT), 0, st, a); break;
+    case VFM_BF16: hipLaunchKernelGGL((gelu_bwd<__hip_bfloat16>), grid, dim3(NT), 0, st, a); break;
+    case VFM_F16: hipLaunchKernelGGL((gelu_bwd<__half>), grid, dim3(NT), 0, st, a); break;
+    default: return VFM_ERR_ARGS;
+    }
+    return launch_status();
+}
+
+#define LSR_DISPATCH(KERNEL)                                                                       \
+    if (dtype_y == VFM_F32 && dtype_x == VFM_F32) hipLaunchKernelGGL((KERNEL<float, float>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_BF16 && dtype_x == VFM_BF16) hipLaunchKernelGGL((KERNEL<__hip_bfloat16, __hip_bfloat16>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_BF16 && dtype_x == VFM_F32) hipLaunchKernelGGL((KERNEL<__hip_bfloat16, float>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_F16 && dtype_x == VFM_F16) hipLaunchKernelGGL((KERNEL<__half, __half>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_F16 && dtype_x == VFM_F32) hipLaunchKernelGGL((KERNEL<__half, float>), grid, dim3(NT), 0, st, a); \
+    else return VFM_ERR_ARGS;
+
+extern "C" int vfm_layer_scale_residual_fwd(const void* y, const float* bias, const float* gamma, const void* x_in,
+                                            void* out, int dtype_y, int dtype_x, int B, int C, int P, void* stream) {
+    if (!y || !x_in || !out || B <= 0 || C <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    RowArgs a{};
+    a.in0 = y; a.in1 = x_in; a.out0 = out; a.cvec0 = bias; a.cvec1 = gamma; a.R = B * C; a.O = C; a.P = P;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid((a.R + 3) / 4);
+    LSR_DISPATCH(lsr_fwd)
+    return launch_status();
+}
+
+extern "C" int vfm_layer_scale_residual_bwd(const void* y, const float* bias, const float* gamma, const void* dout,
+                                            void* dy, float* d_gamma_rows, float* d_sum_rows, int dtype_y, int dtype_x,
+                                            int B, int C, int P, void* stream) {
+    if (!y || !dout || !dy || !d_gamma_rows || !d_sum_rows || B <= 0 || C <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    RowArgs a{};
+    a.in0 = y; a.dout = dout; a.out0 = dy; a.cvec0 = bias; a.cvec1 = gamma; a.rsum0 = d_gamma_rows;
+    a.rsum1 = d_sum_rows; a.R = B * C; a.O = C; a.P = P;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid((a.R + 3) / 4);
+    LSR_DISPATCH(lsr_bwd)
+    return launch_status();
+}
+#undef LSR_DISPATCH
+
+extern "C" int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, int K, int dtype, int B, int C, int H,
+                                    int W, int r, void* stream) {
+    if (!x || !y || !taps || K < 1 || K > 8 || r < 1 || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
+    BlurArgs a{};
+    a.x = x; a.y = y; a.B = B; a.C = C; a.H = H; a.W = W; a.r = r; a.K = K; a.pad0 = (K - 1) / 2;
+    for (int i = 0; i < K; ++i) a.k[i] = taps[i];
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int grid = grid_for((long long)B * C * H * r * W * r);
+    switch (dtype) {
+    case VFM_F32: hipLaunchKernelGGL((blur_fwd<float>), dim3(grid), dim3(NT), 0, st, a); break;
+    case VFM_BF16: hipLaunchKernelGGL((blur_fwd<__hip_bfloat16>), dim3(grid), dim3(NT), 0, st, a); break;
+    case VFM_F16: hipLaunchKernelGGL((blur_fwd<__half>), dim3(grid), dim3(NT), 0, st, a); break;
+    default: return VFM_ERR_ARGS;
+    }
+    return launch_status();
+}
+
+extern "C" int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* taps, int K, int dtype, int B, int C,
+                                    int H, int W, int r, void* stream) {
+    if (!dout || !dx || !taps || K < 1 || K > 8 || r < 1 || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
+    BlurArgs a{};
+    a.B = B; a.C = C; a.H = H; a.W = W; a.r = r; a.K = K; a.pad0 = (K - 1) / 2;
+    for (int i = 0; i < K; ++i) a.k[i] = taps[i];
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int grid = grid_for((long long)B * C * r * r * H * W);
+    switch (dtype) {
+    case VFM_F32: hipLaunchKernelGGL((blur_bwd<float>), dim3(grid), dim3(NT), 0, st, a, dout, dx); break;
+    case VFM_BF16: hipLaunchKernelGGL((blur_bwd<__hip_bfloat16>), dim3(grid), dim3(NT), 0, st, a, dout, dx); break;
+    case VFM_F16: hipLaunchKernelGGL((blur_bwd<__half>), dim3(grid), dim3(NT), 0, st, a, dout, dx); break;
+    default: return VFM_ERR_ARGS;
+    }
+    return launch_status();
+}

@@ -19,6 +19,7 @@ _lib = None
 
 c_int, c_ll, c_float, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
 c_llp = ctypes.POINTER(ctypes.c_longlong)
+c_fp = ctypes.POINTER(ctypes.c_float)
 
 # name -> argtypes (restype is always int). Keep in sync with include/vfmvae.h.
 SIGNATURES = {
@@ -31,6 +32,20 @@ SIGNATURES = {
                            c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_int, c_vp],
     "vfm_filtered_lrelu_act": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_int, c_int, c_int,
                                c_int, c_int, c_float, c_float, c_float, c_vp],
+    "vfm_dwconv2d_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_dwconv2d_bwd_weight_tiles": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "vfm_dwconv2d_bwd_weight": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_group_norm_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_float, c_vp],
+    "vfm_group_norm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                           c_int, c_int, c_int, c_vp],
+    "vfm_scale_bias_gelu_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_scale_bias_gelu_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_layer_scale_residual_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_layer_scale_residual_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                     c_vp],
+    "vfm_shuffle_blur_fwd": [c_vp, c_vp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_shuffle_blur_bwd": [c_vp, c_vp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
 }
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}

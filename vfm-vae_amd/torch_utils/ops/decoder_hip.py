@@ -1,0 +1,326 @@
+"""Autograd wrappers over the gfx950 decoder kernels (`csrc/decoder.hip`, C ABI in
+include/vfmvae.h). Only reached through `decoder_ops.*` for ROCm tensors; the
+library is loaded on import and a missing library raises (no silent fallback).
+
+Shapes the kernels do not cover (spatial size not a multiple of 8 for the row
+ops, kernel sizes outside {1,3,5,7}) are rejected by `supported()` and the
+caller keeps the torch formulation for them — on the same device.
+
+Every launch is bracketed by `kernel_timer.region(name, algorithmic_bytes)`
+(inputs + outputs at the op boundary, each tensor counted once) so bench.py can
+report the dominant kernel's roofline.
+"""
+import ctypes
+
+import torch
+
+from .. import custom_ops
+from . import kernel_timer
+
+_lib = custom_ops.get_native()
+_F32 = 0
+
+
+def _code(t):
+    return custom_ops.dtype_code(t)
+
+
+def _stream():
+    return custom_ops.stream_ptr()
+
+
+def _c(t):
+    """Contiguous and 16-byte aligned (vector loads)."""
+    t = t.contiguous()
+    if t.data_ptr() % 16:
+        t = t.clone()
+    return t
+
+
+def _f32(t):
+    return None if t is None else t.detach().reshape(-1).float().contiguous()
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _nb(*ts):
+    return sum(t.numel() * t.element_size() for t in ts if t is not None)
+
+
+def _check(rc, name):
+    custom_ops.check(rc, name)
+
+
+def supported(op, x, **kw):
+    if x.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+        return False
+    if op == 'dwconv2d':
+        return kw['k'] in (1, 3, 5, 7) and x.ndim == 4
+    if op in ('scale_bias_gelu', 'layer_scale_residual'):
+        return x.shape[-1] % 8 == 0 if x.ndim == 3 else (x.shape[-1] * x.shape[-2]) % 8 == 0
+    if op == 'group_norm':
+        return x.ndim >= 3 and x.shape[1] % kw['groups'] == 0
+    if op == 'shuffle_blur':
+        return 1 <= kw['k'] <= 8
+    return False
+
+
+# ---------------------------------------------------------------------------
+# Depthwise conv (reference convnext_utils.py:121-124 / :243: nn.Conv2d(groups=C)).
+
+
+def _dw_fwd(x, w3, bias, noise, pad, name):
+    B, C, H, W = x.shape
+    K = w3.shape[-1]
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    y = torch.empty([B, C, Ho, Wo], dtype=x.dtype, device=x.device)
+    with kernel_timer.region(name, _nb(x, y)):
+        _check(_lib.vfm_dwconv2d_fwd(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
+                                     B, C, H, W, K, pad, _stream()), name)
+    return y
+
+
+class _DwConv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, noise, pad):
+        x = _c(x)
+        C, K = weight.shape[0], weight.shape[-1]
+        w3 = weight.detach().reshape(C, K, K).float().contiguous()
+        b = _f32(bias)
+        n = None if noise is None else noise.detach().float().contiguous()
+        y = _dw_fwd(x, w3, b, n, pad, 'dwconv2d_fwd')
+        ctx.save_for_backward(x, w3)
+        ctx.pad = pad
+        ctx.meta = (weight.dtype, weight.shape, None if bias is None else bias.dtype,
+                    None if noise is None else noise.dtype)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x, w3 = ctx.saved_tensors
+        pad = ctx.pad
+        wdt, wshape, bdt, ndt = ctx.meta
+        dy = _c(dy.to(x.dtype))
+        B, C, H, W = x.shape
+        K = w3.shape[-1]
+        dx = dw = db = dn = None
+        if ctx.needs_input_grad[0]:
+            dx = _dw_fwd(dy, torch.flip(w3, [1, 2]).contiguous(), None, None, K - 1 - pad, 'dwconv2d_bwd_data')
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            tiles = _lib.vfm_dwconv2d_bwd_weight_tiles(B, C, H, W, K, pad)
+            if tiles <= 0:
+                raise custom_ops.NativeError(f"vfm_dwconv2d_bwd_weight_tiles failed with code {tiles}")
+            part = torch.empty([tiles, B * C, K * K + 1], dtype=torch.float32, device=x.device)
+            with kernel_timer.region('dwconv2d_bwd_weight', _nb(x, dy)):
+                _check(_lib.vfm_dwconv2d_bwd_weight(x.data_ptr(), dy.data_ptr(), part.data_ptr(), _code(x),
+                                                    B, C, H, W, K, pad, _stream()), 'vfm_dwconv2d_bwd_weight')
+            s = part.sum(0).view(B, C, K * K + 1).sum(0)
+            if ctx.needs_input_grad[1]:
+                dw = s[:, :K * K].reshape(wshape).to(wdt)
+            if ctx.needs_input_grad[2]:
+                db = s[:, K * K].to(bdt)
+        if ctx.needs_input_grad[3]:
+            dn = dy.float().sum(dim=(0, 1)).to(ndt)
+        return dx, dw, db, dn, None
+
+
+def dwconv2d(x, weight, bias, padding, noise):
+    return _DwConv2d.apply(x, weight, bias, noise, int(padding))
+
+
+# ---------------------------------------------------------------------------
+# GroupNorm with fp32 statistics and the folded style scale
+# (reference shared.py:165-167 GroupNorm32; convnext_utils.py:126-127).
+
+
+class _GroupNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, style, groups, eps, out_dtype):
+        x = _c(x)
+        B, C = x.shape[:2]
+        HW = x[0, 0].numel()
+        w, b = _f32(weight), _f32(bias)
+        s = None if style is None else style.detach().float().contiguous()
+        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+        mean = torch.empty([B * groups], dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        with kernel_timer.region('group_norm_fwd', _nb(x, y)):
+            _check(_lib.vfm_group_norm_fwd(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), mean.data_ptr(),
+                                           rstd.data_ptr(), _code(x), _code(y), B, C, groups, HW, float(eps),
+                                           _stream()), 'vfm_group_norm_fwd')
+        ctx.save_for_backward(x, w, b, s, mean, rstd)
+        ctx.groups = groups
+        ctx.meta = tuple(None if t is None else t.dtype for t in (weight, bias, style))
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x, w, b, s, mean, rstd = ctx.saved_tensors
+        B, C = x.shape[:2]
+        HW = x[0, 0].numel()
+        dy = _c(dy)
+        dx = torch.empty_like(x)
+        dwp = torch.empty([B, C], dtype=torch.float32, device=x.device)
+        dbp = torch.empty_like(dwp)
+        ds = torch.empty_like(dwp) if s is not None else None
+        with kernel_timer.region('group_norm_bwd', _nb(x, dy, dx)):
+            _check(_lib.vfm_group_norm_bwd(x.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _p(w),
+                                           _p(b), _p(s), dx.data_ptr(), dwp.data_ptr(), dbp.data_ptr(), _p(ds),
+                                           _code(x), _code(dy), B, C, ctx.groups, HW, _stream()),
+                   'vfm_group_norm_bwd')
+        wdt, bdt, sdt = ctx.meta
+        dw = dwp.sum(0).to(wdt) if ctx.needs_input_grad[1] else None
+        db = dbp.sum(0).to(bdt) if ctx.needs_input_grad[2] else None
+        dst = ds.to(sdt) if ctx.needs_input_grad[3] else None
+        return (dx if ctx.needs_input_grad[0] else None), dw, db, dst, None, None, None
+
+
+def group_norm(x, num_groups, weight, bias, eps, out_dtype, style):
+    return _GroupNorm.apply(x, weight, bias, style, int(num_groups), float(eps), out_dtype)
+
+
+# ---------------------------------------------------------------------------
+# Modulated pwconv1 epilogue: gelu(h * dcoef[b, o] + bias[o])
+# (reference convnext_utils.py:60-66 demodulation, :129-130 bias + GELU).
+
+
+class _ScaleBiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, scale, bias):
+        h = _c(h)
+        B, O = h.shape[:2]
+        P = h[0, 0].numel()
+        s, b = _f32(scale), _f32(bias)
+        g = torch.empty_like(h)
+        with kernel_timer.region('scale_bias_gelu_fwd', _nb(h, g)):
+            _check(_lib.vfm_scale_bias_gelu_fwd(h.data_ptr(), _p(s), _p(b), g.data_ptr(), _code(h), B, O, P,
+                                                _stream()), 'vfm_scale_bias_gelu_fwd')
+        ctx.save_for_backward(h, s, b)
+        ctx.meta = (None if scale is None else scale.dtype, None if bias is None else bias.dtype)
+        return g
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dg):
+        h, s, b = ctx.saved_tensors
+        B, O = h.shape[:2]
+        P = h[0, 0].numel()
+        dg = _c(dg)
+        dh = torch.empty_like(h)
+        want_s = s is not None and ctx.needs_input_grad[1]
+        ds_rows = torch.empty([B * O], dtype=torch.float32, device=h.device) if want_s else None
+        db_rows = torch.empty([B * O], dtype=torch.float32, device=h.device)
+        with kernel_timer.region('scale_bias_gelu_bwd', _nb(h, dg, dh)):
+            _check(_lib.vfm_scale_bias_gelu_bwd(h.data_ptr(), dg.data_ptr(), _p(s), _p(b), dh.data_ptr(),
+                                                _p(ds_rows), db_rows.data_ptr(), _code(h), B, O, P, _stream()),
+                   'vfm_scale_bias_gelu_bwd')
+        sdt, bdt = ctx.meta
+        ds = ds_rows.view(B, O).to(sdt) if want_s else None
+        db = db_rows.view(B, O).sum(0).to(bdt) if (b is not None and ctx.needs_input_grad[2]) else None
+        return (dh if ctx.needs_input_grad[0] else None), ds, db
+
+
+def scale_bias_gelu(h, scale, bias):
+    return _ScaleBiasGelu.apply(h, scale, bias)
+
+
+# ---------------------------------------------------------------------------
+# pwconv2 bias + layer scale + residual (reference convnext_utils.py:131-142).
+
+
+class _LayerScaleResidual(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, bias, gamma, x_in):
+        y, x_in = _c(y), _c(x_in)
+        B, C = y.shape[:2]
+        P = y[0, 0].numel()
+        b, g = _f32(bias), _f32(gamma)
+        out = torch.empty(x_in.shape, dtype=x_in.dtype, device=x_in.device)
+        with kernel_timer.region('layer_scale_residual_fwd', _nb(y, x_in, out)):
+            _check(_lib.vfm_layer_scale_residual_fwd(y.data_ptr(), _p(b), _p(g), x_in.data_ptr(), out.data_ptr(),
+                                                     _code(y), _code(x_in), B, C, P, _stream()),
+                   'vfm_layer_scale_residual_fwd')
+        ctx.save_for_backward(y, b, g)
+        ctx.meta = (None if bias is None else bias.dtype, None if gamma is None else gamma.dtype, x_in.dtype)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout):
+        y, b, g = ctx.saved_tensors
+        bdt, gdt, xdt = ctx.meta
+        B, C = y.shape[:2]
+        P = y[0, 0].numel()
+        dout = _c(dout.to(xdt))
+        dy = torch.empty_like(y)
+        r0 = torch.empty([B * C], dtype=torch.float32, device=y.device)
+        r1 = torch.empty_like(r0)
+        with kernel_timer.region('layer_scale_residual_bwd', _nb(y, dout, dy)):
+            _check(_lib.vfm_layer_scale_residual_bwd(y.data_ptr(), _p(b), _p(g), dout.data_ptr(), dy.data_ptr(),
+                                                     r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout), B, C, P,
+                                                     _stream()), 'vfm_layer_scale_residual_bwd')
+        db = dg = None
+        if b is not None and ctx.needs_input_grad[1]:
+            s1 = r1.view(B, C).sum(0)
+            db = (s1 * g if g is not None else s1).to(bdt)
+        if g is not None and ctx.needs_input_grad[2]:
+            dg = r0.view(B, C).sum(0).to(gdt)
+        return (dy if ctx.needs_input_grad[0] else None), db, dg, (dout if ctx.needs_input_grad[3] else None)
+
+
+def layer_scale_residual(y, bias, gamma, x_in):
+    if bias is not None:
+        bias = bias.reshape(-1)
+    if gamma is not None:
+        gamma = gamma.reshape(-1)
+    return _LayerScaleResidual.apply(y, bias, gamma, x_in)
+
+
+# ---------------------------------------------------------------------------
+# PixelShuffle + replicate pad + fixed blur (reference convnext_utils.py:234-257).
+
+
+def _taps(blur1d):
+    k = [float(t) for t in blur1d]
+    s = sum(k)
+    k = [t / s for t in k]
+    return (ctypes.c_float * 8)(*(k + [0.0] * (8 - len(k)))), len(k)
+
+
+class _ShuffleBlur(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blur1d, r):
+        x = _c(x)
+        B, Cr, H, W = x.shape
+        C = Cr // (r * r)
+        taps, K = _taps(blur1d)
+        y = torch.empty([B, C, H * r, W * r], dtype=x.dtype, device=x.device)
+        with kernel_timer.region('shuffle_blur_fwd', _nb(x, y)):
+            _check(_lib.vfm_shuffle_blur_fwd(x.data_ptr(), y.data_ptr(), taps, K, _code(x), B, C, H, W, r, _stream()),
+                   'vfm_shuffle_blur_fwd')
+        ctx.cfg = (tuple(blur1d), r, (B, C, H, W))
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        blur1d, r, (B, C, H, W) = ctx.cfg
+        dy = _c(dy)
+        taps, K = _taps(blur1d)
+        dx = torch.empty([B, C * r * r, H, W], dtype=dy.dtype, device=dy.device)
+        with kernel_timer.region('shuffle_blur_bwd', _nb(dy, dx)):
+            _check(_lib.vfm_shuffle_blur_bwd(dy.data_ptr(), dx.data_ptr(), taps, K, _code(dy), B, C, H, W, r,
+                                             _stream()), 'vfm_shuffle_blur_bwd')
+        return dx, None, None
+
+
+def shuffle_blur(x, blur1d, upscale):
+    return _ShuffleBlur.apply(x, tuple(blur1d), int(upscale))
+
+
+def blur_replicate(x, blur1d):
+    return _ShuffleBlur.apply(x, tuple(blur1d), 1)

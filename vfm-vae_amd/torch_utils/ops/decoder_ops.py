@@ -15,12 +15,19 @@ import math
 import torch
 import torch.nn.functional as F
 
-_HIP_OPS = set()          # names of ops whose HIP path is available (filled by decoder_hip)
+_HIP_OPS = {'group_norm', 'dwconv2d', 'scale_bias_gelu', 'layer_scale_residual', 'shuffle_blur',
+            'blur_replicate'}
 _FORCE_REF = False        # global switch for A/B experiments and CPU restatement timing
 
 
-def _use_hip(name, x, impl):
-    return impl == 'cuda' and x.is_cuda and not _FORCE_REF and name in _HIP_OPS
+def _use_hip(name, x, impl, **kw):
+    """True when the gfx950 kernel runs: ROCm tensor, impl='cuda', op built and shape
+    covered (decoder_hip.supported). Importing decoder_hip loads the kernel library
+    and raises if it is missing."""
+    if not (impl == 'cuda' and x.is_cuda and not _FORCE_REF and name in _HIP_OPS):
+        return False
+    from . import decoder_hip
+    return decoder_hip.supported(name if name != 'blur_replicate' else 'shuffle_blur', x, **kw)
 
 
 def set_force_ref(flag: bool):
@@ -38,7 +45,7 @@ def group_norm(x, num_groups, weight=None, bias=None, eps=1e-5, out_dtype=None, 
     `style` ([B, C]) folds the input modulation of a modulated 1x1 conv into the
     normalisation pass (w_b = W * s_b  <=>  W @ (s_b * x))."""
     out_dtype = out_dtype or x.dtype
-    if _use_hip('group_norm', x, impl):
+    if _use_hip('group_norm', x, impl, groups=num_groups):
         from . import decoder_hip
         return decoder_hip.group_norm(x, num_groups, weight, bias, eps, out_dtype, style)
     y = F.group_norm(x.float(), num_groups, weight.float() if weight is not None else None,
@@ -55,7 +62,7 @@ def group_norm(x, num_groups, weight=None, bias=None, eps=1e-5, out_dtype=None, 
 def dwconv2d(x, weight, bias=None, padding=0, noise=None, impl='cuda'):
     """Depthwise conv: weight [C, 1, k, k], zero padding `padding`, stride 1.
     `noise` ([H_out, W_out], fp32) is added to every channel (legacy noise path)."""
-    if _use_hip('dwconv2d', x, impl):
+    if _use_hip('dwconv2d', x, impl, k=weight.shape[-1]):
         from . import decoder_hip
         return decoder_hip.dwconv2d(x, weight, bias, padding, noise)
     y = F.conv2d(x, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None, padding=padding,
@@ -107,7 +114,7 @@ def layer_scale_residual(y, bias, gamma, x_in, impl='cuda'):
 def shuffle_blur(x, blur1d, upscale=2, impl='cuda'):
     """PixelShuffle(upscale) followed by replicate-pad + depthwise blur with the
     normalised outer product of `blur1d` (a python list of taps)."""
-    if _use_hip('shuffle_blur', x, impl):
+    if _use_hip('shuffle_blur', x, impl, k=len(blur1d)):
         from . import decoder_hip
         return decoder_hip.shuffle_blur(x, blur1d, upscale)
     y = F.pixel_shuffle(x, upscale)
@@ -115,7 +122,7 @@ def shuffle_blur(x, blur1d, upscale=2, impl='cuda'):
 
 
 def blur_replicate(x, blur1d, impl='cuda'):
-    if _use_hip('blur_replicate', x, impl):
+    if _use_hip('blur_replicate', x, impl, k=len(blur1d)):
         from . import decoder_hip
         return decoder_hip.blur_replicate(x, blur1d)
     k = torch.tensor(blur1d, dtype=torch.float32)

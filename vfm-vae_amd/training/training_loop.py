@@ -156,6 +156,7 @@ class TrainingIteration:
         self.ema_kimg = ema_kimg
         self.ema_rampup = ema_rampup
         self._ema_pairs = None
+        self.trace = None          # callable(msg) -> per-phase wall times (synchronising; diagnostics only)
 
     @staticmethod
     def partial_freeze(phase):
@@ -209,9 +210,22 @@ class TrainingIteration:
             be.copy_(b)
 
     def __call__(self, phase_real_img, phase_real_c, cur_nimg):
+        if self.trace is None:
+            for phase in self.phases:
+                self.run_phase(phase, phase_real_img, phase_real_c, cur_nimg)
+            self.update_ema(cur_nimg)
+            return
+        import time
         for phase in self.phases:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             self.run_phase(phase, phase_real_img, phase_real_c, cur_nimg)
+            torch.cuda.synchronize()
+            self.trace(f"phase {phase.name}: {time.perf_counter() - t0:.3f}s")
+        t0 = time.perf_counter()
         self.update_ema(cur_nimg)
+        torch.cuda.synchronize()
+        self.trace(f"ema: {time.perf_counter() - t0:.3f}s")
 
 
 # ---------------------------------------------------------------------------
