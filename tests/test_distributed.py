@@ -1,0 +1,151 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the data-parallel path:
+FlatGradSync's bucketed hook-driven all-reduce reproduces the reference
+`sync_grads` semantics (training_loop.py:281-289: sum over ranks / world, * gain,
+nan_to_num(0, 1e5, -1e5)); a full TrainingIteration keeps the replicas identical."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT, PKG
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn(fn, world=2, *args):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q, args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, out = q.get(timeout=300)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0, p.exitcode
+    for r, out in res.items():
+        if isinstance(out, str) and out.startswith("ERROR"):
+            raise AssertionError(out)
+    return res
+
+
+def _entry(fn, rank, world, port, q, args):
+    for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    try:
+        from torch_utils import distributed as dist
+        dist.init(backend="gloo")
+        out = globals()[fn](rank, world, *args)
+        # plain numpy (tensors would travel as shared-memory handles that die with this process)
+        conv = lambda v: v.detach().numpy().copy() if isinstance(v, torch.Tensor) else v
+        out = {k: conv(v) for k, v in out.items()} if isinstance(out, dict) else out
+        q.put((rank, out))
+        dist.destroy_process_group()
+    except Exception as e:  # report to the parent instead of hanging it
+        import traceback
+        q.put((rank, "ERROR " + traceback.format_exc()))
+
+
+def _toy(seed=0):
+    torch.manual_seed(seed)
+    m = torch.nn.Sequential(torch.nn.Linear(6, 32), torch.nn.Tanh(), torch.nn.Linear(32, 5))
+    m.unused = torch.nn.Parameter(torch.ones(3))
+    return m
+
+
+def _toy_loss(m, rank, poison=False):
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(4, 6, generator=g)
+    y = m(x)
+    loss = y.square().sum() * (rank + 1)
+    if poison and rank == 1:
+        loss = loss + m[2].bias[0] * float("inf")
+    return loss
+
+
+def _flat_sync_worker(rank, world, bucket_mb, poison):
+    from training.training_loop import FlatGradSync
+    m = _toy()
+    sync = FlatGradSync(m, bucket_mb=bucket_mb)
+    sync.prepare()
+    _toy_loss(m, rank, poison).backward()
+    sync.finish(gain=2.0)
+    return {n: (None if p.grad is None else p.grad.clone()) for n, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("bucket_mb", [64.0, 1e-4])      # one bucket / one bucket per parameter
+def test_flat_grad_sync_matches_reference_semantics(bucket_mb):
+    res = _spawn("_flat_sync_worker", 2, bucket_mb, False)
+    expect = {}
+    for r in range(2):
+        m = _toy()
+        _toy_loss(m, r).backward()
+        for n, p in m.named_parameters():
+            if p.grad is not None:
+                expect[n] = expect.get(n, 0) + p.grad
+    for r in range(2):
+        got = res[r]
+        assert got["unused"] is None
+        for n, e in expect.items():
+            torch.testing.assert_close(torch.from_numpy(got[n]), e / 2 * 2.0, rtol=1e-6, atol=1e-6)
+
+
+def test_flat_grad_sync_nan_to_num():
+    res = _spawn("_flat_sync_worker", 2, 64.0, True)
+    for r in range(2):
+        b = torch.from_numpy(res[r]["2.bias"])
+        assert torch.isfinite(b).all()
+        assert float(b[0]) in (1e5, -1e5, 0.0)
+    torch.testing.assert_close(torch.from_numpy(res[0]["0.weight"]), torch.from_numpy(res[1]["0.weight"]))
+
+
+def _iteration_worker(rank, world):
+    import copy
+    import json
+    import tempfile
+    import net_cases
+    from networks.generator import Generator
+    from networks.discriminator import ProjectedDiscriminator
+    from training.loss import TotalLoss
+    from training.training_loop import TrainingIteration, make_optimizer
+    d = os.path.join(tempfile.mkdtemp(), net_cases.VFM_DIRNAME)
+    os.makedirs(d)
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(os.path.join(d, "config.json"), "w"))
+    torch.manual_seed(0)
+    dev = torch.device("cpu")
+    G = Generator(label_dim=0, **net_cases.g_kwargs(d)).train().requires_grad_(False)
+    D = ProjectedDiscriminator(c_dim=0, **net_cases.D_KWARGS).train().requires_grad_(False)
+    loss = TotalLoss(device=dev, G=G, D=D, **net_cases.loss_kwargs(d))
+    opt = dict(class_name='torch.optim.Adam', lr=1e-3, betas=[0.0, 0.99], eps=1e-8)
+    it = TrainingIteration(G, D, copy.deepcopy(G).eval(), loss, make_optimizer(G.parameters(), opt, dev),
+                           make_optimizer(D.parameters(), opt, dev), batch_size=2 * world, bucket_mb=0.5)
+    before = torch.cat([p.detach().flatten() for p in G.parameters()]).clone()
+    g = torch.Generator().manual_seed(rank)
+    img = torch.rand(2, 3, 64, 64, generator=g)
+    it([img], [['x', 'x']], 0)
+    after_g = torch.cat([p.detach().flatten() for p in G.parameters()])
+    after_d = torch.cat([p.detach().flatten() for p in D.parameters()])
+    return dict(moved=float((after_g - before).abs().max()), g=after_g, d=after_d)
+
+
+def test_training_iteration_replicas_stay_identical():
+    res = _spawn("_iteration_worker", 2)
+    assert res[0]["moved"] > 0
+    assert (res[0]["g"] == res[1]["g"]).all()
+    assert (res[0]["d"] == res[1]["d"]).all()

@@ -669,8 +669,7 @@ __device__ __forceinline__ float axis_weight(const BlurArgs& a, int o, int s, in
 }
 
 // d_x at pre-shuffle element (cin, iy, ix) = d_S(Y, X) with Y = iy*r + sy, X = ix*r + sx,
-// d_S(Y, X) = sum_{y, x} wy(y, Y) wx(x, X) dout(y, x), y in [Y - (K-1-pad0), Y + pad0] plus the
-// folded edge range when Y is 0 or n-1.
+// d_S(Y, X) = sum_{y, x} wy(y, Y) wx(x, X) dout(y, x), y in [Y - (K-1-pad0), Y + pad0] (clipped).
 template <class T>
 __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
     const int Ho = a.H * a.r, Wo = a.W * a.r;
@@ -686,19 +685,11 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
         const int c = cin / (a.r * a.r), sub = cin % (a.r * a.r);
         const int Y = iy * a.r + sub / a.r, X = ix * a.r + sub % a.r;
         const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
-        int ylo = Y - reach_hi, yhi = Y + reach_lo;
-        int xlo = X - reach_hi, xhi = X + reach_lo;
-        if (Y == 0) ylo = 0;
-        if (Y == Ho - 1) yhi = Ho - 1;
-        if (X == 0) xlo = 0;
-        if (X == Wo - 1) xhi = Wo - 1;
-        // Edge folding reaches at most K-1 positions inward.
-        if (Y == 0) yhi = min(yhi + a.K, Ho - 1);
-        if (Y == Ho - 1) ylo = max(ylo - a.K, 0);
-        if (X == 0) xhi = min(xhi + a.K, Wo - 1);
-        if (X == Wo - 1) xlo = max(xlo - a.K, 0);
-        ylo = max(ylo, 0); yhi = min(yhi, Ho - 1);
-        xlo = max(xlo, 0); xhi = min(xhi, Wo - 1);
+        // Output y reads source clamp(y + t - pad0): interior sources are reached from
+        // y in [Y - reach_lo, Y + reach_hi]; the replicate-clamped edge reads fall in the
+        // same window, so clipping it to the image covers the folded edge terms too.
+        const int ylo = max(Y - reach_lo, 0), yhi = min(Y + reach_hi, Ho - 1);
+        const int xlo = max(X - reach_lo, 0), xhi = min(X + reach_hi, Wo - 1);
         float acc = 0.f;
         for (int y = ylo; y <= yhi; ++y) {
             const float wy = axis_weight(a, y, Y, Ho);

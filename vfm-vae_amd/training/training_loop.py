@@ -102,12 +102,16 @@ class FlatGradSync:
         self.ready = [0] * len(self.buckets)
         self.pending = {}
         self.last_microbatch = True
+        self.late = False
 
     def _on_grad(self, p):
         self.seen.add(id(p))
         if not self.last_microbatch or self.world <= 1:
             return
         bi = self.bucket_of[id(p)]
+        if bi in self.pending:              # a second backward touched a bucket already in flight
+            self.late = True
+            return
         self.ready[bi] += 1
         if self.ready[bi] == self.buckets[bi][2]:
             self._launch(bi)
@@ -132,6 +136,9 @@ class FlatGradSync:
                     self._launch(bi)
             for bi in sorted(self.pending):
                 self.pending[bi].wait()
+            if self.late:
+                raise RuntimeError("FlatGradSync: more than one backward pass in the last microbatch of a phase "
+                                   "(gradients changed under an in-flight all-reduce)")
             if self.comm_stream is not None:
                 torch.cuda.current_stream(self.flat.device).wait_stream(self.comm_stream)
             self.flat.mul_(1.0 / self.world)
