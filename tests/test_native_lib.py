@@ -58,3 +58,13 @@ def test_argument_validation_without_gpu():
     rc = lib.vfm_filtered_lrelu(p, p, p, None, None, p, 0, 1, 1, 4, 4, xs, 4, 4, xs, 1, 1, 1, 1, 3, 1, 0, 0,
                                 0, 0, 0, 0, 0, 1.0, 0.2, float("inf"), 0, None)
     assert rc == -1
+
+
+def test_dwconv_partial_tiles_host_query():
+    """vfm_dwconv2d_bwd_weight_tiles is pure host logic: one partial per 64-wide column tile."""
+    import torch_utils.custom_ops as co
+    lib = co.get_native()
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 256, 256, 7, 3) == 4
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 16, 16, 3, 1) == 1
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 5, 130, 3, 1) == 3
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 2, 2, 7, 0) == -2      # empty output -> VFM_ERR_ARGS

@@ -1,0 +1,52 @@
+"""Attribute GPU time of one training iteration to torch ops (torch.profiler).
+
+  python tools_dev/torchprof.py [--batch 32] [--out gpurun_out/tp]
+
+Prints the top ops by self device time and the top kernels with the op and
+input shapes that launched them (record_shapes), to find unfused copies etc.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "vfm-vae_amd"))
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--out", default="gpurun_out/tp")
+    ap.add_argument("--rows", type=int, default=60)
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    c, step = bench.build(bench.CONFIG, args.batch, dev, 1)
+    from training.data_synthetic import SyntheticDataset
+    pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=0).make_pool(args.batch, dev)
+    labels = ['a photo'] * args.batch
+    for i in range(2):
+        step([pool[i % len(pool)].float() / 255.], [labels], i * args.batch)
+    torch.cuda.synchronize()
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=False) as prof:
+        step([pool[0].float() / 255.], [labels], 2 * args.batch)
+        torch.cuda.synchronize()
+    sort = "self_cuda_time_total"
+    t1 = prof.key_averages().table(sort_by=sort, row_limit=args.rows, max_name_column_width=60)
+    t2 = prof.key_averages(group_by_input_shape=True).table(sort_by=sort, row_limit=args.rows,
+                                                            max_name_column_width=50, max_shapes_column_width=90)
+    open(os.path.join(args.out, "ops.txt"), "w").write(t1)
+    open(os.path.join(args.out, "ops_shapes.txt"), "w").write(t2)
+    print(t1[:12000])
+
+
+if __name__ == "__main__":
+    main()

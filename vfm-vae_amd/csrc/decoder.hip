@@ -41,6 +41,34 @@ struct DwArgs {
     int tilesX, tilesY, planeGroups;
 };
 
+// Stage ppb halo tiles [LH x LW] (zero padded) into LDS without per-element divisions:
+// a wave covers `rpw` rows per instruction with `lpr` (pow2 >= LW, <= 64) lanes per row.
+template <class T>
+__device__ __forceinline__ void dw_stage(const DwArgs& a, float* lds, int pg, int ox0, int oy0, int LW, int LH) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int lpr = 1;
+    while (lpr < LW && lpr < 64) lpr <<= 1;
+    const int rpw = 64 / lpr;
+    const int sub = lane / lpr, cx = lane - sub * lpr;
+    const int nplanes = a.B * a.C;
+    const int rows = a.ppb * LH;
+    const T* xbase = reinterpret_cast<const T*>(a.x);
+    for (int q0 = wave * rpw; q0 < rows; q0 += 4 * rpw) {
+        const int q = q0 + sub;
+        if (q >= rows) continue;
+        const int p = q / LH, ry = q - p * LH;
+        const int plane = pg * a.ppb + p;
+        const int iy = oy0 + ry - a.pad;
+        const bool rok = plane < nplanes && iy >= 0 && iy < a.H;
+        const T* src = xbase + ((long long)plane * a.H + iy) * a.W;
+        float* dst = lds + (p * LH + ry) * LW;
+        for (int rx = cx; rx < LW; rx += lpr) {
+            const int ix = ox0 + rx - a.pad;
+            dst[rx] = (rok && ix >= 0 && ix < a.W) ? ld(src + ix) : 0.f;
+        }
+    }
+}
+
 template <class T, int K>
 __global__ __launch_bounds__(NT) void dw_fwd(DwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -52,18 +80,8 @@ __global__ __launch_bounds__(NT) void dw_fwd(DwArgs a) {
     const int ox0 = tx * a.TW, oy0 = ty * a.TH;
     const int nplanes = a.B * a.C;
 
-    // Stage ppb input tiles with halo.
     const int per = LW * LH;
-    for (int i = threadIdx.x; i < a.ppb * per; i += NT) {
-        const int pl = i / per, r = i - pl * per;
-        const int ry = r / LW, rx = r - ry * LW;
-        const int plane = pg * a.ppb + pl;
-        const int iy = oy0 + ry - a.pad, ix = ox0 + rx - a.pad;
-        float v = 0.f;
-        if (plane < nplanes && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-            v = ld(reinterpret_cast<const T*>(a.x) + (long long)plane * a.H * a.W + (long long)iy * a.W + ix);
-        lds[i] = v;
-    }
+    dw_stage<T>(a, lds, pg, ox0, oy0, LW, LH);
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -114,32 +132,19 @@ __global__ __launch_bounds__(NT) void dw_fwd(DwArgs a) {
 }
 
 // dW[plane][ky][kx] = sum_{y,x} dy[y][x] * x[y+ky-pad][x+kx-pad]; db[plane] = sum dy.
-// Same tiling as dw_fwd; the grid walks (plane group, tile); each lane accumulates K*K+1
-// partial sums for its strip; a workgroup reduction writes per-(tile, plane) partials that
-// the host sums (fixed order -> deterministic).
+// One workgroup per (plane group, column tile) walks all row tiles of its planes, so the
+// K*K+1 per-lane sums are reduced once per column band. Inner loop = the forward's sliding
+// window: each staged input row is read once (K LDS reads) and meets the RPT dy values held
+// in registers. Per-(column tile, plane) partials are summed by the host in a fixed order.
 template <class T, int K>
 __global__ __launch_bounds__(NT) void dw_bwd_w(DwArgs a, const void* dy, float* partial) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int LW = a.TW + K - 1, LH = a.TH + K - 1;
-    int bid = blockIdx.x;
-    const int tx = bid % a.tilesX; bid /= a.tilesX;
-    const int ty = bid % a.tilesY; bid /= a.tilesY;
-    const int pg = bid;
-    const int tile_id = ty * a.tilesX + tx;
-    const int ox0 = tx * a.TW, oy0 = ty * a.TH;
+    const int tx = blockIdx.x % a.tilesX;
+    const int pg = blockIdx.x / a.tilesX;
+    const int ox0 = tx * a.TW;
     const int nplanes = a.B * a.C;
     const int per = LW * LH;
-    for (int i = threadIdx.x; i < a.ppb * per; i += NT) {
-        const int pl = i / per, r = i - pl * per;
-        const int ry = r / LW, rx = r - ry * LW;
-        const int plane = pg * a.ppb + pl;
-        const int iy = oy0 + ry - a.pad, ix = ox0 + rx - a.pad;
-        float v = 0.f;
-        if (plane < nplanes && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-            v = ld(reinterpret_cast<const T*>(a.x) + (long long)plane * a.H * a.W + (long long)iy * a.W + ix);
-        lds[i] = v;
-    }
-    __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane % a.TW, psub = lane / a.TW;
@@ -149,24 +154,40 @@ __global__ __launch_bounds__(NT) void dw_bwd_w(DwArgs a, const void* dy, float* 
     const int ox = ox0 + col;
     const int r0 = strip * RPT;
     const bool live = pl < a.ppb && plane < nplanes && ox < a.Wo;
+    const T* dyp = reinterpret_cast<const T*>(dy) + (long long)plane * a.Ho * a.Wo + ox;
+    const float* tile = lds + pl * per + col;
 
     float acc[K * K + 1];
 #pragma unroll
     for (int i = 0; i < K * K + 1; ++i) acc[i] = 0.f;
-    if (live) {
-        const T* dyp = reinterpret_cast<const T*>(dy) + (long long)plane * a.Ho * a.Wo + ox;
-        const float* tile = lds + pl * per + col;
+
+    for (int ty = 0; ty < a.tilesY; ++ty) {
+        const int oy0 = ty * a.TH;
+        __syncthreads();                       // previous tile fully consumed
+        dw_stage<T>(a, lds, pg, ox0, oy0, LW, LH);
+        __syncthreads();
+        if (live) {
+            float g[RPT];
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-            const int oy = oy0 + r0 + i;
-            if (oy >= a.Ho) break;
-            const float g = ld(dyp + (long long)oy * a.Wo);
-            acc[K * K] += g;
+            for (int i = 0; i < RPT; ++i) {
+                const int oy = oy0 + r0 + i;
+                g[i] = oy < a.Ho ? ld(dyp + (long long)oy * a.Wo) : 0.f;
+                acc[K * K] += g[i];
+            }
 #pragma unroll
-            for (int ky = 0; ky < K; ++ky)
+            for (int j = 0; j < RPT + K - 1; ++j) {
+                float row[K];
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx)
-                    acc[ky * K + kx] = fmaf(g, tile[(r0 + i + ky) * LW + kx], acc[ky * K + kx]);
+                for (int kx = 0; kx < K; ++kx) row[kx] = tile[(r0 + j) * LW + kx];
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    const int o = j - ky;
+                    if (o >= 0 && o < RPT) {
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx) acc[ky * K + kx] = fmaf(g[o], row[kx], acc[ky * K + kx]);
+                    }
+                }
+            }
         }
     }
     // Reduce over the lanes that belong to the same plane: first within the wave (lanes
@@ -180,7 +201,7 @@ __global__ __launch_bounds__(NT) void dw_bwd_w(DwArgs a, const void* dy, float* 
         if (col == 0) red[(wave * a.ppw + psub) * (K * K + 1) + i] = v;
     }
     __syncthreads();
-    // Planes of this block: pl in [0, ppb); plane pl lives in waves {pgrp*spp .. pgrp*spp+spp-1}, slot psub.
+    // Plane p of this block lives in waves {grp*spp .. grp*spp+spp-1}, slot sub.
     for (int i = threadIdx.x; i < a.ppb * (K * K + 1); i += NT) {
         const int p = i / (K * K + 1), k = i - p * (K * K + 1);
         const int plane_g = pg * a.ppb + p;
@@ -188,7 +209,7 @@ __global__ __launch_bounds__(NT) void dw_bwd_w(DwArgs a, const void* dy, float* 
         const int grp = p / a.ppw, sub = p - grp * a.ppw;
         float s = 0.f;
         for (int st_ = 0; st_ < a.spp; ++st_) s += red[((grp * a.spp + st_) * a.ppw + sub) * (K * K + 1) + k];
-        partial[((long long)tile_id * nplanes + plane_g) * (K * K + 1) + k] = s;
+        partial[((long long)tx * nplanes + plane_g) * (K * K + 1) + k] = s;
     }
 }
 
@@ -196,12 +217,14 @@ template <class T, int K>
 int dw_launch(DwArgs& a, int mode, const void* dy, float* partial, hipStream_t st) {
     const size_t lds = sizeof(float) * (size_t)a.ppb * (a.TW + K - 1) * (a.TH + K - 1);
     const size_t red = sizeof(float) * 4 * a.ppw * (K * K + 1);
-    const long long blocks = (long long)a.tilesX * a.tilesY * a.planeGroups;
-    if (mode == 0)
+    if (mode == 0) {
+        const long long blocks = (long long)a.tilesX * a.tilesY * a.planeGroups;
         hipLaunchKernelGGL((dw_fwd<T, K>), dim3((unsigned)blocks), dim3(NT), lds, st, a);
-    else
+    } else {
+        const long long blocks = (long long)a.tilesX * a.planeGroups;
         hipLaunchKernelGGL((dw_bwd_w<T, K>), dim3((unsigned)blocks), dim3(NT), lds > red ? lds : red, st, a, dy,
                            partial);
+    }
     return launch_status();
 }
 
@@ -615,7 +638,7 @@ __global__ __launch_bounds__(NT) void lsr_bwd(RowArgs a) {
 }
 
 // -------------------------------------------------------------------------------------------
-// PixelShuffle(r) + replicate pad + separable normalised blur (taps k, 1 <= K <= 7).
+// PixelShuffle(r) + replicate pad + separable normalised blur (taps k, 1 <= K <= 8).
 
 struct BlurArgs {
     const void* x;     // [B, C*r*r, H, W]  (pre-shuffle); r == 1: plain blur of [B, C, H, W]
@@ -624,41 +647,21 @@ struct BlurArgs {
     float k[8];        // normalised 1-D taps (2-D kernel = k x k)
 };
 
-template <class T>
-__device__ __forceinline__ float shuffled(const BlurArgs& a, const T* xb, int c, int Y, int X) {
-    // xb points at sample b; (Y, X) already clamped into [0, H*r) x [0, W*r).
-    const int sy = Y % a.r, sx = X % a.r;
-    const int cin = c * a.r * a.r + sy * a.r + sx;
-    return ld(xb + ((long long)cin * a.H + Y / a.r) * a.W + X / a.r);
-}
+// Tiled forms: one workgroup = one (sample, channel) plane x a 64 x 32 tile of the
+// (shuffled, full-resolution) image. The separable blur runs as a row pass then a column
+// pass through LDS, so every input element is read from HBM once per tile (plus halo).
+constexpr int BTW = 64, BTH = 32;
 
 template <class T>
-__global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
-    const int Ho = a.H * a.r, Wo = a.W * a.r;
-    const long long total = (long long)a.B * a.C * Ho * Wo;
-    for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-        long long t = i;
-        const int X = (int)(t % Wo); t /= Wo;
-        const int Y = (int)(t % Ho); t /= Ho;
-        const int c = (int)(t % a.C);
-        const int b = (int)(t / a.C);
-        const T* xb = reinterpret_cast<const T*>(a.x) + (long long)b * a.C * a.r * a.r * a.H * a.W;
-        float acc = 0.f;
-        for (int ty = 0; ty < a.K; ++ty) {
-            const int yy = min(max(Y + ty - a.pad0, 0), Ho - 1);
-            float rowacc = 0.f;
-            for (int tx = 0; tx < a.K; ++tx) {
-                const int xx = min(max(X + tx - a.pad0, 0), Wo - 1);
-                rowacc = fmaf(a.k[tx], shuffled(a, xb, c, yy, xx), rowacc);
-            }
-            acc = fmaf(a.k[ty], rowacc, acc);
-        }
-        st(reinterpret_cast<T*>(a.y) + i, acc);
-    }
+__device__ __forceinline__ float shuffled_at(const BlurArgs& a, const T* xb, int c, int Y, int X) {
+    const int r = a.r;
+    if (r == 1) return ld(xb + ((long long)c * a.H + Y) * a.W + X);
+    const int sy = Y % r, sx = X % r;
+    return ld(xb + ((long long)(c * r * r + sy * r + sx) * a.H + Y / r) * a.W + X / r);
 }
 
 // Weight with which output coordinate o contributes to source coordinate s along one axis:
-// sum over taps t with clamp(o + t - pad, 0, n-1) == s of k[t].
+// sum over taps t with clamp(o + t - pad0, 0, n-1) == s of k[t].
 __device__ __forceinline__ float axis_weight(const BlurArgs& a, int o, int s, int n) {
     float w = 0.f;
     for (int t = 0; t < a.K; ++t) {
@@ -668,47 +671,107 @@ __device__ __forceinline__ float axis_weight(const BlurArgs& a, int o, int s, in
     return w;
 }
 
-// d_x at pre-shuffle element (cin, iy, ix) = d_S(Y, X) with Y = iy*r + sy, X = ix*r + sx,
-// d_S(Y, X) = sum_{y, x} wy(y, Y) wx(x, X) dout(y, x), y in [Y - (K-1-pad0), Y + pad0] (clipped).
 template <class T>
-__global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
+__global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
+    __shared__ float sA[(BTH + 7) * (BTW + 7)];
+    __shared__ float sB[(BTH + 7) * BTW];
     const int Ho = a.H * a.r, Wo = a.W * a.r;
-    const int C_in = a.C * a.r * a.r;
-    const long long total = (long long)a.B * C_in * a.H * a.W;
-    const int reach_lo = a.K - 1 - a.pad0, reach_hi = a.pad0;
-    for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-        long long t = i;
-        const int ix = (int)(t % a.W); t /= a.W;
-        const int iy = (int)(t % a.H); t /= a.H;
-        const int cin = (int)(t % C_in);
-        const int b = (int)(t / C_in);
-        const int c = cin / (a.r * a.r), sub = cin % (a.r * a.r);
-        const int Y = iy * a.r + sub / a.r, X = ix * a.r + sub % a.r;
-        const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
-        // Output y reads source clamp(y + t - pad0): interior sources are reached from
-        // y in [Y - reach_lo, Y + reach_hi]; the replicate-clamped edge reads fall in the
-        // same window, so clipping it to the image covers the folded edge terms too.
-        const int ylo = max(Y - reach_lo, 0), yhi = min(Y + reach_hi, Ho - 1);
-        const int xlo = max(X - reach_lo, 0), xhi = min(X + reach_hi, Wo - 1);
+    const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
+    int bid = blockIdx.x;
+    const int tx = bid % tilesX; bid /= tilesX;
+    const int ty = bid % tilesY; bid /= tilesY;
+    const int c = bid % a.C, b = bid / a.C;
+    const int X0 = tx * BTW, Y0 = ty * BTH;
+    const int K = a.K, LW = BTW + K - 1, LH = BTH + K - 1;
+    const T* xb = reinterpret_cast<const T*>(a.x) + (long long)b * a.C * a.r * a.r * a.H * a.W;
+    // Stage the replicate-clamped source window.
+    for (int i = threadIdx.x; i < LH * LW; i += NT) {
+        const int ry = i / LW, rx = i - ry * LW;
+        const int Y = min(max(Y0 + ry - a.pad0, 0), Ho - 1);
+        const int X = min(max(X0 + rx - a.pad0, 0), Wo - 1);
+        sA[i] = shuffled_at(a, xb, c, Y, X);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int r = wave; r < LH; r += 4) {
         float acc = 0.f;
-        for (int y = ylo; y <= yhi; ++y) {
-            const float wy = axis_weight(a, y, Y, Ho);
-            if (wy == 0.f) continue;
-            float racc = 0.f;
-            for (int x = xlo; x <= xhi; ++x) {
-                const float wx = axis_weight(a, x, X, Wo);
-                if (wx != 0.f) racc = fmaf(wx, ld(gp + (long long)y * Wo + x), racc);
-            }
-            acc = fmaf(wy, racc, acc);
-        }
-        st(reinterpret_cast<T*>(dx) + i, acc);
+        for (int t = 0; t < K; ++t) acc = fmaf(a.k[t], sA[r * LW + lane + t], acc);
+        sB[r * BTW + lane] = acc;
+    }
+    __syncthreads();
+    const int X = X0 + lane;
+    if (X >= Wo) return;
+    T* yp = reinterpret_cast<T*>(a.y) + ((long long)b * a.C + c) * Ho * Wo + X;
+    for (int i = 0; i < BTH / 4; ++i) {
+        const int ry = wave * (BTH / 4) + i;
+        const int Y = Y0 + ry;
+        if (Y >= Ho) break;
+        float acc = 0.f;
+        for (int t = 0; t < K; ++t) acc = fmaf(a.k[t], sB[(ry + t) * BTW + lane], acc);
+        st(yp + (long long)Y * Wo, acc);
     }
 }
 
-int grid_for(long long total) {
-    long long b = (total + NT - 1) / NT;
-    if (b > 16384) b = 16384;
-    return (int)(b < 1 ? 1 : b);
+// Adjoint: dS(Y, X) = sum_{y, x} wy(y, Y) wx(x, X) dout(y, x) with y in
+// [Y - (K-1-pad0), Y + pad0] (clipped); interior weights are k[K-1-j], rows/columns within
+// K of the border use the exact replicate-folded weights. dS is written straight into the
+// pre-shuffle layout of dx.
+template <class T>
+__global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
+    __shared__ float sA[(BTH + 7) * (BTW + 7)];
+    __shared__ float sB[(BTH + 7) * BTW];
+    const int Ho = a.H * a.r, Wo = a.W * a.r;
+    const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
+    int bid = blockIdx.x;
+    const int tx = bid % tilesX; bid /= tilesX;
+    const int ty = bid % tilesY; bid /= tilesY;
+    const int c = bid % a.C, b = bid / a.C;
+    const int X0 = tx * BTW, Y0 = ty * BTH;
+    const int K = a.K, LW = BTW + K - 1, LH = BTH + K - 1;
+    const int rlo = K - 1 - a.pad0;
+    const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
+    for (int i = threadIdx.x; i < LH * LW; i += NT) {
+        const int ry = i / LW, rx = i - ry * LW;
+        const int y = Y0 + ry - rlo, x = X0 + rx - rlo;
+        sA[i] = (y >= 0 && y < Ho && x >= 0 && x < Wo) ? ld(gp + (long long)y * Wo + x) : 0.f;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int X = X0 + lane;
+    const bool xedge = X < K || X >= Wo - K;
+    for (int r = wave; r < LH; r += 4) {
+        float acc = 0.f;
+        if (!xedge) {
+            for (int j = 0; j < K; ++j) acc = fmaf(a.k[K - 1 - j], sA[r * LW + lane + j], acc);
+        } else if (X < Wo) {
+            for (int j = 0; j < K; ++j) {
+                const int x = X - rlo + j;
+                if (x >= 0 && x < Wo) acc = fmaf(axis_weight(a, x, X, Wo), sA[r * LW + lane + j], acc);
+            }
+        }
+        sB[r * BTW + lane] = acc;
+    }
+    __syncthreads();
+    if (X >= Wo) return;
+    const int r = a.r;
+    T* dxb = reinterpret_cast<T*>(dx) + (long long)b * a.C * r * r * a.H * a.W;
+    for (int i = 0; i < BTH / 4; ++i) {
+        const int ry = wave * (BTH / 4) + i;
+        const int Y = Y0 + ry;
+        if (Y >= Ho) break;
+        float acc = 0.f;
+        if (Y >= K && Y < Ho - K) {
+            for (int j = 0; j < K; ++j) acc = fmaf(a.k[K - 1 - j], sB[(ry + j) * BTW + lane], acc);
+        } else {
+            for (int j = 0; j < K; ++j) {
+                const int y = Y - rlo + j;
+                if (y >= 0 && y < Ho) acc = fmaf(axis_weight(a, y, Y, Ho), sB[(ry + j) * BTW + lane], acc);
+            }
+        }
+        const long long off = r == 1 ? ((long long)c * a.H + Y) * a.W + X
+                                     : ((long long)(c * r * r + (Y % r) * r + X % r) * a.H + Y / r) * a.W + X / r;
+        st(dxb + off, acc);
+    }
 }
 
 }  // namespace
@@ -739,7 +802,7 @@ extern "C" int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, 
     a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
     dw_plan(a);
-    return a.tilesX * a.tilesY;
+    return a.tilesX;
 }
 
 extern "C" int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int dtype, int B, int C, int H,
@@ -883,11 +946,11 @@ extern "C" int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, i
     a.x = x; a.y = y; a.B = B; a.C = C; a.H = H; a.W = W; a.r = r; a.K = K; a.pad0 = (K - 1) / 2;
     for (int i = 0; i < K; ++i) a.k[i] = taps[i];
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int grid = grid_for((long long)B * C * H * r * W * r);
+    const long long grid = (long long)((W * r + BTW - 1) / BTW) * ((H * r + BTH - 1) / BTH) * B * C;
     switch (dtype) {
-    case VFM_F32: hipLaunchKernelGGL((blur_fwd<float>), dim3(grid), dim3(NT), 0, st, a); break;
-    case VFM_BF16: hipLaunchKernelGGL((blur_fwd<__hip_bfloat16>), dim3(grid), dim3(NT), 0, st, a); break;
-    case VFM_F16: hipLaunchKernelGGL((blur_fwd<__half>), dim3(grid), dim3(NT), 0, st, a); break;
+    case VFM_F32: hipLaunchKernelGGL((blur_fwd<float>), dim3((unsigned)grid), dim3(NT), 0, st, a); break;
+    case VFM_BF16: hipLaunchKernelGGL((blur_fwd<__hip_bfloat16>), dim3((unsigned)grid), dim3(NT), 0, st, a); break;
+    case VFM_F16: hipLaunchKernelGGL((blur_fwd<__half>), dim3((unsigned)grid), dim3(NT), 0, st, a); break;
     default: return VFM_ERR_ARGS;
     }
     return launch_status();
@@ -900,11 +963,11 @@ extern "C" int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* tap
     a.B = B; a.C = C; a.H = H; a.W = W; a.r = r; a.K = K; a.pad0 = (K - 1) / 2;
     for (int i = 0; i < K; ++i) a.k[i] = taps[i];
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int grid = grid_for((long long)B * C * r * r * H * W);
+    const long long grid = (long long)((W * r + BTW - 1) / BTW) * ((H * r + BTH - 1) / BTH) * B * C;
     switch (dtype) {
-    case VFM_F32: hipLaunchKernelGGL((blur_bwd<float>), dim3(grid), dim3(NT), 0, st, a, dout, dx); break;
-    case VFM_BF16: hipLaunchKernelGGL((blur_bwd<__hip_bfloat16>), dim3(grid), dim3(NT), 0, st, a, dout, dx); break;
-    case VFM_F16: hipLaunchKernelGGL((blur_bwd<__half>), dim3(grid), dim3(NT), 0, st, a, dout, dx); break;
+    case VFM_F32: hipLaunchKernelGGL((blur_bwd<float>), dim3((unsigned)grid), dim3(NT), 0, st, a, dout, dx); break;
+    case VFM_BF16: hipLaunchKernelGGL((blur_bwd<__hip_bfloat16>), dim3((unsigned)grid), dim3(NT), 0, st, a, dout, dx); break;
+    case VFM_F16: hipLaunchKernelGGL((blur_bwd<__half>), dim3((unsigned)grid), dim3(NT), 0, st, a, dout, dx); break;
     default: return VFM_ERR_ARGS;
     }
     return launch_status();

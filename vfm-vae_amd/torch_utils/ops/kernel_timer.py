@@ -68,4 +68,6 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops):
             "frac": round(achieved / peak, 4), "traffic": None, "kernel": name, "launches": r["launches"],
             "avg_us": round(r["total_ms"] * 1e3 / r["launches"], 2),
             "bytes_per_launch": int(r["bytes"] / r["launches"]),
-            "all_kernels_ms": {k: round(v["total_ms"], 3) for k, v in s.items()}}
+            "all_kernels": {k: {"ms": round(v["total_ms"], 3), "launches": v["launches"],
+                                "GBps": round(v["bytes"] / max(v["total_ms"], 1e-9) / 1e6, 1)}
+                            for k, v in sorted(s.items(), key=lambda kv: -kv[1]["total_ms"])}}
