@@ -57,8 +57,11 @@ def _run(fn_hip, fn_ref, inputs, dt, names, out_grad_seed=0):
             assert _rel(a.grad.float(), b.grad) < 4 * tol, (a.shape, _rel(a.grad.float(), b.grad))
 
 
+# Row-streaming kernel: same-size odd K, W in {16..256} a power-of-two multiple of 4;
+# LDS-tile kernel: everything else (ragged widths, narrow planes).
 DW_CASES = [(2, 8, 16, 16, 3), (2, 8, 16, 16, 5), (2, 6, 16, 16, 7), (1, 4, 64, 70, 3), (2, 5, 13, 9, 3),
-            (1, 3, 33, 130, 7), (3, 2, 4, 4, 3), (1, 2, 1, 5, 3)]
+            (1, 3, 33, 130, 7), (3, 2, 4, 4, 3), (1, 2, 1, 5, 3), (2, 3, 37, 128, 7), (1, 2, 20, 256, 5),
+            (2, 4, 9, 32, 3), (1, 3, 300, 64, 7), (2, 2, 256, 256, 7)]
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
@@ -151,7 +154,7 @@ def test_layer_scale_residual(shape, dt_y, dt_x):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("taps", [[1, 2, 1], [1, 3, 3, 1], [1, 4, 6, 4, 1]])
 @pytest.mark.parametrize("shape,r", [((2, 16, 8, 8), 2), ((1, 12, 5, 7), 2), ((2, 4, 9, 6), 1), ((1, 4, 1, 1), 2),
-                                     ((1, 2, 16, 32), 1)])
+                                     ((1, 2, 16, 32), 1), ((1, 8, 40, 70), 2), ((1, 3, 70, 130), 1)])
 def test_shuffle_blur(shape, r, taps, dt):
     ops, _ = _ops()
     torch.manual_seed(7)
@@ -189,3 +192,27 @@ def test_convnext_layer_hip_matches_torch_formulation():
     assert grads[0].keys() == grads[1].keys()
     for n in grads[0]:
         assert _rel(grads[0][n], grads[1][n]) < 1e-4, n
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 32, 256), (3, 24, 40, 64), (1, 8, 3, 5)])
+def test_pointwise_gemm(shape, dt):
+    """Copy-free 1x1 conv GEMM (stride-0 batch bmm) vs torch.matmul in fp32; weight grads fp32."""
+    ops, _ = _ops()
+    B, O, I, P = shape
+    torch.manual_seed(9)
+    w = (torch.randn(O, I) / I ** 0.5).to(DEV).requires_grad_(True)
+    x = torch.randn(B, I, P).to(dt).to(DEV).requires_grad_(True)
+    y = ops.pointwise(w, x)
+    assert y.dtype == dt and y.is_contiguous()
+    g = torch.randn_like(y)
+    y.backward(g)
+    assert w.grad.dtype == torch.float32 and x.grad.is_contiguous()
+    w2 = w.detach().clone().requires_grad_(True)
+    x2 = x.detach().float().requires_grad_(True)
+    y2 = torch.matmul(w2, x2)
+    y2.backward(g.float())
+    tol = _tol(dt)
+    assert _rel(y.float(), y2) < tol
+    assert _rel(w.grad, w2.grad) < 4 * tol
+    assert _rel(x.grad.float(), x2.grad) < 4 * tol

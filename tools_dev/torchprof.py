@@ -36,13 +36,23 @@ def main():
         step([pool[i % len(pool)].float() / 255.], [labels], i * args.batch)
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=False) as prof:
+    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True) as prof:
         step([pool[0].float() / 255.], [labels], 2 * args.batch)
         torch.cuda.synchronize()
     sort = "self_cuda_time_total"
     t1 = prof.key_averages().table(sort_by=sort, row_limit=args.rows, max_name_column_width=60)
     t2 = prof.key_averages(group_by_input_shape=True).table(sort_by=sort, row_limit=args.rows,
                                                             max_name_column_width=50, max_shapes_column_width=90)
+    t3 = prof.key_averages(group_by_stack_n=8).table(sort_by=sort, row_limit=args.rows, max_name_column_width=40)
+    open(os.path.join(args.out, "ops_stack.txt"), "w").write(t3)
+    # copies only, with their stacks
+    evs = [e for e in prof.key_averages(group_by_input_shape=True, group_by_stack_n=10) if e.key in ("aten::copy_", "aten::clone", "aten::contiguous")]
+    evs.sort(key=lambda e: -e.self_device_time_total)
+    with open(os.path.join(args.out, "copies.txt"), "w") as f:
+        for e in evs[:40]:
+            f.write(f"{e.key} calls={e.count} self_dev_ms={e.self_device_time_total / 1e3:.2f} shapes={e.input_shapes}\n")
+            for fr in e.stack:
+                f.write(f"    {fr}\n")
     open(os.path.join(args.out, "ops.txt"), "w").write(t1)
     open(os.path.join(args.out, "ops_shapes.txt"), "w").write(t2)
     print(t1[:12000])

@@ -259,6 +259,250 @@ int dw_dispatch(DwArgs& a, int K, int mode, const void* dy, float* partial, hipS
 }
 
 // -------------------------------------------------------------------------------------------
+// Row-streaming depthwise conv for "same" convolutions (odd K, pad = (K-1)/2) on planes
+// 16..256 wide. One wave owns one plane (so the K*K weights are wave-uniform scalars) and
+// R = 64 / L row bands of it, L = W/4 lanes per image row, 4 adjacent columns per lane.
+// Each lane streams its band top to bottom: one 4-element vector load per input row, the
+// K-1 halo columns from the neighbouring lanes by cross-lane shuffles (a group always spans
+// a full image row, so the group edge is the zero-padded image border), and K rotating
+// output-row accumulators. No LDS, every input byte is loaded ~once (band halo only).
+
+struct DwRowArgs {
+    const void* x;
+    const float* w;       // [C, K, K]
+    const float* bias;    // [C] or null
+    const float* noise;   // [H, W] or null
+    void* y;
+    const void* dy;       // weight-gradient mode
+    float* partial;       // [wpp, B*C, K*K+1]
+    int B, C, H, W;
+    int L, R;             // lanes per row, row groups per wave
+    int BH;               // band height
+    int wpp;              // waves per plane
+};
+
+template <class T>
+__device__ __forceinline__ void ld4(const T* p, float* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = ld(p + i);
+}
+template <>
+__device__ __forceinline__ void ld4<__hip_bfloat16>(const __hip_bfloat16* p, float* v) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16);
+    v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16);
+    v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ void ld4<__half>(const __half* p, float* v) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    const __half2* h = reinterpret_cast<const __half2*>(&u);
+    const float2 a = __half22float2(h[0]), b = __half22float2(h[1]);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+template <>
+__device__ __forceinline__ void ld4<float>(const float* p, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+template <class T>
+__device__ __forceinline__ void st4(T* p, const float* v) {
+    T t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st(&t[i], v[i]);
+    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(t);
+}
+template <>
+__device__ __forceinline__ void st4<float>(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// v[0 .. K+2]: the lane's 4 columns with PAD columns of left and K-1-PAD of right halo.
+template <int K>
+__device__ __forceinline__ void dwr_halo(const float* own, float* v, int q, int L) {
+    constexpr int PAD = (K - 1) / 2;
+#pragma unroll
+    for (int t = 0; t < PAD; ++t) {
+        const float s = __shfl_up(own[4 - PAD + t], 1, L);
+        v[t] = q == 0 ? 0.f : s;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[PAD + c] = own[c];
+#pragma unroll
+    for (int t = 0; t < K - 1 - PAD; ++t) {
+        const float s = __shfl_down(own[t], 1, L);
+        v[PAD + 4 + t] = q == L - 1 ? 0.f : s;
+    }
+}
+
+template <class T, int K>
+__global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
+    constexpr int PAD = (K - 1) / 2;
+    const int wave_g = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+    const int plane = __builtin_amdgcn_readfirstlane(wave_g / a.wpp);
+    const int wv = wave_g - plane * a.wpp;
+    if (plane >= a.B * a.C) return;
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / a.L, q = lane - grp * a.L;
+    const int y0 = (wv * a.R + grp) * a.BH;
+    const int c = __builtin_amdgcn_readfirstlane(plane % a.C);
+    float wk[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + i];
+    const float bias = a.bias ? a.bias[c] : 0.f;
+    const long long poff = (long long)plane * a.H * a.W + 4 * q;
+    const T* xp = reinterpret_cast<const T*>(a.x) + poff;
+    T* yp = reinterpret_cast<T*>(a.y) + poff;
+    const float* np = a.noise ? a.noise + 4 * q : nullptr;
+
+    float acc[K][4];
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) acc[s][c4] = 0.f;
+    const int nrows = a.BH + K - 1;
+    for (int jj0 = 0; jj0 < nrows; jj0 += K) {
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const int jj = jj0 + u;
+            if (jj < nrows) {
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) acc[u][c4] = bias;      // output row jj starts here
+                const int iy = y0 - PAD + jj;
+                float own[4] = {0.f, 0.f, 0.f, 0.f};
+                if (iy >= 0 && iy < a.H) ld4(xp + (long long)iy * a.W, own);
+                float v[K + 3];
+                dwr_halo<K>(own, v, q, a.L);
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    const int sl = (u - ky + K) % K;                    // output row jj - ky
+#pragma unroll
+                    for (int c4 = 0; c4 < 4; ++c4)
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx) acc[sl][c4] = fmaf(v[c4 + kx], wk[ky * K + kx], acc[sl][c4]);
+                }
+                const int ob = jj - (K - 1);                           // completed output row
+                const int oy = y0 + ob;
+                if (ob >= 0 && ob < a.BH && oy < a.H) {
+                    float o[4];
+#pragma unroll
+                    for (int c4 = 0; c4 < 4; ++c4) o[c4] = acc[(u + 1) % K][c4];
+                    if (np) {
+#pragma unroll
+                        for (int c4 = 0; c4 < 4; ++c4) o[c4] += np[oy * a.W + c4];
+                    }
+                    st4(yp + (long long)oy * a.W, o);
+                }
+            }
+        }
+    }
+}
+
+// dW[ky][kx] = sum dy[oy][ox] x[oy + ky - PAD][ox + kx - PAD], db = sum dy, per plane;
+// the wave's total goes to partial[wv][plane][:], summed by the host in a fixed order.
+template <class T, int K>
+__global__ __launch_bounds__(NT) void dwr_bwd_w(DwRowArgs a) {
+    constexpr int PAD = (K - 1) / 2;
+    const int wave_g = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+    const int plane = __builtin_amdgcn_readfirstlane(wave_g / a.wpp);
+    const int wv = wave_g - plane * a.wpp;
+    if (plane >= a.B * a.C) return;
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / a.L, q = lane - grp * a.L;
+    const int y0 = (wv * a.R + grp) * a.BH;
+    const long long poff = (long long)plane * a.H * a.W + 4 * q;
+    const T* xp = reinterpret_cast<const T*>(a.x) + poff;
+    const T* gp = reinterpret_cast<const T*>(a.dy) + poff;
+
+    float acc[K * K + 1];
+#pragma unroll
+    for (int i = 0; i < K * K + 1; ++i) acc[i] = 0.f;
+    float gw[K][4];                                   // dy rows jj-K+1 .. jj (rotating)
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) gw[s][c4] = 0.f;
+    const int nrows = a.BH + K - 1;
+    for (int jj0 = 0; jj0 < nrows; jj0 += K) {
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const int jj = jj0 + u;
+            if (jj < nrows) {
+                const int oy = y0 + jj;
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) gw[u][c4] = 0.f;
+                if (jj < a.BH && oy < a.H) ld4(gp + (long long)oy * a.W, gw[u]);
+                acc[K * K] += (gw[u][0] + gw[u][1]) + (gw[u][2] + gw[u][3]);
+                const int iy = y0 - PAD + jj;
+                float own[4] = {0.f, 0.f, 0.f, 0.f};
+                if (iy >= 0 && iy < a.H) ld4(xp + (long long)iy * a.W, own);
+                float v[K + 3];
+                dwr_halo<K>(own, v, q, a.L);
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    const int sl = (u - ky + K) % K;                    // dy row jj - ky
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) {
+                        float t = acc[ky * K + kx];
+#pragma unroll
+                        for (int c4 = 0; c4 < 4; ++c4) t = fmaf(gw[sl][c4], v[c4 + kx], t);
+                        acc[ky * K + kx] = t;
+                    }
+                }
+            }
+        }
+    }
+    const int nplanes = a.B * a.C;
+#pragma unroll
+    for (int i = 0; i < K * K + 1; ++i) {
+        float t = acc[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off);
+        if (lane == 0) a.partial[((long long)wv * nplanes + plane) * (K * K + 1) + i] = t;
+    }
+}
+
+// Row-streaming plan; returns false when the shape is not covered (caller uses dw_fwd / dw_bwd_w).
+bool dwr_plan(DwRowArgs& a, int K, int pad) {
+    if (K % 2 == 0 || pad != (K - 1) / 2 || K > 7) return false;
+    if (a.W < 16 || a.W > 256 || a.W % 4) return false;
+    const int L = a.W / 4;
+    if (L & (L - 1)) return false;
+    a.L = L;
+    a.R = 64 / L;
+    const long long planes = (long long)a.B * a.C;
+    int BH = 64;
+    for (;;) {
+        const int bands = (a.H + BH - 1) / BH;
+        a.wpp = (bands + a.R - 1) / a.R;
+        if (BH <= 8 || planes * a.wpp >= 16384) break;
+        BH /= 2;
+    }
+    a.BH = BH;
+    return true;
+}
+
+template <class T>
+int dwr_launch(DwRowArgs& a, int K, int mode, hipStream_t st) {
+    const long long waves = (long long)a.B * a.C * a.wpp;
+    const dim3 grid((unsigned)((waves + 3) / 4));
+#define DWR_CASE(KK)                                                                   \
+    case KK:                                                                           \
+        if (mode == 0) hipLaunchKernelGGL((dwr_fwd<T, KK>), grid, dim3(NT), 0, st, a); \
+        else hipLaunchKernelGGL((dwr_bwd_w<T, KK>), grid, dim3(NT), 0, st, a);         \
+        break;
+    switch (K) {
+        DWR_CASE(3)
+        DWR_CASE(5)
+        DWR_CASE(7)
+    default: return VFM_NO_KERNEL;
+    }
+#undef DWR_CASE
+    return launch_status();
+}
+
+// -------------------------------------------------------------------------------------------
 // Block reductions.
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -786,8 +1030,18 @@ extern "C" int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias
     a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
     a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
-    dw_plan(a);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    DwRowArgs r{};
+    r.x = x; r.w = w; r.bias = bias; r.noise = noise; r.y = y; r.B = B; r.C = C; r.H = H; r.W = W;
+    if (dwr_plan(r, K, pad)) {
+        switch (dtype) {
+        case VFM_F32: return dwr_launch<float>(r, K, 0, st);
+        case VFM_F16: return dwr_launch<__half>(r, K, 0, st);
+        case VFM_BF16: return dwr_launch<__hip_bfloat16>(r, K, 0, st);
+        }
+        return VFM_ERR_ARGS;
+    }
+    dw_plan(a);
     switch (dtype) {
     case VFM_F32: return dw_dispatch<float>(a, K, 0, nullptr, nullptr, st);
     case VFM_F16: return dw_dispatch<__half>(a, K, 0, nullptr, nullptr, st);
@@ -801,6 +1055,9 @@ extern "C" int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, 
     a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
     a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
+    DwRowArgs r{};
+    r.B = B; r.C = C; r.H = H; r.W = W;
+    if (dwr_plan(r, K, pad)) return r.wpp;
     dw_plan(a);
     return a.tilesX;
 }
@@ -812,8 +1069,18 @@ extern "C" int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* par
     a.x = x; a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
     a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
-    dw_plan(a);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    DwRowArgs r{};
+    r.x = x; r.dy = dy; r.partial = partial; r.B = B; r.C = C; r.H = H; r.W = W;
+    if (dwr_plan(r, K, pad)) {
+        switch (dtype) {
+        case VFM_F32: return dwr_launch<float>(r, K, 1, st);
+        case VFM_F16: return dwr_launch<__half>(r, K, 1, st);
+        case VFM_BF16: return dwr_launch<__hip_bfloat16>(r, K, 1, st);
+        }
+        return VFM_ERR_ARGS;
+    }
+    dw_plan(a);
     switch (dtype) {
     case VFM_F32: return dw_dispatch<float>(a, K, 1, dy, partial, st);
     case VFM_F16: return dw_dispatch<__half>(a, K, 1, dy, partial, st);

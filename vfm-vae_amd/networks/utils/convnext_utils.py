@@ -31,7 +31,7 @@ def modulated_pointwise_conv2d(x, weight, style, bias=None, demodulate=True):
     B, I, H, W = x.shape
     w2 = weight.reshape(weight.shape[0], I)
     xm = x * style.to(x.dtype)[:, :, None, None]
-    y = torch.matmul(w2.to(x.dtype), xm.reshape(B, I, H * W))
+    y = decoder_ops.pointwise(w2, xm.reshape(B, I, H * W))
     if demodulate:
         y = y * decoder_ops.demod_coefficients(w2, style).to(y.dtype)[:, :, None]
     y = y.reshape(B, -1, H, W)
@@ -98,10 +98,10 @@ class ConvNeXtSynthesisLayer(nn.Module):
         m = decoder_ops.group_norm(d, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps,
                                    out_dtype=cdt, style=style)                 # GN(d) * s_b
         w1 = self.pwconv1.weight.reshape(4 * C, C)
-        h = torch.matmul(w1.to(cdt), m.reshape(B, C, H * W))                  # [B, 4C, HW]
+        h = decoder_ops.pointwise(w1, m.reshape(B, C, H * W))                    # [B, 4C, HW]
         dcoef = decoder_ops.demod_coefficients(w1, style) if self.pwconv1.demodulate else None
         g = decoder_ops.scale_bias_gelu(h, dcoef, self.pwconv1.bias.reshape(-1))
-        y = torch.matmul(self.pwconv2.weight.reshape(C, 4 * C).to(cdt), g)     # [B, C, HW]
+        y = decoder_ops.pointwise(self.pwconv2.weight.reshape(C, 4 * C), g)     # [B, C, HW]
         gamma = self.gamma.reshape(-1) if self.gamma is not None else None
         out = decoder_ops.layer_scale_residual(y, self.pwconv2.bias, gamma, x_in.reshape(B, C, H * W))
         return out.reshape(B, C, H, W)
@@ -127,7 +127,7 @@ class ConvNeXtToRGBLayer(nn.Module):
         style = self.affine(w) * self.weight_gain                              # [B, C]
         if self.kernel_size == 1:
             xm = x * style.to(x.dtype)[:, :, None, None]
-            y = torch.matmul(self.weight.reshape(self.out_channels, C).to(x.dtype), xm.reshape(B, C, H * W))
+            y = decoder_ops.pointwise(self.weight.reshape(self.out_channels, C), xm.reshape(B, C, H * W))
             y = y.reshape(B, self.out_channels, H, W)
         else:
             w_mod = (self.weight[None] * style.reshape(B, 1, -1, 1, 1)).reshape(B * self.out_channels, C,
@@ -186,7 +186,7 @@ class SeparableUpsampleWithFixedBlur(nn.Module):
             x = x.to(cdt)
         x = decoder_ops.dwconv2d(x, self.depthwise.weight, None, 1)
         B, C, H, W = x.shape
-        x = torch.matmul(self.pointwise.weight.reshape(-1, C).to(cdt), x.reshape(B, C, H * W))
+        x = decoder_ops.pointwise(self.pointwise.weight.reshape(-1, C), x.reshape(B, C, H * W))
         x = x.reshape(B, -1, H, W)
         if self.pre_normalize:
             if self.use_gaussian_blur:

@@ -10,6 +10,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from torch_utils.ops import decoder_ops
+
 
 def exists(v):
     return v is not None
@@ -44,8 +46,8 @@ class RMSNorm(nn.Module):
 
 def _pointwise(conv: nn.Conv2d, x3):
     """1x1 conv on a [B, C, P] view as a GEMM."""
-    w = conv.weight.reshape(conv.out_channels, conv.in_channels).to(x3.dtype)
-    y = torch.matmul(w, x3)
+    w = conv.weight.reshape(conv.out_channels, conv.in_channels)
+    y = decoder_ops.pointwise(w, x3)
     if conv.bias is not None:
         y = y + conv.bias.to(y.dtype)[None, :, None]
     return y
@@ -70,7 +72,7 @@ class SelfAttention(nn.Module):
         h, d = self.heads, self.dim_head
         x = self.norm(fmap).reshape(B, C, H * W)
         wqkv = torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], 0).reshape(3 * h * d, C)
-        qkv = torch.matmul(wqkv.to(x.dtype), x)                                # [B, 3hd, P]
+        qkv = decoder_ops.pointwise(wqkv, x)                                   # [B, 3hd, P]
         q, k, v = qkv.reshape(B, 3, h, d, H * W).permute(1, 0, 2, 4, 3).unbind(0)  # [B, h, P, d]
         nk, nv = (t.to(q.dtype)[None, :, None, :].expand(B, h, 1, d) for t in self.null_kv.unbind(0))
         k = torch.cat([nk, k], dim=2)

@@ -68,6 +68,45 @@ def supported(op, x, **kw):
 
 
 # ---------------------------------------------------------------------------
+# 1x1 conv as a stride-0-batch GEMM (hipBLASLt through torch.bmm), no layout copies.
+
+
+class _Pointwise(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, w, x):
+        x = x.contiguous()
+        B, I, P = x.shape
+        O = w.shape[0]
+        wc = w.detach().to(x.dtype)
+        ctx.save_for_backward(wc, x)
+        ctx.wdt = w.dtype
+        return torch.bmm(wc.expand(B, O, I), x)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        wc, x = ctx.saved_tensors
+        B, I, P = x.shape
+        O = wc.shape[0]
+        dy = dy.contiguous()
+        dw = dx = None
+        if ctx.needs_input_grad[0]:
+            # sum_b dy[b] @ x[b]^T with fp32 per-sample products, summed in fp32
+            if dy.dtype != torch.float32:
+                dw = torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32)
+            else:
+                dw = torch.bmm(dy, x.transpose(1, 2))
+            dw = dw.sum(0).to(ctx.wdt)
+        if ctx.needs_input_grad[1]:
+            dx = torch.bmm(wc.t().expand(B, I, O), dy)
+        return dw, dx
+
+
+def pointwise(w, x):
+    return _Pointwise.apply(w, x)
+
+
+# ---------------------------------------------------------------------------
 # Depthwise conv (reference convnext_utils.py:121-124 / :243: nn.Conv2d(groups=C)).
 
 

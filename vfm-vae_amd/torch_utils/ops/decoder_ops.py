@@ -56,6 +56,25 @@ def group_norm(x, num_groups, weight=None, bias=None, eps=1e-5, out_dtype=None, 
 
 
 # ---------------------------------------------------------------------------
+# 1x1 convolution on a flattened plane: y[b] = W @ x[b].
+
+
+def pointwise(weight, x, impl='cuda'):
+    """weight [O, I] (any float dtype; cast to x.dtype for the product), x [B, I, P] -> [B, O, P].
+
+    `torch.matmul(W, x)` folds the batch into the GEMM's M dimension, which for a
+    [B, I, P] operand means a transposing copy in forward and transposed (non-
+    contiguous) results in both passes. On ROCm tensors the product runs as a
+    stride-0-batch bmm (hipBLASLt) whose forward, data-gradient and weight-gradient
+    GEMMs all read and write their operands in place, and the weight gradient is
+    reduced in fp32 and returned in the parameter's dtype (decoder_hip._Pointwise)."""
+    if impl == 'cuda' and x.is_cuda and not _FORCE_REF and x.dim() == 3 and weight.dim() == 2:
+        from . import decoder_hip
+        return decoder_hip.pointwise(weight, x)
+    return torch.matmul(weight.to(x.dtype), x)
+
+
+# ---------------------------------------------------------------------------
 # Depthwise k x k convolution (+bias, + optional additive [H, W] plane).
 
 
