@@ -15,6 +15,7 @@ the timed region) and `cpu_baseline` (the pure-torch CPU restatement of the same
 iteration on the host cores, bounded sample).
 """
 import argparse
+import gc
 import json
 import os
 import random
@@ -49,6 +50,7 @@ def parse_args(argv=None):
     ap.add_argument("--config", default=CONFIG)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
     return ap.parse_args(argv)
@@ -116,6 +118,17 @@ def main(argv=None):
         step([img], [labels], cur_nimg)
 
     step.trace = (lambda m: _log(rank, m)) if args.trace else None
+    if args.trace:
+        _gc_t = {}
+
+        def _gc_cb(phase, info):
+            if phase == "start":
+                _gc_t["t"] = time.perf_counter()
+            elif info.get("generation", 0) >= 1:
+                d = time.perf_counter() - _gc_t.get("t", time.perf_counter())
+                if d > 0.01:
+                    _log(rank, f"gc gen{info['generation']} took {d:.3f}s collected {info.get('collected')}")
+        gc.callbacks.append(_gc_cb)
     cur = 0
     for i in range(args.warmup):
         t1 = time.perf_counter()
@@ -123,7 +136,14 @@ def main(argv=None):
         cur += args.batch * world
         torch.cuda.synchronize()
         _log(rank, f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t1:.2f}s")
-    step.trace = None
+    if not args.trace:
+        step.trace = None
+    # Long-lived objects (modules, optimiser state, autograd caches) leave the collector's
+    # young generations: a full collection over them mid-step stalls the launch stream
+    # for ~100 ms. training_loop.py does the same after its first iteration.
+    gc.collect()
+    if not args.no_gc_freeze:
+        gc.freeze()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -133,6 +153,9 @@ def main(argv=None):
     for i in range(args.steps):
         one(args.warmup + i, cur)
         cur += args.batch * world
+        if args.trace:                      # diagnostics only: per-step wall time (synchronising)
+            torch.cuda.synchronize()
+            _log(rank, f"step {i + 1}: {time.perf_counter() - t0:.3f}s cumulative")
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -140,6 +163,12 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     kernel_timer.enable(False)
     _log(rank, f"timed {args.steps} steps: {dt:.2f}s")
+    if args.trace:
+        ms = torch.cuda.memory_stats(device)
+        _log(rank, "memory: peak alloc {:.1f} GB, reserved {:.1f} GB, alloc retries {}, device allocs {}, frees {}, "
+             "gc counts {}".format(ms.get("allocated_bytes.all.peak", 0) / 2**30, ms.get("reserved_bytes.all.peak", 0) / 2**30,
+                                   ms.get("num_alloc_retries", 0), ms.get("num_device_alloc", 0),
+                                   ms.get("num_device_free", 0), gc.get_count()))
     if world > 1:
         t = torch.tensor([dt], device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

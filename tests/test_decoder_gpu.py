@@ -216,3 +216,25 @@ def test_pointwise_gemm(shape, dt):
     assert _rel(y.float(), y2) < tol
     assert _rel(w.grad, w2.grad) < 4 * tol
     assert _rel(x.grad.float(), x2.grad) < 4 * tol
+
+
+@pytest.mark.parametrize("k", [1, 9])
+def test_spectral_conv1d_gemm_path(k):
+    """Discriminator heads' Conv1d (circular padding) as one batched GEMM vs F.conv1d."""
+    import torch.nn.functional as F
+    from networks.discriminator import SpectralConv1d
+    torch.manual_seed(10)
+    m = SpectralConv1d(24, 16, kernel_size=k, padding=k // 2, padding_mode='circular').to(DEV)
+    m(torch.randn(2, 24, 37, device=DEV))              # one power iteration in train mode
+    m.eval()
+    x = torch.randn(4, 24, 37, device=DEV, requires_grad=True)
+    y = m(x)
+    w = m.weight.detach()
+    x2 = x.detach().clone().requires_grad_(True)
+    xp = F.pad(x2, (k // 2, k // 2), mode='circular') if k > 1 else x2
+    y2 = F.conv1d(xp, w, m.bias)
+    assert _rel(y, y2) < 1e-5
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    assert _rel(x.grad, x2.grad) < 1e-5

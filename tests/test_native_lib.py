@@ -61,10 +61,11 @@ def test_argument_validation_without_gpu():
 
 
 def test_dwconv_partial_tiles_host_query():
-    """vfm_dwconv2d_bwd_weight_tiles is pure host logic: one partial per 64-wide column tile."""
+    """vfm_dwconv2d_bwd_weight_tiles is pure host logic: the number of partial slices the
+    weight-gradient kernel writes (row-streaming path: waves per plane; tile path: column tiles)."""
     import torch_utils.custom_ops as co
     lib = co.get_native()
-    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 256, 256, 7, 3) == 4
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 256, 256, 7, 3) == 32    # bands of 8 rows, 1 per wave
     assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 16, 16, 3, 1) == 1
     assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 5, 130, 3, 1) == 3
     assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 2, 2, 7, 0) == -2      # empty output -> VFM_ERR_ARGS

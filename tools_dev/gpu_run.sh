@@ -19,6 +19,8 @@ for s in "$@"; do
     dtests)  timeout -k 10 600 python -m pytest tests/test_decoder_gpu.py -q -x > $out/dtests.log 2>&1 ;;
     bsmall)  timeout -k 10 900 python bench.py --batch 8 --steps 2 --warmup 2 --trace --no-cpu-baseline > $out/bsmall.log 2>&1 ;;
     btrace)  timeout -k 10 900 python bench.py --steps 3 --warmup 2 --trace --no-cpu-baseline > $out/btrace.log 2>&1 ;;
+    bsteps)  timeout -k 10 900 python bench.py --steps 6 --warmup 2 --trace --no-cpu-baseline > $out/bsteps.log 2>&1 ;;
+    bstepsng) timeout -k 10 900 python bench.py --steps 6 --warmup 2 --trace --no-cpu-baseline --no-gc-freeze > $out/bstepsng.log 2>&1 ;;
     tprof)   timeout -k 10 600 python tools_dev/torchprof.py --out $out/tp > $out/tprof.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

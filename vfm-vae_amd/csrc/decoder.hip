@@ -915,10 +915,11 @@ __device__ __forceinline__ float axis_weight(const BlurArgs& a, int o, int s, in
     return w;
 }
 
-template <class T>
+template <class T, int K>
 __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
-    __shared__ float sA[(BTH + 7) * (BTW + 7)];
-    __shared__ float sB[(BTH + 7) * BTW];
+    constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
+    __shared__ float sA[LH * LW];
+    __shared__ float sB[LH * BTW];
     const int Ho = a.H * a.r, Wo = a.W * a.r;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
@@ -926,33 +927,40 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
     const int ty = bid % tilesY; bid /= tilesY;
     const int c = bid % a.C, b = bid / a.C;
     const int X0 = tx * BTW, Y0 = ty * BTH;
-    const int K = a.K, LW = BTW + K - 1, LH = BTH + K - 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const T* xb = reinterpret_cast<const T*>(a.x) + (long long)b * a.C * a.r * a.r * a.H * a.W;
-    // Stage the replicate-clamped source window.
-    for (int i = threadIdx.x; i < LH * LW; i += NT) {
-        const int ry = i / LW, rx = i - ry * LW;
+    float k[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) k[t] = a.k[t];
+    // Stage the replicate-clamped source window, one row per wave-iteration.
+    for (int ry = wave; ry < LH; ry += 4) {
         const int Y = min(max(Y0 + ry - a.pad0, 0), Ho - 1);
-        const int X = min(max(X0 + rx - a.pad0, 0), Wo - 1);
-        sA[i] = shuffled_at(a, xb, c, Y, X);
+        for (int rx = lane; rx < LW; rx += 64) {
+            const int X = min(max(X0 + rx - a.pad0, 0), Wo - 1);
+            sA[ry * LW + rx] = shuffled_at(a, xb, c, Y, X);
+        }
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int r = wave; r < LH; r += 4) {
         float acc = 0.f;
-        for (int t = 0; t < K; ++t) acc = fmaf(a.k[t], sA[r * LW + lane + t], acc);
+#pragma unroll
+        for (int t = 0; t < K; ++t) acc = fmaf(k[t], sA[r * LW + lane + t], acc);
         sB[r * BTW + lane] = acc;
     }
     __syncthreads();
     const int X = X0 + lane;
     if (X >= Wo) return;
     T* yp = reinterpret_cast<T*>(a.y) + ((long long)b * a.C + c) * Ho * Wo + X;
+#pragma unroll
     for (int i = 0; i < BTH / 4; ++i) {
         const int ry = wave * (BTH / 4) + i;
         const int Y = Y0 + ry;
-        if (Y >= Ho) break;
-        float acc = 0.f;
-        for (int t = 0; t < K; ++t) acc = fmaf(a.k[t], sB[(ry + t) * BTW + lane], acc);
-        st(yp + (long long)Y * Wo, acc);
+        if (Y < Ho) {
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < K; ++t) acc = fmaf(k[t], sB[(ry + t) * BTW + lane], acc);
+            st(yp + (long long)Y * Wo, acc);
+        }
     }
 }
 
@@ -960,10 +968,11 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
 // [Y - (K-1-pad0), Y + pad0] (clipped); interior weights are k[K-1-j], rows/columns within
 // K of the border use the exact replicate-folded weights. dS is written straight into the
 // pre-shuffle layout of dx.
-template <class T>
+template <class T, int K>
 __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
-    __shared__ float sA[(BTH + 7) * (BTW + 7)];
-    __shared__ float sB[(BTH + 7) * BTW];
+    constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
+    __shared__ float sA[LH * LW];
+    __shared__ float sB[LH * BTW];
     const int Ho = a.H * a.r, Wo = a.W * a.r;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
@@ -971,21 +980,24 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
     const int ty = bid % tilesY; bid /= tilesY;
     const int c = bid % a.C, b = bid / a.C;
     const int X0 = tx * BTW, Y0 = ty * BTH;
-    const int K = a.K, LW = BTW + K - 1, LH = BTH + K - 1;
     const int rlo = K - 1 - a.pad0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
-    for (int i = threadIdx.x; i < LH * LW; i += NT) {
-        const int ry = i / LW, rx = i - ry * LW;
-        const int y = Y0 + ry - rlo, x = X0 + rx - rlo;
-        sA[i] = (y >= 0 && y < Ho && x >= 0 && x < Wo) ? ld(gp + (long long)y * Wo + x) : 0.f;
+    for (int ry = wave; ry < LH; ry += 4) {
+        const int y = Y0 + ry - rlo;
+        const bool yok = y >= 0 && y < Ho;
+        for (int rx = lane; rx < LW; rx += 64) {
+            const int x = X0 + rx - rlo;
+            sA[ry * LW + rx] = (yok && x >= 0 && x < Wo) ? ld(gp + (long long)y * Wo + x) : 0.f;
+        }
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int X = X0 + lane;
     const bool xedge = X < K || X >= Wo - K;
     for (int r = wave; r < LH; r += 4) {
         float acc = 0.f;
         if (!xedge) {
+#pragma unroll
             for (int j = 0; j < K; ++j) acc = fmaf(a.k[K - 1 - j], sA[r * LW + lane + j], acc);
         } else if (X < Wo) {
             for (int j = 0; j < K; ++j) {
@@ -1005,6 +1017,7 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
         if (Y >= Ho) break;
         float acc = 0.f;
         if (Y >= K && Y < Ho - K) {
+#pragma unroll
             for (int j = 0; j < K; ++j) acc = fmaf(a.k[K - 1 - j], sB[(ry + j) * BTW + lane], acc);
         } else {
             for (int j = 0; j < K; ++j) {
@@ -1016,6 +1029,22 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
                                      : ((long long)(c * r * r + (Y % r) * r + X % r) * a.H + Y / r) * a.W + X / r;
         st(dxb + off, acc);
     }
+}
+
+template <class T>
+int blur_launch(BlurArgs& a, int mode, const void* dout, void* dx, long long grid, hipStream_t st) {
+    const dim3 g((unsigned)grid);
+#define BLUR_CASE(KK)                                                                        \
+    case KK:                                                                                 \
+        if (mode == 0) hipLaunchKernelGGL((blur_fwd<T, KK>), g, dim3(NT), 0, st, a);         \
+        else hipLaunchKernelGGL((blur_bwd<T, KK>), g, dim3(NT), 0, st, a, dout, dx);         \
+        break;
+    switch (a.K) {
+        BLUR_CASE(1) BLUR_CASE(2) BLUR_CASE(3) BLUR_CASE(4) BLUR_CASE(5) BLUR_CASE(6) BLUR_CASE(7) BLUR_CASE(8)
+    default: return VFM_ERR_ARGS;
+    }
+#undef BLUR_CASE
+    return launch_status();
 }
 
 }  // namespace
@@ -1215,12 +1244,11 @@ extern "C" int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, i
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const long long grid = (long long)((W * r + BTW - 1) / BTW) * ((H * r + BTH - 1) / BTH) * B * C;
     switch (dtype) {
-    case VFM_F32: hipLaunchKernelGGL((blur_fwd<float>), dim3((unsigned)grid), dim3(NT), 0, st, a); break;
-    case VFM_BF16: hipLaunchKernelGGL((blur_fwd<__hip_bfloat16>), dim3((unsigned)grid), dim3(NT), 0, st, a); break;
-    case VFM_F16: hipLaunchKernelGGL((blur_fwd<__half>), dim3((unsigned)grid), dim3(NT), 0, st, a); break;
-    default: return VFM_ERR_ARGS;
+    case VFM_F32: return blur_launch<float>(a, 0, nullptr, nullptr, grid, st);
+    case VFM_BF16: return blur_launch<__hip_bfloat16>(a, 0, nullptr, nullptr, grid, st);
+    case VFM_F16: return blur_launch<__half>(a, 0, nullptr, nullptr, grid, st);
     }
-    return launch_status();
+    return VFM_ERR_ARGS;
 }
 
 extern "C" int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* taps, int K, int dtype, int B, int C,
@@ -1232,10 +1260,9 @@ extern "C" int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* tap
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const long long grid = (long long)((W * r + BTW - 1) / BTW) * ((H * r + BTH - 1) / BTH) * B * C;
     switch (dtype) {
-    case VFM_F32: hipLaunchKernelGGL((blur_bwd<float>), dim3((unsigned)grid), dim3(NT), 0, st, a, dout, dx); break;
-    case VFM_BF16: hipLaunchKernelGGL((blur_bwd<__hip_bfloat16>), dim3((unsigned)grid), dim3(NT), 0, st, a, dout, dx); break;
-    case VFM_F16: hipLaunchKernelGGL((blur_bwd<__half>), dim3((unsigned)grid), dim3(NT), 0, st, a, dout, dx); break;
-    default: return VFM_ERR_ARGS;
+    case VFM_F32: return blur_launch<float>(a, 1, dout, dx, grid, st);
+    case VFM_BF16: return blur_launch<__hip_bfloat16>(a, 1, dout, dx, grid, st);
+    case VFM_F16: return blur_launch<__half>(a, 1, dout, dx, grid, st);
     }
-    return launch_status();
+    return VFM_ERR_ARGS;
 }

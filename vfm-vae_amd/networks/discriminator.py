@@ -17,6 +17,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from torch_utils.ops import decoder_ops
 from torch.nn.utils.spectral_norm import SpectralNorm
 
 from torch_utils import distributed as dist
@@ -31,9 +33,33 @@ IMAGENET_DEFAULT_STD = (0.229, 0.224, 0.225)
 
 
 class SpectralConv1d(nn.Conv1d):
+    """Spectral-normalised Conv1d (reference discriminator.py:39-42).
+
+    On ROCm tensors the convolution runs as one GEMM over the whole batch
+    (k = 1: directly; k > 1: circular/zero pad + unfold to [B, C*k, L]) instead of
+    MIOpen's per-sample im2col + small-GEMM loop; same math."""
+
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)
         SpectralNorm.apply(self, name='weight', n_power_iterations=1, dim=0, eps=1e-12)
+
+    def _conv_forward(self, x, weight, bias):
+        if not x.is_cuda or self.groups != 1 or self.stride != (1,) or self.dilation != (1,) or x.dim() != 3:
+            return super()._conv_forward(x, weight, bias)
+        k = self.kernel_size[0]
+        O = weight.shape[0]
+        if k > 1 or self.padding[0] > 0:
+            p = self.padding[0]
+            mode = 'constant' if self.padding_mode == 'zeros' else self.padding_mode
+            xp = F.pad(x, (p, p), mode=mode) if p > 0 else x
+            B, C, _ = xp.shape
+            cols = xp.unfold(2, k, 1)                                  # [B, C, L, k]
+            L = cols.shape[2]
+            x = cols.permute(0, 1, 3, 2).reshape(B, C * k, L)
+        y = decoder_ops.pointwise(weight.reshape(O, -1), x)
+        if bias is not None:
+            y = y + bias.to(y.dtype)[None, :, None]
+        return y
 
 
 class BatchNormLocal(nn.Module):

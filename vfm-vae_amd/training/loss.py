@@ -93,6 +93,18 @@ class SSIM(nn.Module):
 
 
 class TotalLoss:
+    trace = None            # diagnostics: callable(msg); set by TrainingIteration.trace
+
+    def _mark(self, name):
+        if self.trace is None:
+            return
+        import time
+        torch.cuda.synchronize()
+        now = time.perf_counter()
+        last = getattr(self, '_mark_t', now)
+        self._mark_t = now
+        self.trace(f"  {name}: {now - last:.3f}s")
+
     def __init__(self, device, G, D, vfm_name, resume_kimg, use_equivariance_regularization, blur_init_sigma=2,
                  blur_fade_kimg=0, l1_pixel_loss_weight=1.0, l2_pixel_loss_weight=0.0, perceptual_loss_weight=10.0,
                  ssim_loss_weight=0.0, multiscale_pixel_loss_weights=[], multiscale_block_indices=[],
@@ -271,6 +283,8 @@ class TotalLoss:
 
     def _sync_safety(self, skip_local: bool, marks: list):
         """One collective: returns (skip_any_rank, marks_min_over_ranks)."""
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            return skip_local, list(marks)                 # nothing to agree on: no device round trip
         vec = torch.tensor([int(skip_local)] + [-int(m) for m in marks], dtype=torch.int32, device=self.device)
         if dist.is_initialized():
             torch.distributed.all_reduce(vec, op=torch.distributed.ReduceOp.MAX)
@@ -433,11 +447,14 @@ class TotalLoss:
             return
 
         assert phase == 'G'
+        self._mark('G start')
         out = self.run_G(real_img, real_c)
+        self._mark('G fwd')
         gen_img, gen_ms = out.gen_img, out.gen_multiscale_imgs
         eq_s, eq_a, real_c_enc = out.eq_scale_factor, out.eq_angle_factor, out.global_text_tokens
         c_arg = real_c_enc if is_text_cond else real_c
         gen_d = self.run_D(gen_img, c_arg)
+        self._mark('D(gen) fwd')
 
         st_gen_logits = None
         st_gen = zero()
@@ -486,12 +503,14 @@ class TotalLoss:
         if self._multiscale_pixel_loss_on and sum(self.multiscale_pixel_loss_weights) > 0:
             rec = rec + ms_loss
 
+        self._mark('rec losses (LPIPS, L1, multiscale)')
         vf_loss = zero()
         cur_vf_w = self.vf_loss_weight
         if self.vf_loss_weight > 0:
             vf_loss = out.vf_loss
             cur_vf_w = self.calculate_cur_vf_loss_weight(rec, vf_loss, out.vf_last_layer)
         clip_loss = zero()
+        self._mark('adaptive vf weight')
 
         names = ['l1_pixel_loss', 'l2_pixel_loss', 'perceptual_loss', 'ssim_loss', 'multiscale_pixel_loss',
                  'stylegan_t_gen_loss', 'patchgan_gen_loss', 'feature_matching_loss', 'clip_loss']
@@ -529,7 +548,9 @@ class TotalLoss:
             training_stats.report(f'Loss/G/is_safe/{k}', int(m))
             if not m:
                 dist.print0(f"[SafeLoss][G] Unsafe {k} at {cur_nimg // 1000} kimg - skipping.")
+        self._mark('safe-loss check')
         g_loss.backward()
+        self._mark('G backward')
         if skip:
             return
         self.prev_loss_dict = loss_dict

@@ -19,6 +19,7 @@ MI355X-specific execution (`TrainingIteration`, shared with bench.py):
     p.lerp(p_ema, beta) is the identity and is not recomputed).
 """
 import copy
+import gc
 import json
 import math
 import os
@@ -177,9 +178,24 @@ class TrainingIteration:
             for name, layer in phase.module.named_modules():
                 layer.requires_grad_(any(t in name for t in layers))
 
+    def _apply_freeze(self, phase):
+        """partial_freeze() semantics, evaluated once per (phase, trainable_layers) and then
+        applied as a flat list of per-parameter flags (the module walk costs milliseconds of
+        host time per phase)."""
+        key = (phase.name, tuple(getattr(phase.module, 'trainable_layers', ()) or ()))
+        cache = phase.setdefault('freeze_cache', {})
+        flags = cache.get(key)
+        if flags is None:
+            phase.module.requires_grad_(True)
+            self.partial_freeze(phase)
+            flags = [(p, p.requires_grad) for p in phase.module.parameters()]
+            cache[key] = flags
+            return
+        for p, f in flags:
+            p.requires_grad_(f)
+
     def run_phase(self, phase, real_imgs, real_cs, cur_nimg):
-        phase.module.requires_grad_(True)
-        self.partial_freeze(phase)
+        self._apply_freeze(phase)
         phase.sync.prepare()
         n = len(real_imgs)
         for i, (img, c) in enumerate(zip(real_imgs, real_cs)):
@@ -213,8 +229,9 @@ class TrainingIteration:
         if dst:
             # p_ema <- p.lerp(p_ema, beta) == p_ema + (1 - beta) * (p - p_ema)
             torch._foreach_lerp_(dst, src, 1.0 - beta)
-        for be, b in zip(self.G_ema.buffers(), self.G.buffers()):
-            be.copy_(b)
+        bufs = [(be, b) for be, b in zip(self.G_ema.buffers(), self.G.buffers()) if be.data_ptr() != b.data_ptr()]
+        if bufs:
+            torch._foreach_copy_([be for be, _ in bufs], [b for _, b in bufs])
 
     def __call__(self, phase_real_img, phase_real_c, cur_nimg):
         if self.trace is None:
@@ -226,7 +243,9 @@ class TrainingIteration:
         for phase in self.phases:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            self.loss.trace = self.trace
             self.run_phase(phase, phase_real_img, phase_real_c, cur_nimg)
+            self.loss.trace = None
             torch.cuda.synchronize()
             self.trace(f"phase {phase.name}: {time.perf_counter() - t0:.3f}s")
         t0 = time.perf_counter()
@@ -345,6 +364,9 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
         step(phase_real_img, phase_real_c, cur_nimg)
         cur_nimg += batch_size
         batch_idx += 1
+        if batch_idx == 1:
+            gc.collect()
+            gc.freeze()          # keep full collections over the long-lived objects out of the step
         done = (cur_nimg >= total_kimg * 1000) or (max_iterations is not None and batch_idx >= max_iterations)
         if not done and cur_tick != 0 and cur_nimg < tick_start_nimg + kimg_per_tick * 1000:
             continue
