@@ -132,7 +132,7 @@ int vfm_filtered_lrelu_act(void* x, unsigned char* s, int dtype,
 int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,
                      int dtype, int B, int C, int H, int W, int K, int pad, void* stream);
 
-/* Number of spatial tiles the weight-gradient kernel writes partials for. */
+/* Number of column tiles the weight-gradient kernel writes partials for. */
 int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, int pad);
 
 /* Weight/bias gradient partials: partial[tiles, B*C, K*K + 1] (last slot = bias).

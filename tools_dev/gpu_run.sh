@@ -11,8 +11,8 @@ for s in "$@"; do
   case $s in
     tests)   timeout -k 10 900 python -m pytest tests -m gpu -x -q > $out/tests.log 2>&1 ;;
     testsk)  timeout -k 10 900 python -m pytest tests -m gpu -q > $out/tests.log 2>&1 ;;
-    bench)   timeout -k 10 900 python bench.py --steps 6 --warmup 3 > $out/bench.log 2>&1 ;;
-    benchq)  timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline > $out/bench.log 2>&1 ;;
+    bench)   timeout -k 10 900 python bench.py > $out/bench.log 2>&1 ;;
+    benchq)  timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench.log 2>&1 ;;
     benchref) timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline --force-ref-ops > $out/bench_ref.log 2>&1 ;;
     prof)    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 ;;
     opbench) timeout -k 10 300 python tools_dev/opbench.py > $out/opbench.log 2>&1 ;;

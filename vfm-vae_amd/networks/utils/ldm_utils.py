@@ -322,15 +322,26 @@ class EquivarianceTransform(nn.Module):
     """Draws (scale, quarter-turns, is_prior) for equivariance regularisation from
     python's `random` (same draws and order as reference ldm_utils.py:503-517)."""
 
+    SCALES = (0.25, 0.5, 0.75, 1.0)
+
     def __init__(self, apply=False, p_eq_prior=0.5, p_eq_prior_scale=0.25):
         super().__init__()
         self.apply = apply
         self.p_eq_prior = p_eq_prior
         self.p_eq_prior_scale = p_eq_prior_scale
+        self.forced = None          # (scale, quarter_turns, is_prior): shape warm-up only, consumes no draws
+
+    def variants(self):
+        """Every (scale, quarter_turns, is_prior) shape class forward() can produce."""
+        if not self.apply:
+            return [(1.0, 0, False)]
+        return [(s, 0, p) for p in (False, True) for s in self.SCALES]
 
     def forward(self, validation: bool):
         if not self.apply or validation:
             return 1.0, 0, False
+        if self.forced is not None:
+            return self.forced
         if random.random() < self.p_eq_prior:
             return random.choice([0.25, 0.5, 0.75, 1.0]), random.choice([0, 1, 2, 3]), False
         scale = random.choice([0.25, 0.5, 0.75]) if random.random() < self.p_eq_prior_scale else 1.0
