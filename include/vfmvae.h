@@ -183,6 +183,19 @@ int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, int K, int d
 int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* taps, int K, int dtype,
                          int B, int C, int H, int W, int r, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Discrete latent: codebook lookup of VectorQuantizer (replaces the
+ * `torch.argmax(F.normalize(f) @ F.normalize(codebook).T, dim=1)` of
+ * networks/utils/quant_utils.py:84-86 and f_to_idx :126-131).
+ *   features: fp32 [N, C], row stride `ld` elements (>= C; unit column stride).
+ *   codebook: fp32 [V, C] contiguous (raw weights; normalised inside).
+ *   indices : int64 [N] output = first index of the maximal cosine (NaN = maximal).
+ * Fixed fp32 evaluation order (left-to-right sums, no FMA contraction, IEEE sqrt and
+ * division), so results are bit-reproducible against oracle/ops_oracle.c.
+ * C in {1, 2, 3, 4, 8, 16, 32, 64}; other widths return VFM_NO_KERNEL. */
+int vfm_codebook_argmax(const float* features, long long ld, const float* codebook, int N, int C, int V,
+                        long long* indices, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,10 +14,16 @@
  *   oracle_filtered_lrelu <- torch_utils/ops/filtered_lrelu.py:120-153 (_filtered_lrelu_ref)
  *                            plus the 2-bit sign codes of filtered_lrelu.cu:1105-1160
  *                            (bit0 = negative branch taken, code 2 = clamped).
+ *   oracle_codebook_argmax <- networks/utils/quant_utils.py:84-86 and :126-131
+ *                            (F.normalize(f) @ F.normalize(codebook).T -> argmax), fp32,
+ *                            in the fixed evaluation order the HIP kernel uses
+ *                            (left-to-right rounded squares, IEEE sqrt/division, dot
+ *                            product as a left-to-right FMA chain = torch's CPU order).
  * Parity pin: tests/test_oracle_ops.py checks these against golden vectors generated
- * from the reference itself (tests/golden/make_golden_ops.py).
+ * from the reference itself (tests/golden/make_golden_ops.py, make_golden_vq.py).
  * Layout: all arrays dense NCHW.
  */
+/* Built with -ffp-contract=off (oracle/Makefile): no fused multiply-adds anywhere. */
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -115,4 +121,42 @@ void oracle_filtered_lrelu(const double* x, const double* b, int N, int C, int H
     oracle_upfirdn2d(mid, N, C, ch, cw, fd, fdh, fdw, 1, 1, down, down, 0, 0, flip, 1.0, y, outH, outW);
     free(xb);
     free(mid);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Codebook lookup (fp32 on purpose: the indices must match the fp32 reference bit for bit).
+ * F.normalize(x, dim=-1) = x / clamp_min(||x||_2, 1e-12)  (torch.nn.functional.normalize);
+ * score = <f_hat, w_hat>, idx = first maximal index, NaN counts as maximal (torch.argmax). */
+static void vq_normalize(const float* x, int C, float* o) {
+    float s = x[0] * x[0];
+    for (int i = 1; i < C; ++i) s = s + x[i] * x[i];
+    float n = sqrtf(s);
+    n = n < 1e-12f ? 1e-12f : n;
+    for (int i = 0; i < C; ++i) o[i] = x[i] / n;
+}
+
+void oracle_codebook_argmax(const float* f, long long ld, const float* w, int N, int C, int V, long long* idx) {
+    float* wn = (float*)malloc(sizeof(float) * (size_t)V * C);
+    float* fn = (float*)malloc(sizeof(float) * (size_t)C);
+    for (int v = 0; v < V; ++v) vq_normalize(w + (size_t)v * C, C, wn + (size_t)v * C);
+    for (int n = 0; n < N; ++n) {
+        vq_normalize(f + (size_t)n * ld, C, fn);
+        float best = -INFINITY;
+        long long bi = 0;
+        for (int v = 0; v < V; ++v) {
+            const float* cw = wn + (size_t)v * C;
+            float d = fn[0] * cw[0];
+            for (int i = 1; i < C; ++i) d = fmaf(fn[i], cw[i], d);   /* FMA chain, as torch's CPU sgemm */
+            if (d > best) {
+                best = d;
+                bi = v;
+            } else if (isnan(d)) {
+                bi = v;
+                break;
+            }
+        }
+        idx[n] = bi;
+    }
+    free(wn);
+    free(fn);
 }

@@ -2,7 +2,8 @@
 
 Double-precision CPU restatements of upfirdn2d / bias_act / filtered_lrelu
 (reference torch_utils/ops/{upfirdn2d,bias_act,filtered_lrelu}.py `_ref`
-paths). See ops_oracle.c for the file:line each function follows.
+paths) and the fp32 codebook lookup (networks/utils/quant_utils.py:84-86).
+See ops_oracle.c for the file:line each function follows.
 """
 import ctypes
 import os
@@ -34,7 +35,8 @@ def _load():
         lib.oracle_filtered_lrelu.argtypes = [_dp, _dp, _ci, _ci, _ci, _ci, _dp, _ci, _ci, _dp, _ci, _ci,
                                               _ci, _ci, _ci, _ci, _ci, _ci, _cd, _cd, _cd, _ci,
                                               _dp, _ci, _ci, ctypes.POINTER(ctypes.c_ubyte), _ci, _ci]
-        for fn in (lib.oracle_upfirdn2d, lib.oracle_bias_act, lib.oracle_filtered_lrelu):
+        lib.oracle_codebook_argmax.argtypes = [ctypes.c_void_p, _cll, ctypes.c_void_p, _ci, _ci, _ci, ctypes.c_void_p]
+        for fn in (lib.oracle_upfirdn2d, lib.oracle_bias_act, lib.oracle_filtered_lrelu, lib.oracle_codebook_argmax):
             fn.restype = None
         _lib = lib
     return _lib
@@ -123,3 +125,15 @@ def filtered_lrelu(x, fu=None, fd=None, b=None, up=1, down=1, padding=0, gain=2 
                                   y.ctypes.data_as(_dp), oh, ow,
                                   codes.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), ch, cw)
     return y, codes
+
+
+def codebook_argmax(features, codebook):
+    """features [N, C] fp32, codebook [V, C] fp32 -> int64 [N] (first maximal cosine)."""
+    f = np.ascontiguousarray(features, dtype=np.float32)
+    w = np.ascontiguousarray(codebook, dtype=np.float32)
+    n, c = f.shape
+    v, c2 = w.shape
+    assert c == c2
+    idx = np.zeros(n, dtype=np.int64)
+    _load().oracle_codebook_argmax(f.ctypes.data, c, w.ctypes.data, n, c, v, idx.ctypes.data)
+    return idx

@@ -86,7 +86,9 @@ def test_bias_act_hip(i, dtype):
     if dtype == torch.float64 and grads[0].requires_grad:
         ddx = torch.autograd.grad(grads[0], x, cu(arr["v"]), allow_unused=True)[0]
         ddx = torch.zeros_like(x) if ddx is None else ddx
-        assert rel_err(ddx.cpu(), arr["ddx"]) < 1e-8
+        # alpha/gain/clamp cross the ABI as fp32 (bias_act.cpp:32 takes float): a relative
+        # rounding of up to 2^-24 ~ 6e-8 per scalar, so fp64 cannot be tighter than ~1e-7.
+        assert rel_err(ddx.cpu(), arr["ddx"]) < 2e-7
 
 
 def test_bias_act_channels_last_and_large():
@@ -159,7 +161,7 @@ def test_filtered_lrelu_generic_fallback_path():
     y = filtered_lrelu.filtered_lrelu(x.to(DEV), f.to(DEV), f.to(DEV), up=3, down=1, padding=2, clamp=0.5).cpu()
     yo, _ = ops_oracle.filtered_lrelu(x.numpy(), f.double().numpy(), f.double().numpy(), None, up=3, down=1,
                                       padding=2, clamp=0.5)
-    assert rel_err(y, yo) < 1e-10
+    assert rel_err(y, yo) < 1e-7      # gain=sqrt(2) and slope cross the ABI as fp32 (filtered_lrelu.cpp:16)
 
 
 def test_filtered_lrelu_large_fp16_vs_oracle():

@@ -9,12 +9,15 @@ export TMPDIR=/tmp
 for s in "$@"; do
   echo "=== step $s $(date +%T)" | tee -a $out/steps.log
   case $s in
-    tests)   timeout -k 10 900 python -m pytest tests -m gpu -x -q > $out/tests.log 2>&1 ;;
-    testsk)  timeout -k 10 900 python -m pytest tests -m gpu -q > $out/tests.log 2>&1 ;;
+    tests)   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 ;;
+    testsk)  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 ;;
     bench)   timeout -k 10 900 python bench.py > $out/bench.log 2>&1 ;;
     benchq)  timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench.log 2>&1 ;;
     benchref) timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline --force-ref-ops > $out/bench_ref.log 2>&1 ;;
-    prof)    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 ;;
+    prof)    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 \
+               && python tools_dev/prof_summary.py $(find $out/prof -name '*kernel_trace.csv' | head -1) 3 \
+                    $(sed -n 's/.*timed 3 steps: \([0-9.]*\)s.*/\1/p' $out/prof.log) > $out/prof_summary.txt \
+               && find $out/prof -name '*kernel_trace.csv' -delete ;;
     opbench) timeout -k 10 300 python tools_dev/opbench.py > $out/opbench.log 2>&1 ;;
     dtests)  timeout -k 10 600 python -m pytest tests/test_decoder_gpu.py -q -x > $out/dtests.log 2>&1 ;;
     bsmall)  timeout -k 10 900 python bench.py --batch 8 --steps 2 --warmup 2 --trace --no-cpu-baseline > $out/bsmall.log 2>&1 ;;

@@ -110,7 +110,12 @@ class _BiasActHip(torch.autograd.Function):
         if act != 'linear' or gain != 1 or clamp >= 0 or b is not None:
             y = _run(x, b, None, None, None, 0, dim, spec, alpha, gain, clamp)
         need_x = 'x' in spec.ref or spec.has_2nd_grad
-        ctx.save_for_backward(x if need_x else None, b if need_x else None, y if 'y' in spec.ref else None)
+        # y is also needed for the clamp mask of the gradient. The reference CUDA path drops
+        # it for act='linear' (bias_act.py:151-154 saves y only if 'y' in spec.ref), so its kernel
+        # never zeroes the gradient of clamped outputs there; _bias_act_ref (autograd through
+        # torch.clamp) does. We follow the mathematically exact _ref behaviour.
+        need_y = 'y' in spec.ref or clamp >= 0
+        ctx.save_for_backward(x if need_x else None, b if need_x else None, y if need_y else None)
         ctx.cfg = (dim, act, alpha, gain, clamp)
         return y
 
