@@ -132,11 +132,11 @@ int vfm_filtered_lrelu_act(void* x, unsigned char* s, int dtype,
 int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,
                      int dtype, int B, int C, int H, int W, int K, int pad, void* stream);
 
-/* Number of column tiles the weight-gradient kernel writes partials for. */
+/* Number P of partial slots per channel the weight-gradient kernel writes. */
 int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, int pad);
 
-/* Weight/bias gradient partials: partial[tiles, B*C, K*K + 1] (last slot = bias).
- * The caller sums over tiles and the batch (fixed order, deterministic). */
+/* Weight/bias gradient partials: partial[P, C, K*K + 1] (last slot = bias; P from
+ * vfm_dwconv2d_bwd_weight_tiles). The caller sums over P in a fixed order (deterministic). */
 int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int dtype,
                             int B, int C, int H, int W, int K, int pad, void* stream);
 
@@ -182,6 +182,18 @@ int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, int K, int d
 /* Exact adjoint of vfm_shuffle_blur_fwd: dout [B, C, H r, W r] -> dx [B, C r^2, H, W]. */
 int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* taps, int K, int dtype,
                          int B, int C, int H, int W, int r, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Frozen ViT towers (SigLIP2 encoder): fused residual add + LayerNorm, replacing the
+ * torch `h + delta.float()` / `F.layer_norm(h).to(bf16)` pairs of the HF SiglipEncoderLayer
+ * under bf16 autocast (networks/utils/vfms/siglip2_utils.py:114-137).
+ *   h: fp32 [rows, D]; delta: [rows, D] (dtype_delta) or NULL; h_out: fp32 [rows, D]
+ *   receives h + delta (NULL: not written; ignored when delta is NULL);
+ *   y: [rows, D] (dtype_out) = LayerNorm(h + delta) * w + b (fp32 statistics, eps);
+ *   w, b: fp32 [D] or NULL. D a multiple of 256, at most 2048 (else VFM_NO_KERNEL).
+ * Forward only (the towers are frozen and run without autograd). */
+int vfm_residual_layer_norm(const float* h, const void* delta, float* h_out, const float* w, const float* b,
+                            void* y, int dtype_delta, int dtype_out, int rows, int D, float eps, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Discrete latent: codebook lookup of VectorQuantizer (replaces the

@@ -61,7 +61,9 @@ def _run(fn_hip, fn_ref, inputs, dt, names, out_grad_seed=0):
 # LDS-tile kernel: everything else (ragged widths, narrow planes).
 DW_CASES = [(2, 8, 16, 16, 3), (2, 8, 16, 16, 5), (2, 6, 16, 16, 7), (1, 4, 64, 70, 3), (2, 5, 13, 9, 3),
             (1, 3, 33, 130, 7), (3, 2, 4, 4, 3), (1, 2, 1, 5, 3), (2, 3, 37, 128, 7), (1, 2, 20, 256, 5),
-            (2, 4, 9, 32, 3), (1, 3, 300, 64, 7), (2, 2, 256, 256, 7)]
+            (2, 4, 9, 32, 3), (1, 3, 300, 64, 7), (2, 2, 256, 256, 7),
+            # several samples per wave (narrow planes), multi-band units, partial last wave
+            (20, 3, 16, 16, 5), (33, 2, 32, 64, 7), (9, 3, 64, 64, 7), (5, 2, 8, 16, 3)]
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])

@@ -62,10 +62,12 @@ def test_argument_validation_without_gpu():
 
 def test_dwconv_partial_tiles_host_query():
     """vfm_dwconv2d_bwd_weight_tiles is pure host logic: the number of partial slices the
-    weight-gradient kernel writes (row-streaming path: waves per plane; tile path: column tiles)."""
+    weight-gradient kernel writes per channel (row-streaming path: waves per channel; tile path:
+    column tiles x batch)."""
     import torch_utils.custom_ops as co
     lib = co.get_native()
-    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 256, 256, 7, 3) == 32    # bands of 8 rows, 1 per wave
-    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 16, 16, 3, 1) == 1
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 256, 256, 7, 3) == 64    # 2 samples x 32 bands of 8 rows
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(2, 8, 16, 16, 3, 1) == 1       # 16 units per wave
+    assert lib.vfm_dwconv2d_bwd_weight_tiles(3, 2, 5, 130, 3, 1) == 9       # 3 column tiles x 3 samples
     assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 5, 130, 3, 1) == 3
     assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 2, 2, 7, 0) == -2      # empty output -> VFM_ERR_ARGS

@@ -18,6 +18,7 @@ for s in "$@"; do
                && python tools_dev/prof_summary.py $(find $out/prof -name '*kernel_trace.csv' | head -1) 3 \
                     $(sed -n 's/.*timed 3 steps: \([0-9.]*\)s.*/\1/p' $out/prof.log) > $out/prof_summary.txt \
                && find $out/prof -name '*kernel_trace.csv' -delete ;;
+    decbench) timeout -k 10 300 python tools_dev/decbench.py > $out/decbench.log 2>&1 ;;
     opbench) timeout -k 10 300 python tools_dev/opbench.py > $out/opbench.log 2>&1 ;;
     dtests)  timeout -k 10 600 python -m pytest tests/test_decoder_gpu.py -q -x > $out/dtests.log 2>&1 ;;
     bsmall)  timeout -k 10 900 python bench.py --batch 8 --steps 2 --warmup 2 --trace --no-cpu-baseline > $out/bsmall.log 2>&1 ;;

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default="gpurun_out/tp")
     ap.add_argument("--rows", type=int, default=60)
+    ap.add_argument("--eq-scale", type=float, default=1.0, help="force the equivariance scale of the profiled step")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     dev = torch.device("cuda", 0)
@@ -34,6 +35,8 @@ def main():
     labels = ['a photo'] * args.batch
     for i in range(2):
         step([pool[i % len(pool)].float() / 255.], [labels], i * args.batch)
+    step.G.equivariance_transform.forced = (args.eq_scale, 0, False)
+    step([pool[1].float() / 255.], [labels], 2 * args.batch)
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
     with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True) as prof:
@@ -50,6 +53,18 @@ def main():
     evs.sort(key=lambda e: -e.self_device_time_total)
     with open(os.path.join(args.out, "copies.txt"), "w") as f:
         for e in evs[:40]:
+            f.write(f"{e.key} calls={e.count} self_dev_ms={e.self_device_time_total / 1e3:.2f} shapes={e.input_shapes}\n")
+            for fr in e.stack:
+                f.write(f"    {fr}\n")
+    # every non-GEMM op group (op + input shapes + stack), by self device time
+    skip = ("aten::mm", "aten::bmm", "aten::addmm", "aten::convolution", "aten::cudnn_convolution",
+            "aten::miopen_convolution", "aten::_scaled_dot_product", "aten::_efficient_attention",
+            "aten::_flash_attention", "aten::matmul", "aten::linear", "aten::baddbmm")
+    evs = [e for e in prof.key_averages(group_by_input_shape=True, group_by_stack_n=12)
+           if e.key.startswith("aten::") and not e.key.startswith(skip) and e.self_device_time_total > 0]
+    evs.sort(key=lambda e: -e.self_device_time_total)
+    with open(os.path.join(args.out, "small_ops.txt"), "w") as f:
+        for e in evs[:120]:
             f.write(f"{e.key} calls={e.count} self_dev_ms={e.self_device_time_total / 1e3:.2f} shapes={e.input_shapes}\n")
             for fr in e.stack:
                 f.write(f"    {fr}\n")

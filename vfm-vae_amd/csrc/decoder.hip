@@ -260,12 +260,16 @@ int dw_dispatch(DwArgs& a, int K, int mode, const void* dy, float* partial, hipS
 
 // -------------------------------------------------------------------------------------------
 // Row-streaming depthwise conv for "same" convolutions (odd K, pad = (K-1)/2) on planes
-// 16..256 wide. One wave owns one plane (so the K*K weights are wave-uniform scalars) and
-// R = 64 / L row bands of it, L = W/4 lanes per image row, 4 adjacent columns per lane.
-// Each lane streams its band top to bottom: one 4-element vector load per input row, the
-// K-1 halo columns from the neighbouring lanes by cross-lane shuffles (a group always spans
-// a full image row, so the group edge is the zero-padded image border), and K rotating
-// output-row accumulators. No LDS, every input byte is loaded ~once (band halo only).
+// 16..256 wide. L = W/4 lanes span one image row (4 adjacent columns per lane), so a wave
+// holds R = 64 / L independent row groups. Work unit = (sample b, row band) of ONE channel c:
+// a wave always works on a single channel (the K*K weights are wave-uniform scalars) and
+// its R groups take R consecutive units of that channel -- different bands of one plane for
+// wide planes, different samples for narrow ones -- so every lane is busy even when a plane
+// is only 16 rows tall. Each lane streams its band top to bottom: one 4-element vector load
+// per input row (issued one row ahead in the forward), the K-1 halo columns from the
+// neighbouring lanes by cross-lane shuffles (a group spans a full image row, so the group
+// edge is the zero-padded image border), and K rotating output-row accumulators. No LDS;
+// every input byte is loaded ~once (band halo only).
 
 struct DwRowArgs {
     const void* x;
@@ -274,11 +278,12 @@ struct DwRowArgs {
     const float* noise;   // [H, W] or null
     void* y;
     const void* dy;       // weight-gradient mode
-    float* partial;       // [wpp, B*C, K*K+1]
+    float* partial;       // [wpc, C, K*K+1]
     int B, C, H, W;
     int L, R;             // lanes per row, row groups per wave
     int BH;               // band height
-    int wpp;              // waves per plane
+    int nb;               // bands per plane
+    int wpc;              // waves per channel = ceil(B * nb / R)
 };
 
 template <class T>
@@ -336,24 +341,42 @@ __device__ __forceinline__ void dwr_halo(const float* own, float* v, int q, int 
     }
 }
 
+// Lane -> (channel, plane offset, band start, live) for the unit decomposition above.
+struct DwrLane {
+    int c, q, y0, wv;
+    long long poff;
+    bool live;
+};
+__device__ __forceinline__ DwrLane dwr_lane(const DwRowArgs& a) {
+    DwrLane r;
+    const int wave_g = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+    r.c = __builtin_amdgcn_readfirstlane(wave_g / a.wpc);
+    r.wv = wave_g - r.c * a.wpc;
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / a.L;
+    r.q = lane - grp * a.L;
+    const int u = r.wv * a.R + grp;                    // unit within the channel
+    r.live = r.c < a.C && u < a.B * a.nb;
+    const int b = r.live ? u / a.nb : 0;
+    const int band = r.live ? u - b * a.nb : 0;
+    r.y0 = band * a.BH;
+    r.poff = ((long long)b * a.C + (r.live ? r.c : 0)) * a.H * a.W + 4 * r.q;
+    return r;
+}
+
 template <class T, int K>
 __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
     constexpr int PAD = (K - 1) / 2;
-    const int wave_g = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-    const int plane = __builtin_amdgcn_readfirstlane(wave_g / a.wpp);
-    const int wv = wave_g - plane * a.wpp;
-    if (plane >= a.B * a.C) return;
-    const int lane = threadIdx.x & 63;
-    const int grp = lane / a.L, q = lane - grp * a.L;
-    const int y0 = (wv * a.R + grp) * a.BH;
-    const int c = __builtin_amdgcn_readfirstlane(plane % a.C);
+    const DwrLane ln = dwr_lane(a);
+    if (ln.c >= a.C) return;                            // wave-uniform
+    const int c = ln.c, q = ln.q, y0 = ln.y0;
+    const bool live = ln.live;
     float wk[K * K];
 #pragma unroll
     for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + i];
     const float bias = a.bias ? a.bias[c] : 0.f;
-    const long long poff = (long long)plane * a.H * a.W + 4 * q;
-    const T* xp = reinterpret_cast<const T*>(a.x) + poff;
-    T* yp = reinterpret_cast<T*>(a.y) + poff;
+    const T* xp = reinterpret_cast<const T*>(a.x) + ln.poff;
+    T* yp = reinterpret_cast<T*>(a.y) + ln.poff;
     const float* np = a.noise ? a.noise + 4 * q : nullptr;
 
     float acc[K][4];
@@ -362,6 +385,8 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) acc[s][c4] = 0.f;
     const int nrows = a.BH + K - 1;
+    float nxt[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live && y0 - PAD >= 0 && y0 - PAD < a.H) ld4(xp + (long long)(y0 - PAD) * a.W, nxt);
     for (int jj0 = 0; jj0 < nrows; jj0 += K) {
 #pragma unroll
         for (int u = 0; u < K; ++u) {
@@ -369,9 +394,11 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
             if (jj < nrows) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4) acc[u][c4] = bias;      // output row jj starts here
-                const int iy = y0 - PAD + jj;
-                float own[4] = {0.f, 0.f, 0.f, 0.f};
-                if (iy >= 0 && iy < a.H) ld4(xp + (long long)iy * a.W, own);
+                float own[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+                const int iyn = y0 - PAD + jj + 1;                     // prefetch the next input row
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) nxt[c4] = 0.f;
+                if (live && jj + 1 < nrows && iyn >= 0 && iyn < a.H) ld4(xp + (long long)iyn * a.W, nxt);
                 float v[K + 3];
                 dwr_halo<K>(own, v, q, a.L);
 #pragma unroll
@@ -384,7 +411,7 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
                 }
                 const int ob = jj - (K - 1);                           // completed output row
                 const int oy = y0 + ob;
-                if (ob >= 0 && ob < a.BH && oy < a.H) {
+                if (live && ob >= 0 && ob < a.BH && oy < a.H) {
                     float o[4];
 #pragma unroll
                     for (int c4 = 0; c4 < 4; ++c4) o[c4] = acc[(u + 1) % K][c4];
@@ -399,21 +426,19 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
     }
 }
 
-// dW[ky][kx] = sum dy[oy][ox] x[oy + ky - PAD][ox + kx - PAD], db = sum dy, per plane;
-// the wave's total goes to partial[wv][plane][:], summed by the host in a fixed order.
+// dW[ky][kx] = sum dy[oy][ox] x[oy + ky - PAD][ox + kx - PAD], db = sum dy, per channel;
+// the wave's total (all its lanes share the channel) goes to partial[wv][c][:], summed by
+// the host in a fixed order (deterministic).
 template <class T, int K>
 __global__ __launch_bounds__(NT) void dwr_bwd_w(DwRowArgs a) {
     constexpr int PAD = (K - 1) / 2;
-    const int wave_g = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-    const int plane = __builtin_amdgcn_readfirstlane(wave_g / a.wpp);
-    const int wv = wave_g - plane * a.wpp;
-    if (plane >= a.B * a.C) return;
+    const DwrLane ln = dwr_lane(a);
+    if (ln.c >= a.C) return;                            // wave-uniform
     const int lane = threadIdx.x & 63;
-    const int grp = lane / a.L, q = lane - grp * a.L;
-    const int y0 = (wv * a.R + grp) * a.BH;
-    const long long poff = (long long)plane * a.H * a.W + 4 * q;
-    const T* xp = reinterpret_cast<const T*>(a.x) + poff;
-    const T* gp = reinterpret_cast<const T*>(a.dy) + poff;
+    const int q = ln.q, y0 = ln.y0;
+    const bool live = ln.live;
+    const T* xp = reinterpret_cast<const T*>(a.x) + ln.poff;
+    const T* gp = reinterpret_cast<const T*>(a.dy) + ln.poff;
 
     float acc[K * K + 1];
 #pragma unroll
@@ -432,11 +457,11 @@ __global__ __launch_bounds__(NT) void dwr_bwd_w(DwRowArgs a) {
                 const int oy = y0 + jj;
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4) gw[u][c4] = 0.f;
-                if (jj < a.BH && oy < a.H) ld4(gp + (long long)oy * a.W, gw[u]);
+                if (live && jj < a.BH && oy < a.H) ld4(gp + (long long)oy * a.W, gw[u]);
                 acc[K * K] += (gw[u][0] + gw[u][1]) + (gw[u][2] + gw[u][3]);
                 const int iy = y0 - PAD + jj;
                 float own[4] = {0.f, 0.f, 0.f, 0.f};
-                if (iy >= 0 && iy < a.H) ld4(xp + (long long)iy * a.W, own);
+                if (live && iy >= 0 && iy < a.H) ld4(xp + (long long)iy * a.W, own);
                 float v[K + 3];
                 dwr_halo<K>(own, v, q, a.L);
 #pragma unroll
@@ -453,17 +478,18 @@ __global__ __launch_bounds__(NT) void dwr_bwd_w(DwRowArgs a) {
             }
         }
     }
-    const int nplanes = a.B * a.C;
 #pragma unroll
     for (int i = 0; i < K * K + 1; ++i) {
         float t = acc[i];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off);
-        if (lane == 0) a.partial[((long long)wv * nplanes + plane) * (K * K + 1) + i] = t;
+        if (lane == 0) a.partial[((long long)ln.wv * a.C + ln.c) * (K * K + 1) + i] = t;
     }
 }
 
 // Row-streaming plan; returns false when the shape is not covered (caller uses dw_fwd / dw_bwd_w).
+// Band height: as tall as possible (halo re-reads (K-1)/BH), never much taller than the plane,
+// halved while the grid has fewer than 16384 waves (64 per CU).
 bool dwr_plan(DwRowArgs& a, int K, int pad) {
     if (K % 2 == 0 || pad != (K - 1) / 2 || K > 7) return false;
     if (a.W < 16 || a.W > 256 || a.W % 4) return false;
@@ -471,12 +497,12 @@ bool dwr_plan(DwRowArgs& a, int K, int pad) {
     if (L & (L - 1)) return false;
     a.L = L;
     a.R = 64 / L;
-    const long long planes = (long long)a.B * a.C;
     int BH = 64;
+    while (BH > 8 && BH / 2 >= a.H) BH /= 2;
     for (;;) {
-        const int bands = (a.H + BH - 1) / BH;
-        a.wpp = (bands + a.R - 1) / a.R;
-        if (BH <= 8 || planes * a.wpp >= 16384) break;
+        a.nb = (a.H + BH - 1) / BH;
+        a.wpc = (a.B * a.nb + a.R - 1) / a.R;
+        if (BH <= 8 || (long long)a.C * a.wpc >= 16384) break;
         BH /= 2;
     }
     a.BH = BH;
@@ -485,7 +511,7 @@ bool dwr_plan(DwRowArgs& a, int K, int pad) {
 
 template <class T>
 int dwr_launch(DwRowArgs& a, int K, int mode, hipStream_t st) {
-    const long long waves = (long long)a.B * a.C * a.wpp;
+    const long long waves = (long long)a.C * a.wpc;
     const dim3 grid((unsigned)((waves + 3) / 4));
 #define DWR_CASE(KK)                                                                   \
     case KK:                                                                           \
@@ -889,6 +915,12 @@ struct BlurArgs {
     void* y;           // [B, C, H*r, W*r]
     int B, C, H, W, r, K, pad0;
     float k[8];        // normalised 1-D taps (2-D kernel = k x k)
+    // Adjoint edge terms (replicate padding folds the pad taps onto the border sample):
+    // dS[0]   += sum_{o < P}   clo[o] dy[o],       clo[o] = sum_{t <= P-1-o} k[t]
+    // dS[n-1] += sum_{m < Q}   chi[m] dy[n-1-m],   chi[m] = sum_{t >= P+1+m} k[t]
+    // with P = (K-1)/2 pad before, Q = K-1-P pad after; every other sample is interior.
+    float clo[8];
+    float chi[8];
 };
 
 // Tiled forms: one workgroup = one (sample, channel) plane x a 64 x 32 tile of the
@@ -896,31 +928,15 @@ struct BlurArgs {
 // pass through LDS, so every input element is read from HBM once per tile (plus halo).
 constexpr int BTW = 64, BTH = 32;
 
-template <class T>
-__device__ __forceinline__ float shuffled_at(const BlurArgs& a, const T* xb, int c, int Y, int X) {
-    const int r = a.r;
-    if (r == 1) return ld(xb + ((long long)c * a.H + Y) * a.W + X);
-    const int sy = Y % r, sx = X % r;
-    return ld(xb + ((long long)(c * r * r + sy * r + sx) * a.H + Y / r) * a.W + X / r);
-}
-
-// Weight with which output coordinate o contributes to source coordinate s along one axis:
-// sum over taps t with clamp(o + t - pad0, 0, n-1) == s of k[t].
-__device__ __forceinline__ float axis_weight(const BlurArgs& a, int o, int s, int n) {
-    float w = 0.f;
-    for (int t = 0; t < a.K; ++t) {
-        const int q = min(max(o + t - a.pad0, 0), n - 1);
-        if (q == s) w += a.k[t];
-    }
-    return w;
-}
-
-template <class T, int K>
+// R (shuffle factor) is a template constant: the sub-pixel plane / low-res coordinate of a
+// full-resolution (Y, X) are shifts and masks, not integer divisions.
+template <class T, int R, int K>
 __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
+    constexpr int P = (K - 1) / 2;
     constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
     __shared__ float sA[LH * LW];
     __shared__ float sB[LH * BTW];
-    const int Ho = a.H * a.r, Wo = a.W * a.r;
+    const int Ho = a.H * R, Wo = a.W * R;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
     const int tx = bid % tilesX; bid /= tilesX;
@@ -928,16 +944,19 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
     const int c = bid % a.C, b = bid / a.C;
     const int X0 = tx * BTW, Y0 = ty * BTH;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const T* xb = reinterpret_cast<const T*>(a.x) + (long long)b * a.C * a.r * a.r * a.H * a.W;
+    const long long plane = (long long)a.H * a.W;
+    // the R*R source planes of output channel c of sample b
+    const T* xb = reinterpret_cast<const T*>(a.x) + ((long long)b * a.C + c) * (R * R) * plane;
     float k[K];
 #pragma unroll
     for (int t = 0; t < K; ++t) k[t] = a.k[t];
     // Stage the replicate-clamped source window, one row per wave-iteration.
     for (int ry = wave; ry < LH; ry += 4) {
-        const int Y = min(max(Y0 + ry - a.pad0, 0), Ho - 1);
+        const int Y = min(max(Y0 + ry - P, 0), Ho - 1);
+        const T* src = xb + (Y % R) * R * plane + (long long)(Y / R) * a.W;
         for (int rx = lane; rx < LW; rx += 64) {
-            const int X = min(max(X0 + rx - a.pad0, 0), Wo - 1);
-            sA[ry * LW + rx] = shuffled_at(a, xb, c, Y, X);
+            const int X = min(max(X0 + rx - P, 0), Wo - 1);
+            sA[ry * LW + rx] = ld(src + (X % R) * plane + X / R);
         }
     }
     __syncthreads();
@@ -964,80 +983,74 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
     }
 }
 
-// Adjoint: dS(Y, X) = sum_{y, x} wy(y, Y) wx(x, X) dout(y, x) with y in
-// [Y - (K-1-pad0), Y + pad0] (clipped); interior weights are k[K-1-j], rows/columns within
-// K of the border use the exact replicate-folded weights. dS is written straight into the
-// pre-shuffle layout of dx.
-template <class T, int K>
+// Adjoint, separable: along each axis dS[s] = sum_t k[t] dout[s + P - t] (zero outside the
+// image) for every sample, plus the replicate-padding fold at the two border samples
+// (BlurArgs::clo / chi). dS is written straight into the pre-shuffle layout of dx.
+template <class T, int R, int K>
 __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
+    constexpr int P = (K - 1) / 2, Q = K - 1 - P;
     constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
     __shared__ float sA[LH * LW];
     __shared__ float sB[LH * BTW];
-    const int Ho = a.H * a.r, Wo = a.W * a.r;
+    const int Ho = a.H * R, Wo = a.W * R;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
     const int tx = bid % tilesX; bid /= tilesX;
     const int ty = bid % tilesY; bid /= tilesY;
     const int c = bid % a.C, b = bid / a.C;
     const int X0 = tx * BTW, Y0 = ty * BTH;
-    const int rlo = K - 1 - a.pad0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
+    // window row ry / column rx <-> dout (Y0 - Q + ry, X0 - Q + rx), zero outside the image
     for (int ry = wave; ry < LH; ry += 4) {
-        const int y = Y0 + ry - rlo;
+        const int y = Y0 + ry - Q;
         const bool yok = y >= 0 && y < Ho;
         for (int rx = lane; rx < LW; rx += 64) {
-            const int x = X0 + rx - rlo;
+            const int x = X0 + rx - Q;
             sA[ry * LW + rx] = (yok && x >= 0 && x < Wo) ? ld(gp + (long long)y * Wo + x) : 0.f;
         }
     }
     __syncthreads();
-    const int X = X0 + lane;
-    const bool xedge = X < K || X >= Wo - K;
-    for (int r = wave; r < LH; r += 4) {
-        float acc = 0.f;
-        if (!xedge) {
+    float kr[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) acc = fmaf(a.k[K - 1 - j], sA[r * LW + lane + j], acc);
-        } else if (X < Wo) {
-            for (int j = 0; j < K; ++j) {
-                const int x = X - rlo + j;
-                if (x >= 0 && x < Wo) acc = fmaf(axis_weight(a, x, X, Wo), sA[r * LW + lane + j], acc);
-            }
-        }
+    for (int j = 0; j < K; ++j) kr[j] = a.k[K - 1 - j];
+    const int X = X0 + lane;
+    for (int r = wave; r < LH; r += 4) {
+        const float* row = sA + r * LW;
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc = fmaf(kr[j], row[lane + j], acc);
+        if (X == 0)
+            for (int o = 0; o < P && o < Wo; ++o) acc = fmaf(a.clo[o], row[o + Q], acc);
+        if (X == Wo - 1)
+            for (int m = 0; m < Q && m < Wo; ++m) acc = fmaf(a.chi[m], row[lane - m + Q], acc);
         sB[r * BTW + lane] = acc;
     }
     __syncthreads();
     if (X >= Wo) return;
-    const int r = a.r;
-    T* dxb = reinterpret_cast<T*>(dx) + (long long)b * a.C * r * r * a.H * a.W;
+    const long long plane = (long long)a.H * a.W;
+    T* dxb = reinterpret_cast<T*>(dx) + ((long long)b * a.C + c) * (R * R) * plane + (X % R) * plane + X / R;
     for (int i = 0; i < BTH / 4; ++i) {
         const int ry = wave * (BTH / 4) + i;
         const int Y = Y0 + ry;
         if (Y >= Ho) break;
         float acc = 0.f;
-        if (Y >= K && Y < Ho - K) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) acc = fmaf(a.k[K - 1 - j], sB[(ry + j) * BTW + lane], acc);
-        } else {
-            for (int j = 0; j < K; ++j) {
-                const int y = Y - rlo + j;
-                if (y >= 0 && y < Ho) acc = fmaf(axis_weight(a, y, Y, Ho), sB[(ry + j) * BTW + lane], acc);
-            }
-        }
-        const long long off = r == 1 ? ((long long)c * a.H + Y) * a.W + X
-                                     : ((long long)(c * r * r + (Y % r) * r + X % r) * a.H + Y / r) * a.W + X / r;
-        st(dxb + off, acc);
+        for (int j = 0; j < K; ++j) acc = fmaf(kr[j], sB[(ry + j) * BTW + lane], acc);
+        if (Y == 0)
+            for (int o = 0; o < P && o < Ho; ++o) acc = fmaf(a.clo[o], sB[(o + Q) * BTW + lane], acc);
+        if (Y == Ho - 1)
+            for (int m = 0; m < Q && m < Ho; ++m) acc = fmaf(a.chi[m], sB[(ry - m + Q) * BTW + lane], acc);
+        st(dxb + (Y % R) * R * plane + (long long)(Y / R) * a.W, acc);
     }
 }
 
-template <class T>
-int blur_launch(BlurArgs& a, int mode, const void* dout, void* dx, long long grid, hipStream_t st) {
-    const dim3 g((unsigned)grid);
+template <class T, int R>
+int blur_launch_r(BlurArgs& a, int mode, const void* dout, void* dx, const dim3& g, hipStream_t st) {
 #define BLUR_CASE(KK)                                                                        \
     case KK:                                                                                 \
-        if (mode == 0) hipLaunchKernelGGL((blur_fwd<T, KK>), g, dim3(NT), 0, st, a);         \
-        else hipLaunchKernelGGL((blur_bwd<T, KK>), g, dim3(NT), 0, st, a, dout, dx);         \
+        if (mode == 0) hipLaunchKernelGGL((blur_fwd<T, R, KK>), g, dim3(NT), 0, st, a);      \
+        else hipLaunchKernelGGL((blur_bwd<T, R, KK>), g, dim3(NT), 0, st, a, dout, dx);      \
         break;
     switch (a.K) {
         BLUR_CASE(1) BLUR_CASE(2) BLUR_CASE(3) BLUR_CASE(4) BLUR_CASE(5) BLUR_CASE(6) BLUR_CASE(7) BLUR_CASE(8)
@@ -1045,6 +1058,22 @@ int blur_launch(BlurArgs& a, int mode, const void* dout, void* dx, long long gri
     }
 #undef BLUR_CASE
     return launch_status();
+}
+
+template <class T>
+int blur_launch(BlurArgs& a, int mode, const void* dout, void* dx, long long grid, hipStream_t st) {
+    const dim3 g((unsigned)grid);
+    // edge-fold weights of the adjoint (see BlurArgs)
+    const int P = (a.K - 1) / 2, Q = a.K - 1 - P;
+    for (int o = 0; o < 8; ++o) {
+        a.clo[o] = 0.f;
+        for (int t = 0; o < P && t <= P - 1 - o; ++t) a.clo[o] += a.k[t];
+        a.chi[o] = 0.f;
+        for (int t = P + 1 + o; o < Q && t < a.K; ++t) a.chi[o] += a.k[t];
+    }
+    if (a.r == 1) return blur_launch_r<T, 1>(a, mode, dout, dx, g, st);
+    if (a.r == 2) return blur_launch_r<T, 2>(a, mode, dout, dx, g, st);
+    return VFM_ERR_ARGS;
 }
 
 }  // namespace
@@ -1086,9 +1115,9 @@ extern "C" int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, 
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
     DwRowArgs r{};
     r.B = B; r.C = C; r.H = H; r.W = W;
-    if (dwr_plan(r, K, pad)) return r.wpp;
+    if (dwr_plan(r, K, pad)) return r.wpc;       // partial [wpc, C, K*K+1]
     dw_plan(a);
-    return a.tilesX;
+    return a.tilesX * B;                          // partial [tilesX][B][C][K*K+1] = [tilesX*B, C, K*K+1]
 }
 
 extern "C" int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int dtype, int B, int C, int H,

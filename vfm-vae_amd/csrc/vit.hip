@@ -1,0 +1,152 @@
+// Row kernels of the frozen ViT towers (SigLIP2 encoder) for gfx950.
+//
+// Reference: HF SiglipEncoderLayer under bf16 autocast, as called by
+// networks/utils/vfms/siglip2_utils.py:114-137: the fp32 residual stream h is normalised by
+// LayerNorm (fp32 statistics) and handed to the bf16 GEMMs, and every sub-block output is
+// added back to h in fp32. Unfused, torch runs LayerNorm (fp32 out) + a cast kernel, and a
+// cast + add for every residual; here one pass per row does
+//     h' = h + delta            (optional; delta in the GEMM dtype, h' written in fp32)
+//     y  = LN(h') * w + b       (written directly in the GEMM dtype)
+// so each residual/LN pair moves 4+2 bytes in and 4+2 bytes out per element.
+//
+// One wave per row, D = 256 * NCH (NCH float4 chunks per lane kept in registers: exact
+// two-pass mean / variance, no re-read).
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+struct LnArgs {
+    const float* h;       // [rows, D] fp32
+    const void* delta;    // [rows, D] (dtype_delta) or null
+    float* h_out;         // [rows, D] fp32 or null (h + delta)
+    const float* w;       // [D] or null
+    const float* b;       // [D] or null
+    void* y;              // [rows, D] dtype_out
+    int rows, D;
+    float eps;
+};
+
+template <class T>
+__device__ __forceinline__ void ld4v(const T* p, float* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = ld(p + i);
+}
+template <>
+__device__ __forceinline__ void ld4v<__hip_bfloat16>(const __hip_bfloat16* p, float* v) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16);
+    v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16);
+    v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ void ld4v<float>(const float* p, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+template <class T>
+__device__ __forceinline__ void st4v(T* p, const float* v) {
+    T t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st(&t[i], v[i]);
+    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(t);
+}
+template <>
+__device__ __forceinline__ void st4v<float>(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+template <class TD, class TO, int NCH>
+__global__ __launch_bounds__(256) void ln_rows(LnArgs a) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= a.rows) return;
+    const int lane = threadIdx.x & 63;
+    const long long off = (long long)row * a.D;
+    float v[NCH][4];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) ld4v(a.h + off + (j * 64 + lane) * 4, v[j]);
+    if (a.delta) {
+        const TD* dp = reinterpret_cast<const TD*>(a.delta) + off;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            float d[4];
+            ld4v(dp + (j * 64 + lane) * 4, d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[j][i] += d[i];
+        }
+        if (a.h_out) {
+#pragma unroll
+            for (int j = 0; j < NCH; ++j) st4v(a.h_out + off + (j * 64 + lane) * 4, v[j]);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    const float mean = wsum(s) / (float)a.D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float d = v[j][i] - mean;
+            q = fmaf(d, d, q);
+        }
+    const float rstd = rsqrtf(wsum(q) / (float)a.D + a.eps);
+    TO* yp = reinterpret_cast<TO*>(a.y) + off;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+        const int c0 = (j * 64 + lane) * 4;
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float wv = a.w ? a.w[c0 + i] : 1.f, bv = a.b ? a.b[c0 + i] : 0.f;
+            o[i] = fmaf((v[j][i] - mean) * rstd, wv, bv);
+        }
+        st4v(yp + c0, o);
+    }
+}
+
+template <class TD, class TO>
+int ln_dispatch(LnArgs& a, hipStream_t st) {
+    const dim3 grid((unsigned)((a.rows + 3) / 4)), blk(256);
+    switch (a.D / 256) {
+    case 1: hipLaunchKernelGGL((ln_rows<TD, TO, 1>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((ln_rows<TD, TO, 2>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((ln_rows<TD, TO, 3>), grid, blk, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((ln_rows<TD, TO, 4>), grid, blk, 0, st, a); break;
+    case 5: hipLaunchKernelGGL((ln_rows<TD, TO, 5>), grid, blk, 0, st, a); break;
+    case 6: hipLaunchKernelGGL((ln_rows<TD, TO, 6>), grid, blk, 0, st, a); break;
+    case 8: hipLaunchKernelGGL((ln_rows<TD, TO, 8>), grid, blk, 0, st, a); break;
+    default: return VFM_NO_KERNEL;
+    }
+    return launch_status();
+}
+
+}  // namespace
+
+extern "C" int vfm_residual_layer_norm(const float* h, const void* delta, float* h_out, const float* w,
+                                       const float* b, void* y, int dtype_delta, int dtype_out, int rows, int D,
+                                       float eps, void* stream) {
+    if (!h || !y || rows < 0 || D <= 0) return VFM_ERR_ARGS;
+    if (D % 256 || D > 2048) return VFM_NO_KERNEL;
+    if (rows == 0) return VFM_OK;
+    LnArgs a{h, delta, h_out, w, b, y, rows, D, eps};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define LN_OUT(TD)                                                            \
+    if (dtype_out == VFM_F32) return ln_dispatch<TD, float>(a, st);           \
+    if (dtype_out == VFM_BF16) return ln_dispatch<TD, __hip_bfloat16>(a, st); \
+    if (dtype_out == VFM_F16) return ln_dispatch<TD, __half>(a, st);
+    if (!delta || dtype_delta == VFM_F32) { LN_OUT(float) }
+    else if (dtype_delta == VFM_BF16) { LN_OUT(__hip_bfloat16) }
+    else if (dtype_delta == VFM_F16) { LN_OUT(__half) }
+#undef LN_OUT
+    return VFM_ERR_ARGS;
+}

@@ -158,6 +158,17 @@ class SiglipEncoderLayer(nn.Module):
         m = self.mlp(vit_ops.layer_norm(h, self.layer_norm2, compute_dtype))
         return vit_ops.residual_add(h, m)
 
+    def forward_chained(self, h, y1, next_ln, next_dtype, compute_dtype=torch.bfloat16):
+        """Same math as forward() with the LayerNorms fused into the residual adds:
+        y1 = layer_norm1(h) (computed by the caller), returns (h_out, next_ln(h_out))
+        (next_ln None -> (h_out, None))."""
+        a = self.self_attn(y1)
+        h, y2 = vit_ops.residual_layer_norm(h, a, self.layer_norm2, compute_dtype)
+        m = self.mlp(y2)
+        if next_ln is None:
+            return vit_ops.residual_add(h, m), None
+        return vit_ops.residual_layer_norm(h, m, next_ln, next_dtype)
+
 
 class SiglipEncoder(nn.Module):
     def __init__(self, cfg):
@@ -268,14 +279,24 @@ class SiglipVisionModel(nn.Module):
         saved = {0: h} if 0 in want else {}
         n_layers = len(vm.encoder.layers)
         last_needed = n_layers if (want_last or want_pooled) else max([i for i in want if i > 0], default=0)
-        for i, layer in enumerate(vm.encoder.layers[:last_needed], start=1):
-            h = layer(h, compute_dtype)
-            if i in want:
-                saved[i] = h
+        layers = vm.encoder.layers[:last_needed]
         last = pooled = None
-        if want_last or want_pooled:
-            last = F.layer_norm(h, (h.shape[-1],), vm.post_layernorm.weight, vm.post_layernorm.bias,
-                                vm.post_layernorm.eps)
+        if layers:
+            # each layer's input LayerNorm is fused into the previous residual add; the last
+            # one's into post_layernorm (fp32 out, as LayerNorm under autocast)
+            y = vit_ops.layer_norm(h, layers[0].layer_norm1, compute_dtype)
+            for i, layer in enumerate(layers, start=1):
+                if i < len(layers):
+                    nxt, ndt = layers[i].layer_norm1, compute_dtype
+                elif want_last or want_pooled:
+                    nxt, ndt = vm.post_layernorm, torch.float32
+                else:
+                    nxt, ndt = None, None
+                h, y = layer.forward_chained(h, y, nxt, ndt, compute_dtype)
+                if i in want:
+                    saved[i] = h
+            if want_last or want_pooled:
+                last = y
         if want_pooled and vm.use_head:
             pooled = vm.head(last).float()
         return saved, last, pooled

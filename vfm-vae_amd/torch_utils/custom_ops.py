@@ -47,6 +47,7 @@ SIGNATURES = {
     "vfm_shuffle_blur_fwd": [c_vp, c_vp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_shuffle_blur_bwd": [c_vp, c_vp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_codebook_argmax": [c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp, c_vp],
+    "vfm_residual_layer_norm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_vp],
 }
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}

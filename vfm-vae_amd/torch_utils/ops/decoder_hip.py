@@ -63,7 +63,7 @@ def supported(op, x, **kw):
     if op == 'group_norm':
         return x.ndim >= 3 and x.shape[1] % kw['groups'] == 0
     if op == 'shuffle_blur':
-        return 1 <= kw['k'] <= 8
+        return 1 <= kw['k'] <= 8 and kw.get('r', 1) in (1, 2)
     return False
 
 
@@ -152,11 +152,11 @@ class _DwConv2d(torch.autograd.Function):
             tiles = _lib.vfm_dwconv2d_bwd_weight_tiles(B, C, H, W, K, pad)
             if tiles <= 0:
                 raise custom_ops.NativeError(f"vfm_dwconv2d_bwd_weight_tiles failed with code {tiles}")
-            part = torch.empty([tiles, B * C, K * K + 1], dtype=torch.float32, device=x.device)
+            part = torch.empty([tiles, C, K * K + 1], dtype=torch.float32, device=x.device)
             with kernel_timer.region('dwconv2d_bwd_weight', _nb(x, dy)):
                 _check(_lib.vfm_dwconv2d_bwd_weight(x.data_ptr(), dy.data_ptr(), part.data_ptr(), _code(x),
                                                     B, C, H, W, K, pad, _stream()), 'vfm_dwconv2d_bwd_weight')
-            s = part.sum(0).view(B, C, K * K + 1).sum(0)
+            s = part.sum(0)
             if ctx.needs_input_grad[1]:
                 dw = s[:, :K * K].reshape(wshape).to(wdt)
             if ctx.needs_input_grad[2]:

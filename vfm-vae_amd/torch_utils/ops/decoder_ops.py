@@ -133,7 +133,7 @@ def layer_scale_residual(y, bias, gamma, x_in, impl='cuda'):
 def shuffle_blur(x, blur1d, upscale=2, impl='cuda'):
     """PixelShuffle(upscale) followed by replicate-pad + depthwise blur with the
     normalised outer product of `blur1d` (a python list of taps)."""
-    if _use_hip('shuffle_blur', x, impl, k=len(blur1d)):
+    if _use_hip('shuffle_blur', x, impl, k=len(blur1d), r=upscale):
         from . import decoder_hip
         return decoder_hip.shuffle_blur(x, blur1d, upscale)
     y = F.pixel_shuffle(x, upscale)

@@ -5,18 +5,19 @@ Reference math: HF `SiglipEncoderLayer` / timm `Block` as used by
 under bf16 autocast: GEMMs in the compute dtype with fp32 accumulation,
 LayerNorm and residual stream in fp32.
 
-GEMMs are plain library GEMMs (hipBLASLt through torch.matmul, MFMA); the
-epilogues (bias + tanh-GELU) and LayerNorm->bf16 have HIP kernels registered
-by `vit_hip` when the native library is present.
+GEMMs are plain library GEMMs (hipBLASLt through torch.matmul, MFMA). On ROCm
+tensors outside autograd (the frozen towers), fc1's bias + tanh-GELU runs as the
+hipBLASLt GELU_BIAS epilogue (torch._addmm_activation, the tanh form SigLIP
+uses), and LayerNorm -> compute dtype (optionally fused with the residual add)
+is one HIP row kernel (`vit_hip`, csrc/vit.hip).
 """
 import torch
 import torch.nn.functional as F
 
-_HIP_OPS = set()
 
-
-def _hip(name, x):
-    return x.is_cuda and name in _HIP_OPS
+def _frozen(*ts):
+    """ROCm tensors that need no autograd graph."""
+    return ts[0].is_cuda and not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
 
 
 def patch_embed(pixels, weight, bias, patch, compute_dtype):
@@ -40,18 +41,30 @@ def linear(x, w, b=None):
 
 
 def linear_gelu_tanh(x, w, b=None):
-    if _hip("bias_gelu_tanh", x):
-        from . import vit_hip
-        return vit_hip.linear_gelu_tanh(x, w, b)
+    """gelu_tanh(x @ w^T + b): GEMM with the GELU_BIAS epilogue on ROCm (frozen towers)."""
+    if b is not None and x.dtype != torch.float32 and _frozen(x, w, b):
+        y = torch._addmm_activation(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
+        return y.reshape(*x.shape[:-1], w.shape[0])
     return F.gelu(linear(x, w, b), approximate="tanh")
 
 
 def layer_norm(h, ln, out_dtype):
     """LayerNorm of the fp32 residual stream, emitted in the GEMM compute dtype."""
-    if _hip("layer_norm", h):
+    if _frozen(h):
         from . import vit_hip
-        return vit_hip.layer_norm(h, ln.weight, ln.bias, ln.eps, out_dtype)
+        if vit_hip.supported(h):
+            return vit_hip.residual_layer_norm(h, None, ln, out_dtype)[1]
     return F.layer_norm(h.float(), (h.shape[-1],), ln.weight.float(), ln.bias.float(), ln.eps).to(out_dtype)
+
+
+def residual_layer_norm(h, delta, ln, out_dtype):
+    """(h + delta, LayerNorm(h + delta) in out_dtype) -- one pass on ROCm (frozen towers)."""
+    if _frozen(h, delta):
+        from . import vit_hip
+        if vit_hip.supported(h):
+            return vit_hip.residual_layer_norm(h, delta, ln, out_dtype)
+    h = residual_add(h, delta)
+    return h, F.layer_norm(h, (h.shape[-1],), ln.weight.float(), ln.bias.float(), ln.eps).to(out_dtype)
 
 
 def residual_add(h, delta):
