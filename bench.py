@@ -38,6 +38,7 @@ import yaml
 
 CONFIG = os.path.join(PKG, "configs", "vfm_vae_f16d32_siglip2_stage_0_synthetic.yaml")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 BF16_PEAK_TFLOPS = 2500.0      # dense
 
 
@@ -187,7 +188,12 @@ def main(argv=None):
     ms_per_step = dt / args.steps * 1e3
     value = args.batch * world * args.steps / dt
 
-    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS)
+    traffic_table = None
+    if os.path.exists(PMC_TRAFFIC):       # committed PMC passes of this workload (tools_dev/pmc_traffic.py)
+        traffic_table = json.load(open(PMC_TRAFFIC)).get("kernels")
+    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table)
+    if roof is not None:
+        roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -18,6 +18,10 @@ for s in "$@"; do
                && python tools_dev/prof_summary.py $(find $out/prof -name '*kernel_trace.csv' | head -1) 3 \
                     $(sed -n 's/.*timed 3 steps: \([0-9.]*\)s.*/\1/p' $out/prof.log) > $out/prof_summary.txt \
                && find $out/prof -name '*kernel_trace.csv' -delete ;;
+    pmc)     re=${PMC_RE:-gelu_bwd}
+             timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" -d $out/pmc_f -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_f.log 2>&1 \
+               && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" -d $out/pmc_w -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_w.log 2>&1 \
+               && python tools_dev/pmc_traffic.py $out/pmc_f $out/pmc_w > $out/pmc_traffic.json ;;
     decbench) timeout -k 10 300 python tools_dev/decbench.py > $out/decbench.log 2>&1 ;;
     opbench) timeout -k 10 300 python tools_dev/opbench.py > $out/opbench.log 2>&1 ;;
     dtests)  timeout -k 10 600 python -m pytest tests/test_decoder_gpu.py -q -x > $out/dtests.log 2>&1 ;;

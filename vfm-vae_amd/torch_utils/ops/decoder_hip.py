@@ -45,12 +45,49 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+_DT = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16", torch.float64: "f64"}
+
+
+def _rn(name, t, *extra):
+    """kernel_timer region name: op + template parameters (dtype, tap count), so a timed
+    entry maps onto one kernel instantiation of the rocprofv3 trace."""
+    return f"{name}<{','.join([_DT.get(t.dtype, str(t.dtype))] + [str(e) for e in extra])}>"
+
+
 def _nb(*ts):
     return sum(t.numel() * t.element_size() for t in ts if t is not None)
 
 
 def _check(rc, name):
     custom_ops.check(rc, name)
+
+
+def _edges(ctx, *args):
+    """Map forward-argument index -> index into ctx.next_functions (which has one entry per
+    tensor argument, None/int arguments have no edge)."""
+    n, edge = 0, []
+    for a in args:
+        edge.append(n if isinstance(a, torch.Tensor) else None)
+        n += isinstance(a, torch.Tensor)
+    ctx.edge = edge
+
+
+def _wanted(ctx, i):
+    """Input i needs a gradient in THIS backward pass: requires_grad at forward time AND the
+    autograd engine will run the node that consumes it. `torch.autograd.grad(loss, inputs)`
+    executes only the graph between loss and `inputs` -- e.g. the adaptive VF weight's
+    grad(rec_loss, last_layer) (reference training/loss.py:262-271) runs the decoder backward
+    for the data path only -- so parameter gradients are skipped there exactly as torch's
+    built-in conv/matmul backward nodes skip them."""
+    if not ctx.needs_input_grad[i]:
+        return False
+    fn = ctx.next_functions[ctx.edge[i]][0]
+    if fn is None:
+        return False
+    try:
+        return bool(torch._C._will_engine_execute_node(fn))
+    except RuntimeError:          # not inside an engine-driven backward
+        return True
 
 
 def supported(op, x, **kw):
@@ -74,6 +111,7 @@ def supported(op, x, **kw):
 class _Pointwise(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, x):
+        _edges(ctx, w, x)
         x = x.contiguous()
         B, I, P = x.shape
         O = w.shape[0]
@@ -90,14 +128,14 @@ class _Pointwise(torch.autograd.Function):
         O = wc.shape[0]
         dy = dy.contiguous()
         dw = dx = None
-        if ctx.needs_input_grad[0]:
+        if _wanted(ctx, 0):
             # sum_b dy[b] @ x[b]^T with fp32 per-sample products, summed in fp32
             if dy.dtype != torch.float32:
                 dw = torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32)
             else:
                 dw = torch.bmm(dy, x.transpose(1, 2))
             dw = dw.sum(0).to(ctx.wdt)
-        if ctx.needs_input_grad[1]:
+        if _wanted(ctx, 1):
             dx = torch.bmm(wc.t().expand(B, I, O), dy)
         return dw, dx
 
@@ -115,7 +153,7 @@ def _dw_fwd(x, w3, bias, noise, pad, name):
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
     y = torch.empty([B, C, Ho, Wo], dtype=x.dtype, device=x.device)
-    with kernel_timer.region(name, _nb(x, y)):
+    with kernel_timer.region(_rn(name, x, K), _nb(x, y)):
         _check(_lib.vfm_dwconv2d_fwd(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
                                      B, C, H, W, K, pad, _stream()), name)
     return y
@@ -124,6 +162,7 @@ def _dw_fwd(x, w3, bias, noise, pad, name):
 class _DwConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, noise, pad):
+        _edges(ctx, x, weight, bias, noise, pad)
         x = _c(x)
         C, K = weight.shape[0], weight.shape[-1]
         w3 = weight.detach().reshape(C, K, K).float().contiguous()
@@ -146,22 +185,23 @@ class _DwConv2d(torch.autograd.Function):
         B, C, H, W = x.shape
         K = w3.shape[-1]
         dx = dw = db = dn = None
-        if ctx.needs_input_grad[0]:
+        want_w, want_b = _wanted(ctx, 1), _wanted(ctx, 2)
+        if _wanted(ctx, 0):
             dx = _dw_fwd(dy, torch.flip(w3, [1, 2]).contiguous(), None, None, K - 1 - pad, 'dwconv2d_bwd_data')
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        if want_w or want_b:
             tiles = _lib.vfm_dwconv2d_bwd_weight_tiles(B, C, H, W, K, pad)
             if tiles <= 0:
                 raise custom_ops.NativeError(f"vfm_dwconv2d_bwd_weight_tiles failed with code {tiles}")
             part = torch.empty([tiles, C, K * K + 1], dtype=torch.float32, device=x.device)
-            with kernel_timer.region('dwconv2d_bwd_weight', _nb(x, dy)):
+            with kernel_timer.region(_rn('dwconv2d_bwd_weight', x, K), _nb(x, dy)):
                 _check(_lib.vfm_dwconv2d_bwd_weight(x.data_ptr(), dy.data_ptr(), part.data_ptr(), _code(x),
                                                     B, C, H, W, K, pad, _stream()), 'vfm_dwconv2d_bwd_weight')
             s = part.sum(0)
-            if ctx.needs_input_grad[1]:
+            if want_w:
                 dw = s[:, :K * K].reshape(wshape).to(wdt)
-            if ctx.needs_input_grad[2]:
+            if want_b:
                 db = s[:, K * K].to(bdt)
-        if ctx.needs_input_grad[3]:
+        if _wanted(ctx, 3):
             dn = dy.float().sum(dim=(0, 1)).to(ndt)
         return dx, dw, db, dn, None
 
@@ -178,6 +218,7 @@ def dwconv2d(x, weight, bias, padding, noise):
 class _GroupNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, style, groups, eps, out_dtype):
+        _edges(ctx, x, weight, bias, style, groups, eps, out_dtype)
         x = _c(x)
         B, C = x.shape[:2]
         HW = x[0, 0].numel()
@@ -186,7 +227,7 @@ class _GroupNorm(torch.autograd.Function):
         y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
         mean = torch.empty([B * groups], dtype=torch.float32, device=x.device)
         rstd = torch.empty_like(mean)
-        with kernel_timer.region('group_norm_fwd', _nb(x, y)):
+        with kernel_timer.region(_rn('group_norm_fwd', x), _nb(x, y)):
             _check(_lib.vfm_group_norm_fwd(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), mean.data_ptr(),
                                            rstd.data_ptr(), _code(x), _code(y), B, C, groups, HW, float(eps),
                                            _stream()), 'vfm_group_norm_fwd')
@@ -206,15 +247,15 @@ class _GroupNorm(torch.autograd.Function):
         dwp = torch.empty([B, C], dtype=torch.float32, device=x.device)
         dbp = torch.empty_like(dwp)
         ds = torch.empty_like(dwp) if s is not None else None
-        with kernel_timer.region('group_norm_bwd', _nb(x, dy, dx)):
+        with kernel_timer.region(_rn('group_norm_bwd', x), _nb(x, dy, dx)):
             _check(_lib.vfm_group_norm_bwd(x.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _p(w),
                                            _p(b), _p(s), dx.data_ptr(), dwp.data_ptr(), dbp.data_ptr(), _p(ds),
                                            _code(x), _code(dy), B, C, ctx.groups, HW, _stream()),
                    'vfm_group_norm_bwd')
         wdt, bdt, sdt = ctx.meta
-        dw = dwp.sum(0).to(wdt) if ctx.needs_input_grad[1] else None
-        db = dbp.sum(0).to(bdt) if ctx.needs_input_grad[2] else None
-        dst = ds.to(sdt) if ctx.needs_input_grad[3] else None
+        dw = dwp.sum(0).to(wdt) if _wanted(ctx, 1) else None
+        db = dbp.sum(0).to(bdt) if _wanted(ctx, 2) else None
+        dst = ds.to(sdt) if _wanted(ctx, 3) else None
         return (dx if ctx.needs_input_grad[0] else None), dw, db, dst, None, None, None
 
 
@@ -230,12 +271,13 @@ def group_norm(x, num_groups, weight, bias, eps, out_dtype, style):
 class _ScaleBiasGelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, scale, bias):
+        _edges(ctx, h, scale, bias)
         h = _c(h)
         B, O = h.shape[:2]
         P = h[0, 0].numel()
         s, b = _f32(scale), _f32(bias)
         g = torch.empty_like(h)
-        with kernel_timer.region('scale_bias_gelu_fwd', _nb(h, g)):
+        with kernel_timer.region(_rn('scale_bias_gelu_fwd', h), _nb(h, g)):
             _check(_lib.vfm_scale_bias_gelu_fwd(h.data_ptr(), _p(s), _p(b), g.data_ptr(), _code(h), B, O, P,
                                                 _stream()), 'vfm_scale_bias_gelu_fwd')
         ctx.save_for_backward(h, s, b)
@@ -250,16 +292,16 @@ class _ScaleBiasGelu(torch.autograd.Function):
         P = h[0, 0].numel()
         dg = _c(dg)
         dh = torch.empty_like(h)
-        want_s = s is not None and ctx.needs_input_grad[1]
+        want_s = s is not None and _wanted(ctx, 1)
         ds_rows = torch.empty([B * O], dtype=torch.float32, device=h.device) if want_s else None
         db_rows = torch.empty([B * O], dtype=torch.float32, device=h.device)
-        with kernel_timer.region('scale_bias_gelu_bwd', _nb(h, dg, dh)):
+        with kernel_timer.region(_rn('scale_bias_gelu_bwd', h), _nb(h, dg, dh)):
             _check(_lib.vfm_scale_bias_gelu_bwd(h.data_ptr(), dg.data_ptr(), _p(s), _p(b), dh.data_ptr(),
                                                 _p(ds_rows), db_rows.data_ptr(), _code(h), B, O, P, _stream()),
                    'vfm_scale_bias_gelu_bwd')
         sdt, bdt = ctx.meta
         ds = ds_rows.view(B, O).to(sdt) if want_s else None
-        db = db_rows.view(B, O).sum(0).to(bdt) if (b is not None and ctx.needs_input_grad[2]) else None
+        db = db_rows.view(B, O).sum(0).to(bdt) if (b is not None and _wanted(ctx, 2)) else None
         return (dh if ctx.needs_input_grad[0] else None), ds, db
 
 
@@ -274,12 +316,13 @@ def scale_bias_gelu(h, scale, bias):
 class _LayerScaleResidual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, bias, gamma, x_in):
+        _edges(ctx, y, bias, gamma, x_in)
         y, x_in = _c(y), _c(x_in)
         B, C = y.shape[:2]
         P = y[0, 0].numel()
         b, g = _f32(bias), _f32(gamma)
         out = torch.empty(x_in.shape, dtype=x_in.dtype, device=x_in.device)
-        with kernel_timer.region('layer_scale_residual_fwd', _nb(y, x_in, out)):
+        with kernel_timer.region(_rn('layer_scale_residual_fwd', y), _nb(y, x_in, out)):
             _check(_lib.vfm_layer_scale_residual_fwd(y.data_ptr(), _p(b), _p(g), x_in.data_ptr(), out.data_ptr(),
                                                      _code(y), _code(x_in), B, C, P, _stream()),
                    'vfm_layer_scale_residual_fwd')
@@ -298,15 +341,15 @@ class _LayerScaleResidual(torch.autograd.Function):
         dy = torch.empty_like(y)
         r0 = torch.empty([B * C], dtype=torch.float32, device=y.device)
         r1 = torch.empty_like(r0)
-        with kernel_timer.region('layer_scale_residual_bwd', _nb(y, dout, dy)):
+        with kernel_timer.region(_rn('layer_scale_residual_bwd', y), _nb(y, dout, dy)):
             _check(_lib.vfm_layer_scale_residual_bwd(y.data_ptr(), _p(b), _p(g), dout.data_ptr(), dy.data_ptr(),
                                                      r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout), B, C, P,
                                                      _stream()), 'vfm_layer_scale_residual_bwd')
         db = dg = None
-        if b is not None and ctx.needs_input_grad[1]:
+        if b is not None and _wanted(ctx, 1):
             s1 = r1.view(B, C).sum(0)
             db = (s1 * g if g is not None else s1).to(bdt)
-        if g is not None and ctx.needs_input_grad[2]:
+        if g is not None and _wanted(ctx, 2):
             dg = r0.view(B, C).sum(0).to(gdt)
         return (dy if ctx.needs_input_grad[0] else None), db, dg, (dout if ctx.needs_input_grad[3] else None)
 
@@ -338,7 +381,7 @@ class _ShuffleBlur(torch.autograd.Function):
         C = Cr // (r * r)
         taps, K = _taps(blur1d)
         y = torch.empty([B, C, H * r, W * r], dtype=x.dtype, device=x.device)
-        with kernel_timer.region('shuffle_blur_fwd', _nb(x, y)):
+        with kernel_timer.region(_rn('shuffle_blur_fwd', x, K), _nb(x, y)):
             _check(_lib.vfm_shuffle_blur_fwd(x.data_ptr(), y.data_ptr(), taps, K, _code(x), B, C, H, W, r, _stream()),
                    'vfm_shuffle_blur_fwd')
         ctx.cfg = (tuple(blur1d), r, (B, C, H, W))
@@ -351,7 +394,7 @@ class _ShuffleBlur(torch.autograd.Function):
         dy = _c(dy)
         taps, K = _taps(blur1d)
         dx = torch.empty([B, C * r * r, H, W], dtype=dy.dtype, device=dy.device)
-        with kernel_timer.region('shuffle_blur_bwd', _nb(dy, dx)):
+        with kernel_timer.region(_rn('shuffle_blur_bwd', dy, K), _nb(dy, dx)):
             _check(_lib.vfm_shuffle_blur_bwd(dy.data_ptr(), dx.data_ptr(), taps, K, _code(dy), B, C, H, W, r,
                                              _stream()), 'vfm_shuffle_blur_bwd')
         return dx, None, None

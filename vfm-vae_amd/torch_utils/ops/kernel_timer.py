@@ -52,7 +52,34 @@ def summary():
     return out
 
 
-def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops):
+# region name (op<dtype[,taps]>) -> the kernel instantiation(s) it launches, as rocprofv3 prints
+# them (anonymous namespace and call arguments stripped); used to match the HIP-event timing
+# against the rocprof summary and the PMC traffic of the same kernel.
+_ROC = {
+    "scale_bias_gelu_fwd": "gelu_fwd<{T}>", "scale_bias_gelu_bwd": "gelu_bwd<{T}>",
+    "layer_scale_residual_fwd": "lsr_fwd<{T}, ", "layer_scale_residual_bwd": "lsr_bwd<{T}, ",
+    "group_norm_fwd": "gn_fwd<{T}, ", "group_norm_bwd": "gn_bwd<{T}, ",
+    "dwconv2d_fwd": "dwr_fwd<{T}, {K}>", "dwconv2d_bwd_data": "dwr_fwd<{T}, {K}>",
+    "dwconv2d_bwd_weight": "dwr_bwd_w<{T}, {K}>",
+    "shuffle_blur_fwd": "blur_fwd<{T}, 2, {K}>", "shuffle_blur_bwd": "blur_bwd<{T}, 2, {K}>",
+    "residual_layer_norm": "ln_rows<", "codebook_argmax": "codebook_argmax_kernel<",
+}
+_TNAME = {"f32": "float", "bf16": "__hip_bfloat16", "f16": "__half", "f64": "double"}
+
+
+def rocprof_name(region):
+    """'scale_bias_gelu_bwd<bf16>' -> 'gelu_bwd<__hip_bfloat16>' (a prefix of the rocprof name)."""
+    base, _, args = region.partition("<")
+    args = args.rstrip(">").split(",") if args else []
+    pat = _ROC.get(base)
+    if pat is None:
+        return None
+    T = _TNAME.get(args[0], args[0]) if args else ""
+    K = args[1] if len(args) > 1 else ""
+    return pat.format(T=T, K=K)
+
+
+def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None):
     s = summary()
     if not s:
         return None
@@ -64,8 +91,17 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops):
     else:
         achieved = r["bytes"] / t / 1e9
         peak, unit = hbm_peak_gbs, "GB/s"
+    roc = rocprof_name(name)
+    traffic = None
+    if traffic_table and roc:
+        hits = [(v["dispatches_fetch_pass"], v["traffic_bytes_per_launch"]) for k, v in traffic_table.items()
+                if k.startswith(roc) and v.get("traffic_bytes_per_launch")]
+        n = sum(h[0] for h in hits)
+        if n:
+            traffic = int(sum(c * t for c, t in hits) / n)
     return {"bound": r["bound"], "achieved": round(achieved, 1), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": None, "kernel": name, "launches": r["launches"],
+            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": name, "rocprof_kernel": roc,
+            "launches": r["launches"],
             "avg_us": round(r["total_ms"] * 1e3 / r["launches"], 2),
             "bytes_per_launch": int(r["bytes"] / r["launches"]),
             "all_kernels": {k: {"ms": round(v["total_ms"], 3), "launches": v["launches"],
