@@ -25,6 +25,21 @@ def main():
         agg[k][1] += 1
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])[:45]:
         print(f"{v[0] / steps / 1e6:8.2f} ms/step {v[1] / steps:7.1f}/step {v[0] / v[1] / 1e3:8.1f} us  {k}")
+    # idle time on the GPU (launch-bound stretches): gap before each kernel, by kernel name
+    gaps = collections.defaultdict(lambda: [0, 0])
+    idle = 0
+    end = sel[0][1]
+    for s_, e_, n in sel[1:]:
+        g = s_ - end
+        if g > 0:
+            idle += g
+            k = n.replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:110]
+            gaps[k][0] += g
+            gaps[k][1] += 1
+        end = max(end, e_)
+    print(f"\nGPU idle {idle / steps / 1e6:.1f} ms/step; largest idle before:")
+    for k, v in sorted(gaps.items(), key=lambda kv: -kv[1][0])[:25]:
+        print(f"{v[0] / steps / 1e6:8.2f} ms/step {v[1] / steps:7.1f}/step  {k}")
 
 
 if __name__ == "__main__":

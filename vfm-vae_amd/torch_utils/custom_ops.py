@@ -101,7 +101,20 @@ def strides(t: torch.Tensor):
     return arr
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
+    """hipStream_t of the current stream (the raw handle, without building a Stream object:
+    this runs once per kernel launch)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        else:
+            idx = device.index if isinstance(device, torch.device) else int(device)
+            if idx is None:
+                idx = torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -38,7 +38,11 @@ def _c(t):
 
 
 def _f32(t):
-    return None if t is None else t.detach().reshape(-1).float().contiguous()
+    if t is None:
+        return None
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t                      # only the device pointer crosses the ABI
+    return t.detach().reshape(-1).float().contiguous()
 
 
 def _p(t):
@@ -108,6 +112,25 @@ def supported(op, x, **kw):
 # 1x1 conv as a stride-0-batch GEMM (hipBLASLt through torch.bmm), no layout copies.
 
 
+def _cast_cached(w, dtype):
+    """w.detach().to(dtype), cached on the parameter until it changes (its version counter
+    moves at every optimizer step): the D-phase and G-phase forwards of one iteration share
+    one cast of each decoder weight."""
+    if w.dtype == dtype:
+        return w.detach()
+    base = w._base if w._base is not None else w
+    key = (tuple(w.shape), w.stride(), w.storage_offset(), dtype, base._version)
+    hit = getattr(base, "_vfm_cast", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    wc = w.detach().to(dtype)
+    try:
+        base._vfm_cast = (key, wc)
+    except AttributeError:
+        pass
+    return wc
+
+
 class _Pointwise(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, x):
@@ -115,7 +138,7 @@ class _Pointwise(torch.autograd.Function):
         x = x.contiguous()
         B, I, P = x.shape
         O = w.shape[0]
-        wc = w.detach().to(x.dtype)
+        wc = _cast_cached(w, x.dtype)
         ctx.save_for_backward(wc, x)
         ctx.wdt = w.dtype
         return torch.bmm(wc.expand(B, O, I), x)

@@ -26,11 +26,19 @@ def is_enabled():
     return _enabled
 
 
+class _Null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _Null()
+
+
 @contextlib.contextmanager
-def region(name, nbytes=0, flops=0, bound="hbm"):
-    if not _enabled:
-        yield
-        return
+def _timed(name, nbytes, flops, bound):
     st = torch.cuda.current_stream()
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
@@ -40,6 +48,14 @@ def region(name, nbytes=0, flops=0, bound="hbm"):
     finally:
         e.record(st)
         _records.setdefault(name, []).append((s, e, nbytes, flops, bound))
+
+
+def region(name, nbytes=0, flops=0, bound="hbm"):
+    """Context manager around one native launch; a shared no-op object when timing is off
+    (this is on every launch's host path)."""
+    if not _enabled:
+        return _NULL
+    return _timed(name, nbytes, flops, bound)
 
 
 def summary():
