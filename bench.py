@@ -53,6 +53,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
+    ap.add_argument("--no-graphs", action="store_true", help="A/B: eager D-phase generator forward")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
     return ap.parse_args(argv)
 
@@ -110,6 +111,8 @@ def main(argv=None):
     t_start = time.perf_counter()
     c, step = build(args.config, args.batch, device, world)
     _log(rank, f"built in {time.perf_counter() - t_start:.1f}s")
+    if not args.no_graphs:
+        step.loss.enable_graphed_nograd_forward()
     from training.data_synthetic import SyntheticDataset
     pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=rank).make_pool(args.batch, device)
     labels = ['a photo'] * args.batch
@@ -129,6 +132,10 @@ def main(argv=None):
     eqt.forced = None
     torch.cuda.synchronize()
     _log(rank, f"shape warm-up ({len(eqt.variants())} variants): {time.perf_counter() - t1:.1f}s")
+    gr = getattr(step.loss, "graphed_nograd", None)
+    if gr is not None:
+        _log(rank, f"D-phase G forward: {len(gr.graphs)} HIP graphs captured"
+                   + (f"; capture disabled ({gr.disabled})" if gr.disabled else ""))
     step.trace = (lambda m: _log(rank, m)) if args.trace else None
     if args.trace:
         _gc_t = {}
@@ -212,7 +219,8 @@ def main(argv=None):
                        "model": "VFM-VAE f16d32 (SigLIP2-L @512 + ConvNeXt decoder + DINO ViT-S D + LPIPS-VGG16)",
                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "seq_len": 1024,
                        "resolution": 256, "parallelism": f"dp{world}",
-                       "decoder_ops": "torch" if args.force_ref_ops else "hip"},
+                       "decoder_ops": "torch" if args.force_ref_ops else "hip",
+                       "d_phase_g_forward": "eager" if args.no_graphs else "hip_graph"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -1,0 +1,96 @@
+"""The D phase's no-grad generator forward replayed from HIP graphs
+(training/graphed_forward.py) against the eager forward it replaces
+(reference training/loss.py:254-256, `with torch.no_grad(): self.run_G(...)`).
+
+Same python-random / torch-CPU seeds on both sides: the equivariance variant and the
+posterior noise must be identical, and the output must agree to rounding, including after
+parameters change between replays (weight casts are recomputed inside the graph) and the
+mapping's x_avg buffer update. Not bit-exact: hipBLASLt may choose another reduction split
+for a few fp32 GEMMs under stream capture (1-ulp fp32 differences in the low-resolution
+blocks, <= a few bf16 ulps at the bf16 output). A wrong noise draw, variant or stale weight
+shows up as O(0.1) differences."""
+import json
+import os
+import random
+
+import pytest
+import torch
+
+import net_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gen(tmp_path_factory):
+    from networks.generator import Generator
+    d = str(tmp_path_factory.mktemp("m") / net_cases.VFM_DIRNAME)
+    os.makedirs(d)
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(os.path.join(d, "config.json"), "w"))
+    torch.manual_seed(0)
+    kw = net_cases.g_kwargs(d, use_equivariance_regularization=True)
+    G = Generator(label_dim=0, **kw).train().requires_grad_(False).cuda()
+    return G
+
+
+def _eager(G, img, seed):
+    random.seed(seed)
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        out = G(img, ['x'] * img.shape[0])
+    return out.gen_img.clone(), (out.eq_scale_factor, out.eq_angle_factor)
+
+
+def _graphed(runner, img, seed):
+    random.seed(seed)
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        out = runner(img, ['x'] * img.shape[0])
+    return out.gen_img.clone(), (out.eq_scale_factor, out.eq_angle_factor)
+
+
+def test_graph_replay_matches_eager(gen):
+    from training.graphed_forward import GraphedNoGradForward
+    G = gen
+    runner = GraphedNoGradForward(G)
+    img = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(5)).cuda()
+    xavg = G.mapping.x_avg
+    seen = set()
+    step = 0
+    for seed in range(100, 200):
+        if step == 6:
+            break
+        if step == 3:      # an "optimizer step": every decoder / adapter weight moves
+            with torch.no_grad():
+                for p in G.synthesis.parameters():
+                    p.mul_(1.01)
+                for p in G.ldm_adapter.parameters():
+                    p.add_(1e-3)
+        x0 = xavg.clone()
+        try:
+            ref, v_ref = _eager(G, img, seed)
+        except RuntimeError:     # outcome too small for the 64 px toy decoder (eager raises too)
+            xavg.copy_(x0)
+            continue
+        step += 1
+        x_ref = xavg.clone()
+        xavg.copy_(x0)
+        got, v_got = _graphed(runner, img, seed)
+        assert runner.disabled is None, runner.disabled
+        assert v_got == v_ref
+        seen.add(v_ref)
+        d = (got.float() - ref.float()).abs()
+        assert float(d.max()) <= 2e-2 and float(d.mean()) <= 2e-4, (seed, float(d.max()), float(d.mean()))
+        assert torch.allclose(xavg, x_ref, rtol=0, atol=1e-5)
+    assert runner.replays == 6
+    assert len(runner.graphs) == len(G.equivariance_transform.outcomes())
+    assert len(seen) > 1
+
+
+def test_graph_runner_passes_grad_mode_through(gen):
+    from training.graphed_forward import GraphedNoGradForward
+    runner = GraphedNoGradForward(gen)
+    img = torch.rand(1, 3, 64, 64, device="cuda")
+    with torch.enable_grad():
+        assert not runner.eligible(img, ['x'])
+    assert not runner.eligible(img.cpu(), ['x']) or not torch.is_grad_enabled()

@@ -22,6 +22,9 @@ for s in "$@"; do
              timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" -d $out/pmc_f -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_f.log 2>&1 \
                && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" -d $out/pmc_w -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_w.log 2>&1 \
                && python tools_dev/pmc_traffic.py $out/pmc_f $out/pmc_w > $out/pmc_traffic.json ;;
+    gtest)   timeout -k 10 300 python -u -m pytest tests/test_graphed_forward_gpu.py -m gpu -x -v --timeout 240 --timeout-method thread > $out/gtest.log 2>&1 ;;
+    gdebug)  timeout -k 10 300 python tools_dev/graph_debug.py > $out/gdebug.log 2>&1 ;;
+    benchng) timeout -k 10 600 python bench.py --no-cpu-baseline --no-graphs > $out/benchng.log 2>&1 ;;
     decbench) timeout -k 10 300 python tools_dev/decbench.py > $out/decbench.log 2>&1 ;;
     opbench) timeout -k 10 300 python tools_dev/opbench.py > $out/opbench.log 2>&1 ;;
     dtests)  timeout -k 10 600 python -m pytest tests/test_decoder_gpu.py -q -x > $out/dtests.log 2>&1 ;;

@@ -807,8 +807,9 @@ __global__ __launch_bounds__(NT) void gelu_fwd(RowArgs a) {
     const int o = row % a.O;
     const float sc = a.rscale ? a.rscale[row] : 1.f;
     const float bi = a.cvec0 ? a.cvec0[o] : 0.f;
-    const T* hp = reinterpret_cast<const T*>(a.in0) + (long long)row * a.P;
-    T* gp = reinterpret_cast<T*>(a.out0) + (long long)row * a.P;
+    const T* __restrict__ hp = reinterpret_cast<const T*>(a.in0) + (long long)row * a.P;
+    T* __restrict__ gp = reinterpret_cast<T*>(a.out0) + (long long)row * a.P;
+#pragma unroll 4
     for (int i = lane; i < a.P / 8; i += 64) {
         float v[8];
         load8(hp + i * 8, v);
@@ -827,10 +828,11 @@ __global__ __launch_bounds__(NT) void gelu_bwd(RowArgs a) {
     const int o = row % a.O;
     const float sc = a.rscale ? a.rscale[row] : 1.f;
     const float bi = a.cvec0 ? a.cvec0[o] : 0.f;
-    const T* hp = reinterpret_cast<const T*>(a.in0) + (long long)row * a.P;
-    const T* gp = reinterpret_cast<const T*>(a.dout) + (long long)row * a.P;
-    T* dp = reinterpret_cast<T*>(a.out0) + (long long)row * a.P;
+    const T* __restrict__ hp = reinterpret_cast<const T*>(a.in0) + (long long)row * a.P;
+    const T* __restrict__ gp = reinterpret_cast<const T*>(a.dout) + (long long)row * a.P;
+    T* __restrict__ dp = reinterpret_cast<T*>(a.out0) + (long long)row * a.P;
     float s0 = 0.f, s1 = 0.f;
+#pragma unroll 4
     for (int i = lane; i < a.P / 8; i += 64) {
         float h[8], g[8], d[8];
         load8(hp + i * 8, h);
@@ -861,9 +863,10 @@ __global__ __launch_bounds__(NT) void lsr_fwd(RowArgs a) {
     const int c = row % a.O;
     const float b = a.cvec0 ? a.cvec0[c] : 0.f;
     const float gm = a.cvec1 ? a.cvec1[c] : 1.f;
-    const TY* yp = reinterpret_cast<const TY*>(a.in0) + (long long)row * a.P;
-    const TX* xp = reinterpret_cast<const TX*>(a.in1) + (long long)row * a.P;
-    TX* op = reinterpret_cast<TX*>(a.out0) + (long long)row * a.P;
+    const TY* __restrict__ yp = reinterpret_cast<const TY*>(a.in0) + (long long)row * a.P;
+    const TX* __restrict__ xp = reinterpret_cast<const TX*>(a.in1) + (long long)row * a.P;
+    TX* __restrict__ op = reinterpret_cast<TX*>(a.out0) + (long long)row * a.P;
+#pragma unroll 4
     for (int i = lane; i < a.P / 8; i += 64) {
         float y[8], x[8];
         load8(yp + i * 8, y);
@@ -883,10 +886,11 @@ __global__ __launch_bounds__(NT) void lsr_bwd(RowArgs a) {
     const int c = row % a.O;
     const float b = a.cvec0 ? a.cvec0[c] : 0.f;
     const float gm = a.cvec1 ? a.cvec1[c] : 1.f;
-    const TY* yp = reinterpret_cast<const TY*>(a.in0) + (long long)row * a.P;
-    const TX* gp = reinterpret_cast<const TX*>(a.dout) + (long long)row * a.P;
-    TY* dp = reinterpret_cast<TY*>(a.out0) + (long long)row * a.P;
+    const TY* __restrict__ yp = reinterpret_cast<const TY*>(a.in0) + (long long)row * a.P;
+    const TX* __restrict__ gp = reinterpret_cast<const TX*>(a.dout) + (long long)row * a.P;
+    TY* __restrict__ dp = reinterpret_cast<TY*>(a.out0) + (long long)row * a.P;
     float s0 = 0.f, s1 = 0.f;
+#pragma unroll 4
     for (int i = lane; i < a.P / 8; i += 64) {
         float y[8], g[8], d[8];
         load8(yp + i * 8, y);

@@ -337,6 +337,12 @@ class EquivarianceTransform(nn.Module):
             return [(1.0, 0, False)]
         return [(s, 0, p) for p in (False, True) for s in self.SCALES]
 
+    def outcomes(self):
+        """Every distinct value forward(validation=False) can return."""
+        if not self.apply:
+            return [(1.0, 0, False)]
+        return [(s, a, False) for s in self.SCALES for a in range(4)] + [(s, 0, True) for s in self.SCALES]
+
     def forward(self, validation: bool):
         if not self.apply or validation:
             return 1.0, 0, False

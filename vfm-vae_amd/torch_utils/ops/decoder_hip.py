@@ -115,9 +115,12 @@ def supported(op, x, **kw):
 def _cast_cached(w, dtype):
     """w.detach().to(dtype), cached on the parameter until it changes (its version counter
     moves at every optimizer step): the D-phase and G-phase forwards of one iteration share
-    one cast of each decoder weight."""
+    one cast of each decoder weight. Not while a HIP graph is being captured (the cached tensor
+would be baked into the graph and go stale after the next optimizer step)."""
     if w.dtype == dtype:
         return w.detach()
+    if torch.cuda.is_current_stream_capturing():
+        return w.detach().to(dtype)     # a graph must recompute the cast at every replay
     base = w._base if w._base is not None else w
     key = (tuple(w.shape), w.stride(), w.storage_offset(), dtype, base._version)
     hit = getattr(base, "_vfm_cast", None)

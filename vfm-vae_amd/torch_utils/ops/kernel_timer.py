@@ -50,6 +50,18 @@ def _timed(name, nbytes, flops, bound):
         _records.setdefault(name, []).append((s, e, nbytes, flops, bound))
 
 
+@contextlib.contextmanager
+def suspended():
+    """No timing inside (HIP-graph capture: events cannot be recorded into a capture and the
+    replayed kernels are not launched through the wrappers)."""
+    global _enabled
+    prev, _enabled = _enabled, False
+    try:
+        yield
+    finally:
+        _enabled = prev
+
+
 def region(name, nbytes=0, flops=0, bound="hbm"):
     """Context manager around one native launch; a shared no-op object when timing is off
     (this is on every launch's host path)."""

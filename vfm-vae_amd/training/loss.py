@@ -10,7 +10,10 @@ skip/flag semantics are the reference's.
 Host-sync economy (same results): the nine per-microbatch `.item()` reads of the
 safe-loss check are one stacked device->host copy, and the two safe-loss
 collectives are merged into one all_reduce of a small int vector (MAX of the skip
-flag == MIN of the negated marks).
+flag == MIN of the negated marks). Before the safe-loss check is active
+(`safe_loss_checking_start_nimg`) and while no warm-up window can switch a loss on,
+nothing in the step reads those values, so their copy is non-blocking and read
+lazily (`_HostValues`): the G backward is then issued without draining the GPU.
 """
 import math
 from collections import deque
@@ -29,6 +32,39 @@ from networks.utils.vfm_utils import VFM2INTERPOLATION
 from networks.utils.dataclasses import GeneratorForwardOutput, DiscriminatorForwardOutput
 
 SAFE_MARK, UNSAFE_MARK = 1, 0
+
+
+class _HostValues:
+    """Loss scalars on their way to the host: one non-blocking device->host copy into pinned
+    memory, read (after its event) only when a value is first needed. Used when nothing in
+    the current step depends on them (safe-loss check not active yet, no live warm-up
+    window), so the G backward is issued without first draining the GPU queue."""
+
+    def __init__(self, names, vec):
+        self.names = list(names)
+        self._vals = None
+        if vec.is_cuda:
+            self._host = torch.empty(vec.shape, dtype=vec.dtype, pin_memory=True)
+            self._host.copy_(vec, non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+        else:
+            self._vals = vec.tolist()
+
+    def _resolve(self):
+        if self._vals is None:
+            self._event.synchronize()
+            self._vals = self._host.tolist()
+        return self._vals
+
+    def __getitem__(self, name):
+        return self._resolve()[self.names.index(name)]
+
+    def keys(self):
+        return list(self.names)
+
+    def items(self):
+        return list(zip(self.names, self._resolve()))
 
 
 class ImageTransform(nn.Module):
@@ -197,6 +233,16 @@ class TotalLoss:
     def run_G(self, z, c) -> GeneratorForwardOutput:
         return self.G(z, c)
 
+    def enable_graphed_nograd_forward(self, flag=True):
+        """Replay the D phase's no-grad generator forward from HIP graphs
+        (training/graphed_forward.py); numerics and RNG draws as the eager pass."""
+        from training.graphed_forward import GraphedNoGradForward
+        self.graphed_nograd = GraphedNoGradForward(self.G) if flag else None
+
+    def run_G_nograd(self, z, c) -> GeneratorForwardOutput:
+        g = getattr(self, 'graphed_nograd', None)
+        return self.G(z, c) if g is None else g(z, c)
+
     def run_D(self, img, c_enc) -> DiscriminatorForwardOutput:
         return self.D(self.blur(img, self.blur_curr_sigma), c_enc)
 
@@ -291,10 +337,32 @@ class TotalLoss:
         vals = vec.tolist()
         return bool(vals[0]), [-v for v in vals[1:]]
 
+    def _phase_windows_live(self):
+        """True while a warm-up window can still switch a discriminator loss on."""
+        return ((self.use_stylegan_t_disc_warmup and not self._stylegan_t_on)
+                or (self.use_patchgan_disc_warmup and not self._patchgan_on))
+
+    def _update_phase_deferred(self, host):
+        """_update_phase when no warm-up window is live: no flag can change this step, so the
+        D-loss window entry waits for its device->host copy and the (unchanged) flags are
+        not re-broadcast. Entries are resolved when the window is next read."""
+        if (not dist.is_initialized()) or dist.get_rank() == 0:
+            key = 'stylegan_t_gen_loss' if self.stylegan_t_discriminator_loss_weight > 0 else None
+            self._d_window.append((host, key))
+        if self._patchgan_on and not self._off_done:
+            self._off_reconstruction_and_quantization_losses()
+            self._off_done = True
+
+    def _resolve_windows(self):
+        if any(isinstance(v, tuple) for v in self._d_window):
+            self._d_window = deque([(v[0][v[1]] if v[1] else 0.) if isinstance(v, tuple) else v
+                                    for v in self._d_window], maxlen=self._d_window.maxlen)
+
     def _update_phase(self, cur_nimg, pixel_loss_now, d_now):
         """Warm-up bookkeeping on rank 0, flags broadcast to all ranks (reference :381-492)."""
         cur_kimg = cur_nimg // 1000
         need_freeze32 = False
+        self._resolve_windows()
         if (not dist.is_initialized()) or dist.get_rank() == 0:
             self._d_window.append(d_now)
             d_mean = np.mean(self._d_window)
@@ -362,7 +430,7 @@ class TotalLoss:
         if phase == 'D':
             d_loss = torch.zeros([], device=self.device, requires_grad=True)
             with torch.no_grad():
-                out = self.run_G(real_img, real_c)
+                out = self.run_G_nograd(real_img, real_c)
             gen_img = out.gen_img.detach()
             eq_s, eq_a, real_c_enc = out.eq_scale_factor, out.eq_angle_factor, out.global_text_tokens
             del out
@@ -515,8 +583,11 @@ class TotalLoss:
         names = ['l1_pixel_loss', 'l2_pixel_loss', 'perceptual_loss', 'ssim_loss', 'multiscale_pixel_loss',
                  'stylegan_t_gen_loss', 'patchgan_gen_loss', 'feature_matching_loss', 'clip_loss']
         base = [l1, l2, perc, ssim, ms_loss, st_gen, pg_gen, fm_loss, clip_loss]
-        host = torch.stack([v.detach().float().reshape([]) for v in base]).tolist()   # one D2H copy
-        loss_dict = dict(zip(names, host))
+        vec = torch.stack([v.detach().float().reshape([]) for v in base])
+        if (check_now and self.prev_loss_dict is not None) or self._phase_windows_live():
+            loss_dict = dict(zip(names, vec.tolist()))          # read now: it decides this step
+        else:
+            loss_dict = _HostValues(names, vec)                 # nothing reads it before the next step
         marks = [SAFE_MARK] * len(names)
         skip = False
         if check_now and self.prev_loss_dict is not None:
@@ -590,6 +661,9 @@ class TotalLoss:
             if self.vq_loss_weight > 0:
                 training_stats.report('Loss/G/vq_loss', out.vq_loss)
                 training_stats.report('Loss/G/codebook_usages', out.codebook_usages)
+        if isinstance(loss_dict, _HostValues):
+            self._update_phase_deferred(loss_dict)
+            return
         pixel_now = loss_dict['l1_pixel_loss'] if self._pixel_loss_window_type == 'l1' else loss_dict['l2_pixel_loss']
         d_now = loss_dict['stylegan_t_gen_loss'] if self.stylegan_t_discriminator_loss_weight > 0 else 0.
         self._update_phase(cur_nimg, pixel_now, d_now)
