@@ -208,6 +208,23 @@ int vfm_residual_layer_norm(const float* h, const void* delta, float* h_out, con
 int vfm_codebook_argmax(const float* features, long long ld, const float* codebook, int N, int C, int V,
                         long long* indices, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * ConvNeXt MLP channel GEMM with the GELU fused into its epilogue (replaces the
+ * modulated 1x1 conv + GELU of convnext_utils.py:135-138, and in backward the
+ * 4C->C conv's data gradient + GELU backward). bf16 operands, fp32 accumulation.
+ *   A: bf16 [M, K] row-major (W1 [4C, C]; backward: W2^T [4C, C]);
+ *   X: bf16 [B, K, N] (forward: the GroupNorm output m; backward: dy);
+ *   scale: fp32 [B, M] demodulation (NULL = 1); bias: fp32 [M] (NULL = 0).
+ *   mode 0: out0 = bf16(A.X) (NULL: not written), out1 = bf16(GELU(out0 * scale + bias)).
+ *   mode 1: dg = bf16(A.X), z = h * scale + bias (h: bf16 [B, M, N]), dz = dg * GELU'(z);
+ *           out0 = bf16(dz * scale); part0 / part1: fp32 [B, tiles, M] per-tile sums over N of
+ *           dz * h and dz (tiles = vfm_pw_gemm_gelu_tiles(N)), reduced by the caller.
+ * K in {128, 256, 512}, M % 128 == 0, N % 128 == 0 (else VFM_NO_KERNEL). */
+int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale, const float* bias, const void* h,
+                     void* out0, void* out1, float* part0, float* part1, int mode, int B, int M, int K, int N,
+                     void* stream);
+int vfm_pw_gemm_gelu_tiles(int N);
+
 #ifdef __cplusplus
 }
 #endif

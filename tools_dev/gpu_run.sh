@@ -23,6 +23,8 @@ for s in "$@"; do
                && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" -d $out/pmc_w -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_w.log 2>&1 \
                && python tools_dev/pmc_traffic.py $out/pmc_f $out/pmc_w > $out/pmc_traffic.json ;;
     gtest)   timeout -k 10 300 python -u -m pytest tests/test_graphed_forward_gpu.py -m gpu -x -v --timeout 240 --timeout-method thread > $out/gtest.log 2>&1 ;;
+    pwtest)  timeout -k 10 300 python -u -m pytest tests/test_pwgemm_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > $out/pwtest.log 2>&1 ;;
+    pwbench) timeout -k 10 300 python tools_dev/pwbench.py > $out/pwbench.log 2>&1 ;;
     gdebug)  timeout -k 10 300 python tools_dev/graph_debug.py > $out/gdebug.log 2>&1 ;;
     benchng) timeout -k 10 600 python bench.py --no-cpu-baseline --no-graphs > $out/benchng.log 2>&1 ;;
     decbench) timeout -k 10 300 python tools_dev/decbench.py > $out/decbench.log 2>&1 ;;

@@ -786,27 +786,9 @@ __global__ __launch_bounds__(NT) void gn_bwd(GnBwdArgs a) {
 // rather than HBM-bound. Here Phi(z) comes from the branch-free Abramowitz-Stegun 7.1.26
 // form, |erf error| <= 1.5e-7 (about 1 fp32 ulp at 1.0): one v_rcp, one v_exp, five FMAs,
 // and the exp(-z^2/2) it needs is the same factor the derivative's z*phi(z) term uses.
-struct GeluParts {
-    float cdf;    // Phi(z)
-    float zpdf;   // z * phi(z)
-};
-__device__ __forceinline__ GeluParts gelu_parts(float z) {
-    const float x = z * 0.70710678118654752f;
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, fabsf(x), 1.f));
-    float p = fmaf(t, 1.061405429f, -1.453152027f);
-    p = fmaf(p, t, 1.421413741f);
-    p = fmaf(p, t, -0.284496736f);
-    p = fmaf(p, t, 0.254829592f);
-    const float e = __builtin_amdgcn_exp2f(-(x * x) * 1.4426950408889634f);   // exp(-z^2/2)
-    const float q = 0.5f * (p * t) * e;                                        // 0.5 * erfc(|x|)
-    GeluParts r;
-    r.cdf = x < 0.f ? q : 1.f - q;
-    r.zpdf = z * 0.39894228040143268f * e;
-    return r;
-}
-__device__ __forceinline__ float gelu_erf(float z) { return z * gelu_parts(z).cdf; }
+__device__ __forceinline__ float gelu_erf(float z) { return z * vfm::gelu_parts(z).cdf; }
 __device__ __forceinline__ float gelu_erf_grad(float z) {
-    const GeluParts g = gelu_parts(z);
+    const vfm::GeluParts g = vfm::gelu_parts(z);
     return g.cdf + g.zpdf;
 }
 

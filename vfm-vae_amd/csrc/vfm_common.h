@@ -54,6 +54,24 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
     return (t + n) >> f.s;
 }
 
+struct GeluParts {
+    float cdf;    // Phi(z)
+    float zpdf;   // z * phi(z)
+};
+__device__ __forceinline__ GeluParts gelu_parts(float z) {
+    const float x = z * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, fabsf(x), 1.f));
+    float p = fmaf(t, 1.061405429f, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    const float e = __builtin_amdgcn_exp2f(-(x * x) * 1.4426950408889634f);   // exp(-z^2/2)
+    const float q = 0.5f * (p * t) * e;                                        // 0.5 * erfc(|x|)
+    GeluParts r;
+    r.cdf = x < 0.f ? q : 1.f - q;
+    r.zpdf = z * 0.39894228040143268f * e;
+    return r;
+}
 inline int launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? VFM_OK : (int)e;
