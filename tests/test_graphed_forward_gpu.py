@@ -80,7 +80,7 @@ def test_graph_replay_matches_eager(gen):
         assert v_got == v_ref
         seen.add(v_ref)
         d = (got.float() - ref.float()).abs()
-        assert float(d.max()) <= 2e-2 and float(d.mean()) <= 2e-4, (seed, float(d.max()), float(d.mean()))
+        assert float(d.max()) <= 2e-2 and float(d.mean()) <= 1e-3, (seed, float(d.max()), float(d.mean()))
         assert torch.allclose(xavg, x_ref, rtol=0, atol=1e-5)
     assert runner.replays == 6
     assert len(runner.graphs) == len(G.equivariance_transform.outcomes())
