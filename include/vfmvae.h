@@ -218,8 +218,9 @@ int vfm_codebook_argmax(const float* features, long long ld, const float* codebo
  *   mode 0: out0 = bf16(A.X) (NULL: not written), out1 = bf16(GELU(out0 * scale + bias)).
  *   mode 1: dg = bf16(A.X), z = h * scale + bias (h: bf16 [B, M, N]), dz = dg * GELU'(z);
  *           out0 = bf16(dz * scale); part0 / part1: fp32 [B, tiles, M] per-tile sums over N of
- *           dz * h and dz (tiles = vfm_pw_gemm_gelu_tiles(N)), reduced by the caller.
- * K in {128, 256, 512}, M % 128 == 0, N % 128 == 0 (else VFM_NO_KERNEL). */
+ *           dz * h and dz over 64-column tiles (tiles = vfm_pw_gemm_gelu_tiles(N) = N / 64), reduced by
+ *           the caller.
+ * K in {128, 256, 512}, M % 128 == 0, M <= 2048, N % 128 == 0 (else VFM_NO_KERNEL). */
 int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale, const float* bias, const void* h,
                      void* out0, void* out1, float* part0, float* part1, int mode, int B, int M, int K, int N,
                      void* stream);

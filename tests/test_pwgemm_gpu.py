@@ -60,7 +60,7 @@ def test_backward_gemm_gelu(B, M, K, N):
     A, X, s, bias = _inputs(B, M, K, N, 1)
     hin = torch.randn(B, M, N, generator=torch.Generator().manual_seed(2)).bfloat16().cuda()
     tiles = lib.vfm_pw_gemm_gelu_tiles(N)
-    assert tiles == N // 128
+    assert tiles == N // 64
     dh = torch.empty(B, M, N, dtype=torch.bfloat16, device="cuda")
     p0 = torch.empty(B, tiles, M, device="cuda")
     p1 = torch.empty_like(p0)

@@ -37,7 +37,7 @@ def main():
         bias = torch.randn(M, device="cuda")
         h = torch.empty(B, M, N, dtype=torch.bfloat16, device="cuda")
         g = torch.empty_like(h)
-        tiles = N // 128
+        tiles = N // 64
         p0 = torch.empty(B, tiles, M, device="cuda")
         p1 = torch.empty_like(p0)
         ux = B * K * N * 2

@@ -19,17 +19,21 @@
 // Layout: A [M, K] row-major (W1, or W2^T), X [B, K, N] (channels x pixels), outputs
 // [B, M, N]. One workgroup = one sample x 128 pixel columns; it stages X[b][:, n0:n0+128]
 // once in LDS (K rows of 256 B, 16-B chunks XOR-swizzled) and sweeps all M rows in steps
-// of 128 (4 waves x 32 rows), so X is read from HBM exactly once. A fragments come straight
+// of 128 (8 waves: 4 row blocks of 32 x 2 column halves of 64), so X is read from HBM
+// exactly once. A fragments come straight
 // from global memory (the weight is tiny and L2-resident). v_mfma_f32_32x32x16_bf16:
 // A lane l holds A[r][8h+j] (r = l&31, h = l>>5), B lane l holds B[8h+j][r], taken from the
 // row-major X image with two ds_read_b64_tr_b16; C/D: col = l&31, row = (i&3)+8(i>>2)+4h.
 //
 // Status: parity-tested (tests/test_pwgemm_gpu.py), not yet on the training path. Measured
-// at batch 32 (tools_dev/pwbench.py, MI355X): forward with h written 1.33 ms vs 1.67 ms for
-// bmm + GELU kernel at C=128 / 256^2, 0.82 vs 0.90 ms at C=256 / 128^2, but 0.87 vs 0.61 ms
-// at C=512 / 64^2; backward 2-4x slower than the unfused pair. The epilogue is VALU-bound
-// (GELU math on 4C x P elements with 2 waves/SIMD), not store-bound: staging the tile through
-// LDS for whole-row stores was slower. Next: packed-f32 epilogue math, more waves per SIMD.
+// at batch 32 (tools_dev/pwbench.py, MI355X) against hipBLASLt bmm + the GELU row kernels:
+//   C=128 @256^2: fwd h+g 1.36 ms (unfused 1.64), fwd g only 1.05 ms, bwd 1.94 ms (2.08)
+//   C=256 @128^2: fwd h+g 0.87 ms (0.87), g only 0.70 ms, bwd 1.18 ms (1.03)
+//   C=512 @64^2:  fwd h+g 0.83 ms (0.62), g only 0.58 ms, bwd 1.01 ms (0.66)
+// What moved it: per-row scale/bias staged in LDS instead of a dependent global load per
+// row in the epilogue, h prefetched before the MFMA loop, 8 waves x 2 column blocks (4-5
+// waves/SIMD), lane-pair packing for 4-byte h loads and outputs. Staging whole output rows
+// through LDS was slower. Next: find what still caps the epilogue (PMC VALU/wait counters).
 #include "vfm_common.h"
 
 namespace {
@@ -43,7 +47,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int NT = 128;   // pixel columns per workgroup
-constexpr int WAVES = 4;  // each wave owns 32 output rows of every 128-row M step
+constexpr int WAVES = 8;  // wave w: rows 32(w&3) of every 128-row M step, columns 64(w>>2)..+63
+constexpr int NBW = 2;    // 32-column MFMA blocks per wave
+constexpr int PT = 64;    // columns summed into one backward partial (one wave's share)
 
 struct PwArgs {
     const __hip_bfloat16* A;
@@ -65,21 +71,45 @@ __device__ __forceinline__ int swz(int row, int ch) {
 
 __device__ __forceinline__ float bf16_round(float v) { return __bfloat162float(__float2bfloat16(v)); }
 
+__device__ __forceinline__ uint32_t bf16_bits(float v) {
+    const __hip_bfloat16 b = __float2bfloat16(v);
+    return (uint32_t)__builtin_bit_cast(uint16_t, b);
+}
+
+// Registers i (even) and i+1 of a 32x32 accumulator are rows m and m+1 of the same column
+// (the lane). Lane pairs (r, r+1) trade one value so that the even lane holds columns
+// (r, r+1) of row m and the odd lane columns (r-1, r) of row m+1: one 4-byte access per lane
+// instead of two 2-byte ones. Returns the packed bf16 pair this lane stores.
+__device__ __forceinline__ uint32_t pair_pack(float vi, float vi1, bool odd) {
+    const uint32_t send = bf16_bits(odd ? vi : vi1);
+    const uint32_t x = (uint32_t)__shfl_xor((int)send, 1);
+    return odd ? (x | (bf16_bits(vi1) << 16)) : (bf16_bits(vi) | (x << 16));
+}
+
 template <int MODE, int K>
-__global__ __launch_bounds__(256) void pw_gemm_gelu(PwArgs a) {
+__global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y;
     const int tile = blockIdx.x;
     const int n0 = tile * NT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rw = wave & 3, cw = wave >> 2;
     const int M = a.M, N = a.N;
 
     const __hip_bfloat16* xb = a.X + (long long)b * K * N + n0;
 #pragma unroll 4
-    for (int i = tid; i < K * 16; i += 256) {
+    for (int i = tid; i < K * 16; i += 64 * WAVES) {
         const int row = i >> 4, ch = i & 15;
         const uint4 v = *reinterpret_cast<const uint4*>(xb + (long long)row * N + ch * 8);
         *reinterpret_cast<uint4*>(lds + swz(row, ch)) = v;
+    }
+    // per-row epilogue constants of this sample, read from LDS in the epilogue (a global load
+    // per row there would put its latency on the critical path of every row)
+    float* s_sc = reinterpret_cast<float*>(lds + K * 256);
+    float* s_bi = s_sc + M;
+    for (int i = tid; i < M; i += 64 * WAVES) {
+        s_sc[i] = a.scale ? a.scale[(long long)b * M + i] : 1.f;
+        s_bi[i] = a.bias ? a.bias[i] : 0.f;
     }
     __syncthreads();
 
@@ -87,83 +117,115 @@ __global__ __launch_bounds__(256) void pw_gemm_gelu(PwArgs a) {
     const int g1 = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
     // transposed-read byte offsets for k-step 0; rows advance by 16 per k-step (the XOR term
     // depends on row & 15 only, so the offset of k-step s is base + 16 * 256 * s)
-    int tro[4][2];
+    int tro[NBW][2];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-        const int c0 = 4 * nb + 2 * g1 + (p >> 1);
-        tro[nb][0] = swz(8 * hh + q, c0) + 8 * (p & 1);
-        tro[nb][1] = swz(8 * hh + 4 + q, c0) + 8 * (p & 1);
+    for (int j = 0; j < NBW; ++j) {
+        const int c0 = 4 * (NBW * cw + j) + 2 * g1 + (p >> 1);
+        tro[j][0] = swz(8 * hh + q, c0) + 8 * (p & 1);
+        tro[j][1] = swz(8 * hh + 4 + q, c0) + 8 * (p & 1);
     }
 
-    const long long outb = (long long)b * M * N + n0 + r;
-    for (int mc = 0; mc < M; mc += 32 * WAVES) {
-        const int m0 = mc + 32 * wave;
+    const long long outb = (long long)b * M * N + n0 + 64 * cw + r;
+    for (int mc = 0; mc < M; mc += 128) {
+        const int m0 = mc + 32 * rw;
         const __hip_bfloat16* arow = a.A + (long long)(m0 + r) * K + 8 * hh;
-        f32x16 acc[4];
+        f32x16 acc[NBW];
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb) acc[nb] = f32x16{};
-        bf16x8 af[K / 16];
+        for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x16{};
+        const bool odd = r & 1;
+        uint32_t hraw[MODE == 1 ? 8 : 1][NBW];     // packed pairs, see pair_pack
+        if (MODE == 1) {
 #pragma unroll
-        for (int s = 0; s < K / 16; ++s) af[s] = *reinterpret_cast<const bf16x8*>(arow + 16 * s);
+            for (int i = 0; i < 16; i += 2)
+#pragma unroll
+                for (int nb = 0; nb < NBW; ++nb) {
+                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh + (odd ? 1 : 0);
+                    hraw[i / 2][nb] = *reinterpret_cast<const uint32_t*>(a.h + outb - (odd ? 1 : 0) +
+                                                                         (long long)m * N + 32 * nb);
+                }
+        }
+        bf16x8 a0 = *reinterpret_cast<const bf16x8*>(arow);
+        bf16x8 a1 = *reinterpret_cast<const bf16x8*>(arow + 16);
 #pragma unroll
         for (int s = 0; s < K / 16; ++s) {
+            const bf16x8 af = a0;
+            a0 = a1;
+            if (s + 2 < K / 16) a1 = *reinterpret_cast<const bf16x8*>(arow + 16 * (s + 2));
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) {
+            for (int nb = 0; nb < NBW; ++nb) {
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                     (lds_s16x4*)(lds + tro[nb][0] + 4096 * s));
                 const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                     (lds_s16x4*)(lds + tro[nb][1] + 4096 * s));
                 const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], __builtin_bit_cast(bf16x8, both),
+                acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, __builtin_bit_cast(bf16x8, both),
                                                                   acc[nb], 0, 0, 0);
             }
         }
 
         // epilogue: register i of acc[nb] is row m0 + (i&3) + 8(i>>2) + 4hh, column n0 + 32nb + r
         if (MODE == 0) {
-            // direct per-lane stores: staging the tile through LDS for whole-row stores measured
-            // slower (the epilogue is VALU-bound, not store-bound)
+            const bool odd = r & 1;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                const float sc = a.scale ? a.scale[(long long)b * M + m] : 1.f;
-                const float bi = a.bias ? a.bias[m] : 0.f;
-                const long long row = outb + (long long)m * N;
+            for (int i = 0; i < 16; i += 2) {
+                const int mA = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                const long long rowst = outb - (odd ? 1 : 0) + (long long)(mA + (odd ? 1 : 0)) * N;
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb) {
-                    const __hip_bfloat16 hv = __float2bfloat16(acc[nb][i]);
-                    if (a.out0) a.out0[row + 32 * nb] = hv;
-                    const float z = fmaf(__bfloat162float(hv), sc, bi);
-                    a.out1[row + 32 * nb] = __float2bfloat16(z * gelu_parts(z).cdf);
+                for (int nb = 0; nb < NBW; ++nb) {
+                    float hv[2], gv[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        hv[t] = bf16_round(acc[nb][i + t]);
+                        const float z = fmaf(hv[t], s_sc[mA + t], s_bi[mA + t]);
+                        gv[t] = z * gelu_parts(z).cdf;
+                    }
+                    if (a.out0)
+                        *reinterpret_cast<uint32_t*>(a.out0 + rowst + 32 * nb) = pair_pack(hv[0], hv[1], odd);
+                    *reinterpret_cast<uint32_t*>(a.out1 + rowst + 32 * nb) = pair_pack(gv[0], gv[1], odd);
                 }
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                const float sc = a.scale ? a.scale[(long long)b * M + m] : 1.f;
-                const float bi = a.bias ? a.bias[m] : 0.f;
-                const long long row = outb + (long long)m * N;
-                float s0 = 0.f, s1 = 0.f;
+            for (int i = 0; i < 16; i += 2) {
+                const int mA = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh;      // row of register i; i+1 is mA+1
+                float s0[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f};
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb) {
-                    const float dg = bf16_round(acc[nb][i]);
-                    const float hv = __bfloat162float(a.h[row + 32 * nb]);
-                    const GeluParts gp = gelu_parts(fmaf(hv, sc, bi));
-                    const float dz = dg * (gp.cdf + gp.zpdf);
-                    a.out0[row + 32 * nb] = __float2bfloat16(dz * sc);
-                    s0 = fmaf(dz, hv, s0);
-                    s1 += dz;
+                for (int nb = 0; nb < NBW; ++nb) {
+                    // unpack this lane's h for rows mA, mA+1 (column r)
+                    const uint32_t own = hraw[i / 2][nb];
+                    const uint32_t x = (uint32_t)__shfl_xor((int)(odd ? (own & 0xffffu) : (own >> 16)), 1);
+                    const uint32_t hb0 = odd ? x : (own & 0xffffu);
+                    const uint32_t hb1 = odd ? (own >> 16) : x;
+                    float dhv[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int m = mA + t;
+                        const float sc = s_sc[m];
+                        const float bi = s_bi[m];
+                        const float hv = __uint_as_float((t ? hb1 : hb0) << 16);
+                        const float dg = bf16_round(acc[nb][i + t]);
+                        const GeluParts gp = gelu_parts(fmaf(hv, sc, bi));
+                        const float dz = dg * (gp.cdf + gp.zpdf);
+                        dhv[t] = dz * sc;
+                        s0[t] = fmaf(dz, hv, s0[t]);
+                        s1[t] += dz;
+                    }
+                    const uint32_t pk = pair_pack(dhv[0], dhv[1], odd);
+                    *reinterpret_cast<uint32_t*>(a.out0 + outb - (odd ? 1 : 0) + (long long)(mA + (odd ? 1 : 0)) * N +
+                                                 32 * nb) = pk;
                 }
 #pragma unroll
-                for (int off = 16; off >= 1; off >>= 1) {     // sum over the 32 columns of this half
-                    s0 += __shfl_xor(s0, off);
-                    s1 += __shfl_xor(s1, off);
-                }
-                if (r == 0) {
-                    const long long pi = ((long long)b * a.ntiles + tile) * M + m;
-                    a.part0[pi] = s0;
-                    a.part1[pi] = s1;
+                for (int t = 0; t < 2; ++t) {
+#pragma unroll
+                    for (int off = 16; off >= 1; off >>= 1) {     // sum over the 32 columns of this half
+                        s0[t] += __shfl_xor(s0[t], off);
+                        s1[t] += __shfl_xor(s1[t], off);
+                    }
+                    if (r == 0) {
+                        const long long pi = ((long long)b * a.ntiles + 2 * tile + cw) * M + mA + t;
+                        a.part0[pi] = s0[t];
+                        a.part1[pi] = s1[t];
+                    }
                 }
             }
         }
@@ -172,13 +234,14 @@ __global__ __launch_bounds__(256) void pw_gemm_gelu(PwArgs a) {
 
 template <int MODE, int K>
 int launch(const PwArgs& a, int B, hipStream_t st) {
-    const size_t lds = (size_t)K * 256;
+    const size_t lds = (size_t)K * 256 + 8 * (size_t)a.M;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)pw_gemm_gelu<MODE, K>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)pw_gemm_gelu<MODE, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  K * 256 + 8 * 2048);
         attr = true;
     }
-    hipLaunchKernelGGL((pw_gemm_gelu<MODE, K>), dim3(a.ntiles, B), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((pw_gemm_gelu<MODE, K>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
     return launch_status();
 }
 
@@ -188,7 +251,7 @@ extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale
                                 const void* h, void* out0, void* out1, float* part0, float* part1, int mode,
                                 int B, int M, int K, int N, void* stream) {
     if (!A || !X || B <= 0 || M <= 0 || N <= 0) return VFM_ERR_ARGS;
-    if (M % (32 * WAVES) != 0 || N % NT != 0 || (K != 128 && K != 256 && K != 512)) return VFM_NO_KERNEL;
+    if (M % 128 != 0 || M > 2048 || N % NT != 0 || (K != 128 && K != 256 && K != 512)) return VFM_NO_KERNEL;
     if (mode == 0 && !out1) return VFM_ERR_ARGS;
     if (mode == 1 && (!h || !out0 || !part0 || !part1)) return VFM_ERR_ARGS;
     if (mode != 0 && mode != 1) return VFM_ERR_ARGS;
@@ -204,7 +267,7 @@ extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale
     a.part1 = part1;
     a.M = M;
     a.N = N;
-    a.ntiles = N / NT;
+    a.ntiles = N / PT;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (mode == 0) {
         switch (K) {
@@ -220,4 +283,4 @@ extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale
     }
 }
 
-extern "C" int vfm_pw_gemm_gelu_tiles(int N) { return (N > 0 && N % NT == 0) ? N / NT : VFM_NO_KERNEL; }
+extern "C" int vfm_pw_gemm_gelu_tiles(int N) { return (N > 0 && N % NT == 0) ? N / PT : VFM_NO_KERNEL; }
