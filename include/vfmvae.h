@@ -226,6 +226,16 @@ int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale, const flo
                      void* stream);
 int vfm_pw_gemm_gelu_tiles(int N);
 
+/* The whole ConvNeXt MLP of convnext_utils.py:135-142 without autograd (the D phase's
+ * no-grad generator pass), bf16 in/out, fp32 accumulation, hidden tensor kept on chip:
+ *   out = x_in + gamma * (bf16(W2 . g) + b2),  g = bf16(GELU(bf16(W1 . m) * s + b1)).
+ *   W1: bf16 [4C, C]; m, x_in, out: bf16 [B, C, N]; s: fp32 [B, 4C] (NULL = 1);
+ *   b1: fp32 [4C]; W2: bf16 [C, 4C]; b2, gamma: fp32 [C] (NULL = 0 / 1).
+ * C in {128, 256}, N % 128 == 0 (else VFM_NO_KERNEL). */
+int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* s, const float* b1, const void* W2,
+                         const float* b2, const float* gamma, const void* xin, void* out, int B, int C, int N,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,3 +86,56 @@ def test_unsupported_shapes_report_no_kernel():
         rc = lib.vfm_pw_gemm_gelu(A.data_ptr(), X.data_ptr(), None, None, None, None, out.data_ptr(), None,
                                   None, 0, 1, M, K, N, co.stream_ptr())
         assert rc == co.VFM_NO_KERNEL
+
+
+@pytest.mark.parametrize("B,C,N", [(2, 128, 256), (3, 256, 384), (1, 128, 4096), (2, 256, 2304)])
+def test_convnext_mlp_forward(B, C, N):
+    """vfm_convnext_mlp_fwd vs the unfused chain with the same bf16 roundings
+    (pointwise -> scale_bias_gelu -> pointwise -> layer_scale_residual)."""
+    lib, co = _native()
+    g = torch.Generator().manual_seed(4)
+    W1 = (torch.randn(4 * C, C, generator=g) / C ** 0.5).bfloat16().cuda()
+    W2 = (torch.randn(C, 4 * C, generator=g) / (4 * C) ** 0.5).bfloat16().cuda()
+    m = torch.randn(B, C, N, generator=g).bfloat16().cuda()
+    x = torch.randn(B, C, N, generator=g).bfloat16().cuda()
+    s = (torch.rand(B, 4 * C, generator=g) + 0.5).cuda()
+    b1 = torch.randn(4 * C, generator=g).cuda()
+    b2 = torch.randn(C, generator=g).cuda()
+    gamma = torch.randn(C, generator=g).cuda()
+    out = torch.empty_like(x)
+    rc = lib.vfm_convnext_mlp_fwd(W1.data_ptr(), m.data_ptr(), s.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                                  b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), out.data_ptr(), B, C, N,
+                                  co.stream_ptr())
+    torch.cuda.synchronize()
+    assert rc == 0
+    h = torch.matmul(W1.float(), m.float()).bfloat16().float()
+    gv = F.gelu(h * s[:, :, None] + b1[None, :, None]).bfloat16().float()
+    y = torch.matmul(W2.float(), gv).bfloat16().float()
+    ref = x.float() + gamma[None, :, None] * (y + b2[None, :, None])
+    assert _rel(out.float(), ref) < 1e-2
+    assert lib.vfm_convnext_mlp_fwd(W1.data_ptr(), m.data_ptr(), None, None, W2.data_ptr(), None, None,
+                                    x.data_ptr(), out.data_ptr(), B, 512, N, co.stream_ptr()) == co.VFM_NO_KERNEL
+
+
+@pytest.mark.parametrize("res", [16, 32])
+def test_convnext_layer_nograd_uses_fused_mlp(res):
+    """ConvNeXtSynthesisLayer (C=128, bf16) without autograd takes the fused MLP kernel and
+    matches the autograd (unfused) forward to bf16 rounding."""
+    from networks.utils.convnext_utils import ConvNeXtSynthesisLayer
+    from torch_utils.ops import kernel_timer
+    torch.manual_seed(0)
+    lyr = ConvNeXtSynthesisLayer(128, 512, 7, layer_scale_init=0.5, block_index=2, legacy=True).cuda()
+    with torch.no_grad():
+        for p in lyr.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    x = torch.randn(2, 128, res, res, device="cuda").bfloat16()
+    w = torch.randn(2, 512, device="cuda")
+    with torch.enable_grad():
+        ref = lyr(x, w, torch.bfloat16)
+    kernel_timer.enable(True)
+    with torch.no_grad():
+        got = lyr(x, w, torch.bfloat16)
+    names = set(kernel_timer._records)
+    kernel_timer.enable(False)
+    assert any(n.startswith("convnext_mlp_fwd") for n in names), names
+    assert _rel(got.float(), ref.float()) < 2e-2

@@ -59,11 +59,22 @@ def main():
             return decoder_hip._gelu_bwd_only(h, dg, s, bias) if hasattr(decoder_hip, "_gelu_bwd_only") else dg
 
         t1, t2, t3 = timeit(f_grad), timeit(f_nograd), timeit(f_bwd)
+        tm = None
+        if C in (128, 256):
+            W2 = (torch.randn(C, M, device="cuda") / M ** 0.5).bfloat16()
+            xin = torch.randn(B, C, N, device="cuda").bfloat16()
+            outm = torch.empty_like(xin)
+            b2 = torch.randn(C, device="cuda")
+            gam = torch.randn(C, device="cuda")
+            tm = timeit(lambda: lib.vfm_convnext_mlp_fwd(A.data_ptr(), X.data_ptr(), s.data_ptr(), bias.data_ptr(),
+                                                         W2.data_ptr(), b2.data_ptr(), gam.data_ptr(), xin.data_ptr(),
+                                                         outm.data_ptr(), B, C, N, st))
         t4 = timeit(unfused_fwd)
         t5 = timeit(lambda: torch.bmm(A.expand(B, M, K), X))
         print(f"{name}: fused fwd(h+g) {t1:8.1f} us {(ux + 2 * uh) / t1 / 1e3:7.0f} GB/s | fwd(g) {t2:8.1f} us "
               f"{(ux + uh) / t2 / 1e3:7.0f} GB/s | bwd {t3:8.1f} us {(ux + 2 * uh) / t3 / 1e3:7.0f} GB/s | "
-              f"unfused fwd {t4:8.1f} us (bmm alone {t5:8.1f} us)", flush=True)
+              f"unfused fwd {t4:8.1f} us (bmm alone {t5:8.1f} us)"
+              + (f" | whole MLP fwd {tm:8.1f} us {3 * ux / tm / 1e3:6.0f} GB/s" if tm else ""), flush=True)
 
 
 if __name__ == "__main__":

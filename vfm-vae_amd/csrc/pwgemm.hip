@@ -245,6 +245,157 @@ int launch(const PwArgs& a, int B, hipStream_t st) {
     return launch_status();
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Whole ConvNeXt MLP forward without autograd (the D phase's no-grad generator pass):
+//   out = x_in + gamma * (bf16(W2 . g) + b2),  g = bf16(GELU(bf16(W1 . m) * s + b1))
+// per sample, with the 4C hidden tensor never leaving the chip: for every 128-row chunk of
+// the hidden dimension the workgroup computes h (GEMM 1, X = m from LDS), writes g as bf16
+// into an LDS image laid out like the X image, and accumulates GEMM 2 (B operand = that g
+// image) into the C x 128 output accumulators it keeps across the chunks. HBM traffic is
+// m + x_in + out instead of ~21 C x P tensors for the unfused pointwise/GELU/pointwise/
+// residual chain. C in {128, 256}.
+struct MlpArgs {
+    const __hip_bfloat16* W1;   // [4C, C]
+    const __hip_bfloat16* m;    // [B, C, N]
+    const float* s;             // [B, 4C] or null
+    const float* b1;            // [4C] or null
+    const __hip_bfloat16* W2;   // [C, 4C]
+    const float* b2;            // [C] or null
+    const float* gamma;         // [C] or null
+    const __hip_bfloat16* xin;  // [B, C, N]
+    __hip_bfloat16* out;        // [B, C, N]
+    int N;
+};
+
+template <int C>
+__global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
+    constexpr int M = 4 * C;
+    constexpr int YB = C / 128;                 // 32-row output blocks per wave (1 or 2)
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* gimg = lds + C * 256;        // [128 hidden rows][128 cols] bf16 image
+    float* s_sc = reinterpret_cast<float*>(gimg + 128 * 256);
+    float* s_bi = s_sc + M;
+    const int b = blockIdx.y;
+    const int n0 = blockIdx.x * NT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rw = wave & 3, cw = wave >> 2;
+    const int N = a.N;
+
+    const __hip_bfloat16* xb = a.m + (long long)b * C * N + n0;
+#pragma unroll 4
+    for (int i = tid; i < C * 16; i += 64 * WAVES) {
+        const int row = i >> 4, ch = i & 15;
+        *reinterpret_cast<uint4*>(lds + swz(row, ch)) =
+            *reinterpret_cast<const uint4*>(xb + (long long)row * N + ch * 8);
+    }
+    for (int i = tid; i < M; i += 64 * WAVES) {
+        s_sc[i] = a.s ? a.s[(long long)b * M + i] : 1.f;
+        s_bi[i] = a.b1 ? a.b1[i] : 0.f;
+    }
+    __syncthreads();
+
+    const int r = lane & 31, hh = lane >> 5;
+    const int g1 = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    const bool odd = r & 1;
+    int tro[NBW][2];
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+        const int c0 = 4 * (NBW * cw + j) + 2 * g1 + (p >> 1);
+        tro[j][0] = swz(8 * hh + q, c0) + 8 * (p & 1);
+        tro[j][1] = swz(8 * hh + 4 + q, c0) + 8 * (p & 1);
+    }
+    f32x16 accy[YB][NBW];
+#pragma unroll
+    for (int yb = 0; yb < YB; ++yb)
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) accy[yb][nb] = f32x16{};
+
+    for (int mc = 0; mc < M; mc += 128) {
+        // GEMM 1: h rows mc + 32rw .. +31, this wave's 64 columns
+        const int m0 = mc + 32 * rw;
+        const __hip_bfloat16* arow = a.W1 + (long long)(m0 + r) * C + 8 * hh;
+        f32x16 acc[NBW];
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x16{};
+#pragma unroll
+        for (int st = 0; st < C / 16; ++st) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + 16 * st);
+#pragma unroll
+            for (int nb = 0; nb < NBW; ++nb) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tro[nb][0] + 4096 * st));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tro[nb][1] + 4096 * st));
+                const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, __builtin_bit_cast(bf16x8, both), acc[nb], 0, 0, 0);
+            }
+        }
+        // GELU epilogue into the g image (row = hidden row within the chunk, column = pixel)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            const int lr = 32 * rw + (i & 3) + 8 * (i >> 2) + 4 * hh;     // chunk-local row of register i
+#pragma unroll
+            for (int nb = 0; nb < NBW; ++nb) {
+                float gv[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const float z = fmaf(bf16_round(acc[nb][i + t]), s_sc[mc + lr + t], s_bi[mc + lr + t]);
+                    gv[t] = z * gelu_parts(z).cdf;
+                }
+                const uint32_t pk = pair_pack(gv[0], gv[1], odd);
+                const int row = lr + (odd ? 1 : 0);
+                const int col = 64 * cw + 32 * nb + r - (odd ? 1 : 0);
+                *reinterpret_cast<uint32_t*>(gimg + swz(row, col >> 3) + 2 * (col & 7)) = pk;
+            }
+        }
+        __syncthreads();
+        // GEMM 2: y[c] += W2[c, mc : mc + 128] . g
+#pragma unroll
+        for (int yb = 0; yb < YB; ++yb) {
+            const __hip_bfloat16* a2 = a.W2 + (long long)(32 * (rw + 4 * yb) + r) * M + mc + 8 * hh;
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(a2 + 16 * st);
+#pragma unroll
+                for (int nb = 0; nb < NBW; ++nb) {
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(gimg + tro[nb][0] + 4096 * st));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(gimg + tro[nb][1] + 4096 * st));
+                    const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    accy[yb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, __builtin_bit_cast(bf16x8, both),
+                                                                           accy[yb][nb], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // out = x_in + gamma * (bf16(y) + b2)
+    const long long base = (long long)b * C * N + n0 + 64 * cw + r - (odd ? 1 : 0);
+#pragma unroll
+    for (int yb = 0; yb < YB; ++yb)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            const int cA = 32 * (rw + 4 * yb) + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const int cme = cA + (odd ? 1 : 0);
+            float bb[2], gg[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                bb[t] = a.b2 ? a.b2[cA + t] : 0.f;
+                gg[t] = a.gamma ? a.gamma[cA + t] : 1.f;
+            }
+#pragma unroll
+            for (int nb = 0; nb < NBW; ++nb) {
+                const long long idx = base + (long long)cme * N + 32 * nb;
+                const uint32_t own = *reinterpret_cast<const uint32_t*>(a.xin + idx);
+                const uint32_t x = (uint32_t)__shfl_xor((int)(odd ? (own & 0xffffu) : (own >> 16)), 1);
+                const float xv0 = __uint_as_float((odd ? x : (own & 0xffffu)) << 16);
+                const float xv1 = __uint_as_float((odd ? (own >> 16) : x) << 16);
+                const float o0 = fmaf(gg[0], bf16_round(accy[yb][nb][i]) + bb[0], xv0);
+                const float o1 = fmaf(gg[1], bf16_round(accy[yb][nb][i + 1]) + bb[1], xv1);
+                *reinterpret_cast<uint32_t*>(a.out + idx) = pair_pack(o0, o1, odd);
+            }
+        }
+}
+
 }  // namespace
 
 extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale, const float* bias,
@@ -284,3 +435,39 @@ extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale
 }
 
 extern "C" int vfm_pw_gemm_gelu_tiles(int N) { return (N > 0 && N % NT == 0) ? N / PT : VFM_NO_KERNEL; }
+
+extern "C" int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* s, const float* b1, const void* W2,
+                                    const float* b2, const float* gamma, const void* xin, void* out, int B, int C,
+                                    int N, void* stream) {
+    if (!W1 || !m || !W2 || !xin || !out || B <= 0 || N <= 0) return VFM_ERR_ARGS;
+    if ((C != 128 && C != 256) || N % NT != 0) return VFM_NO_KERNEL;
+    MlpArgs a;
+    a.W1 = static_cast<const __hip_bfloat16*>(W1);
+    a.m = static_cast<const __hip_bfloat16*>(m);
+    a.s = s;
+    a.b1 = b1;
+    a.W2 = static_cast<const __hip_bfloat16*>(W2);
+    a.b2 = b2;
+    a.gamma = gamma;
+    a.xin = static_cast<const __hip_bfloat16*>(xin);
+    a.out = static_cast<__hip_bfloat16*>(out);
+    a.N = N;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t lds = (size_t)C * 256 + 128 * 256 + 8 * 4 * (size_t)C;
+    if (C == 128) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)mlp_fwd<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL((mlp_fwd<128>), dim3(N / NT, B), dim3(64 * WAVES), lds, st, a);
+    } else {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)mlp_fwd<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL((mlp_fwd<256>), dim3(N / NT, B), dim3(64 * WAVES), lds, st, a);
+    }
+    return launch_status();
+}

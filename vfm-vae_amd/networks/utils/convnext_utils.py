@@ -98,11 +98,17 @@ class ConvNeXtSynthesisLayer(nn.Module):
         m = decoder_ops.group_norm(d, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps,
                                    out_dtype=cdt, style=style)                 # GN(d) * s_b
         w1 = self.pwconv1.weight.reshape(4 * C, C)
-        h = decoder_ops.pointwise(w1, m.reshape(B, C, H * W))                    # [B, 4C, HW]
         dcoef = decoder_ops.demod_coefficients(w1, style) if self.pwconv1.demodulate else None
+        gamma = self.gamma.reshape(-1) if self.gamma is not None else None
+        if decoder_ops.convnext_mlp_fusable(m, C, H * W, x_in):
+            # no autograd (the D phase's generator pass): the whole MLP in one kernel
+            out = decoder_ops.convnext_mlp_nograd(m.reshape(B, C, H * W), w1, dcoef, self.pwconv1.bias.reshape(-1),
+                                                  self.pwconv2.weight.reshape(C, 4 * C), self.pwconv2.bias, gamma,
+                                                  x_in.reshape(B, C, H * W))
+            return out.reshape(B, C, H, W)
+        h = decoder_ops.pointwise(w1, m.reshape(B, C, H * W))                    # [B, 4C, HW]
         g = decoder_ops.scale_bias_gelu(h, dcoef, self.pwconv1.bias.reshape(-1))
         y = decoder_ops.pointwise(self.pwconv2.weight.reshape(C, 4 * C), g)     # [B, C, HW]
-        gamma = self.gamma.reshape(-1) if self.gamma is not None else None
         out = decoder_ops.layer_scale_residual(y, self.pwconv2.bias, gamma, x_in.reshape(B, C, H * W))
         return out.reshape(B, C, H, W)
 

@@ -389,6 +389,35 @@ def layer_scale_residual(y, bias, gamma, x_in):
 
 
 # ---------------------------------------------------------------------------
+# Whole ConvNeXt MLP without autograd (reference convnext_utils.py:135-142): the D phase's
+# no-grad generator pass keeps the 4C hidden tensor on chip (csrc/pwgemm.hip mlp_fwd).
+
+MLP_CHANNELS = (128,)     # measured faster than the unfused chain only at C = 128 (b5 256^2)
+
+
+def convnext_mlp_supported(m, C, P):
+    return (m.is_cuda and m.dtype == torch.bfloat16 and C in MLP_CHANNELS and P % 128 == 0
+            and not torch.is_grad_enabled())
+
+
+def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
+    """m, x_in: bf16 [B, C, P]; w1 [4C, C], w2 [C, 4C] (any float dtype, cast to bf16);
+    dcoef [B, 4C] fp32 or None; b1 [4C], b2, gamma [C] or None. Returns bf16 [B, C, P]."""
+    m, x_in = _c(m), _c(x_in)
+    B, C, P = m.shape
+    w1c = _cast_cached(w1, torch.bfloat16).contiguous()
+    w2c = _cast_cached(w2, torch.bfloat16).contiguous()
+    s = None if dcoef is None else dcoef.detach().float().contiguous()
+    out = torch.empty_like(x_in)
+    with kernel_timer.region(_rn('convnext_mlp_fwd', m), _nb(m, x_in, out), flops=4.0 * B * P * C * 4 * C,
+                             bound="hbm"):
+        _check(_lib.vfm_convnext_mlp_fwd(w1c.data_ptr(), m.data_ptr(), _p(s), _p(_f32(b1)), w2c.data_ptr(),
+                                         _p(_f32(b2)), _p(_f32(gamma)), x_in.data_ptr(), out.data_ptr(), B, C, P,
+                                         _stream()), 'vfm_convnext_mlp_fwd')
+    return out
+
+
+# ---------------------------------------------------------------------------
 # PixelShuffle + replicate pad + fixed blur (reference convnext_utils.py:234-257).
 
 

@@ -155,6 +155,20 @@ def blur_replicate(x, blur1d, impl='cuda'):
     return F.conv2d(F.pad(x, pad, mode='replicate'), w, groups=c)
 
 
+def convnext_mlp_fusable(m, C, P, x_in):
+    """True when the layer's pointwise -> GELU -> pointwise -> residual chain can run as
+    one kernel: no autograd, ROCm bf16 activations, a supported width (decoder_hip)."""
+    if _FORCE_REF or not m.is_cuda or x_in.dtype != torch.bfloat16:
+        return False
+    from . import decoder_hip
+    return decoder_hip.convnext_mlp_supported(m, C, P)
+
+
+def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
+    from . import decoder_hip
+    return decoder_hip.convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in)
+
+
 def demod_coefficients(weight2d, style, eps=1e-8):
     """dcoef[b, o] = rsqrt(sum_i (W[o, i] * s[b, i])^2 + eps), computed as a tiny GEMM."""
     return torch.rsqrt(style.float().square() @ weight2d.float().square().t() + eps)
