@@ -269,13 +269,15 @@ struct MlpArgs {
 };
 
 template <int C>
-__global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
+__global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
     constexpr int M = 4 * C;
     constexpr int YB = C / 128;                 // 32-row output blocks per wave (1 or 2)
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     unsigned char* gimg = lds + C * 256;        // [128 hidden rows][128 cols] bf16 image
     float* s_sc = reinterpret_cast<float*>(gimg + 128 * 256);
     float* s_bi = s_sc + M;
+    float* s_b2 = s_bi + M;
+    float* s_gm = s_b2 + C;
     const int b = blockIdx.y;
     const int n0 = blockIdx.x * NT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -293,6 +295,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
         s_sc[i] = a.s ? a.s[(long long)b * M + i] : 1.f;
         s_bi[i] = a.b1 ? a.b1[i] : 0.f;
     }
+    for (int i = tid; i < C; i += 64 * WAVES) {
+        s_b2[i] = a.b2 ? a.b2[i] : 0.f;
+        s_gm[i] = a.gamma ? a.gamma[i] : 1.f;
+    }
     __syncthreads();
 
     const int r = lane & 31, hh = lane >> 5;
@@ -305,6 +311,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
         tro[j][0] = swz(8 * hh + q, c0) + 8 * (p & 1);
         tro[j][1] = swz(8 * hh + 4 + q, c0) + 8 * (p & 1);
     }
+    const long long base = (long long)b * C * N + n0 + 64 * cw + r - (odd ? 1 : 0);
     f32x16 accy[YB][NBW];
 #pragma unroll
     for (int yb = 0; yb < YB; ++yb)
@@ -318,9 +325,13 @@ __global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
         f32x16 acc[NBW];
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x16{};
+        bf16x8 p0 = *reinterpret_cast<const bf16x8*>(arow);
+        bf16x8 p1 = *reinterpret_cast<const bf16x8*>(arow + 16);
 #pragma unroll
         for (int st = 0; st < C / 16; ++st) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + 16 * st);
+            const bf16x8 af = p0;
+            p0 = p1;
+            if (st + 2 < C / 16) p1 = *reinterpret_cast<const bf16x8*>(arow + 16 * (st + 2));
 #pragma unroll
             for (int nb = 0; nb < NBW; ++nb) {
                 const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tro[nb][0] + 4096 * st));
@@ -329,6 +340,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
                 acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, __builtin_bit_cast(bf16x8, both), acc[nb], 0, 0, 0);
             }
         }
+        // first two W2 fragments of GEMM 2, in flight during the GELU epilogue
+        const __hip_bfloat16* a2row = a.W2 + (long long)(32 * rw + r) * M + mc + 8 * hh;
+        bf16x8 q0 = *reinterpret_cast<const bf16x8*>(a2row);
+        bf16x8 q1 = *reinterpret_cast<const bf16x8*>(a2row + 16);
         // GELU epilogue into the g image (row = hidden row within the chunk, column = pixel)
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
@@ -351,10 +366,16 @@ __global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
         // GEMM 2: y[c] += W2[c, mc : mc + 128] . g
 #pragma unroll
         for (int yb = 0; yb < YB; ++yb) {
-            const __hip_bfloat16* a2 = a.W2 + (long long)(32 * (rw + 4 * yb) + r) * M + mc + 8 * hh;
+            const __hip_bfloat16* a2 = a2row + (long long)128 * yb * M;
+            if (yb > 0) {
+                q0 = *reinterpret_cast<const bf16x8*>(a2);
+                q1 = *reinterpret_cast<const bf16x8*>(a2 + 16);
+            }
 #pragma unroll
             for (int st = 0; st < 8; ++st) {
-                const bf16x8 af = *reinterpret_cast<const bf16x8*>(a2 + 16 * st);
+                const bf16x8 af = q0;
+                q0 = q1;
+                if (st + 2 < 8) q1 = *reinterpret_cast<const bf16x8*>(a2 + 16 * (st + 2));
 #pragma unroll
                 for (int nb = 0; nb < NBW; ++nb) {
                     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(gimg + tro[nb][0] + 4096 * st));
@@ -368,34 +389,36 @@ __global__ __launch_bounds__(64 * WAVES, 1) void mlp_fwd(MlpArgs a) {
         __syncthreads();
     }
 
-    // out = x_in + gamma * (bf16(y) + b2)
-    const long long base = (long long)b * C * N + n0 + 64 * cw + r - (odd ? 1 : 0);
+    // out = x_in + gamma * (bf16(y) + b2); all residual loads are issued before the first store
+    // (CDNA4 vmcnt counts stores, so interleaving would serialise every load behind them)
 #pragma unroll
-    for (int yb = 0; yb < YB; ++yb)
+    for (int yb = 0; yb < YB; ++yb) {
+        uint32_t xraw[8][NBW];
+#pragma unroll
+        for (int i = 0; i < 16; i += 2)
+#pragma unroll
+            for (int nb = 0; nb < NBW; ++nb) {
+                const int cme = 32 * (rw + 4 * yb) + (i & 3) + 8 * (i >> 2) + 4 * hh + (odd ? 1 : 0);
+                xraw[i / 2][nb] = *reinterpret_cast<const uint32_t*>(a.xin + base + (long long)cme * N + 32 * nb);
+            }
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
             const int cA = 32 * (rw + 4 * yb) + (i & 3) + 8 * (i >> 2) + 4 * hh;
             const int cme = cA + (odd ? 1 : 0);
-            float bb[2], gg[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                bb[t] = a.b2 ? a.b2[cA + t] : 0.f;
-                gg[t] = a.gamma ? a.gamma[cA + t] : 1.f;
-            }
+            const float bb0 = s_b2[cA], bb1 = s_b2[cA + 1], gg0 = s_gm[cA], gg1 = s_gm[cA + 1];
 #pragma unroll
             for (int nb = 0; nb < NBW; ++nb) {
-                const long long idx = base + (long long)cme * N + 32 * nb;
-                const uint32_t own = *reinterpret_cast<const uint32_t*>(a.xin + idx);
+                const uint32_t own = xraw[i / 2][nb];
                 const uint32_t x = (uint32_t)__shfl_xor((int)(odd ? (own & 0xffffu) : (own >> 16)), 1);
                 const float xv0 = __uint_as_float((odd ? x : (own & 0xffffu)) << 16);
                 const float xv1 = __uint_as_float((odd ? (own >> 16) : x) << 16);
-                const float o0 = fmaf(gg[0], bf16_round(accy[yb][nb][i]) + bb[0], xv0);
-                const float o1 = fmaf(gg[1], bf16_round(accy[yb][nb][i + 1]) + bb[1], xv1);
-                *reinterpret_cast<uint32_t*>(a.out + idx) = pair_pack(o0, o1, odd);
+                const float o0 = fmaf(gg0, bf16_round(accy[yb][nb][i]) + bb0, xv0);
+                const float o1 = fmaf(gg1, bf16_round(accy[yb][nb][i + 1]) + bb1, xv1);
+                *reinterpret_cast<uint32_t*>(a.out + base + (long long)cme * N + 32 * nb) = pair_pack(o0, o1, odd);
             }
         }
+    }
 }
-
 }  // namespace
 
 extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale, const float* bias,
@@ -453,7 +476,7 @@ extern "C" int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* 
     a.out = static_cast<__hip_bfloat16*>(out);
     a.N = N;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t lds = (size_t)C * 256 + 128 * 256 + 8 * 4 * (size_t)C;
+    const size_t lds = (size_t)C * 256 + 128 * 256 + 8 * 4 * (size_t)C + 8 * (size_t)C;
     if (C == 128) {
         static bool attr = false;
         if (!attr) {
