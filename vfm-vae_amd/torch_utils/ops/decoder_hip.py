@@ -11,6 +11,7 @@ Every launch is bracketed by `kernel_timer.region(name, algorithmic_bytes)`
 report the dominant kernel's roofline.
 """
 import ctypes
+import os
 
 import torch
 
@@ -392,7 +393,8 @@ def layer_scale_residual(y, bias, gamma, x_in):
 # Whole ConvNeXt MLP without autograd (reference convnext_utils.py:135-142): the D phase's
 # no-grad generator pass keeps the 4C hidden tensor on chip (csrc/pwgemm.hip mlp_fwd).
 
-MLP_CHANNELS = (128,)     # measured faster than the unfused chain only at C = 128 (b5 256^2)
+# measured faster than the unfused chain only at C = 128 (b5 256^2); VFM_NO_FUSED_MLP=1 for A/B
+MLP_CHANNELS = () if os.environ.get("VFM_NO_FUSED_MLP") else (128,)
 
 
 def convnext_mlp_supported(m, C, P):
