@@ -231,10 +231,12 @@ int vfm_pw_gemm_gelu_tiles(int N);
  *   out = x_in + gamma * (bf16(W2 . g) + b2),  g = bf16(GELU(bf16(W1 . m) * s + b1)).
  *   W1: bf16 [4C, C]; m, x_in, out: bf16 [B, C, N]; s: fp32 [B, 4C] (NULL = 1);
  *   b1: fp32 [4C]; W2: bf16 [C, 4C]; b2, gamma: fp32 [C] (NULL = 0 / 1).
+ *   hout, gout: bf16 [B, 4C, N] (both or neither; NULL: not written) = bf16(W1 . m) and g,
+ *   yout: bf16 [B, C, N] (NULL: not written) = bf16(W2 . g) — what the backward needs.
  * C in {128, 256}, N % 128 == 0 (else VFM_NO_KERNEL). */
 int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* s, const float* b1, const void* W2,
-                         const float* b2, const float* gamma, const void* xin, void* out, int B, int C, int N,
-                         void* stream);
+                         const float* b2, const float* gamma, const void* xin, void* out, void* hout, void* gout,
+                         void* yout, int B, int C, int N, void* stream);
 
 #ifdef __cplusplus
 }

@@ -104,7 +104,7 @@ def test_convnext_mlp_forward(B, C, N):
     gamma = torch.randn(C, generator=g).cuda()
     out = torch.empty_like(x)
     rc = lib.vfm_convnext_mlp_fwd(W1.data_ptr(), m.data_ptr(), s.data_ptr(), b1.data_ptr(), W2.data_ptr(),
-                                  b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), out.data_ptr(), B, C, N,
+                                  b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), out.data_ptr(), None, None, None, B, C, N,
                                   co.stream_ptr())
     torch.cuda.synchronize()
     assert rc == 0
@@ -114,15 +114,15 @@ def test_convnext_mlp_forward(B, C, N):
     ref = x.float() + gamma[None, :, None] * (y + b2[None, :, None])
     assert _rel(out.float(), ref) < 1e-2
     assert lib.vfm_convnext_mlp_fwd(W1.data_ptr(), m.data_ptr(), None, None, W2.data_ptr(), None, None,
-                                    x.data_ptr(), out.data_ptr(), B, 512, N, co.stream_ptr()) == co.VFM_NO_KERNEL
+                                    x.data_ptr(), out.data_ptr(), None, None, None, B, 512, N, co.stream_ptr()) == co.VFM_NO_KERNEL
 
 
 @pytest.mark.parametrize("res", [16, 32])
 def test_convnext_layer_nograd_uses_fused_mlp(res):
     """ConvNeXtSynthesisLayer (C=128, bf16) without autograd takes the fused MLP kernel and
-    matches the autograd (unfused) forward to bf16 rounding."""
+    matches the unfused forward to bf16 rounding."""
     from networks.utils.convnext_utils import ConvNeXtSynthesisLayer
-    from torch_utils.ops import kernel_timer
+    from torch_utils.ops import decoder_hip, kernel_timer
     torch.manual_seed(0)
     lyr = ConvNeXtSynthesisLayer(128, 512, 7, layer_scale_init=0.5, block_index=2, legacy=True).cuda()
     with torch.no_grad():
@@ -130,8 +130,11 @@ def test_convnext_layer_nograd_uses_fused_mlp(res):
             p.add_(torch.randn_like(p) * 0.05)
     x = torch.randn(2, 128, res, res, device="cuda").bfloat16()
     w = torch.randn(2, 512, device="cuda")
+    saved = decoder_hip.MLP_CHANNELS
+    decoder_hip.MLP_CHANNELS = ()
     with torch.enable_grad():
-        ref = lyr(x, w, torch.bfloat16)
+        ref = lyr(x, w, torch.bfloat16)          # unfused chain
+    decoder_hip.MLP_CHANNELS = saved
     kernel_timer.enable(True)
     with torch.no_grad():
         got = lyr(x, w, torch.bfloat16)
@@ -139,3 +142,46 @@ def test_convnext_layer_nograd_uses_fused_mlp(res):
     kernel_timer.enable(False)
     assert any(n.startswith("convnext_mlp_fwd") for n in names), names
     assert _rel(got.float(), ref.float()) < 2e-2
+
+
+def test_convnext_layer_grad_fused_matches_unfused():
+    """Autograd path at C=128: fused forward (h, g, y saved) + residual backward + fused
+    GELU-backward GEMM, against the unfused Functions; output and every gradient."""
+    from networks.utils.convnext_utils import ConvNeXtSynthesisLayer
+    from torch_utils.ops import decoder_hip, kernel_timer
+    torch.manual_seed(1)
+    lyr = ConvNeXtSynthesisLayer(128, 512, 7, layer_scale_init=0.5, block_index=2, legacy=True).cuda()
+    with torch.no_grad():
+        for p in lyr.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    x0 = torch.randn(2, 128, 32, 32, device="cuda").bfloat16()
+    w0 = torch.randn(2, 512, device="cuda")
+    dout = torch.randn(2, 128, 32, 32, device="cuda").bfloat16()
+
+    def run(fused):
+        saved = decoder_hip.MLP_CHANNELS
+        decoder_hip.MLP_CHANNELS = (128,) if fused else ()
+        try:
+            lyr.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            kernel_timer.enable(True)
+            out = lyr(x, w, torch.bfloat16)
+            out.backward(dout)
+            names = set(kernel_timer._records)
+            kernel_timer.enable(False)
+            grads = {n: p.grad.detach().clone() for n, p in lyr.named_parameters() if p.grad is not None}
+            return out.detach(), x.grad.detach(), w.grad.detach(), grads, names
+        finally:
+            decoder_hip.MLP_CHANNELS = saved
+
+    o1, gx1, gw1, g1, n1 = run(True)
+    o0, gx0, gw0, g0, n0 = run(False)
+    assert any(n.startswith("convnext_mlp_fwd") for n in n1) and any(n.startswith("pw_gemm_gelu_bwd") for n in n1)
+    assert not any(n.startswith("convnext_mlp_fwd") for n in n0)
+    assert _rel(o1.float(), o0.float()) < 2e-2
+    assert _rel(gx1.float(), gx0.float()) < 3e-2
+    assert _rel(gw1.float(), gw0.float()) < 3e-2
+    assert set(g1) == set(g0)
+    for k in g0:
+        assert _rel(g1[k].float(), g0[k].float()) < 3e-2, k

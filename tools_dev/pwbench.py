@@ -68,7 +68,7 @@ def main():
             gam = torch.randn(C, device="cuda")
             tm = timeit(lambda: lib.vfm_convnext_mlp_fwd(A.data_ptr(), X.data_ptr(), s.data_ptr(), bias.data_ptr(),
                                                          W2.data_ptr(), b2.data_ptr(), gam.data_ptr(), xin.data_ptr(),
-                                                         outm.data_ptr(), B, C, N, st))
+                                                         outm.data_ptr(), None, None, None, B, C, N, st))
         t4 = timeit(unfused_fwd)
         t5 = timeit(lambda: torch.bmm(A.expand(B, M, K), X))
         print(f"{name}: fused fwd(h+g) {t1:8.1f} us {(ux + 2 * uh) / t1 / 1e3:7.0f} GB/s | fwd(g) {t2:8.1f} us "

@@ -265,6 +265,9 @@ struct MlpArgs {
     const float* gamma;         // [C] or null
     const __hip_bfloat16* xin;  // [B, C, N]
     __hip_bfloat16* out;        // [B, C, N]
+    __hip_bfloat16* hout;       // [B, 4C, N] bf16(W1 . m) for the backward, or null
+    __hip_bfloat16* gout;       // [B, 4C, N] g, or null
+    __hip_bfloat16* yout;       // [B, C, N] bf16(W2 . g), or null
     int N;
 };
 
@@ -360,6 +363,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
                 const int row = lr + (odd ? 1 : 0);
                 const int col = 64 * cw + 32 * nb + r - (odd ? 1 : 0);
                 *reinterpret_cast<uint32_t*>(gimg + swz(row, col >> 3) + 2 * (col & 7)) = pk;
+                if (a.hout) {           // saved for the backward (autograd pass)
+                    const long long gi = ((long long)b * M + mc + row) * N + n0 + col;
+                    *reinterpret_cast<uint32_t*>(a.gout + gi) = pk;
+                    *reinterpret_cast<uint32_t*>(a.hout + gi) =
+                        pair_pack(bf16_round(acc[nb][i]), bf16_round(acc[nb][i + 1]), odd);
+                }
             }
         }
         __syncthreads();
@@ -412,9 +421,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
                 const uint32_t x = (uint32_t)__shfl_xor((int)(odd ? (own & 0xffffu) : (own >> 16)), 1);
                 const float xv0 = __uint_as_float((odd ? x : (own & 0xffffu)) << 16);
                 const float xv1 = __uint_as_float((odd ? (own >> 16) : x) << 16);
-                const float o0 = fmaf(gg0, bf16_round(accy[yb][nb][i]) + bb0, xv0);
-                const float o1 = fmaf(gg1, bf16_round(accy[yb][nb][i + 1]) + bb1, xv1);
+                const float y0 = bf16_round(accy[yb][nb][i]), y1 = bf16_round(accy[yb][nb][i + 1]);
+                const float o0 = fmaf(gg0, y0 + bb0, xv0);
+                const float o1 = fmaf(gg1, y1 + bb1, xv1);
                 *reinterpret_cast<uint32_t*>(a.out + base + (long long)cme * N + 32 * nb) = pair_pack(o0, o1, odd);
+                if (a.yout)
+                    *reinterpret_cast<uint32_t*>(a.yout + base + (long long)cme * N + 32 * nb) = pair_pack(y0, y1, odd);
             }
         }
     }
@@ -460,9 +472,10 @@ extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale
 extern "C" int vfm_pw_gemm_gelu_tiles(int N) { return (N > 0 && N % NT == 0) ? N / PT : VFM_NO_KERNEL; }
 
 extern "C" int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* s, const float* b1, const void* W2,
-                                    const float* b2, const float* gamma, const void* xin, void* out, int B, int C,
-                                    int N, void* stream) {
+                                    const float* b2, const float* gamma, const void* xin, void* out, void* hout,
+                                    void* gout, void* yout, int B, int C, int N, void* stream) {
     if (!W1 || !m || !W2 || !xin || !out || B <= 0 || N <= 0) return VFM_ERR_ARGS;
+    if ((hout == nullptr) != (gout == nullptr)) return VFM_ERR_ARGS;
     if ((C != 128 && C != 256) || N % NT != 0) return VFM_NO_KERNEL;
     MlpArgs a;
     a.W1 = static_cast<const __hip_bfloat16*>(W1);
@@ -474,6 +487,9 @@ extern "C" int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* 
     a.gamma = gamma;
     a.xin = static_cast<const __hip_bfloat16*>(xin);
     a.out = static_cast<__hip_bfloat16*>(out);
+    a.hout = static_cast<__hip_bfloat16*>(hout);
+    a.gout = static_cast<__hip_bfloat16*>(gout);
+    a.yout = static_cast<__hip_bfloat16*>(yout);
     a.N = N;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t lds = (size_t)C * 256 + 128 * 256 + 8 * 4 * (size_t)C + 8 * (size_t)C;

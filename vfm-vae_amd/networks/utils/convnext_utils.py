@@ -101,7 +101,7 @@ class ConvNeXtSynthesisLayer(nn.Module):
         dcoef = decoder_ops.demod_coefficients(w1, style) if self.pwconv1.demodulate else None
         gamma = self.gamma.reshape(-1) if self.gamma is not None else None
         if decoder_ops.convnext_mlp_fusable(m, C, H * W, x_in):
-            # no autograd (the D phase's generator pass): the whole MLP in one kernel
+            # the whole MLP forward in one kernel (hidden 4C tensor on chip without autograd)
             out = decoder_ops.convnext_mlp_nograd(m.reshape(B, C, H * W), w1, dcoef, self.pwconv1.bias.reshape(-1),
                                                   self.pwconv2.weight.reshape(C, 4 * C), self.pwconv2.bias, gamma,
                                                   x_in.reshape(B, C, H * W))

@@ -398,8 +398,87 @@ MLP_CHANNELS = () if os.environ.get("VFM_NO_FUSED_MLP") else (128,)
 
 
 def convnext_mlp_supported(m, C, P):
-    return (m.is_cuda and m.dtype == torch.bfloat16 and C in MLP_CHANNELS and P % 128 == 0
-            and not torch.is_grad_enabled())
+    return m.is_cuda and m.dtype == torch.bfloat16 and C in MLP_CHANNELS and P % 128 == 0
+
+
+class _ConvNeXtMLP(torch.autograd.Function):
+    """pointwise(W1) -> GELU(h*s+b1) -> pointwise(W2) -> x_in + gamma*(y+b2) with autograd.
+    Forward: one kernel that also writes h, g and y for the backward. Backward: the layer-
+    scale residual kernel, then the 4C->C conv's data gradient with GELU' fused into its
+    epilogue (vfm_pw_gemm_gelu mode 1), and hipBLASLt GEMMs for the two weight gradients
+    and dm; the same arithmetic as the unfused Functions above (bf16 roundings included)."""
+
+    @staticmethod
+    def forward(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in):
+        _edges(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in)
+        m, x_in = _c(m), _c(x_in)
+        B, C, P = m.shape
+        w1c = _cast_cached(w1, torch.bfloat16).contiguous()
+        w2c = _cast_cached(w2, torch.bfloat16).contiguous()
+        s = None if dcoef is None else dcoef.detach().float().contiguous()
+        fb1, fb2, fg = _f32(b1), _f32(b2), _f32(gamma)
+        out = torch.empty_like(x_in)
+        h = torch.empty([B, 4 * C, P], dtype=torch.bfloat16, device=m.device)
+        g = torch.empty_like(h)
+        y = torch.empty_like(m)
+        with kernel_timer.region(_rn('convnext_mlp_fwd', m), _nb(m, x_in, out, h, g, y)):
+            _check(_lib.vfm_convnext_mlp_fwd(w1c.data_ptr(), m.data_ptr(), _p(s), _p(fb1), w2c.data_ptr(), _p(fb2),
+                                             _p(fg), x_in.data_ptr(), out.data_ptr(), h.data_ptr(), g.data_ptr(),
+                                             y.data_ptr(), B, C, P, _stream()), 'vfm_convnext_mlp_fwd')
+        ctx.save_for_backward(m, h, g, y, w1c, w2c, s, fb1, fb2, fg)
+        ctx.meta = (w1.dtype, w2.dtype, None if dcoef is None else dcoef.dtype, None if b1 is None else b1.dtype,
+                    None if b2 is None else b2.dtype, None if gamma is None else gamma.dtype)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout):
+        m, h, g, y, w1c, w2c, s, fb1, fb2, fg = ctx.saved_tensors
+        w1dt, w2dt, sdt, b1dt, b2dt, gdt = ctx.meta
+        B, C, P = m.shape
+        O = 4 * C
+        dout = _c(dout.to(torch.bfloat16))
+        # layer-scale residual: dy = gamma * dout, sums for d_b2 / d_gamma
+        dy = torch.empty_like(y)
+        r0 = torch.empty([B * C], dtype=torch.float32, device=m.device)
+        r1 = torch.empty_like(r0)
+        with kernel_timer.region(_rn('layer_scale_residual_bwd', y), _nb(y, dout, dy)):
+            _check(_lib.vfm_layer_scale_residual_bwd(y.data_ptr(), _p(fb2), _p(fg), dout.data_ptr(), dy.data_ptr(),
+                                                     r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout), B, C, P,
+                                                     _stream()), 'vfm_layer_scale_residual_bwd')
+        dw1 = db1 = ds = dw2 = db2 = dgm = dm = None
+        if fb2 is not None and _wanted(ctx, 5):
+            s1 = r1.view(B, C).sum(0)
+            db2 = (s1 * fg if fg is not None else s1).to(b2dt)
+        if fg is not None and _wanted(ctx, 6):
+            dgm = r0.view(B, C).sum(0).to(gdt)
+        if _wanted(ctx, 4):
+            dw2 = torch.bmm(dy, g.transpose(1, 2), out_dtype=torch.float32).sum(0).to(w2dt)
+        # dh = (W2^T dy) * GELU'(h*s+b1) * s, with the per-(b, o) sums for d_s and d_b1
+        tiles = _lib.vfm_pw_gemm_gelu_tiles(P)
+        w2t = w2c.t().contiguous()
+        dh = torch.empty_like(h)
+        p0 = torch.empty([B, tiles, O], dtype=torch.float32, device=m.device)
+        p1 = torch.empty_like(p0)
+        with kernel_timer.region(_rn('pw_gemm_gelu_bwd', h), _nb(dy, h, dh)):
+            _check(_lib.vfm_pw_gemm_gelu(w2t.data_ptr(), dy.data_ptr(), _p(s), _p(fb1), h.data_ptr(), dh.data_ptr(),
+                                         None, p0.data_ptr(), p1.data_ptr(), 1, B, O, C, P, _stream()),
+                   'vfm_pw_gemm_gelu')
+        if s is not None and _wanted(ctx, 2):
+            ds = p0.sum(1).to(sdt)
+        if fb1 is not None and _wanted(ctx, 3):
+            db1 = p1.sum((0, 1)).to(b1dt)
+        if _wanted(ctx, 1):
+            dw1 = torch.bmm(dh, m.transpose(1, 2), out_dtype=torch.float32).sum(0).to(w1dt)
+        if ctx.needs_input_grad[0]:
+            dm = torch.bmm(w1c.t().expand(B, C, O), dh)
+        dx = dout if ctx.needs_input_grad[7] else None
+        return dm, dw1, ds, db1, dw2, db2, dgm, dx
+
+
+def convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in):
+    """Autograd form of the fused MLP (same arguments as convnext_mlp_nograd)."""
+    return _ConvNeXtMLP.apply(m, w1, dcoef, b1, w2, b2, gamma, x_in)
 
 
 def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
@@ -414,7 +493,7 @@ def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
     with kernel_timer.region(_rn('convnext_mlp_fwd', m), _nb(m, x_in, out), flops=4.0 * B * P * C * 4 * C,
                              bound="hbm"):
         _check(_lib.vfm_convnext_mlp_fwd(w1c.data_ptr(), m.data_ptr(), _p(s), _p(_f32(b1)), w2c.data_ptr(),
-                                         _p(_f32(b2)), _p(_f32(gamma)), x_in.data_ptr(), out.data_ptr(), B, C, P,
+                                         _p(_f32(b2)), _p(_f32(gamma)), x_in.data_ptr(), out.data_ptr(), None, None, None, B, C, P,
                                          _stream()), 'vfm_convnext_mlp_fwd')
     return out
 

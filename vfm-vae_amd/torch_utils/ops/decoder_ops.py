@@ -157,7 +157,8 @@ def blur_replicate(x, blur1d, impl='cuda'):
 
 def convnext_mlp_fusable(m, C, P, x_in):
     """True when the layer's pointwise -> GELU -> pointwise -> residual chain can run as
-    one kernel: no autograd, ROCm bf16 activations, a supported width (decoder_hip)."""
+    one forward kernel (with or without autograd): ROCm bf16 activations, a supported
+    width (decoder_hip.MLP_CHANNELS)."""
     if _FORCE_REF or not m.is_cuda or x_in.dtype != torch.bfloat16:
         return False
     from . import decoder_hip
@@ -166,6 +167,8 @@ def convnext_mlp_fusable(m, C, P, x_in):
 
 def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
     from . import decoder_hip
+    if torch.is_grad_enabled():
+        return decoder_hip.convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in)
     return decoder_hip.convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in)
 
 

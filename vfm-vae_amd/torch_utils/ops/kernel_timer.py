@@ -91,6 +91,7 @@ _ROC = {
     "dwconv2d_bwd_weight": "dwr_bwd_w<{T}, {K}>",
     "shuffle_blur_fwd": "blur_fwd<{T}, 2, {K}>", "shuffle_blur_bwd": "blur_bwd<{T}, 2, {K}>",
     "residual_layer_norm": "ln_rows<", "codebook_argmax": "codebook_argmax_kernel<",
+    "convnext_mlp_fwd": "mlp_fwd<", "pw_gemm_gelu_bwd": "pw_gemm_gelu<1, ",
 }
 _TNAME = {"f32": "float", "bf16": "__hip_bfloat16", "f16": "__half", "f64": "double"}
 
