@@ -31,8 +31,10 @@
 //   C=256 @128^2: fwd h+g 0.87 ms (0.87), g only 0.70 ms, bwd 1.18 ms (1.03)
 //   C=512 @64^2:  fwd h+g 0.83 ms (0.62), g only 0.58 ms, bwd 1.01 ms (0.66)
 // What moved it: per-row scale/bias staged in LDS instead of a dependent global load per
-// row in the epilogue, h prefetched before the MFMA loop, 8 waves x 2 column blocks (4-5
-// waves/SIMD), lane-pair packing for 4-byte h loads and outputs. Staging whole output rows
+// row in the epilogue, the epilogue's h loads issued together right after the MFMAs (not
+// before them: that kept them live across the loop and cost occupancy; one step ahead was
+// slower still), 8 waves x 2 column blocks (4 waves/SIMD), lane-pair packing for 4-byte h
+// loads and outputs. Backward at C=128 / 256^2 is now 1.82 ms. Staging whole output rows
 // through LDS was slower. Next: find what still caps the epilogue (PMC VALU/wait counters).
 #include "vfm_common.h"
 
@@ -132,18 +134,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
         f32x16 acc[NBW];
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x16{};
-        const bool odd = r & 1;
-        uint32_t hraw[MODE == 1 ? 8 : 1][NBW];     // packed pairs, see pair_pack
-        if (MODE == 1) {
-#pragma unroll
-            for (int i = 0; i < 16; i += 2)
-#pragma unroll
-                for (int nb = 0; nb < NBW; ++nb) {
-                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh + (odd ? 1 : 0);
-                    hraw[i / 2][nb] = *reinterpret_cast<const uint32_t*>(a.h + outb - (odd ? 1 : 0) +
-                                                                         (long long)m * N + 32 * nb);
-                }
-        }
         bf16x8 a0 = *reinterpret_cast<const bf16x8*>(arow);
         bf16x8 a1 = *reinterpret_cast<const bf16x8*>(arow + 16);
 #pragma unroll
@@ -163,6 +153,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
             }
         }
 
+        const bool odd = r & 1;
+        uint32_t hraw[MODE == 1 ? 8 : 1][NBW];     // packed pairs, see pair_pack
+        if (MODE == 1) {
+#pragma unroll
+            for (int i = 0; i < 16; i += 2)
+#pragma unroll
+                for (int nb = 0; nb < NBW; ++nb) {
+                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh + (odd ? 1 : 0);
+                    hraw[i / 2][nb] = *reinterpret_cast<const uint32_t*>(a.h + outb - (odd ? 1 : 0) +
+                                                                         (long long)m * N + 32 * nb);
+                }
+        }
         // epilogue: register i of acc[nb] is row m0 + (i&3) + 8(i>>2) + 4hh, column n0 + 32nb + r
         if (MODE == 0) {
             const bool odd = r & 1;
