@@ -25,7 +25,9 @@
 // A lane l holds A[r][8h+j] (r = l&31, h = l>>5), B lane l holds B[8h+j][r], taken from the
 // row-major X image with two ds_read_b64_tr_b16; C/D: col = l&31, row = (i&3)+8(i>>2)+4h.
 //
-// Status: parity-tested (tests/test_pwgemm_gpu.py), not yet on the training path. Measured
+// Status: parity-tested (tests/test_pwgemm_gpu.py); mode 1 runs the backward of the b5
+// (C=128) ConvNeXt layers (torch_utils/ops/decoder_hip.py _ConvNeXtMLP); mode 0 is kept for
+// the other widths' future use (the forward at C=128 is mlp_fwd below). Measured
 // at batch 32 (tools_dev/pwbench.py, MI355X) against hipBLASLt bmm + the GELU row kernels:
 //   C=128 @256^2: fwd h+g 1.36 ms (unfused 1.64), fwd g only 1.05 ms, bwd 1.94 ms (2.08)
 //   C=256 @128^2: fwd h+g 0.87 ms (0.87), g only 0.70 ms, bwd 1.18 ms (1.03)
