@@ -1,0 +1,196 @@
+"""Inference tools: reconstruct / decode / evaluate run end to end on CPU
+with a tiny generator built from a YAML config and a training snapshot, and their outputs equal
+a direct `G(img, names, validation=True)` / `G.decode(z)` of the same batches, quantised the way
+torchvision's `to_pil_image` does (`mul(255).byte()`)."""
+import importlib.util
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+import net_cases
+from conftest import PKG
+
+TOOLS = os.path.join(PKG, "tools")
+
+
+def _load(rel):
+    path = os.path.join(TOOLS, rel)
+    spec = importlib.util.spec_from_file_location(os.path.basename(rel)[:-3] + "_tool", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="module")
+def setup(tmp_path_factory):
+    root = tmp_path_factory.mktemp("tools")
+    vfm = root / net_cases.VFM_DIRNAME
+    vfm.mkdir()
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(vfm / "config.json", "w"))
+    gkw = dict(net_cases.g_kwargs(str(vfm)), class_name="networks.generator.Generator")
+    cfg = root / "tiny.yaml"
+    yaml.safe_dump({"G_kwargs": gkw}, open(cfg, "w"))
+    common = _load("common.py")
+    torch.manual_seed(3)
+    G = common.build_vae(str(cfg), 64, torch.device("cpu"))
+    with torch.no_grad():                       # non-trivial weights everywhere (zero-init layers too)
+        for p in G.parameters():
+            p.add_(torch.randn_like(p) * 0.02)
+    ckpt = root / "snap.pth"
+    torch.save({"G": {}, "D": {}, "G_ema": G.state_dict(), "training_set_kwargs": {}}, ckpt)
+    return dict(root=root, cfg=str(cfg), ckpt=str(ckpt), common=common)
+
+
+def _fresh_vae(s):
+    common = s["common"]
+    G = common.build_vae(s["cfg"], 64, torch.device("cpu"))
+    inc = common.load_vae_weights(G, s["ckpt"], torch.device("cpu"), log=lambda *a: None)
+    assert not inc.missing_keys and not inc.unexpected_keys
+    return G
+
+
+def test_load_image_matches_torchvision_semantics(setup):
+    from PIL import Image
+    common = setup["common"]
+    d = setup["root"] / "img_sem"
+    d.mkdir()
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (70, 90, 3), dtype=np.uint8)          # H=70, W=90 → resize to 64x82 → crop
+    Image.fromarray(a).save(d / "a.png")
+    out = common.load_image(str(d / "a.png"), 64)
+    ref = np.asarray(Image.fromarray(a).resize((82, 64), Image.BILINEAR))[:, 9:73]
+    assert out.shape == (64, 64, 3) and (out == ref).all()
+    b = rng.integers(0, 256, (64, 64, 3), dtype=np.uint8)            # already at size: untouched
+    Image.fromarray(b).save(d / "b.png")
+    assert (common.load_image(str(d / "b.png"), 64) == b).all()
+    t = torch.tensor([[[[0.0, 0.999, 1.5, -0.2]]]]).expand(1, 3, 1, 4)
+    assert common.to_uint8(t)[0, 0, :, 0].tolist() == [0, 254, 255, 0]   # truncation, clamp
+
+
+def test_reconstruct_matches_direct_forward(setup):
+    from PIL import Image
+    common = setup["common"]
+    src = setup["root"] / "src"
+    src.mkdir()
+    rng = np.random.default_rng(1)
+    sizes = [(64, 64), (72, 96), (80, 64), (64, 64), (100, 70)]
+    for i, (h, w) in enumerate(sizes):
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(src / f"im{i}.png")
+    out = setup["root"] / "rec"
+    rec = _load("reconstruct/reconstruct.py")
+    rec.main(["--input-dir", str(src), "--output-dir", str(out), "--vae-pth", setup["ckpt"],
+              "--use-config", setup["cfg"], "--resolution", "64", "--batch-size-per-gpu", "2",
+              "--device", "cpu"])
+    names = sorted(os.listdir(src))
+    assert sorted(os.listdir(out / "inputs")) == names == sorted(os.listdir(out / "outputs"))
+    # validation forward samples the posterior from the global CPU RNG (as the reference's
+    # does), so compare tool and direct path from the same seed
+    G = _fresh_vae(setup)
+    rk = common.Rank("cpu")
+    out = setup["root"] / "rec2"
+    torch.manual_seed(11)
+    assert rec.run_rfid_reconstruction(G, str(src), str(out), 64, 2, rk, log=lambda *a: None) == 5
+    torch.manual_seed(11)
+    for s in range(0, len(names), 2):
+        batch = names[s:s + 2]
+        arrays = [common.load_image(str(src / n), 64) for n in batch]
+        x = torch.from_numpy(np.stack(arrays)).permute(0, 3, 1, 2).float() / 255
+        with torch.no_grad():
+            gen = G(x, batch, validation=True).gen_img
+        exp = common.to_uint8((gen + 1) / 2).numpy()
+        for i, n in enumerate(batch):
+            assert (common.load_png_uint8(str(out / "inputs" / n)) == arrays[i]).all()
+            got = common.load_png_uint8(str(out / "outputs" / n))
+            assert (got == exp[i]).all()
+
+
+def test_decode_latents_matches_direct_decode(setup):
+    from safetensors.torch import save_file
+    common = setup["common"]
+    lat = setup["root"] / "lat"
+    lat.mkdir()
+    g = torch.Generator().manual_seed(5)
+    z0 = torch.randn(3, 32, 4, 4, generator=g)
+    z1 = torch.randn(2, 32, 4, 4, generator=g)
+    save_file({"latents": z0, "labels": torch.arange(3)}, str(lat / "a.safetensors"))
+    save_file({"latents": z1}, str(lat / "b.safetensors"))
+    save_file({"other": z1}, str(lat / "c.safetensors"))                 # skipped: no latents
+    out = setup["root"] / "dec"
+    dec = _load("decode/decode_latents_to_images.py")
+    dec.main(["--input-dir", str(lat), "--output-dir", str(out), "--vae-pth", setup["ckpt"],
+              "--use-config", setup["cfg"], "--batch-size-per-gpu", "2", "--max-images-per-gpu", "4",
+              "--device", "cpu"])
+    files = sorted(os.listdir(out))
+    assert files == [f"rank00_{i:06d}.png" for i in range(4)]
+    G = _fresh_vae(setup)
+    with torch.no_grad():
+        imgs = torch.cat([G.decode(z0[0:2]), G.decode(z0[2:3]), G.decode(z1[0:2])])[:4]
+    exp = common.to_uint8((imgs + 1) / 2).numpy()
+    for i, f in enumerate(files):
+        assert (common.load_png_uint8(str(out / f)) == exp[i]).all()
+
+
+def test_rank_sharding_covers_every_file_once(setup):
+    common = setup["common"]
+    files = [f"f{i}" for i in range(7)]
+    parts = []
+    for r in range(3):
+        rk = common.Rank.__new__(common.Rank)
+        rk.rank, rk.world_size = r, 3
+        parts.append(rk.shard(files))
+    assert parts[0] == ["f0", "f3", "f6"] and sorted(sum(parts, [])) == files
+
+
+def test_evaluate_metrics(setup):
+    from PIL import Image
+    common = setup["common"]
+    ev = _load("reconstruct/evaluate.py")
+    a, b = setup["root"] / "ev_a", setup["root"] / "ev_b"
+    a.mkdir()
+    b.mkdir()
+    rng = np.random.default_rng(7)
+    imgs = [rng.integers(0, 256, (32, 32, 3), dtype=np.uint8) for _ in range(3)]
+    noisy = [np.clip(x.astype(int) + rng.integers(-8, 9, x.shape), 0, 255).astype(np.uint8) for x in imgs]
+    for i, (x, y) in enumerate(zip(imgs, noisy)):
+        Image.fromarray(x).save(a / f"{i}.png")
+        Image.fromarray(y).save(b / f"{i}.png")
+    Image.fromarray(imgs[0]).save(b / "only_in_b.png")
+    res = ev.evaluate_image_metrics(str(a), str(b), batch_size=2, num_workers=2, device="cpu", log=lambda *x: None)
+    assert res["total"] == 3
+    psnr = [10 * np.log10(4.0 / np.mean(((y.astype(np.float64) - x) / 127.5) ** 2)) for x, y in zip(imgs, noisy)]
+    assert abs(res["psnr"] - np.mean(psnr)) < 1e-6
+    assert 0.0 < res["ssim"] < 1.0 and res["lpips"] >= 0.0
+    same = ev.evaluate_image_metrics(str(a), str(a), batch_size=2, num_workers=2, device="cpu", log=lambda *x: None)
+    assert abs(same["ssim"] - 1.0) < 1e-6 and abs(same["lpips"]) < 1e-6
+    _ = common
+
+
+@pytest.mark.gpu
+def test_reconstruct_on_gpu_matches_cpu(setup):
+    """The tool on cuda:0 (decoder through the HIP kernels, fp32 as `num_fp16_res = 0` asks)
+    against the same tool on the CPU, same posterior noise (CPU RNG, same seed); tolerance:
+    ≤ 2 uint8 levels per pixel, ≥ 99 % identical, PSNR ≥ 50 dB."""
+    from PIL import Image
+    common = setup["common"]
+    rec = _load("reconstruct/reconstruct.py")
+    src = setup["root"] / "src_gpu"
+    src.mkdir()
+    rng = np.random.default_rng(2)
+    for i in range(4):
+        Image.fromarray(rng.integers(0, 256, (64, 64, 3), dtype=np.uint8)).save(src / f"g{i}.png")
+    outs = {}
+    for dev in ("cpu", "cuda:0"):
+        G = _fresh_vae(setup).to(dev)
+        out = setup["root"] / f"rec_{dev.replace(':', '')}"
+        torch.manual_seed(13)
+        rec.run_rfid_reconstruction(G, str(src), str(out), 64, 4, common.Rank(dev), log=lambda *a: None)
+        outs[dev] = out
+    for n in sorted(os.listdir(src)):
+        a = common.load_png_uint8(str(outs["cpu"] / "outputs" / n)).astype(int)
+        b = common.load_png_uint8(str(outs["cuda:0"] / "outputs" / n)).astype(int)
+        assert np.abs(a - b).max() <= 2 and (a == b).mean() >= 0.99
+        assert 10 * np.log10(255.0 ** 2 / max(np.mean((a - b) ** 2), 1e-12)) >= 50

@@ -125,6 +125,10 @@ class SSIM(nn.Module):
         c2 = (self.k2 * self.data_range) ** 2
         s_pp, s_tt, s_pt = e_pp - mu_p ** 2, e_tt - mu_t ** 2, e_pt - mu_p * mu_t
         ssim = ((2 * mu_p * mu_t + c1) * (2 * s_pt + c2)) / ((mu_p ** 2 + mu_t ** 2 + c1) * (s_pp + s_tt + c2))
+        # torchmetrics drops the reflect-padded border from the SSIM map before the mean
+        # (functional/image/ssim.py `_ssim_update`: ssim_idx_full_image[..., pad:-pad, pad:-pad])
+        if pad > 0:
+            ssim = ssim[..., pad:-pad, pad:-pad]
         return ssim.mean()
 
 
