@@ -104,7 +104,7 @@ def main(argv=None):
     torch.cuda.set_device(device)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
-    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.benchmark = bool(int(os.environ.get("VFM_CUDNN_BENCHMARK", "0")))
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
 

@@ -27,6 +27,7 @@ for s in "$@"; do
     pwbench) timeout -k 10 300 python tools_dev/pwbench.py > $out/pwbench.log 2>&1 ;;
     pwpmc)   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex pw_gemm_gelu -d $out/pwpmc -o run --output-format csv -- python3 tools_dev/pwbench.py > $out/pwpmc.log 2>&1 ;;
     gdebug)  timeout -k 10 300 python tools_dev/graph_debug.py > $out/gdebug.log 2>&1 ;;
+    benchfind) MIOPEN_FIND_MODE=NORMAL VFM_CUDNN_BENCHMARK=1 timeout -k 10 900 python bench.py --no-cpu-baseline > $out/benchfind.log 2>&1 ;;
     benchnf) VFM_NO_FUSED_MLP=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/benchnf.log 2>&1 ;;
     benchng) timeout -k 10 600 python bench.py --no-cpu-baseline --no-graphs > $out/benchng.log 2>&1 ;;
     decbench) timeout -k 10 300 python tools_dev/decbench.py > $out/decbench.log 2>&1 ;;

@@ -77,6 +77,12 @@ class SelfAttention(nn.Module):
         nk, nv = (t.to(q.dtype)[None, :, None, :].expand(B, h, 1, d) for t in self.null_kv.unbind(0))
         k = torch.cat([nk, k], dim=2)
         v = torch.cat([nv, v], dim=2)
+        # the fused SDPA kernels (AOTriton mem-efficient, fp32 too) need stride(-1) == 1 on q;
+        # the channel-first GEMM output gives stride P, which silently drops the op to the
+        # math path (explicit [B,h,P,P+1] fp32 scores: 5.4 vs ~1 ms fwd+bwd at P=1024).
+        # The CPU keeps the reference's view layout (and with it torch-CPU's math-path order).
+        if q.is_cuda:
+            q = q.contiguous()
         out = F.scaled_dot_product_attention(q, k, v)                          # [B, h, P, d]
         out = out.permute(0, 1, 3, 2).reshape(B, h * d, H * W)
         return _pointwise(self.to_out, out).reshape(B, C, H, W)
@@ -103,6 +109,8 @@ class CrossAttention(nn.Module):
         x = self.norm(fmap).reshape(B, C, H * W)
         ctx = self.norm_context(context)
         q = _pointwise(self.to_q, x).reshape(B, h, d, H * W).transpose(2, 3)
+        if q.is_cuda:                                   # fused SDPA needs stride(-1) == 1 (see SelfAttention)
+            q = q.contiguous()
         k, v = self.to_kv(ctx).chunk(2, dim=-1)
         k = k.reshape(B, -1, h, d).transpose(1, 2)
         v = v.reshape(B, -1, h, d).transpose(1, 2)
