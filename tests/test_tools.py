@@ -195,3 +195,98 @@ def test_reconstruct_on_gpu_matches_cpu(setup):
         b = common.load_png_uint8(str(outs["cuda:0"] / "outputs" / n)).astype(int)
         assert np.abs(a - b).max() <= 2 and (a == b).mean() >= 0.95
         assert 10 * np.log10(255.0 ** 2 / max(np.mean((a - b) ** 2), 1e-12)) >= 50
+
+
+def _make_wds_tar(path, samples):
+    import io as _io
+    import tarfile
+    with tarfile.open(path, "w") as tf:
+        for key, members in samples:
+            for ext, data in members.items():
+                ti = tarfile.TarInfo(f"{key}.{ext}")
+                ti.size = len(data)
+                tf.addfile(ti, _io.BytesIO(data))
+
+
+def test_lightningdit_prefetch_matches_direct_encode(setup):
+    """WebDataset-layout tar → ADM crop → G.encode(x), G.encode(flip(x)) → shard file with
+    latents / latents_flip / labels, then ImgLatentDataset stats (reference
+    tools/preprocess_for_lightningdit/prefetch.py)."""
+    import io as _io
+    from PIL import Image
+    from safetensors.torch import load_file
+    common = setup["common"]
+    pf = _load("preprocess_for_lightningdit/prefetch.py")
+    rng = np.random.default_rng(3)
+    raw, samples = [], []
+    for i, (h, w) in enumerate([(150, 130), (64, 64), (200, 90), (70, 140)]):
+        a = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        buf = _io.BytesIO()
+        Image.fromarray(a).save(buf, format="png")
+        samples.append((f"s{i:04d}", {"png": buf.getvalue(), "cls": str(10 + i).encode()}))
+        raw.append(a)
+    samples.insert(2, ("bad0", {"png": b"not an image", "cls": b"1"}))          # logged + skipped
+    samples.insert(3, ("nolab", {"png": samples[0][1]["png"]}))                    # no cls: skipped
+    d = setup["root"] / "wds"
+    d.mkdir()
+    _make_wds_tar(str(d / "shard-000000.tar"), samples)
+    crop = pf.center_crop_imagenet(64, raw[2])
+    assert crop.shape == (64, 64, 3)
+    out = setup["root"] / "latents"
+    G = _fresh_vae(setup)
+    torch.manual_seed(21)
+    n = pf.run_latent_extraction_wds(G, str(d), str(out), common.Rank("cpu"), 64, 2, max_images_per_gpu=3,
+                                     log=lambda *a: None)
+    assert n == 3
+    got = load_file(str(out / "latents_rank00_shard000.safetensors"))
+    assert got["latents"].shape == (3, 32, 4, 4) and got["latents_flip"].shape == (3, 32, 4, 4)
+    assert got["labels"].tolist() == [10, 11, 12]
+    torch.manual_seed(21)
+    exp, exp_f = [], []
+    for s in (slice(0, 2), slice(2, 3)):
+        x = torch.from_numpy(np.stack([pf.center_crop_imagenet(64, a) for a in raw[s]])).permute(0, 3, 1, 2).float() / 255
+        exp.append(G.encode(x))
+        exp_f.append(G.encode(torch.flip(x, dims=[-1])))
+    assert torch.equal(got["latents"], torch.cat(exp)) and torch.equal(got["latents_flip"], torch.cat(exp_f))
+    ds = pf.ImgLatentDataset(str(out), latent_norm=True, log=lambda *a: None)
+    assert len(ds) == 3 and os.path.exists(out / "latents_stats.pt")
+    m = got["latents"].mean(dim=[0, 2, 3], keepdim=True)
+    assert torch.allclose(ds._latent_mean, m, atol=1e-6)
+    feat, lab = ds[1]
+    assert feat.shape == (32, 4, 4) and int(lab) == 11
+
+
+def test_reg_prefetch_outputs(setup):
+    """preprocess_for_reg: per-image mean‖std .npy (== G.encode(x, return_z_before_quantize=True)
+    through mean_logvar_to_mean_std), PNGs, per-rank and merged dataset.json, latents_stats.pt."""
+    import io as _io
+    from PIL import Image
+    pf = _load("preprocess_for_reg/prefetch.py")
+    wds = _load("wds.py")
+    rng = np.random.default_rng(4)
+    samples, raw = [], []
+    for i, key in enumerate(["n01_0001", "n01_0002", "n02_0001"]):
+        a = rng.integers(0, 256, (96, 80, 3), dtype=np.uint8)
+        buf = _io.BytesIO()
+        Image.fromarray(a).save(buf, format="png")
+        samples.append((key, {"png": buf.getvalue(), "cls": str(i).encode()}))
+        raw.append(a)
+    d = setup["root"] / "wds_reg"
+    d.mkdir()
+    _make_wds_tar(str(d / "a.tar"), samples)
+    out = setup["root"] / "reg"
+    G = _fresh_vae(setup)
+    n = pf.run_extraction(G, str(d), str(out), setup["common"].Rank("cpu"), 64, 2, log=lambda *a: None)
+    assert n == 3
+    ds = json.load(open(out / "vae_latents" / "dataset.json"))
+    assert ds["labels"] == [["n01/n01_0001.npy", 0], ["n01/n01_0002.npy", 1], ["n02/n02_0001.npy", 2]]
+    img = json.load(open(out / "images_png" / "dataset.json"))
+    assert [r[0] for r in img["labels"]] == ["n01/n01_0001.png", "n01/n01_0002.png", "n02/n02_0001.png"]
+    crop = wds.center_crop_imagenet(64, raw[2])
+    assert (setup["common"].load_png_uint8(str(out / "images_png" / "n02" / "n02_0001.png")) == crop).all()
+    x = torch.from_numpy(np.stack([wds.center_crop_imagenet(64, a) for a in raw[2:]])).permute(0, 3, 1, 2).float() / 255
+    exp = pf.mean_logvar_to_mean_std(G.encode(x, return_z_before_quantize=True)).numpy()[0]
+    got = np.load(out / "vae_latents" / "n02" / "n02_0001.npy")
+    assert got.shape == (64, 4, 4) and np.allclose(got, exp, rtol=1e-5, atol=1e-6)
+    st = torch.load(out / "vae_latents" / "latents_stats.pt", weights_only=True)
+    assert st["mean"].shape == (1, 32, 1, 1)

@@ -63,10 +63,14 @@ class Rank:
             torch.distributed.destroy_process_group()
 
 
-def vae_kwargs_from_config(path, resolution=256):
+def vae_kwargs_from_config(path, resolution=256, keys=("G_kwargs",)):
     with open(path, "r") as f:
         cfg = yaml.safe_load(f)
-    kw = dict(cfg.get("G_kwargs", {}))
+    kw = {}
+    for k in keys:                                     # first key present wins
+        if k in cfg:
+            kw = dict(cfg[k])
+            break
     kw["label_dim"] = 1000
     kw["img_resolution"] = resolution
     kw["conditional"] = False
@@ -77,8 +81,8 @@ def vae_kwargs_from_config(path, resolution=256):
     return kw
 
 
-def build_vae(config_path, resolution, device, vae_kwargs_override=None):
-    kw = vae_kwargs_from_config(config_path, resolution)
+def build_vae(config_path, resolution, device, vae_kwargs_override=None, keys=("G_kwargs",)):
+    kw = vae_kwargs_from_config(config_path, resolution, keys)
     if vae_kwargs_override:
         kw.update(vae_kwargs_override)
     vae = dnnlib.util.construct_class_by_name(**kw).to(device)
