@@ -55,7 +55,40 @@ def parse_args(argv=None):
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--no-graphs", action="store_true", help="A/B: eager D-phase generator forward")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
+    ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="off",
+                    help="GEMM solution table (torch TunableOp over hipBLASLt/rocBLAS): 'use' reads the "
+                         "committed table without tuning, 'tune' measures every GEMM shape and writes "
+                         "the table to --tunableop-out")
+    ap.add_argument("--tunableop-out", default=os.path.join(ROOT, "gpurun_out", "tunableop", "gemm_results.csv"))
     return ap.parse_args(argv)
+
+
+TUNABLEOP_TABLE = os.path.join(PKG, "tunableop", "gemm_results.csv")
+
+
+def setup_tunableop(mode, out_path):
+    """TunableOp: per-shape GEMM solution choice. 'use' loads the committed table (tuned on an
+    MI355X with this image; validators = torch/ROCm/hipBLASLt versions + gfx950) and never
+    tunes, so a fresh box pays no tuning time; shapes missing from the table keep the default
+    heuristic. Nothing is written back into the repo."""
+    if mode == "off":
+        return None
+    import torch.cuda.tunable as tun
+    tun.enable(True)
+    if mode == "use":
+        if not os.path.exists(TUNABLEOP_TABLE):
+            raise FileNotFoundError(TUNABLEOP_TABLE)
+        tun.tuning_enable(False)
+        tun.set_filename(os.path.join("/tmp", f"vfm_tunableop_{os.getpid()}.csv"))
+        ok = tun.read_file(TUNABLEOP_TABLE)
+        return {"mode": "use", "table": os.path.relpath(TUNABLEOP_TABLE, ROOT), "loaded": bool(ok),
+                "entries": len(tun.get_results())}
+    os.makedirs(os.path.dirname(out_path), exist_ok=True)
+    tun.tuning_enable(True)
+    tun.set_max_tuning_duration(int(os.environ.get("VFM_TUNE_MS", "25")))
+    tun.set_max_tuning_iterations(int(os.environ.get("VFM_TUNE_ITERS", "20")))
+    tun.set_filename(out_path)
+    return {"mode": "tune", "out": out_path}
 
 
 def build(cfg_path, batch_gpu, device, world):
@@ -107,6 +140,11 @@ def main(argv=None):
     torch.backends.cudnn.benchmark = bool(int(os.environ.get("VFM_CUDNN_BENCHMARK", "0")))
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
+    if args.tunableop == "tune":
+        args.no_graphs = True            # a GEMM cannot be tuned inside a HIP-graph capture
+    tunable = setup_tunableop(args.tunableop, args.tunableop_out)
+    if tunable:
+        _log(rank, f"tunableop: {tunable}")
 
     t_start = time.perf_counter()
     c, step = build(args.config, args.batch, device, world)
@@ -220,11 +258,14 @@ def main(argv=None):
                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "seq_len": 1024,
                        "resolution": 256, "parallelism": f"dp{world}",
                        "decoder_ops": "torch" if args.force_ref_ops else "hip",
-                       "d_phase_g_forward": "eager" if args.no_graphs else "hip_graph"},
+                       "d_phase_g_forward": "eager" if args.no_graphs else "hip_graph",
+                       "gemm_table": tunable["table"] if tunable and tunable["mode"] == "use" else None},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if tunable and tunable["mode"] == "tune":
+        _log(rank, f"tunableop table is written at exit: {tunable['out']}")
     if world > 1:
         torch.distributed.barrier()
         dist.destroy_process_group()

@@ -28,6 +28,10 @@ for s in "$@"; do
     pwpmc)   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex pw_gemm_gelu -d $out/pwpmc -o run --output-format csv -- python3 tools_dev/pwbench.py > $out/pwpmc.log 2>&1 ;;
     gdebug)  timeout -k 10 300 python tools_dev/graph_debug.py > $out/gdebug.log 2>&1 ;;
     benchfind) MIOPEN_FIND_MODE=NORMAL VFM_CUDNN_BENCHMARK=1 timeout -k 10 900 python bench.py --no-cpu-baseline > $out/benchfind.log 2>&1 ;;
+    tune)    ( while sleep 30; do echo "tick $(date +%T)"; done ) & tk=$!
+             timeout -k 10 1000 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --tunableop tune --tunableop-out $out/gemm_results.csv > $out/tune.log 2>&1; rc0=$?
+             kill $tk; (exit $rc0) ;;
+    benchtun) timeout -k 10 600 python bench.py --no-cpu-baseline --tunableop use > $out/benchtun.log 2>&1 ;;
     benchnf) VFM_NO_FUSED_MLP=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/benchnf.log 2>&1 ;;
     benchng) timeout -k 10 600 python bench.py --no-cpu-baseline --no-graphs > $out/benchng.log 2>&1 ;;
     decbench) timeout -k 10 300 python tools_dev/decbench.py > $out/decbench.log 2>&1 ;;
