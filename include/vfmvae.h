@@ -238,6 +238,19 @@ int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* s, const fl
                          const float* b2, const float* gamma, const void* xin, void* out, void* hout, void* gout,
                          void* yout, int B, int C, int N, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * LPIPS distance head (replaces the per-tap tail of training/lpips.py LPIPS.forward:
+ * `(normalize_tensor(f0) - normalize_tensor(f1)) ** 2` -> `lin` 1x1 conv C->1 (no bias);
+ * the `spatial_average` stays a mean over r in the caller).
+ *   f0, f1: fp32 [B, C, HW] contiguous (NCHW VGG16 taps); w: fp32 [C] (lin weight).
+ *   fwd writes r [B, HW] and the channel norms n0, n1 [B, HW] (saved for backward).
+ *   bwd: gs fp32 [B] = upstream gradient of each r[b, :]; writes g0 and/or g1 [B, C, HW]
+ *   (either may be NULL). */
+int vfm_lpips_head_fwd(const float* f0, const float* f1, const float* w, float* r, float* n0, float* n1,
+                       int B, int C, long long HW, void* stream);
+int vfm_lpips_head_bwd(const float* f0, const float* f1, const float* w, const float* n0, const float* n1,
+                       const float* gs, float* g0, float* g1, int B, int C, long long HW, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,86 @@
+"""LPIPS distance head (csrc/lpips.hip) against the reference expression of training/lpips.py
+(`normalize_tensor` → diff² → `lin` 1×1 → `spatial_average`) evaluated in float64 by torch.
+Tolerance: fp32 kernel vs fp64 reference, relative 2e-5 on the head value and 1e-4 (max-abs
+over max-abs) on the feature gradients."""
+import pytest
+import torch
+
+from torch_utils.ops import lpips_ops
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-30))
+
+
+def test_head_ref_is_the_reference_expression():
+    from training.lpips import normalize_tensor, spatial_average
+    g = torch.Generator().manual_seed(0)
+    f0, f1 = torch.rand(2, 16, 5, 7, generator=g), torch.rand(2, 16, 5, 7, generator=g)
+    w = torch.rand(1, 16, 1, 1, generator=g)
+    d = (normalize_tensor(f0) - normalize_tensor(f1)) ** 2
+    exp = spatial_average(torch.nn.functional.conv2d(d, w), keepdim=True)
+    assert torch.allclose(lpips_ops.head_ref(f0, f1, w), exp, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,H,W", [(3, 64, 33, 31), (2, 130, 16, 16), (4, 512, 16, 16), (2, 64, 256, 256)])
+def test_lpips_head_matches_reference(B, C, H, W):
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(B * C + H)
+    # ReLU-like features (non-negative, some exact zeros) as the VGG taps are
+    f0 = torch.relu(torch.randn(B, C, H, W, generator=g))
+    f1 = torch.relu(f0 + 0.3 * torch.randn(B, C, H, W, generator=g))
+    w = torch.rand(C, generator=g) / C
+    x0 = f0.to(dev).requires_grad_(True)
+    x1 = f1.to(dev).requires_grad_(True)
+    out = lpips_ops.lpips_head(x0, x1, w.to(dev))
+    gout = torch.rand(B, 1, 1, 1, generator=g)
+    out.backward(gout.to(dev))
+    r0 = f0.double().requires_grad_(True)
+    r1 = f1.double().requires_grad_(True)
+    ref = lpips_ops.head_ref(r0, r1, w.double())
+    ref.backward(gout.double())
+    assert out.shape == (B, 1, 1, 1)
+    assert _rel(out.cpu(), ref) < 2e-5
+    assert _rel(x1.grad.cpu(), r1.grad) < 1e-4
+    assert _rel(x0.grad.cpu(), r0.grad) < 1e-4
+
+
+@pytest.mark.gpu
+def test_lpips_head_only_target_grad_and_zero_pixel():
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(5)
+    f0 = torch.relu(torch.randn(2, 64, 8, 8, generator=g))
+    f1 = torch.relu(torch.randn(2, 64, 8, 8, generator=g))
+    f1[0, :, 3, 4] = 0.0                                    # all-zero pixel: gradient defined as finite
+    w = torch.rand(64, generator=g) / 64
+    x1 = f1.to(dev).requires_grad_(True)
+    out = lpips_ops.lpips_head(f0.to(dev), x1, w.to(dev))
+    out.sum().backward()
+    assert torch.isfinite(x1.grad).all()
+    m = torch.ones_like(f1, dtype=torch.bool)
+    m[0, :, 3, 4] = False
+    r1 = f1.double().requires_grad_(True)
+    lpips_ops.head_ref(f0.double(), r1, w.double()).sum().backward()
+    assert _rel(out.cpu(), lpips_ops.head_ref(f0.double(), f1.double(), w.double())) < 2e-5
+    assert _rel(x1.grad.cpu()[m], r1.grad[m]) < 1e-4
+
+
+@pytest.mark.gpu
+def test_lpips_module_gpu_matches_cpu():
+    """Whole LPIPS (VGG16 on MIOpen + the HIP head) on cuda:0 vs the CPU module, same weights."""
+    from training.lpips import LPIPS
+    torch.manual_seed(0)
+    m = LPIPS().eval()
+    g = torch.Generator().manual_seed(1)
+    a = torch.rand(2, 3, 64, 64, generator=g) * 2 - 1
+    b = (a + 0.2 * torch.randn(2, 3, 64, 64, generator=g)).clamp(-1, 1)
+    bc = b.clone().requires_grad_(True)
+    ref = m(a, bc)
+    ref.sum().backward()
+    md = m.to("cuda:0")
+    bg = b.to("cuda:0").requires_grad_(True)
+    out = md(a.to("cuda:0"), bg)
+    out.sum().backward()
+    assert _rel(out.cpu(), ref) < 1e-4
+    assert _rel(bg.grad.cpu(), bc.grad) < 1e-3

@@ -53,6 +53,8 @@ SIGNATURES = {
     "vfm_pw_gemm_gelu_tiles": [c_int],
     "vfm_convnext_mlp_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                              c_int, c_vp],
+    "vfm_lpips_head_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
+    "vfm_lpips_head_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
 }
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}

@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 
 from torch_utils import distributed as dist
+from torch_utils.ops import lpips_ops
 
 # torchvision vgg16 `features` (cfg D): channels per conv; 'M' = max-pool.
 _VGG16_CFG = [64, 64, 'M', 128, 128, 'M', 256, 256, 256, 'M', 512, 512, 512, 'M', 512, 512, 512]
@@ -132,7 +133,12 @@ class LPIPS(nn.Module):
         outs1 = self.net(self.scaling_layer(target))
         val = None
         for kk in range(len(self.chns)):
-            d = (normalize_tensor(outs0[kk]) - normalize_tensor(outs1[kk])) ** 2
-            r = spatial_average(getattr(self, f"lin{kk}").model(d), keepdim=True)
+            lin = getattr(self, f"lin{kk}").model
+            if outs0[kk].is_cuda and not (self.training and len(lin) > 1):
+                # normalise -> diff -> square -> lin -> mean in one HIP pass (torch_utils/ops/lpips_ops.py)
+                r = lpips_ops.lpips_head(outs0[kk], outs1[kk], lin[-1].weight)
+            else:
+                d = (normalize_tensor(outs0[kk]) - normalize_tensor(outs1[kk])) ** 2
+                r = spatial_average(lin(d), keepdim=True)
             val = r if val is None else val + r
         return val
