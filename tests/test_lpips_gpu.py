@@ -67,8 +67,10 @@ def test_lpips_head_only_target_grad_and_zero_pixel():
 
 
 @pytest.mark.gpu
-def test_lpips_module_gpu_matches_cpu():
-    """Whole LPIPS (VGG16 on MIOpen + the HIP head) on cuda:0 vs the CPU module, same weights."""
+def test_lpips_module_hip_head_matches_torch_head():
+    """Whole LPIPS on cuda:0 with the HIP head vs the same module with the torch head (same
+    MIOpen VGG features, so only the head differs: 1e-5 / 1e-4), and vs the CPU module (the
+    MIOpen fp32 Winograd convolutions differ from the CPU's direct ones: 1e-4 / 1e-2)."""
     from training.lpips import LPIPS
     torch.manual_seed(0)
     m = LPIPS().eval()
@@ -79,8 +81,15 @@ def test_lpips_module_gpu_matches_cpu():
     ref = m(a, bc)
     ref.sum().backward()
     md = m.to("cuda:0")
-    bg = b.to("cuda:0").requires_grad_(True)
-    out = md(a.to("cuda:0"), bg)
-    out.sum().backward()
-    assert _rel(out.cpu(), ref) < 1e-4
-    assert _rel(bg.grad.cpu(), bc.grad) < 1e-3
+    res = {}
+    for impl in ("ref", "cuda"):
+        md.head_impl = impl
+        bg = b.to("cuda:0").requires_grad_(True)
+        out = md(a.to("cuda:0"), bg)
+        out.sum().backward()
+        res[impl] = (out.detach().cpu(), bg.grad.cpu())
+    md.head_impl = "cuda"
+    assert _rel(res["cuda"][0], res["ref"][0]) < 1e-5
+    assert _rel(res["cuda"][1], res["ref"][1]) < 1e-4
+    assert _rel(res["cuda"][0], ref) < 1e-4
+    assert _rel(res["cuda"][1], bc.grad) < 1e-2

@@ -109,6 +109,8 @@ def spatial_average(x, keepdim=True):
 
 
 class LPIPS(nn.Module):
+    head_impl = 'cuda'          # 'ref': the torch expression for the distance head (A/B, tests)
+
     def __init__(self, use_dropout=True):
         super().__init__()
         self.scaling_layer = ScalingLayer()
@@ -134,7 +136,7 @@ class LPIPS(nn.Module):
         val = None
         for kk in range(len(self.chns)):
             lin = getattr(self, f"lin{kk}").model
-            if outs0[kk].is_cuda and not (self.training and len(lin) > 1):
+            if outs0[kk].is_cuda and self.head_impl == 'cuda' and not (self.training and len(lin) > 1):
                 # normalise -> diff -> square -> lin -> mean in one HIP pass (torch_utils/ops/lpips_ops.py)
                 r = lpips_ops.lpips_head(outs0[kk], outs1[kk], lin[-1].weight)
             else:
