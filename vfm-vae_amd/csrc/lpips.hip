@@ -75,7 +75,19 @@ __global__ __launch_bounds__(LP_NT) void lpips_head_bwd(const float* __restrict_
     const float n0e = n0 + LP_EPS, n1e = n1 + LP_EPS;
     const float s2 = 2.f * gs[b];
     float dot0 = 0.f, dot1 = 0.f;
-    for (int c = 0; c < C; ++c) {
+    int c = 0;
+    for (; c + 8 <= C; c += 8) {                       // 16 loads in flight per lane
+        float x[8], y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { x[j] = a[(c + j) * HW]; y[j] = u[(c + j) * HW]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float G = s2 * w[c + j] * (x[j] / n0e - y[j] / n1e);
+            dot0 += G * x[j];
+            dot1 += G * y[j];
+        }
+    }
+    for (; c < C; ++c) {
         const float x = a[c * HW], y = u[c * HW];
         const float G = s2 * w[c] * (x / n0e - y / n1e);
         dot0 += G * x;
@@ -83,7 +95,19 @@ __global__ __launch_bounds__(LP_NT) void lpips_head_bwd(const float* __restrict_
     }
     const float k0 = n0 > 0.f ? dot0 / (n0e * n0e * n0) : 0.f;
     const float k1 = n1 > 0.f ? dot1 / (n1e * n1e * n1) : 0.f;
-    for (int c = 0; c < C; ++c) {
+    c = 0;
+    for (; c + 8 <= C; c += 8) {
+        float x[8], y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { x[j] = a[(c + j) * HW]; y[j] = u[(c + j) * HW]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float G = s2 * w[c + j] * (x[j] / n0e - y[j] / n1e);
+            if (g0) g0[off + (c + j) * HW] = G / n0e - x[j] * k0;
+            if (g1) g1[off + (c + j) * HW] = -G / n1e + y[j] * k1;
+        }
+    }
+    for (; c < C; ++c) {
         const float x = a[c * HW], y = u[c * HW];
         const float G = s2 * w[c] * (x / n0e - y / n1e);
         if (g0) g0[off + c * HW] = G / n0e - x * k0;

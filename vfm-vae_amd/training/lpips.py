@@ -109,7 +109,8 @@ def spatial_average(x, keepdim=True):
 
 
 class LPIPS(nn.Module):
-    head_impl = 'cuda'          # 'ref': the torch expression for the distance head (A/B, tests)
+    # 'ref': the torch expression for the distance head (A/B, tests)
+    head_impl = os.environ.get('VFM_LPIPS_HEAD', 'cuda')
 
     def __init__(self, use_dropout=True):
         super().__init__()
