@@ -149,3 +149,48 @@ def test_training_iteration_replicas_stay_identical():
     assert res[0]["moved"] > 0
     assert (res[0]["g"] == res[1]["g"]).all()
     assert (res[0]["d"] == res[1]["d"]).all()
+
+
+def _tools_decode_worker(rank, world, lat_dir, out_dir, cfg, ckpt):
+    """tools/decode on a 2-rank gloo group: each rank decodes sorted(files)[rank::2]."""
+    import importlib.util
+    tools = os.path.join(PKG, "tools")
+    spec = importlib.util.spec_from_file_location("decode_tool", os.path.join(tools, "decode", "decode_latents_to_images.py"))
+    dec = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(dec)
+    import common
+    rk = common.Rank("cpu")
+    assert (rk.rank, rk.world_size) == (rank, world) and not rk.pg     # uses the existing group
+    G = common.build_vae(cfg, 64, torch.device("cpu"))
+    common.load_vae_weights(G, ckpt, torch.device("cpu"), log=lambda *a: None)
+    n = dec.run_latent_decoding(G, lat_dir, out_dir, 2, rk, log=lambda *a: None)
+    return {"n": n}
+
+
+def test_tools_decode_shards_over_two_ranks(tmp_path):
+    import json
+    import yaml
+    import net_cases
+    from safetensors.torch import save_file
+    vfm = tmp_path / net_cases.VFM_DIRNAME
+    vfm.mkdir()
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(vfm / "config.json", "w"))
+    cfg = tmp_path / "tiny.yaml"
+    yaml.safe_dump({"G_kwargs": dict(net_cases.g_kwargs(str(vfm)), class_name="networks.generator.Generator")},
+                   open(cfg, "w"))
+    sys.path.insert(0, os.path.join(PKG, "tools"))
+    import common
+    torch.manual_seed(0)
+    G = common.build_vae(str(cfg), 64, torch.device("cpu"))
+    ckpt = tmp_path / "snap.pth"
+    torch.save({"G_ema": G.state_dict()}, ckpt)
+    lat = tmp_path / "lat"
+    lat.mkdir()
+    g = torch.Generator().manual_seed(1)
+    for i, n in enumerate([3, 2, 1]):                          # files 0, 2 -> rank 0; file 1 -> rank 1
+        save_file({"latents": torch.randn(n, 32, 4, 4, generator=g)}, str(lat / f"f{i}.safetensors"))
+    out = tmp_path / "dec"
+    res = _spawn("_tools_decode_worker", 2, str(lat), str(out), str(cfg), str(ckpt))
+    assert res[0]["n"] == 4 and res[1]["n"] == 2
+    files = sorted(os.listdir(out))
+    assert files == [f"rank00_{i:06d}.png" for i in range(4)] + [f"rank01_{i:06d}.png" for i in range(2)]
