@@ -69,8 +69,10 @@ def test_lpips_head_only_target_grad_and_zero_pixel():
 @pytest.mark.gpu
 def test_lpips_module_hip_head_matches_torch_head():
     """Whole LPIPS on cuda:0 with the HIP head vs the same module with the torch head (same
-    MIOpen VGG features, so only the head differs: 1e-5 / 1e-4), and vs the CPU module (the
-    MIOpen fp32 Winograd convolutions differ from the CPU's direct ones: 1e-4 / 1e-2)."""
+    MIOpen VGG features, so only the head differs: value 1e-5; the input gradient then runs
+    13 fp32 MIOpen backward convolutions whose solver/accumulation order is not fixed between
+    calls — measured 1.6e-3 in a full-suite run — so 1e-2), and vs the CPU module (1e-4 / 1e-2).
+    The head's own gradient is checked at 1e-4 against fp64 in the tests above."""
     from training.lpips import LPIPS
     torch.manual_seed(0)
     m = LPIPS().eval()
@@ -90,6 +92,6 @@ def test_lpips_module_hip_head_matches_torch_head():
         res[impl] = (out.detach().cpu(), bg.grad.cpu())
     md.head_impl = "cuda"
     assert _rel(res["cuda"][0], res["ref"][0]) < 1e-5
-    assert _rel(res["cuda"][1], res["ref"][1]) < 1e-4
+    assert _rel(res["cuda"][1], res["ref"][1]) < 1e-2
     assert _rel(res["cuda"][0], ref) < 1e-4
     assert _rel(res["cuda"][1], bc.grad) < 1e-2
