@@ -28,10 +28,6 @@ for _p in (PKG, ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-# MIOpen: immediate-mode convolution solutions (no exhaustive find on a fresh box;
-# the find-db does not survive between boxes).
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
-
 import numpy as np
 import torch
 import yaml
@@ -91,24 +87,21 @@ def setup_tunableop(mode, out_path):
     return {"mode": "tune", "out": out_path}
 
 
-def build(cfg_path, batch_gpu, device, world):
-    """Construct G, G_ema, D, loss, optimisers and the shared TrainingIteration."""
-    import copy
-    import dnnlib
+def build(cfg_path, batch_gpu, device, world, graphs=True):
+    """G, G_ema, D, loss, optimisers and the TrainingIteration, through the SAME helpers
+    training_loop() uses (training/training_loop.py construct_networks / construct_iteration /
+    configure_backends), so the measured iteration is the one train.py runs."""
     from train import resolve_config
-    from training.training_loop import TrainingIteration, make_optimizer
+    from training.training_loop import configure_backends, construct_networks, construct_iteration
     c = resolve_config(yaml.safe_load(open(cfg_path)))
+    configure_backends(c.get("cudnn_benchmark", True))
     torch.manual_seed(c.get("random_seed", 42))
     random.seed(c.get("random_seed", 42))
     np.random.seed(c.get("random_seed", 42))
-    G = dnnlib.util.construct_class_by_name(label_dim=0, **c.G_kwargs).train().requires_grad_(False).to(device)
-    G_ema = copy.deepcopy(G).eval()
-    D = dnnlib.util.construct_class_by_name(c_dim=G.c_dim, **c.D_kwargs).train().requires_grad_(False).to(device)
-    loss = dnnlib.util.construct_class_by_name(device=device, G=G, D=D, **c.loss_kwargs)
-    G_opt = make_optimizer(G.parameters(), c.G_opt_kwargs, device)
-    D_opt = make_optimizer(D.parameters(), c.D_opt_kwargs, device)
-    step = TrainingIteration(G, D, G_ema, loss, G_opt, D_opt, batch_size=batch_gpu * world, n_batch_acc=1,
-                             ema_kimg=c.ema_kimg, ema_rampup=c.ema_rampup)
+    G, G_ema, D = construct_networks(c.G_kwargs, c.D_kwargs, device, label_dim=0)
+    step = construct_iteration(G, D, G_ema, device, c.loss_kwargs, c.G_opt_kwargs, c.D_opt_kwargs,
+                               batch_size=batch_gpu * world, accumulate_gradients=1, ema_kimg=c.ema_kimg,
+                               ema_rampup=c.ema_rampup, graph_nograd_forward=graphs)
     return c, step
 
 
@@ -135,9 +128,6 @@ def main(argv=None):
     assert world == args.gpus or world_env == 1, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(device)
-    torch.backends.cuda.matmul.allow_tf32 = False
-    torch.backends.cudnn.allow_tf32 = False
-    torch.backends.cudnn.benchmark = bool(int(os.environ.get("VFM_CUDNN_BENCHMARK", "0")))
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
     if args.tunableop == "tune":
@@ -147,10 +137,8 @@ def main(argv=None):
         _log(rank, f"tunableop: {tunable}")
 
     t_start = time.perf_counter()
-    c, step = build(args.config, args.batch, device, world)
+    c, step = build(args.config, args.batch, device, world, graphs=not args.no_graphs)
     _log(rank, f"built in {time.perf_counter() - t_start:.1f}s")
-    if not args.no_graphs:
-        step.loss.enable_graphed_nograd_forward()
     from training.data_synthetic import SyntheticDataset
     pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=rank).make_pool(args.batch, device)
     labels = ['a photo'] * args.batch

@@ -194,3 +194,48 @@ def test_tools_decode_shards_over_two_ranks(tmp_path):
     assert res[0]["n"] == 4 and res[1]["n"] == 2
     files = sorted(os.listdir(out))
     assert files == [f"rank00_{i:06d}.png" for i in range(4)] + [f"rank01_{i:06d}.png" for i in range(2)]
+
+
+def _disagree_worker(rank, world):
+    from training.training_loop import FlatGradSync
+    m = _toy()
+    sync = FlatGradSync(m, bucket_mb=64.0)
+    sync.prepare()
+    loss = _toy_loss(m, rank)
+    if rank == 1:
+        loss = loss + m.unused.sum()          # a gradient only rank 1 produces
+    loss.backward()
+    sync.finish()
+    try:
+        sync.prepare()                        # the agreement check of the previous step runs here
+    except RuntimeError as e:
+        return {"raised": "different parameter sets" in str(e)}
+    return {"raised": False}
+
+
+def test_flat_grad_sync_detects_rank_disagreement():
+    res = _spawn("_disagree_worker", 2)
+    assert res[0]["raised"] and res[1]["raised"]
+
+
+def _stats_worker(rank, world):
+    from torch_utils import training_stats
+    training_stats.init_multiprocessing(rank, torch.device("cpu"))
+    col = training_stats.Collector(regex="Loss/.*")
+    training_stats.report("Loss/a", torch.tensor([1.0, 2.0]) * (rank + 1))
+    training_stats.report0("Loss/r0", 5.0)
+    training_stats.report("Other/x", 1.0)
+    col.update()
+    return {"names": col.names(), "num": col.num("Loss/a"), "mean": col.mean("Loss/a"), "std": col.std("Loss/a"),
+            "r0": (col.num("Loss/r0"), col.mean("Loss/r0"))}
+
+
+def test_training_stats_reduce_over_ranks():
+    res = _spawn("_stats_worker", 2)
+    vals = torch.tensor([1.0, 2.0, 2.0, 4.0], dtype=torch.float64)
+    for r in range(2):
+        out = res[r]
+        assert out["names"] == ["Loss/a", "Loss/r0"]
+        assert out["num"] == 4 and abs(out["mean"] - 2.25) < 1e-12
+        assert abs(out["std"] - float(vals.std(unbiased=False))) < 1e-12
+        assert out["r0"] == (1.0, 5.0)

@@ -1,0 +1,77 @@
+"""Host-side training infrastructure (CPU): statistics collection semantics and the
+shared setup helpers that train.py and bench.py both go through."""
+import math
+
+import pytest
+import torch
+
+
+def test_collector_intervals_and_keep_previous():
+    from torch_utils import training_stats as ts
+    a = ts.Collector(regex="T1/.*", keep_previous=True)
+    b = ts.Collector(regex="T1/.*", keep_previous=False)
+    ts.report("T1/x", [1.0, 3.0])
+    a.update()
+    b.update()
+    assert a.num("T1/x") == 2 and a.mean("T1/x") == 2.0 and a.std("T1/x") == 1.0
+    assert b.mean("T1/x") == 2.0
+    a.update()                      # nothing new reported: a keeps the previous interval, b clears it
+    b.update()
+    assert a.mean("T1/x") == 2.0
+    assert b.num("T1/x") == 0 and math.isnan(b.mean("T1/x"))
+    ts.report("T1/x", 10.0)
+    a.update()
+    assert a.num("T1/x") == 1 and a.mean("T1/x") == 10.0 and a.std("T1/x") == 0.0
+    assert a["T1/x"] == 10.0
+    d = a.as_dict()
+    assert d["T1/x"].num == 1
+    with pytest.raises(KeyError):
+        a.mean("Other/y")
+
+
+def test_report_returns_value_and_ignores_empty():
+    from torch_utils import training_stats as ts
+    v = torch.ones(3)
+    assert ts.report("T2/v", v) is v
+    ts.report("T2/empty", [])
+    c = ts.Collector(regex="T2/.*")
+    assert c.num("T2/empty") == 0
+
+
+def test_misc_helpers():
+    from torch_utils import misc
+    x = torch.zeros(2, 3, 4)
+    misc.assert_shape(x, [2, None, 4])
+    with pytest.raises(AssertionError):
+        misc.assert_shape(x, [2, 4, 4])
+    with pytest.raises(AssertionError):
+        misc.assert_shape(x, [2, 3])
+    a, b = torch.nn.BatchNorm1d(3), torch.nn.BatchNorm1d(3)
+    with torch.no_grad():
+        a.weight.fill_(2.0)
+        a.running_mean.fill_(0.5)
+    misc.copy_params_and_buffers(a, b, require_all=True)
+    assert torch.equal(b.weight, a.weight) and torch.equal(b.running_mean, a.running_mean)
+    assert len(misc.params_and_buffers(a)) == 5
+
+
+def test_construct_iteration_matches_training_loop_setup(tmp_path):
+    """bench.build and training_loop() share construct_networks / construct_iteration; on a GPU
+    device the iteration replays the D-phase generator forward from graphs (the measured path)."""
+    import json
+    import net_cases
+    from training.training_loop import construct_networks, construct_iteration, configure_backends
+    vfm = tmp_path / net_cases.VFM_DIRNAME
+    vfm.mkdir()
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(vfm / "config.json", "w"))
+    configure_backends(True)
+    assert torch.backends.cuda.matmul.allow_tf32 is False
+    dev = torch.device("cpu")
+    G, G_ema, D = construct_networks(dict(net_cases.g_kwargs(str(vfm)), class_name="networks.generator.Generator"),
+                                     dict(net_cases.D_KWARGS, class_name="networks.discriminator.ProjectedDiscriminator"),
+                                     dev)
+    opt = dict(class_name='torch.optim.Adam', lr=1e-3, betas=[0.0, 0.99], eps=1e-8)
+    lk = dict(net_cases.loss_kwargs(str(vfm)), class_name="training.loss.TotalLoss")
+    step = construct_iteration(G, D, G_ema, dev, lk, opt, opt, batch_size=2)
+    assert getattr(step.loss, "graphed_nograd", None) is None       # CPU: eager
+    assert step.G is G and step.G_ema is G_ema and step.D is D

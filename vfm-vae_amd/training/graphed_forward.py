@@ -26,7 +26,8 @@ decoder's unshuffle at a toy resolution) is left uncaptured and runs eagerly if 
 raising exactly as the eager pass would. Outputs (`gen_img` and the loss terms) live in
 the graphs' shared memory pool and are valid until the next replay, which is all the D
 phase needs. A failed capture turns the runner off (eager from then on), with the
-reason kept in `self.disabled`.
+reason kept in `self.disabled`. Generators with a vector quantiser (discrete latent,
+config 4) always run eagerly (`_has_host_state`).
 """
 import torch
 
@@ -46,7 +47,19 @@ class GraphedNoGradForward:
 
     def eligible(self, img, c):
         return (self.disabled is None and img.is_cuda and getattr(self.G, 'c_dim', 0) == 0
-                and not torch.is_grad_enabled())
+                and not torch.is_grad_enabled() and not self._has_host_state())
+
+    def _has_host_state(self):
+        """Modules whose forward branches on Python-side state that changes between calls
+        (VectorQuantizer.vocab_usage_record_times selects the usage-EMA rate) or issues a
+        collective (the usage bincount all_reduce under DDP) must stay eager: a replay would
+        freeze the branch taken at capture time and re-run a captured collective."""
+        cached = getattr(self, '_host_state', None)
+        if cached is None:
+            from networks.utils.quant_utils import VectorQuantizer
+            cached = any(isinstance(m, VectorQuantizer) for m in self.G.modules())
+            self._host_state = cached
+        return cached
 
     def _key(self, outcome, img):
         return (tuple(outcome), tuple(img.shape), img.dtype, self.G.training)

@@ -468,8 +468,11 @@ class TotalLoss:
                     c_shuf = [real_c[i] for i in perm]
                 else:
                     c_shuf = real_c_enc[torch.randperm(len(real_c_enc), device=real_c_enc.device)]
-                ma_loss = self.calculate_matching_aware_loss(self.run_D(real_img, c_shuf).stylegan_t_logits,
-                                                             self.run_D(gen_img, c_shuf).stylegan_t_logits)
+                # gen before real, as the reference (loss.py:608-610): D draws its augmentation
+                # and crops per call, so the call order fixes the RNG stream
+                ma_gen = self.run_D(gen_img, c_shuf).stylegan_t_logits
+                ma_real = self.run_D(real_img, c_shuf).stylegan_t_logits
+                ma_loss = self.calculate_matching_aware_loss(ma_real, ma_gen)
             d_loss = d_loss + self.matching_aware_loss_weight * ma_loss
 
             names = ['stylegan_t_gen_loss', 'stylegan_t_real_loss', 'stylegan_t_disc_loss', 'patchgan_gen_loss',

@@ -104,6 +104,40 @@ class FlatGradSync:
         self.pending = {}
         self.last_microbatch = True
         self.late = False
+        self._check_agreement()
+
+    def _check_agreement(self):
+        """Verify (one phase late, without a host sync on the step) that every rank produced
+        gradients for the same parameter set in the previous step of this phase. A parameter
+        whose grad is None on some ranks only would be stepped by Adam on those ranks alone
+        and the replicas would drift silently (the reference fails with mismatched
+        all-reduce sizes instead)."""
+        chk = getattr(self, '_agree', None)
+        self._agree = None
+        if chk is None:
+            return
+        host, event = chk
+        if event is not None:
+            event.synchronize()
+        if int(host[0]) != 0:
+            raise RuntimeError("FlatGradSync: ranks produced gradients for different parameter sets in the "
+                               "previous step (replicas would diverge)")
+
+    def _launch_agreement(self):
+        mask = torch.tensor([id(p) in self.seen for p in self.params], dtype=torch.int32)
+        dev = self.flat.device
+        mask = mask.pin_memory().to(dev, non_blocking=True) if dev.type == 'cuda' else mask
+        tot = mask.clone()
+        torch.distributed.all_reduce(tot)
+        bad = ((tot != 0) & (tot != self.world)).any().to(torch.int32).reshape(1)
+        if dev.type == 'cuda':
+            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            host.copy_(bad, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._agree = (host, ev)
+        else:
+            self._agree = (bad, None)
 
     def _on_grad(self, p):
         self.seen.add(id(p))
@@ -142,6 +176,7 @@ class FlatGradSync:
                                    "(gradients changed under an in-flight all-reduce)")
             if self.comm_stream is not None:
                 torch.cuda.current_stream(self.flat.device).wait_stream(self.comm_stream)
+            self._launch_agreement()
             self.flat.mul_(1.0 / self.world)
         if gain is not None and gain != 1:
             self.flat.mul_(gain)
@@ -295,6 +330,47 @@ def make_optimizer(params, opt_kwargs, device):
     return dnnlib.util.construct_class_by_name(params=params, **kw)
 
 
+def configure_backends(cudnn_benchmark=True):
+    """Backend switches shared by training_loop() and bench.py (reference :503-506).
+
+    TF32 stays off (gfx950 has no xf32 anyway). `cudnn_benchmark` selects MIOpen's
+    exhaustive per-shape convolution search on ROCm; its find-db does not persist between
+    fresh boxes and the search takes > 10 minutes for the LPIPS/PatchGAN shapes, so it is
+    honoured only with VFM_CUDNN_BENCHMARK=1 (immediate-mode solutions otherwise)."""
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    if torch.version.hip is not None:
+        cudnn_benchmark = bool(cudnn_benchmark) and os.environ.get("VFM_CUDNN_BENCHMARK", "0") == "1"
+        os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+    torch.backends.cudnn.benchmark = bool(cudnn_benchmark)
+    conv2d_gradfix.enabled = True
+
+
+def construct_networks(G_kwargs, D_kwargs, device, label_dim=0):
+    """G (train mode, frozen until a phase unfreezes it), G_ema = deepcopy(G), D (reference :573-575)."""
+    G = dnnlib.util.construct_class_by_name(label_dim=label_dim, **G_kwargs)
+    G = G.train().requires_grad_(False).to(device)
+    G_ema = copy.deepcopy(G).eval()
+    D = dnnlib.util.construct_class_by_name(c_dim=G.c_dim, **D_kwargs).train().requires_grad_(False).to(device)
+    return G, G_ema, D
+
+
+def construct_iteration(G, D, G_ema, device, loss_kwargs, G_opt_kwargs, D_opt_kwargs, batch_size,
+                        accumulate_gradients=1, ema_kimg=10.0, ema_rampup=0.05, graph_nograd_forward=True,
+                        bucket_mb=64.0):
+    """TotalLoss + optimisers + the TrainingIteration that train.py and bench.py both run.
+    graph_nograd_forward: replay the D phase's no-grad generator forward from HIP graphs
+    (training/graphed_forward.py; falls back to eager where capture is not eligible)."""
+    loss = dnnlib.util.construct_class_by_name(device=device, G=G, D=D, **loss_kwargs)
+    if graph_nograd_forward and device.type == 'cuda':
+        loss.enable_graphed_nograd_forward()
+    G_opt = make_optimizer(G.parameters(), G_opt_kwargs, device)
+    D_opt = make_optimizer(D.parameters(), D_opt_kwargs, device)
+    return TrainingIteration(G, D, G_ema, loss, G_opt, D_opt, batch_size=batch_size,
+                             n_batch_acc=accumulate_gradients, ema_kimg=ema_kimg, ema_rampup=ema_rampup,
+                             bucket_mb=bucket_mb)
+
+
 def save_snapshot(path, G, D, G_ema, training_set_kwargs):
     torch.save({"G": G.state_dict(), "D": D.state_dict(), "G_ema": G_ema.state_dict(),
                 "training_set_kwargs": dict(training_set_kwargs)}, path)
@@ -309,17 +385,14 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
                   total_kimg=25000, kimg_per_tick=4, image_snapshot_ticks=50, network_snapshot_ticks=50,
                   resume_path=None, resume_kimg=0, resume_discriminator=True, cudnn_benchmark=True, abort_fn=None,
                   progress_fn=None, one_epoch=False, device=None, train_sample_dir=None, wandb_project_name=None,
-                  wandb_run_name=None, max_iterations=None, **_unused):
+                  wandb_run_name=None, max_iterations=None, graph_nograd_forward=True, **_unused):
     device = device or (torch.device('cuda') if torch.cuda.is_available() else torch.device('cpu'))
     start_time = time.time()
     base_seed = random_seed * dist.get_world_size() + dist.get_rank()
     np.random.seed(base_seed)
     torch.manual_seed(base_seed)
     random.seed(base_seed)
-    torch.backends.cudnn.benchmark = cudnn_benchmark
-    torch.backends.cuda.matmul.allow_tf32 = False
-    torch.backends.cudnn.allow_tf32 = False
-    conv2d_gradfix.enabled = True
+    configure_backends(cudnn_benchmark)
 
     dist.print0('Loading training set...')
     training_set = dnnlib.util.construct_class_by_name(**training_set_kwargs)
@@ -327,10 +400,7 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
                                          world=dist.get_world_size(), seed=base_seed))
 
     dist.print0('Constructing networks...')
-    G = dnnlib.util.construct_class_by_name(label_dim=getattr(training_set, 'label_dim', 0), **G_kwargs)
-    G = G.train().requires_grad_(False).to(device)
-    G_ema = copy.deepcopy(G).eval()
-    D = dnnlib.util.construct_class_by_name(c_dim=G.c_dim, **D_kwargs).train().requires_grad_(False).to(device)
+    G, G_ema, D = construct_networks(G_kwargs, D_kwargs, device, getattr(training_set, 'label_dim', 0))
 
     if resume_path is not None and dist.get_rank() == 0:
         ckpt = torch.load(resume_path, map_location=device, weights_only=True)
@@ -344,11 +414,9 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
             for t in misc.params_and_buffers(module):
                 torch.distributed.broadcast(t, src=0)
 
-    loss = dnnlib.util.construct_class_by_name(device=device, G=G, D=D, **loss_kwargs)
-    G_opt = make_optimizer(G.parameters(), G_opt_kwargs, device)
-    D_opt = make_optimizer(D.parameters(), D_opt_kwargs, device)
-    step = TrainingIteration(G, D, G_ema, loss, G_opt, D_opt, batch_size=batch_size,
-                             n_batch_acc=accumulate_gradients, ema_kimg=ema_kimg, ema_rampup=ema_rampup)
+    step = construct_iteration(G, D, G_ema, device, loss_kwargs, G_opt_kwargs, D_opt_kwargs, batch_size,
+                               accumulate_gradients, ema_kimg, ema_rampup, graph_nograd_forward)
+    loss = step.loss
 
     stats_collector = training_stats.Collector(regex='.*')
     stats_jsonl = open(os.path.join(run_dir, 'stats.jsonl'), 'at') if dist.get_rank() == 0 else None
