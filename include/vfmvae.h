@@ -196,6 +196,44 @@ int vfm_residual_layer_norm(const float* h, const void* delta, float* h_out, con
                             void* y, int dtype_delta, int dtype_out, int rows, int D, float eps, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Frozen ViT towers: fused multi-head self-attention forward (flash-style).
+ * Replaces `F.scaled_dot_product_attention(q, k, v)` of HF SiglipAttention under bf16
+ * autocast (reference networks/utils/vfms/siglip2_utils.py:121, SiglipVisionModel forward)
+ * and of the DINOv2 / CLIP towers (configs 0, 3).
+ *   q, k, v, o: bf16 [B, N, H, head_dim] views; sq/sk/sv/so = element strides
+ *   {batch, token, head} (multiples of 8; unit stride along head_dim; 16-B aligned bases).
+ *   o = softmax(q k^T * scale) v, fp32 softmax statistics, P rounded to bf16 for P.V.
+ * head_dim 64 only (else VFM_NO_KERNEL). Forward only. */
+int vfm_attention_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int N, int head_dim,
+                      const long long* sq, const long long* sk, const long long* sv, const long long* so,
+                      float scale, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Dense GEMM on the MFMA cores with a fused epilogue (replaces the hipBLASLt GEMMs behind
+ * torch.addmm / torch.bmm for the frozen ViT projections, reference
+ * networks/utils/vfms/siglip2_utils.py:121 (HF SiglipEncoderLayer q/k/v/o, fc1 + gelu_tanh,
+ * fc2), the fusion adapter (ldm_utils.py:55-166) and the decoder's 1x1 convolutions
+ * (convnext_utils.py:36-142, gigagan_utils.py:53-185)):
+ *   C[z] = epi(alpha * A[z] . B[z] + beta * C[z]), A: M x K, B: K x N, z < batch,
+ *   epi = (+ bias[n] if bias_mode 1 | + bias[m] if bias_mode 2), then GELU (act 1 tanh,
+ *   act 2 erf); fp32 accumulation.
+ *   in_dtype VFM_BF16: bf16 operands; VFM_F32: fp32 operands evaluated as three bf16 MFMA
+ *   products of a hi/lo split (relative error per product <= ~2^-15.5; see csrc/gemm.hip).
+ *   out_dtype VFM_BF16 / VFM_F32. Operand layouts: a_kcont = 1: A is [M][K] (row stride lda),
+ *   0: A is [K][M]; b_kcont = 1: B is [N][K], 0: B is [K][N]; C is [M][N] (row stride ldc);
+ *   sA/sB/sC = element batch strides (0 = shared operand). The contiguous extents, lda/ldb
+ *   and sA/sB must be multiples of 8 (bf16) / 4 (fp32) elements (else VFM_NO_KERNEL).
+ *   splits > 1: K split over workgroups; partial tiles go to `workspace` (fp32, at least
+ *   vfm_gemm_workspace_floats(...) elements) and are summed in a fixed order by a second
+ *   kernel that applies the epilogue. reduce_batch = 1: C (single matrix) = epi(sum over z)
+ *   -- the weight gradient of a batched 1x1 convolution. */
+int vfm_gemm_workspace_floats(int M, int N, int batch, int splits, int reduce_batch);
+int vfm_gemm(const void* A, const void* B, void* C, const float* bias, float* workspace, int in_dtype,
+             int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,
+             int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
+             int bias_mode, int act, int splits, int reduce_batch, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Discrete latent: codebook lookup of VectorQuantizer (replaces the
  * `torch.argmax(F.normalize(f) @ F.normalize(codebook).T, dim=1)` of
  * networks/utils/quant_utils.py:84-86 and f_to_idx :126-131).

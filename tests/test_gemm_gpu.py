@@ -1,0 +1,131 @@
+"""MFMA GEMM (csrc/gemm.hip) against the plain PyTorch fp32 reference of the same product.
+
+Tolerances (max |err| / max |ref|):
+  bf16 operands, fp32 accumulation: 1e-5 for fp32 output (same products, other summation
+  order), 8e-3 for bf16 output (one output rounding);
+  f32x3 (fp32 operands as three bf16 products of a hi/lo split): 5e-5 -- the split's error
+  bound is ~2^-15.5 per product, far below the 2^-10 of TF32 (which the reference disables)
+  and above fp32's 2^-24.
+Layouts: every (A, B) contiguity combination, batched with shared and per-batch operands,
+ragged M/N/K (tails inside a tile), bias per row / per column, tanh/erf GELU, alpha/beta
+accumulation, split-K and the batch-reducing form used for 1x1-conv weight gradients."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-30))
+
+
+def _make(shape, dtype, g, kcont_last=True):
+    t = torch.randn(*shape, generator=g)
+    return t.to(dtype).to(DEV)
+
+
+def _ref_epi(c, bias=None, bias_dim=1, act=None):
+    if bias is not None:
+        c = c + (bias[None, :] if bias_dim == 1 else bias[:, None])
+    if act == "gelu_tanh":
+        c = torch.nn.functional.gelu(c, approximate="tanh")
+    elif act == "gelu":
+        c = torch.nn.functional.gelu(c)
+    return c
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (8, 520, 1024)])
+def test_gemm_layouts(dtype, a_t, b_t, M, N, K):
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(M + N + K)
+    A = _make((K, M) if a_t else (M, K), dtype, g)
+    B = _make((N, K) if b_t else (K, N), dtype, g)
+    Av = A.t() if a_t else A
+    Bv = B.t() if b_t else B
+    out = gemm_hip.gemm(Av, Bv, out_dtype=torch.float32)
+    ref = Av.float() @ Bv.float()
+    tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
+    assert _rel(out, ref) < tol
+
+
+@pytest.mark.parametrize("act", [None, "gelu_tanh", "gelu"])
+@pytest.mark.parametrize("bias_dim", [None, 1, 0])
+def test_gemm_epilogue_bf16(act, bias_dim):
+    """The SigLIP2 fc1 form: x [M, K] @ W^T [K, N] + bias, tanh-GELU, bf16 out."""
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 300, 264, 136
+    x = _make((M, K), torch.bfloat16, g)
+    w = _make((N, K), torch.bfloat16, g)
+    bias = None if bias_dim is None else torch.randn(N if bias_dim == 1 else M, generator=g).to(DEV)
+    out = gemm_hip.gemm(x, w.t(), bias=bias, bias_dim=bias_dim, act=act)
+    assert out.dtype == torch.bfloat16
+    ref = _ref_epi(x.float() @ w.float().t(), bias, bias_dim if bias_dim is not None else 1, act)
+    assert _rel(out.float(), ref) < 8e-3
+
+
+def test_gemm_alpha_beta_accumulate():
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(4)
+    A = _make((96, 64), torch.float32, g)
+    B = _make((64, 72), torch.float32, g)
+    C = _make((96, 72), torch.float32, g)
+    ref = 0.5 * (A @ B) + 2.0 * C
+    gemm_hip.gemm(A, B, out=C, alpha=0.5, beta=2.0)
+    assert _rel(C, ref) < 5e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_batched_1x1_conv_forms(dtype):
+    """Decoder 1x1 conv: W [O, I] . x[b] [I, P] (shared weight); its data gradient
+    W^T . dy[b]; its weight gradient sum_b dy[b] . x[b]^T (reduce_batch, split-K)."""
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(5)
+    Bn, O, I, P = 3, 96, 64, 200
+    W = _make((O, I), dtype, g)
+    x = _make((Bn, I, P), dtype, g)
+    dy = _make((Bn, O, P), dtype, g)
+    tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
+    y = gemm_hip.gemm(W, x, out_dtype=torch.float32)
+    assert y.shape == (Bn, O, P) and _rel(y, W.float() @ x.float()) < tol
+    dx = gemm_hip.gemm(W.t(), dy, out_dtype=torch.float32)
+    assert _rel(dx, W.float().t() @ dy.float()) < tol
+    for splits in (1, 3):
+        dW = gemm_hip.gemm(dy, x.transpose(1, 2), out_dtype=torch.float32, reduce_batch=True, splits=splits)
+        assert dW.shape == (O, I)
+        assert _rel(dW, (dy.float() @ x.float().transpose(1, 2)).sum(0)) < tol
+
+
+def test_gemm_split_k_deterministic():
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(6)
+    A = _make((128, 4096), torch.float32, g)
+    B = _make((4096, 256), torch.float32, g)
+    o1 = gemm_hip.gemm(A, B, splits=8)
+    o2 = gemm_hip.gemm(A, B, splits=8)
+    assert torch.equal(o1, o2)
+    assert _rel(o1, A @ B) < 5e-5
+
+
+def test_gemm_f32x3_accuracy_bound():
+    """The hi/lo split's error stays within its analytic bound relative to sum |a||b|."""
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(7)
+    A = torch.randn(256, 1024, generator=g, dtype=torch.float64)
+    B = torch.randn(1024, 256, generator=g, dtype=torch.float64)
+    out = gemm_hip.gemm(A.float().to(DEV), B.float().to(DEV)).double().cpu()
+    exact = A.float().double() @ B.float().double()
+    bound = (A.abs() @ B.abs()) * 2.0 ** -15.5 + 1024 * 2.0 ** -24 * (A.abs() @ B.abs())
+    assert bool(((out - exact).abs() <= bound).all())
+
+
+def test_gemm_unsupported_shape_returns_none():
+    from torch_utils.ops import gemm_hip
+    A = torch.randn(10, 7, device=DEV)         # K = 7: not a multiple of 4 fp32 elements
+    B = torch.randn(7, 12, device=DEV)
+    assert gemm_hip.try_gemm(A, B) is None

@@ -1,0 +1,168 @@
+"""GPU parity of the real hot path against the reference's own network vectors
+(tests/golden/networks_golden.npz, produced by tests/golden/make_golden_networks.py
+from the reference itself): the exact cases of test_networks_parity.py, run on
+cuda:0 through the HIP decoder / LPIPS-head kernels.
+
+fp32 variant (decoder num_fp16_res=0, VFM tower in fp32): the same tolerances as the
+CPU parity test -- outputs 1e-4 of max magnitude, gradient norms 1e-3 (2e-3 for the
+TotalLoss step) -- since only the summation order differs (hipBLASLt / MIOpen / HIP
+kernels vs torch CPU).
+
+bf16 variant (the training configuration: decoder blocks 3-5 and the SigLIP2 tower
+in bf16, as on the benchmark): outputs within 3e-2 of max magnitude, gradient norms
+within 5e-2, stated per assertion; these bound the bf16 rounding (2^-8 relative per
+op, accumulated over ~60 ops) and catch layout or indexing errors, which show up as
+O(1) differences.
+
+Each test also asserts that the native kernels ran (kernel_timer records every native
+launch), so a silent torch fallback cannot pass.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import net_cases
+from det_init import det_init
+from test_networks_parity import _arr, _meta, _rel, _check_grads
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def vfm_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("vfmg") / net_cases.VFM_DIRNAME
+    d.mkdir()
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(d / "config.json", "w"))
+    return str(d)
+
+
+def _native_ran(kt, *names):
+    got = {k.split("<")[0] for k in kt.summary()}
+    for n in names:
+        assert n in got, (n, sorted(got))
+
+
+def _gen(vfm_dir, precision):
+    from networks.generator import Generator
+    over = {} if precision == "bf16" else dict(num_fp16_res=0)
+    torch.manual_seed(0)
+    G = Generator(label_dim=0, **net_cases.g_kwargs(vfm_dir, **over)).train()
+    det_init(G)
+    G = G.to(DEV)
+    G.vfm_encoder.encoder.amp_enabled = precision == "bf16"
+    return G
+
+
+TOL = {"fp32": dict(out=1e-4, loss=1e-5, norm=1e-3, full=2e-3, sums=1e-3),
+       "bf16": dict(out=3e-2, loss=3e-2, norm=5e-2, full=1e-1, sums=5e-2)}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_generator_forward_backward_gpu(vfm_dir, precision):
+    from torch_utils.ops import kernel_timer as kt
+    tol = TOL[precision]
+    G = _gen(vfm_dir, precision)
+    G.zero_grad(set_to_none=True)
+    G.requires_grad_(False)
+    for m in (G.synthesis, G.mapping, G.ldm_adapter):
+        m.requires_grad_(True)
+    img = torch.from_numpy(_arr("G/img")).to(DEV)
+    torch.manual_seed(123)                          # posterior noise: CPU RNG, as the reference
+    kt.enable(True)
+    out = G(img, ['x'] * 2, validation=True)
+    assert _rel(out.gen_img.detach().cpu(), _arr("G/gen_img")) < tol["out"]
+    for i, m in enumerate(out.gen_multiscale_imgs):
+        assert _rel(m.detach().cpu(), _arr(f"G/ms{i}")) < tol["out"], i
+    assert _rel(out.vf_loss.detach().cpu(), _arr("G/vf_loss")) < tol["loss"]
+    assert _rel(out.kl_loss.detach().cpu(), _arr("G/kl_loss")) < tol["loss"]
+    R = torch.from_numpy(_arr("G/R")).to(DEV)
+    Rs = [torch.from_numpy(_arr(f"G/R{i}")).to(DEV) for i in range(len(out.gen_multiscale_imgs))]
+    loss = (out.gen_img * R).sum() + sum((m * r).sum() for m, r in zip(out.gen_multiscale_imgs, Rs)) \
+        + 3.0 * out.vf_loss + 1e3 * out.kl_loss
+    loss.backward()
+    torch.cuda.synchronize()
+    _native_ran(kt, "dwconv2d_fwd", "dwconv2d_bwd_data", "dwconv2d_bwd_weight", "group_norm_fwd",
+                "group_norm_bwd", "shuffle_blur_fwd", "shuffle_blur_bwd")
+    kt.enable(False)
+    _check_grads("G", G, norm_tol=tol["norm"], full_tol=tol["full"], sum_tol=tol["sums"])
+
+
+def test_discriminator_gpu():
+    from networks.discriminator import ProjectedDiscriminator
+    D = ProjectedDiscriminator(c_dim=0, **net_cases.D_KWARGS).train()
+    det_init(D)
+    D = D.to(DEV)
+    x = torch.from_numpy(_arr("D/x")).to(DEV).requires_grad_(True)
+    out = D(x, None)
+    assert _rel(out.stylegan_t_logits.detach().cpu(), _arr("D/logits")) < 1e-4
+    for s, scale in enumerate(out.patchgan_logits):
+        assert _rel(scale[-1].detach().cpu(), _arr(f"D/patch{s}")) < 1e-4
+        for t, ref in zip(scale, _meta()[f"D/patch{s}_feat_sums"]):
+            assert abs(float(t.detach().double().sum()) - ref) <= 1e-4 * max(1.0, abs(ref)) + 1e-3 * t.numel() ** 0.5
+    R = torch.from_numpy(_arr("D/R")).to(DEV)
+    dl = (out.stylegan_t_logits * R).sum() + sum(s[-1].square().mean() for s in out.patchgan_logits)
+    dl.backward()
+    assert _rel(x.grad.cpu(), _arr("D/dx")) < 1e-3
+    _check_grads("D", D)
+
+
+def test_lpips_gpu():
+    from training.lpips import LPIPS
+    from torch_utils.ops import kernel_timer as kt
+    L = LPIPS().eval()
+    det_init(L)
+    L = L.to(DEV)
+    a = torch.from_numpy(_arr("L/a")).to(DEV)
+    b = torch.from_numpy(_arr("L/b")).to(DEV).requires_grad_(True)
+    kt.enable(True)
+    v = L(a, b)
+    assert _rel(v.detach().cpu(), _arr("L/val")) < 1e-5
+    v.sum().backward()
+    torch.cuda.synchronize()
+    _native_ran(kt, "lpips_head_fwd", "lpips_head_bwd")
+    kt.enable(False)
+    assert _rel(b.grad.cpu(), _arr("L/db")) < 1e-4
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_total_loss_step_gpu(vfm_dir, graphed):
+    """One full D + G accumulate_gradients step on cuda:0 (fp32), optionally with the D phase's
+    no-grad generator forward replayed from HIP graphs (the benchmarked path)."""
+    from networks.generator import Generator
+    from networks.discriminator import ProjectedDiscriminator
+    from training.loss import TotalLoss
+    torch.manual_seed(5)
+    G2 = Generator(label_dim=0, **net_cases.g_kwargs(vfm_dir, num_fp16_res=0)).train().requires_grad_(False)
+    D2 = ProjectedDiscriminator(c_dim=0, **net_cases.D_KWARGS).train().requires_grad_(False)
+    det_init(G2)
+    det_init(D2)
+    G2, D2 = G2.to(DEV), D2.to(DEV)
+    G2.vfm_encoder.encoder.amp_enabled = False
+    loss = TotalLoss(device=DEV, G=G2, D=D2, **net_cases.loss_kwargs(vfm_dir))
+    det_init(loss.perceptual_module)
+    if graphed:
+        loss.enable_graphed_nograd_forward()
+    real = torch.from_numpy(_arr("T/real")).to(DEV)
+    D2.requires_grad_(True)
+    D2.dino.requires_grad_(False)
+    torch.manual_seed(321)
+    loss.accumulate_gradients(phase='D', real_img=real, real_c=['x'] * 2, cur_nimg=0)
+    if graphed:
+        assert loss.graphed_nograd.replays == 1 and loss.graphed_nograd.disabled is None
+    D2.requires_grad_(False)
+    # fp32, but the LPIPS VGG and PatchGAN convolutions run on MIOpen, whose fp32 solvers
+    # differ from torch-CPU by up to ~1.6e-3 relative on these scalar reductions
+    _check_grads("T/D", D2, norm_tol=2e-3, full_tol=1e-2, sum_tol=2e-3)
+    for name, layer in G2.named_modules():
+        layer.requires_grad_(any(t in name for t in G2.trainable_layers))
+    torch.manual_seed(654)
+    loss.accumulate_gradients(phase='G', real_img=real, real_c=['x'] * 2, cur_nimg=0)
+    for k, v in _meta()["T/prev_loss_dict"].items():
+        assert abs(loss.prev_loss_dict[k] - v) <= 1e-4 * max(1.0, abs(v)), k
+    # worst case: the scalar `noise_strength` gradients, full-image reductions whose terms
+    # cancel to ~1e-3 of their magnitude, see the MIOpen LPIPS backward's rounding (3.4e-3)
+    _check_grads("T/G", G2, norm_tol=5e-3, full_tol=1e-2, sum_tol=5e-3)
+    assert loss._off_done

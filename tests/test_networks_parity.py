@@ -44,7 +44,9 @@ def vfm_dir(tmp_path_factory):
     return str(d)
 
 
-def _check_grads(prefix, module, names_key=None, norm_tol=1e-3, full_tol=2e-3):
+def _check_grads(prefix, module, names_key=None, norm_tol=1e-3, full_tol=2e-3, sum_tol=1e-3):
+    """Every parameter gradient of `module` (any device) against the reference's norms,
+    sums and (where stored) full tensors. Returns the worst relative norm error."""
     names = [canonical(n) for n in _meta()[f"{prefix}/grad_names"]]
     sums, norms = _arr(f"{prefix}/grad_sum"), _arr(f"{prefix}/grad_norm")
     params = {canonical(n): p for n, p in module.named_parameters()}
@@ -53,12 +55,12 @@ def _check_grads(prefix, module, names_key=None, norm_tol=1e-3, full_tol=2e-3):
     worst = 0.0
     floor = 1e-4 * float(np.max(norms))        # grads that are ~0 in exact math (bias before a norm layer)
     for n, s, nm in zip(names, sums, norms):
-        g = got[n].grad.double()
+        g = got[n].grad.detach().double().cpu()
         scale = max(nm, floor, 1e-12)
         err = abs(float(g.norm()) - nm) / scale
         worst = max(worst, err)
         assert err < norm_tol, (n, float(g.norm()), nm)
-        assert abs(float(g.sum()) - s) <= 1e-3 * scale * max(1.0, g.numel() ** 0.5), (n, float(g.sum()), s)
+        assert abs(float(g.sum()) - s) <= sum_tol * scale * max(1.0, g.numel() ** 0.5), (n, float(g.sum()), s)
         arrays = golden_io.load(G_FILE)[0]
         key = next((k for k in (f"{prefix}/grad/{n}", f"{prefix}/grad/{n.replace('vision_model.', 'vision_model.vision_model.', 1)}") if k in arrays), None)
         if key is not None:

@@ -75,3 +75,45 @@ def test_construct_iteration_matches_training_loop_setup(tmp_path):
     step = construct_iteration(G, D, G_ema, dev, lk, opt, opt, batch_size=2)
     assert getattr(step.loss, "graphed_nograd", None) is None       # CPU: eager
     assert step.G is G and step.G_ema is G_ema and step.D is D
+
+
+@pytest.mark.parametrize("outcomes,hit", [(((1.0, 2, False), (0.5, 0, False)), True),     # both: unresized input
+                                          (((1.0, 0, False), (0.5, 0, True)), False)])    # G phase resizes
+def test_vfm_feature_reuse_is_exact(tmp_path, outcomes, hit):
+    """The G phase reuses the D phase's frozen-tower features only when both phases feed the
+    tower the same input, and the G-phase gradients equal a run that recomputes them."""
+    import json
+    import net_cases
+    from det_init import det_init
+    from networks.generator import Generator
+    from networks.discriminator import ProjectedDiscriminator
+    from training.loss import TotalLoss
+    vfm = tmp_path / net_cases.VFM_DIRNAME
+    vfm.mkdir()
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(vfm / "config.json", "w"))
+    grads = {}
+    for reuse in (True, False):
+        torch.manual_seed(0)
+        G = Generator(label_dim=0, **net_cases.g_kwargs(str(vfm), use_equivariance_regularization=True,
+                                                         img_resolution=128)).train().requires_grad_(False)
+        D = ProjectedDiscriminator(c_dim=0, **net_cases.D_KWARGS).train().requires_grad_(False)
+        det_init(G)
+        det_init(D)
+        loss = TotalLoss(device=torch.device('cpu'), G=G, D=D, **dict(net_cases.loss_kwargs(str(vfm)),
+                                                                       use_equivariance_regularization=True))
+        G.vfm_encoder.reuse_features = reuse
+        img = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(3))
+        G.equivariance_transform.forced = outcomes[0]
+        torch.manual_seed(1)
+        loss.accumulate_gradients(phase='D', real_img=img, real_c=['x'] * 2, cur_nimg=0)
+        G.equivariance_transform.forced = outcomes[1]
+        for name, layer in G.named_modules():
+            layer.requires_grad_(any(t in name for t in G.trainable_layers))
+        torch.manual_seed(2)
+        loss.accumulate_gradients(phase='G', real_img=img, real_c=['x'] * 2, cur_nimg=0)
+        grads[reuse] = {n: p.grad.clone() for n, p in G.named_parameters() if p.grad is not None}
+        if reuse:
+            assert getattr(G.vfm_encoder, 'reuse_hits', 0) == (1 if hit else 0)
+    assert grads[True].keys() == grads[False].keys() and grads[True]
+    for n in grads[True]:
+        assert torch.equal(grads[True][n], grads[False][n]), n

@@ -125,9 +125,7 @@ class SiglipAttention(nn.Module):
         B, N, D = x.shape
         w, b = self.fused_qkv(x.dtype)
         qkv = vit_ops.linear(x, w, b)                                         # [B, N, 3D]
-        q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
-        o = F.scaled_dot_product_attention(q, k, v)                           # [B, h, N, d]
-        o = o.transpose(1, 2).reshape(B, N, D)
+        o = vit_ops.attention_packed(qkv, self.num_heads)                     # [B, N, D]
         return vit_ops.linear(o, self.out_proj.weight.to(x.dtype), self.out_proj.bias)
 
 

@@ -63,8 +63,7 @@ def mha(x, wq, bq, wk, bk, wv, bv, wo, bo, heads):
     w = torch.cat([wq, wk, wv], 0).to(x.dtype)
     b = torch.cat([bq, bk, bv], 0) if bq is not None else None
     qkv = vit_ops.linear(x, w, b)
-    q, k, v = qkv.reshape(B, N, 3, heads, D // heads).permute(2, 0, 3, 1, 4).unbind(0)
-    o = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, N, D)
+    o = vit_ops.attention_packed(qkv, heads)
     return vit_ops.linear(o, wo.to(x.dtype), bo)
 
 

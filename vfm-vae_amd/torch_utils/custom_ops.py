@@ -55,6 +55,11 @@ SIGNATURES = {
                              c_int, c_vp],
     "vfm_lpips_head_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_lpips_head_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
+    "vfm_gemm_workspace_floats": [c_int, c_int, c_int, c_int, c_int],
+    "vfm_gemm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int,
+                 c_ll, c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_attention_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp, c_llp, c_float,
+                          c_vp],
 }
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}
@@ -106,6 +111,11 @@ def dtype_code(t: torch.Tensor) -> int:
 def strides(t: torch.Tensor):
     arr = (ctypes.c_longlong * t.ndim)(*t.stride())
     return arr
+
+
+def strides_of(values):
+    """ctypes long long array of arbitrary element strides."""
+    return (ctypes.c_longlong * len(values))(*values)
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)

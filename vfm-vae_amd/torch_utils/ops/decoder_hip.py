@@ -113,6 +113,9 @@ def supported(op, x, **kw):
 # 1x1 conv as a stride-0-batch GEMM (hipBLASLt through torch.bmm), no layout copies.
 
 
+_NO_CAST_CACHE = os.environ.get("VFM_NO_CAST_CACHE", "0") == "1"
+
+
 def _cast_cached(w, dtype):
     """w.detach().to(dtype), cached on the parameter until it changes (its version counter
     moves at every optimizer step): the D-phase and G-phase forwards of one iteration share
@@ -120,7 +123,7 @@ def _cast_cached(w, dtype):
 would be baked into the graph and go stale after the next optimizer step)."""
     if w.dtype == dtype:
         return w.detach()
-    if torch.cuda.is_current_stream_capturing():
+    if _NO_CAST_CACHE or torch.cuda.is_current_stream_capturing():
         return w.detach().to(dtype)     # a graph must recompute the cast at every replay
     base = w._base if w._base is not None else w
     key = (tuple(w.shape), w.stride(), w.storage_offset(), dtype, base._version)
@@ -135,6 +138,37 @@ would be baked into the graph and go stale after the next optimizer step)."""
     return wc
 
 
+# Dense products of the decoder on the MFMA GEMM (csrc/gemm.hip: bf16, or fp32 operands as a
+# 3-term bf16 split); VFM_GEMM=torch keeps hipBLASLt (A/B switch). Shapes the kernel does not
+# cover fall back to torch.bmm explicitly.
+_USE_HIP_GEMM = os.environ.get("VFM_GEMM", "hip") != "torch"
+
+
+def _gemm(A, B, **kw):
+    if not _USE_HIP_GEMM:
+        return None
+    from . import gemm_hip
+    return gemm_hip.try_gemm(A, B, **kw)
+
+
+def weight_grad_1x1(dy, x, wdt):
+    """sum_b dy[b] @ x[b]^T in fp32 -> wdt ([O, P] x [I, P] per sample)."""
+    dw = _gemm(dy, x.transpose(1, 2), out_dtype=torch.float32, reduce_batch=True,
+               splits=_splits(dy.shape[1], x.shape[1], dy.shape[2], dy.shape[0]))
+    if dw is None:
+        dw = torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32) if dy.dtype != torch.float32 else \
+            torch.bmm(dy, x.transpose(1, 2))
+        dw = dw.sum(0)
+    return dw.to(wdt)
+
+
+def _splits(M, N, K, z):
+    """K splits so that the grid has >= ~1024 workgroups (256 CUs x 4), each split >= 512 deep."""
+    tiles = -(-M // 128) * -(-N // 128) * z
+    want = -(-1024 // tiles)
+    return max(1, min(want, K // 512, 64))
+
+
 class _Pointwise(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, x):
@@ -145,7 +179,8 @@ class _Pointwise(torch.autograd.Function):
         wc = _cast_cached(w, x.dtype)
         ctx.save_for_backward(wc, x)
         ctx.wdt = w.dtype
-        return torch.bmm(wc.expand(B, O, I), x)
+        y = _gemm(wc, x)
+        return y if y is not None else torch.bmm(wc.expand(B, O, I), x)
 
     @staticmethod
     @torch.autograd.function.once_differentiable
@@ -157,13 +192,11 @@ class _Pointwise(torch.autograd.Function):
         dw = dx = None
         if _wanted(ctx, 0):
             # sum_b dy[b] @ x[b]^T with fp32 per-sample products, summed in fp32
-            if dy.dtype != torch.float32:
-                dw = torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32)
-            else:
-                dw = torch.bmm(dy, x.transpose(1, 2))
-            dw = dw.sum(0).to(ctx.wdt)
+            dw = weight_grad_1x1(dy, x, ctx.wdt)
         if _wanted(ctx, 1):
-            dx = torch.bmm(wc.t().expand(B, I, O), dy)
+            dx = _gemm(wc.t(), dy)
+            if dx is None:
+                dx = torch.bmm(wc.t().expand(B, I, O), dy)
         return dw, dx
 
 
@@ -453,7 +486,7 @@ class _ConvNeXtMLP(torch.autograd.Function):
         if fg is not None and _wanted(ctx, 6):
             dgm = r0.view(B, C).sum(0).to(gdt)
         if _wanted(ctx, 4):
-            dw2 = torch.bmm(dy, g.transpose(1, 2), out_dtype=torch.float32).sum(0).to(w2dt)
+            dw2 = weight_grad_1x1(dy, g, w2dt)
         # dh = (W2^T dy) * GELU'(h*s+b1) * s, with the per-(b, o) sums for d_s and d_b1
         tiles = _lib.vfm_pw_gemm_gelu_tiles(P)
         w2t = w2c.t().contiguous()
@@ -469,9 +502,11 @@ class _ConvNeXtMLP(torch.autograd.Function):
         if fb1 is not None and _wanted(ctx, 3):
             db1 = p1.sum((0, 1)).to(b1dt)
         if _wanted(ctx, 1):
-            dw1 = torch.bmm(dh, m.transpose(1, 2), out_dtype=torch.float32).sum(0).to(w1dt)
+            dw1 = weight_grad_1x1(dh, m, w1dt)
         if ctx.needs_input_grad[0]:
-            dm = torch.bmm(w1c.t().expand(B, C, O), dh)
+            dm = _gemm(w1c.t(), dh)
+            if dm is None:
+                dm = torch.bmm(w1c.t().expand(B, C, O), dh)
         dx = dout if ctx.needs_input_grad[7] else None
         return dm, dw1, ds, db1, dw2, db2, dgm, dx
 

@@ -1,0 +1,106 @@
+"""MFMA GEMM with fused epilogues (csrc/gemm.hip, C ABI `vfm_gemm` in include/vfmvae.h).
+
+Replaces hipBLASLt (torch.addmm / torch.bmm) on the hot path's dense products: the frozen
+ViT projections (bf16, bias / bias+tanh-GELU epilogue; reference
+networks/utils/vfms/siglip2_utils.py:121), and the fp32 1x1 convolutions / linear layers of
+the decoder and fusion adapter (convnext_utils.py:36-142, gigagan_utils.py:53-185,
+ldm_utils.py:55-166), whose fp32 operands run as three bf16 MFMA products of a hi/lo split
+(`f32x3`, error per product <= ~2^-15.5 relative; csrc/gemm.hip header).
+
+`gemm(A, B, ...)` takes 2-D or batched 3-D views and the layout of each operand, so no
+transposes are materialised. A missing kernel library raises; shapes the kernel does not
+cover (contiguous extents not multiples of 8/4 elements) return None from `try_gemm` so the
+caller can take its torch path explicitly.
+"""
+import torch
+
+from .. import custom_ops
+from . import kernel_timer
+
+_lib = custom_ops.get_native()
+_CODES = {torch.float32: 0, torch.bfloat16: 2}
+ACTS = {None: 0, "gelu_tanh": 1, "gelu": 2}
+
+
+def _layout(t, kdim_last):
+    """(is_k_contiguous, leading dim, batch stride) of a [z, rows, cols] / [rows, cols] operand
+    view whose last two dims are (outer, k) if kdim_last else (k, outer)."""
+    if t.dim() == 2:
+        t = t.unsqueeze(0)
+        sb = 0
+    else:
+        sb = t.stride(0) if t.shape[0] > 1 else 0
+    r, c = t.stride(1), t.stride(2)
+    if c == 1 or t.shape[2] == 1:
+        return kdim_last, r, sb
+    if r == 1 or t.shape[1] == 1:
+        return (not kdim_last), c, sb
+    return None
+
+
+def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=0.0, out_dtype=None,
+             splits=1, reduce_batch=False):
+    """C = epi(alpha * A @ B + beta * out). A: [M, K] or [z, M, K]; B: [K, N] or [z, K, N]
+    (any strides with one unit-stride dim each). bias: fp32 [N] (bias_dim=1) or [M]
+    (bias_dim=0). Returns C ([M, N] / [z, M, N], or [M, N] when reduce_batch sums over z),
+    or None when the kernel does not cover the shapes/strides."""
+    if A.dtype != B.dtype or A.dtype not in _CODES or not A.is_cuda:
+        return None
+    a3 = A if A.dim() == 3 else A.unsqueeze(0)
+    b3 = B if B.dim() == 3 else B.unsqueeze(0)
+    z = max(a3.shape[0], b3.shape[0])
+    if a3.shape[0] not in (1, z) or b3.shape[0] not in (1, z):
+        return None
+    M, K = a3.shape[1], a3.shape[2]
+    K2, N = b3.shape[1], b3.shape[2]
+    if K != K2:
+        raise RuntimeError(f"gemm: inner dims differ ({K} vs {K2})")
+    la = _layout(a3, True)                       # A rows = m, cols = k
+    lb = _layout(b3.transpose(1, 2), True)       # B^T rows = n, cols = k
+    if la is None or lb is None:
+        return None
+    a_kc, lda, sA = la
+    b_kc, ldb, sB = lb
+    if a3.shape[0] == 1:
+        sA = 0
+    if b3.shape[0] == 1:
+        sB = 0
+    out_dtype = out_dtype or A.dtype
+    zc = 1 if reduce_batch else z
+    if out is None:
+        if beta != 0.0:
+            raise RuntimeError("gemm: beta != 0 needs `out`")
+        out = torch.empty((zc, M, N) if (A.dim() == 3 or B.dim() == 3) and not reduce_batch else (M, N),
+                          dtype=out_dtype, device=A.device)
+    o3 = out if out.dim() == 3 else out.unsqueeze(0)
+    if o3.stride(2) != 1 or o3.dtype != out_dtype:
+        raise RuntimeError("gemm: output must be row-major in the requested dtype")
+    ldc, sC = o3.stride(1), (o3.stride(0) if o3.shape[0] > 1 else 0)
+    bias_mode = 0
+    if bias is not None:
+        bias = bias.detach().float().contiguous()
+        bias_mode = 1 if bias_dim in (None, 1) else 2
+    ws = None
+    if splits > 1 or reduce_batch:
+        n = _lib.vfm_gemm_workspace_floats(M, N, z, splits, int(reduce_batch))
+        ws = torch.empty(n, dtype=torch.float32, device=A.device)
+    flops = 2.0 * z * M * N * K
+    tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
+    with kernel_timer.region(f"gemm<{tag}>", 0, flops, "mfma"):
+        rc = _lib.vfm_gemm(A.data_ptr(), B.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(ws),
+                           _CODES[A.dtype], _CODES[out_dtype], M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB,
+                           ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], int(splits), int(reduce_batch),
+                           custom_ops.stream_ptr(A.device))
+    if rc == custom_ops.VFM_NO_KERNEL:
+        return None
+    custom_ops.check(rc, "vfm_gemm")
+    return out
+
+
+def gemm(A, B, **kw):
+    """try_gemm that raises instead of returning None."""
+    out = try_gemm(A, B, **kw)
+    if out is None:
+        raise custom_ops.NativeError(f"vfm_gemm does not cover A {tuple(A.shape)} {A.stride()} / "
+                                     f"B {tuple(B.shape)} {B.stride()} {A.dtype}")
+    return out

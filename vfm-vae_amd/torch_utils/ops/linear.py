@@ -1,0 +1,82 @@
+"""nn.Linear on the MFMA GEMM (csrc/gemm.hip) with autograd.
+
+Used by the trainable fusion adapter (reference networks/utils/ldm_utils.py:55-166:
+PlainAttention.qkv / proj, AttnProjectionBlock.proj, GeGluMlp w0/w1/w2; fp32, outside
+autocast) and the frozen DINO ViT-S of the projected discriminator (discriminator.py:145-168,
+fp32, gradients w.r.t. its input only). `Linear` is a drop-in nn.Linear subclass (same
+parameters and state-dict keys); on ROCm tensors its forward and backward products run on
+the HIP GEMM (fp32 operands as the 3-term bf16 split, csrc/gemm.hip), elsewhere F.linear.
+
+  forward   y  = x W^T + b            (bias in the GEMM epilogue)
+  backward  dx = dy W,  dW = dy^T x (fp32),  db = sum dy
+Gradients that the autograd engine will not consume in this pass are not computed (see
+decoder_hip._wanted: the adaptive-VF `autograd.grad` runs data-only backward passes).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import gemm_hip
+
+
+def _wanted(ctx, i):
+    from .decoder_hip import _wanted as w
+    return w(ctx, i)
+
+
+def _edges(ctx, *args):
+    from .decoder_hip import _edges as e
+    e(ctx, *args)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        _edges(ctx, x, w, b)
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if x2.stride(-1) != 1:
+            x2 = x2.contiguous()
+        wc = w if w.dtype == x.dtype else w.to(x.dtype)
+        y = gemm_hip.try_gemm(x2, wc.t(), bias=b, bias_dim=1)
+        if y is None:
+            y = F.linear(x2, wc, None if b is None else b.to(x.dtype))
+        ctx.save_for_backward(x2, wc)
+        ctx.meta = (shape, w.dtype, None if b is None else b.dtype)
+        return y.reshape(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x2, wc = ctx.saved_tensors
+        shape, wdt, bdt = ctx.meta
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.stride(-1) != 1 or dy2.dtype != x2.dtype:
+            dy2 = dy2.contiguous().to(x2.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0] and _wanted(ctx, 0):
+            dx = gemm_hip.try_gemm(dy2, wc)
+            if dx is None:
+                dx = dy2 @ wc
+            dx = dx.reshape(shape)
+        if ctx.needs_input_grad[1] and _wanted(ctx, 1):
+            dw = gemm_hip.try_gemm(dy2.t(), x2, out_dtype=torch.float32)
+            if dw is None:
+                dw = dy2.t().float() @ x2.float()
+            dw = dw.to(wdt)
+        if bdt is not None and ctx.needs_input_grad[2] and _wanted(ctx, 2):
+            db = dy2.float().sum(0).to(bdt)
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16):
+        return _LinearFn.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+class Linear(nn.Linear):
+    """nn.Linear whose ROCm forward/backward run on the HIP GEMM."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)

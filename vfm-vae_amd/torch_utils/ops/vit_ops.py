@@ -69,3 +69,19 @@ def residual_layer_norm(h, delta, ln, out_dtype):
 
 def residual_add(h, delta):
     return h + delta.float()
+
+
+def attention_packed(qkv, heads):
+    """Multi-head self-attention of a packed [B, N, 3*D] (q | k | v) projection -> [B, N, D].
+    ROCm bf16 tensors outside autograd with head dim 64 (the frozen towers) run the fused
+    HIP kernel (attn_hip, csrc/attention.hip) straight on the packed layout; everything
+    else (CPU, fp32 parity runs, other head dims) is torch SDPA."""
+    B, N, D3 = qkv.shape
+    D = D3 // 3
+    d = D // heads
+    if _frozen(qkv):
+        from . import attn_hip
+        if attn_hip.supported(qkv, d):
+            return attn_hip.attention_packed(qkv, heads)
+    q, k, v = qkv.reshape(B, N, 3, heads, d).permute(2, 0, 3, 1, 4).unbind(0)
+    return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, N, D)

@@ -33,7 +33,7 @@ class StatsRegistry:
         self.totals = {}               # name -> fp64 cpu tensor [3]
 
     def configure(self, rank, sync_device):
-        if self.frozen:
+        if self.frozen and (rank, sync_device) != (self.rank, self.sync_device):
             raise RuntimeError("training_stats.init_multiprocessing() must run before the first Collector.update()")
         self.rank, self.sync_device = rank, sync_device
 

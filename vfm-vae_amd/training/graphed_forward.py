@@ -157,12 +157,14 @@ class GraphedNoGradForward:
                 et.forced = prev_forced
         if len(served) != len(bufs):
             raise RuntimeError("noise draws differ between warm-up and capture")
-        return _Entry(graph, static_img, bufs, out, self)
+        vfm = getattr(G.vfm_encoder, 'last_features', None) if G.vfm_encoder.reuse_features else None
+        return _Entry(graph, static_img, bufs, out, self, vfm)
 
 
 class _Entry:
-    def __init__(self, graph, static_img, bufs, out, owner):
+    def __init__(self, graph, static_img, bufs, out, owner, vfm=None):
         self.graph, self.static_img, self.bufs, self.out, self.owner = graph, static_img, bufs, out, owner
+        self.vfm = vfm          # (input transform, features, pooled): the captured tower outputs
         self.pinned = [torch.empty(b.shape, dtype=b.dtype, pin_memory=True) for b in bufs]
         self.copied = None      # event after the last host->device noise copy
 
@@ -178,4 +180,6 @@ class _Entry:
         self.static_img.copy_(img)
         self.graph.replay()
         self.owner.replays += 1
+        if self.vfm is not None:
+            self.owner.G.vfm_encoder.last_features = self.vfm
         return self.out

@@ -216,7 +216,9 @@ class TotalLoss:
         self._freeze_done = False
         self._off_done = False
         self.total_kimg = total_kimg
-        self.grad_sync = {}        # phase name -> GradBucketer (set by the training loop / bench)
+        enc = getattr(G, 'vfm_encoder', None)
+        if enc is not None and hasattr(enc, 'offer_features'):
+            enc.reuse_features = True      # G phase reuses the D phase's tower features when exact
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -433,8 +435,16 @@ class TotalLoss:
 
         if phase == 'D':
             d_loss = torch.zeros([], device=self.device, requires_grad=True)
+            enc = getattr(self.G, 'vfm_encoder', None)
+            reuse = enc is not None and getattr(enc, 'reuse_features', False)
+            if reuse:
+                enc.clear_features()
             with torch.no_grad():
                 out = self.run_G_nograd(real_img, real_c)
+            if reuse and enc.last_features is not None:
+                # same microbatch in the G phase: its run_G skips the tower if it draws the same
+                # input transform (networks/utils/vfm_utils.py VFMEncoder.encode_image)
+                enc.offer_features(real_img, *enc.last_features)
             gen_img = out.gen_img.detach()
             eq_s, eq_a, real_c_enc = out.eq_scale_factor, out.eq_angle_factor, out.global_text_tokens
             del out

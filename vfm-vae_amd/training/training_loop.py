@@ -304,6 +304,15 @@ def preprocess_image(image, device):
     return image.to(device, non_blocking=True).to(torch.float32) / 255.
 
 
+def _sync_all_done(local_done, device):
+    """True once any rank's one-epoch stream is exhausted (all ranks stop together)."""
+    if dist.get_world_size() == 1:
+        return bool(local_done)
+    flag = torch.tensor([int(local_done)], dtype=torch.int32, device=device)
+    torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+    return bool(flag.item())
+
+
 def fetch_data(iterator, device, batch_gpu):
     real_img, real_cs = next(iterator)
     real_img = preprocess_image(real_img, device)
@@ -393,6 +402,9 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
     torch.manual_seed(base_seed)
     random.seed(base_seed)
     configure_backends(cudnn_benchmark)
+    if metrics:
+        raise NotImplementedError(f"metrics {metrics}: the FID/IS detectors need URL downloads (reference "
+                                  "metrics/), which this offline build does not fetch; set `metrics: []`")
 
     dist.print0('Loading training set...')
     training_set = dnnlib.util.construct_class_by_name(**training_set_kwargs)
@@ -428,7 +440,19 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
     batch_idx = 0
     dist.print0(f'Training started at {resume_kimg} kimg.')
     while True:
-        phase_real_img, phase_real_c = fetch_data(iterator, device, batch_gpu)
+        try:
+            phase_real_img, phase_real_c = fetch_data(iterator, device, batch_gpu)
+            exhausted = False
+        except StopIteration:
+            if not one_epoch:
+                raise
+            exhausted = True
+        if one_epoch and _sync_all_done(exhausted, device):      # reference _sync_all_done :349-353
+            dist.print0(f'[one-epoch] data exhausted at {cur_nimg / 1e3:.1f} kimg')
+            if dist.get_rank() == 0 and network_snapshot_ticks is not None:
+                save_snapshot(os.path.join(run_dir, f'network-snapshot-{cur_nimg // 1000:08d}.pth'), G, D, G_ema,
+                              training_set_kwargs)
+            break
         step(phase_real_img, phase_real_c, cur_nimg)
         cur_nimg += batch_size
         batch_idx += 1
