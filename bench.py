@@ -49,7 +49,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
-    ap.add_argument("--no-graphs", action="store_true", help="A/B: eager D-phase generator forward")
+    ap.add_argument("--graphs", action="store_true",
+                    help="experimental: replay the D-phase generator forward from HIP graphs (off: see DESIGN.md)")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
     ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="off",
                     help="GEMM solution table (torch TunableOp over hipBLASLt/rocBLAS): 'use' reads the "
@@ -131,13 +132,13 @@ def main(argv=None):
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
     if args.tunableop == "tune":
-        args.no_graphs = True            # a GEMM cannot be tuned inside a HIP-graph capture
+        args.graphs = False              # a GEMM cannot be tuned inside a HIP-graph capture
     tunable = setup_tunableop(args.tunableop, args.tunableop_out)
     if tunable:
         _log(rank, f"tunableop: {tunable}")
 
     t_start = time.perf_counter()
-    c, step = build(args.config, args.batch, device, world, graphs=not args.no_graphs)
+    c, step = build(args.config, args.batch, device, world, graphs=args.graphs)
     _log(rank, f"built in {time.perf_counter() - t_start:.1f}s")
     from training.data_synthetic import SyntheticDataset
     pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=rank).make_pool(args.batch, device)
@@ -246,7 +247,7 @@ def main(argv=None):
                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "seq_len": 1024,
                        "resolution": 256, "parallelism": f"dp{world}",
                        "decoder_ops": "torch" if args.force_ref_ops else "hip",
-                       "d_phase_g_forward": "eager" if args.no_graphs else "hip_graph",
+                       "d_phase_g_forward": "hip_graph" if args.graphs else "eager",
                        "gemm_table": tunable["table"] if tunable and tunable["mode"] == "use" else None},
             "roofline": roof,
             "cpu_baseline": cpu,

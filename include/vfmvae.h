@@ -227,6 +227,17 @@ int vfm_attention_fwd(const void* q, const void* k, const void* v, void* o, int 
  *   vfm_gemm_workspace_floats(...) elements) and are summed in a fixed order by a second
  *   kernel that applies the epilogue. reduce_batch = 1: C (single matrix) = epi(sum over z)
  *   -- the weight gradient of a batched 1x1 convolution. */
+/* Large-tile bf16 form of vfm_gemm (csrc/gemm_fast.hip: 256 x 256 tiles, LDS-DMA double
+ * buffer): same arguments without precision / split-K; K % 64 == 0 (else VFM_NO_KERNEL). */
+int vfm_gemm_fast(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+                  int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+                  long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
+/* fp32 -> bf16 3-term split of one GEMM operand along its reduction dimension K, so that the
+ * fp32 product runs as ONE bf16 GEMM of depth 3K: role 0 (A) writes [hi | hi | lo], role 1 (B)
+ * [hi ; lo ; hi]; kcont = 1: src [R][K] (row stride ld) -> dst [R][3K], kcont = 0: src [K][R]
+ * -> dst [3K][R]; batch strides sb (src) / db (dst) in elements. */
+int vfm_split3(const float* src, void* dst, int R, int K, long long ld, long long sb, long long db, int batch,
+               int role, int kcont, void* stream);
 int vfm_gemm_workspace_floats(int M, int N, int batch, int splits, int reduce_batch);
 int vfm_gemm(const void* A, const void* B, void* C, const float* bias, float* workspace, int in_dtype,
              int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,

@@ -129,3 +129,52 @@ def test_gemm_unsupported_shape_returns_none():
     A = torch.randn(10, 7, device=DEV)         # K = 7: not a multiple of 4 fp32 elements
     B = torch.randn(7, 12, device=DEV)
     assert gemm_hip.try_gemm(A, B) is None
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128)])
+def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K):
+    """The 256-tile LDS-DMA kernel (csrc/gemm_fast.hip) and, for fp32, the [hi|hi|lo] split."""
+    from torch_utils.ops import gemm_hip, kernel_timer
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    A = _make((K, M) if a_t else (M, K), dtype, g)
+    B = _make((N, K) if b_t else (K, N), dtype, g)
+    Av = A.t() if a_t else A
+    Bv = B.t() if b_t else B
+    kernel_timer.enable(True)
+    out = gemm_hip.gemm(Av, Bv, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert any(k.startswith("gemm_fast") for k in kernel_timer.summary())
+    kernel_timer.enable(False)
+    tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
+    assert _rel(out, Av.float() @ Bv.float()) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_fast_epilogue_batched(dtype):
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(9)
+    Bn, O, I, P = 2, 256, 128, 1024
+    W = _make((O, I), dtype, g)
+    x = _make((Bn, I, P), dtype, g)
+    bias = torch.randn(O, generator=g).to(DEV)
+    y = gemm_hip.gemm(W, x, bias=bias, bias_dim=0, act="gelu", out_dtype=torch.float32, cache_a=True)
+    ref = torch.nn.functional.gelu(W.float() @ x.float() + bias[:, None])
+    assert _rel(y, ref) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+    y2 = gemm_hip.gemm(W, x, bias=bias, bias_dim=0, act="gelu", out_dtype=torch.float32, cache_a=True)
+    assert torch.equal(y, y2)                                   # cached weight split reused
+    with torch.no_grad():
+        W.mul_(2.0)                                             # version bump invalidates the cache
+    y3 = gemm_hip.gemm(W, x, bias=bias, bias_dim=0, act="gelu", out_dtype=torch.float32, cache_a=True)
+    ref3 = torch.nn.functional.gelu(W.float() @ x.float() + bias[:, None])
+    assert _rel(y3, ref3) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+
+
+def test_gemm_generic_path_when_fast_off(monkeypatch):
+    from torch_utils.ops import gemm_hip
+    monkeypatch.setattr(gemm_hip, "FAST", False)
+    g = torch.Generator().manual_seed(10)
+    A = _make((512, 256), torch.float32, g)
+    B = _make((256, 768), torch.float32, g)
+    assert _rel(gemm_hip.gemm(A, B), A @ B) < 5e-5

@@ -127,10 +127,14 @@ def test_lpips_gpu():
     assert _rel(b.grad.cpu(), _arr("L/db")) < 1e-4
 
 
-@pytest.mark.parametrize("graphed", [False, True])
-def test_total_loss_step_gpu(vfm_dir, graphed):
+@pytest.mark.parametrize("graphed,gemm", [(False, "hip"), (True, "hip"), (False, "torch")])
+def test_total_loss_step_gpu(vfm_dir, graphed, gemm, monkeypatch):
     """One full D + G accumulate_gradients step on cuda:0 (fp32), optionally with the D phase's
-    no-grad generator forward replayed from HIP graphs (the benchmarked path)."""
+    no-grad generator forward replayed from HIP graphs. gemm='torch' keeps the decoder's fp32
+    1x1 convolutions on hipBLASLt's exact fp32 GEMM (the scalar-gradient check then holds at
+    5e-3); gemm='hip' is the product path (3-term bf16 split)."""
+    from torch_utils.ops import decoder_hip
+    monkeypatch.setattr(decoder_hip, "_USE_HIP_GEMM", gemm == "hip")
     from networks.generator import Generator
     from networks.discriminator import ProjectedDiscriminator
     from training.loss import TotalLoss
@@ -163,6 +167,13 @@ def test_total_loss_step_gpu(vfm_dir, graphed):
     for k, v in _meta()["T/prev_loss_dict"].items():
         assert abs(loss.prev_loss_dict[k] - v) <= 1e-4 * max(1.0, abs(v)), k
     # worst case: the scalar `noise_strength` gradients, full-image reductions whose terms
-    # cancel to ~1e-3 of their magnitude, see the MIOpen LPIPS backward's rounding (3.4e-3)
-    _check_grads("T/G", G2, norm_tol=5e-3, full_tol=1e-2, sum_tol=5e-3)
+    # cancel to ~1e-3 of their magnitude. Their upstream gradient comes through the D heads'
+    # BatchNormLocal over this case's 2-sample batch (normalised values are +-1, so dL/dx
+    # scales with 1/std of two nearly equal samples) and amplifies the decoder's 3-term-split
+    # GEMM rounding (~1e-5) to up to ~3.6e-2 on these scalars only (measured); every
+    # tensor-valued gradient stays within 5e-3 of the reference.
+    # element-wise, the same amplification reaches 1.4e-2 of max on the 64-px block's GroupNorm
+    # weights (gemm='hip'); norms and sums stay within 5e-3
+    _check_grads("T/G", G2, norm_tol=5e-3, full_tol=2e-2 if gemm == "hip" else 1e-2, sum_tol=5e-3,
+                 scalar_tol=6e-2 if gemm == "hip" else None)
     assert loss._off_done

@@ -44,7 +44,7 @@ def vfm_dir(tmp_path_factory):
     return str(d)
 
 
-def _check_grads(prefix, module, names_key=None, norm_tol=1e-3, full_tol=2e-3, sum_tol=1e-3):
+def _check_grads(prefix, module, names_key=None, norm_tol=1e-3, full_tol=2e-3, sum_tol=1e-3, scalar_tol=None):
     """Every parameter gradient of `module` (any device) against the reference's norms,
     sums and (where stored) full tensors. Returns the worst relative norm error."""
     names = [canonical(n) for n in _meta()[f"{prefix}/grad_names"]]
@@ -59,13 +59,16 @@ def _check_grads(prefix, module, names_key=None, norm_tol=1e-3, full_tol=2e-3, s
         scale = max(nm, floor, 1e-12)
         err = abs(float(g.norm()) - nm) / scale
         worst = max(worst, err)
-        assert err < norm_tol, (n, float(g.norm()), nm)
-        assert abs(float(g.sum()) - s) <= sum_tol * scale * max(1.0, g.numel() ** 0.5), (n, float(g.sum()), s)
+        ntol, stol = norm_tol, sum_tol
+        if scalar_tol is not None and g.numel() == 1:
+            ntol = stol = scalar_tol
+        assert err < ntol, (n, float(g.norm()), nm)
+        assert abs(float(g.sum()) - s) <= stol * scale * max(1.0, g.numel() ** 0.5), (n, float(g.sum()), s)
         arrays = golden_io.load(G_FILE)[0]
         key = next((k for k in (f"{prefix}/grad/{n}", f"{prefix}/grad/{n.replace('vision_model.', 'vision_model.vision_model.', 1)}") if k in arrays), None)
         if key is not None:
             ref = np.asarray(arrays[key], np.float64)
-            assert float(np.abs(g.numpy() - ref).max()) <= full_tol * max(float(np.abs(ref).max()), floor), n
+            assert float(np.abs(g.numpy() - ref).max()) <= (max(full_tol, ntol) if g.numel() == 1 else full_tol) * max(float(np.abs(ref).max()), floor), n
     return worst
 
 

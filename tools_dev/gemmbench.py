@@ -1,4 +1,6 @@
-"""Microbench: MFMA GEMM (csrc/gemm.hip) vs hipBLASLt (torch) on the hot path's shapes."""
+"""Microbench: MFMA GEMM (csrc/gemm.hip, csrc/gemm_fast.hip) vs hipBLASLt (torch) on the hot
+path's shapes, including the decoder's fp32 1x1 convolutions at batch 32 (forward, data
+gradient, batch-reduced weight gradient) and the adapter projections."""
 import os
 import sys
 
@@ -22,21 +24,32 @@ def bench(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
-cases = [
-    # (name, dtype, M, N, K, a_t, b_t)   a_t: A stored [K][M]; b_t: B stored [N][K]
-    ("siglip qkv", torch.bfloat16, 32768, 3072, 1024, False, True),
-    ("siglip fc1", torch.bfloat16, 32768, 4096, 1024, False, True),
-    ("siglip fc2", torch.bfloat16, 32768, 1024, 4096, False, True),
-    ("siglip o", torch.bfloat16, 32768, 1024, 1024, False, True),
-    ("dec b2 mlp W1.x (fp32)", torch.float32, 2048, 1024, 512, False, False),
-    ("adapter qkv (fp32)", torch.float32, 32768, 3072, 1024, False, True),
-    ("dec b5 1x1 W.x (bf16)", torch.bfloat16, 512, 65536, 128, False, False),
-]
-for name, dt, M, N, K, a_t, b_t in cases:
-    A = torch.randn(K, M, device="cuda").to(dt).t() if a_t else torch.randn(M, K, device="cuda").to(dt)
-    B = torch.randn(N, K, device="cuda").to(dt).t() if b_t else torch.randn(K, N, device="cuda").to(dt)
-    fl = 2.0 * M * N * K
-    th = bench(lambda: gemm_hip.gemm(A, B))
-    tt = bench(lambda: A @ B)
-    print(f"{name:28s} M={M} N={N} K={K}: hip {th:.3f} ms {fl / th / 1e9:7.1f} TF/s | torch {tt:.3f} ms "
-          f"{fl / tt / 1e9:7.1f} TF/s", flush=True)
+def row(name, fl, fh, ft):
+    th, tt = bench(fh), bench(ft)
+    print(f"{name:34s} hip {th:7.3f} ms {fl / th / 1e9:7.1f} TF/s | torch {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF/s",
+          flush=True)
+
+
+dev = "cuda"
+for name, dt, M, N, K in [("siglip qkv bf16", torch.bfloat16, 32768, 3072, 1024),
+                          ("siglip fc2 bf16", torch.bfloat16, 32768, 1024, 4096),
+                          ("adapter qkv fp32", torch.float32, 32768, 3072, 1024)]:
+    A = torch.randn(M, K, device=dev).to(dt)
+    W = torch.randn(N, K, device=dev).to(dt)
+    row(name, 2.0 * M * N * K, lambda: gemm_hip.gemm(A, W.t(), cache_b=True), lambda: A @ W.t())
+
+# decoder fp32 1x1 convs at batch 32: (O, I, P) per block
+for name, O, I, P in [("b2 W1 (512->2048 @32^2)", 2048, 512, 1024), ("b2 W2 (2048->512 @32^2)", 512, 2048, 1024),
+                      ("b1 W1 (512->2048 @16^2)", 2048, 512, 256), ("b0 W1 (512->2048 @8^2)", 2048, 512, 64)]:
+    Bn = 32
+    W = torch.randn(O, I, device=dev)
+    x = torch.randn(Bn, I, P, device=dev)
+    dy = torch.randn(Bn, O, P, device=dev)
+    fl = 2.0 * Bn * O * I * P
+    row(f"fwd  {name}", fl, lambda: gemm_hip.gemm(W, x, cache_a=True), lambda: torch.bmm(W.expand(Bn, O, I), x))
+    row(f"dx   {name}", fl, lambda: gemm_hip.gemm(W.t(), dy, cache_a=True),
+        lambda: torch.bmm(W.t().expand(Bn, I, O), dy))
+    sp = max(1, min(-(-1024 // (-(-O // 128) * -(-I // 128) * Bn)), P // 512, 64))
+    row(f"dW   {name} (splits {sp})", fl,
+        lambda: gemm_hip.gemm(dy, x.transpose(1, 2), out_dtype=torch.float32, reduce_batch=True, splits=sp),
+        lambda: torch.bmm(dy, x.transpose(1, 2)).sum(0))

@@ -55,6 +55,7 @@ for s in "$@"; do
                env $cfg timeout -k 10 300 python tools_dev/graph_c1_debug5.py 2>&1 | grep flags >> $out/gc6.log || break; done ;;
     gc7)     for cfg in "PART=synthesis HIPBLASLT_WORKSPACE_SIZE=0" "PART=synthesis TORCH_BLAS_PREFER_HIPBLASLT=0" "PART=synthesis VFM_GEMM=torch"; do
                env $cfg timeout -k 10 300 python tools_dev/graph_c1_debug5.py 2>&1 | grep flags | sed "s/^/$cfg: /" >> $out/gc7.log || break; done ;;
+    dhead)   timeout -k 10 300 python tools_dev/dhead_debug.py > $out/dhead.log 2>&1 && SPY_MODE=torch_out timeout -k 10 300 python tools_dev/dhead_debug.py > $out/dhead2.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from torch_utils import distributed as dist
+from torch_utils.ops.linear import Linear, linear
 from networks.utils.kl_utils import DiagonalGaussianDistribution
 from networks.utils.quant_utils import VectorQuantizerM
 from networks.utils.dataclasses import EncodeOutput
@@ -57,7 +58,7 @@ class PlainAttention(nn.Module):
         super().__init__()
         width = in_dim if in_dim > out_dim else out_dim
         self.head_dim = width // num_heads
-        self.qkv = nn.Linear(in_dim, width * 3, bias=False)
+        self.qkv = Linear(in_dim, width * 3, bias=False)
         self.q_bias = nn.Parameter(torch.zeros(width))
         self.v_bias = nn.Parameter(torch.zeros(width))
         self.register_buffer('zero_k_bias', torch.zeros(width))
@@ -65,12 +66,12 @@ class PlainAttention(nn.Module):
         self.out_dim = out_dim
         self.num_heads = num_heads
         self.scale = self.head_dim ** -0.5
-        self.proj = nn.Linear(out_dim, out_dim)
+        self.proj = Linear(out_dim, out_dim)
 
     def forward(self, x):
         B, N, C = x.shape
         bias = torch.cat((self.q_bias, self.zero_k_bias, self.v_bias))
-        qkv = F.linear(x, self.qkv.weight, bias)
+        qkv = linear(x, self.qkv.weight, bias)
         q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
         x = F.scaled_dot_product_attention(q, k, v)                          # [B, h, N, d]
         if self.in_dim > self.out_dim:
@@ -87,9 +88,9 @@ class GeGluMlp(nn.Module):
         super().__init__()
         self.norm = nn.LayerNorm(in_features, eps=1e-6)
         self.act = nn.GELU(approximate='tanh')
-        self.w0 = nn.Linear(in_features, hidden_features)
-        self.w1 = nn.Linear(in_features, hidden_features)
-        self.w2 = nn.Linear(hidden_features, in_features)
+        self.w0 = Linear(in_features, hidden_features)
+        self.w1 = Linear(in_features, hidden_features)
+        self.w2 = Linear(hidden_features, in_features)
 
     def forward(self, x):
         x = self.norm(x)
@@ -104,7 +105,7 @@ class AttnProjectionBlock(nn.Module):
         self.out_dim = out_dim
         self.norm1 = norm_layer(in_dim)
         self.attn = PlainAttention(in_dim, out_dim, num_heads)
-        self.proj = nn.Linear(in_dim, out_dim)
+        self.proj = Linear(in_dim, out_dim)
         self.norm3 = norm_layer(in_dim)
         self.norm2 = norm_layer(out_dim)
         self.mlp = GeGluMlp(in_features=out_dim, hidden_features=int(out_dim * mlp_ratio))

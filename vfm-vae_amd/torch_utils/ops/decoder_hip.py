@@ -148,7 +148,7 @@ def _gemm(A, B, **kw):
     if not _USE_HIP_GEMM:
         return None
     from . import gemm_hip
-    return gemm_hip.try_gemm(A, B, **kw)
+    return gemm_hip.try_gemm(A, B, auto=True, **kw)
 
 
 def weight_grad_1x1(dy, x, wdt):
@@ -179,7 +179,7 @@ class _Pointwise(torch.autograd.Function):
         wc = _cast_cached(w, x.dtype)
         ctx.save_for_backward(wc, x)
         ctx.wdt = w.dtype
-        y = _gemm(wc, x)
+        y = _gemm(wc, x, cache_a=True)
         return y if y is not None else torch.bmm(wc.expand(B, O, I), x)
 
     @staticmethod
@@ -194,7 +194,7 @@ class _Pointwise(torch.autograd.Function):
             # sum_b dy[b] @ x[b]^T with fp32 per-sample products, summed in fp32
             dw = weight_grad_1x1(dy, x, ctx.wdt)
         if _wanted(ctx, 1):
-            dx = _gemm(wc.t(), dy)
+            dx = _gemm(wc.t(), dy, cache_a=True)
             if dx is None:
                 dx = torch.bmm(wc.t().expand(B, I, O), dy)
         return dw, dx

@@ -38,8 +38,52 @@ def _layout(t, kdim_last):
     return None
 
 
+FAST = True                 # large-tile LDS-DMA kernel where it applies
+FAST_MIN_MN = 1 << 18       # below ~256k outputs the 128-tile kernel fills the chip better
+
+
+def _split3(t3, R, K, kc, ld, sb, role, cache, stream):
+    """bf16 [hi|hi|lo] (role 0) / [hi;lo;hi] (role 1) copy of an fp32 operand view t3 [z, R, K]
+    (kc: K-contiguous) -> (tensor, kcont, ld, batch stride) in the split layout; cached on the
+    tensor's storage owner until its version moves when `cache` (parameters)."""
+    z = t3.shape[0] if sb else 1
+    key = None
+    if cache:
+        base = t3._base if t3._base is not None else t3
+        key = (t3.data_ptr(), tuple(t3.shape), t3.stride(), base._version, role)
+        hit = getattr(base, "_vfm_split3", None)
+        if hit is not None and hit[0] == key and not torch.cuda.is_current_stream_capturing():
+            return hit[1]
+    if kc:
+        dst = torch.empty((z, R, 3 * K), dtype=torch.bfloat16, device=t3.device)
+        res = (dst, True, 3 * K, R * 3 * K if sb else 0)
+    else:
+        dst = torch.empty((z, 3 * K, R), dtype=torch.bfloat16, device=t3.device)
+        res = (dst, False, R, 3 * K * R if sb else 0)
+    rc = _lib.vfm_split3(t3.data_ptr(), dst.data_ptr(), R, K, ld, sb, res[3], z, role, int(kc), stream)
+    if rc == custom_ops.VFM_NO_KERNEL:
+        return None, None, None, None
+    custom_ops.check(rc, "vfm_split3")
+    if key is not None and not torch.cuda.is_current_stream_capturing():
+        try:
+            base._vfm_split3 = (key, res)
+        except AttributeError:
+            pass
+    return res
+
+
+def preferred(A, M, N, reduce_batch=False):
+    """Where this kernel family beats hipBLASLt (tools_dev/gemmbench.py, MI355X): fp32 operands
+    (the 3-term split runs 1.5-1.9x hipBLASLt's fp32 MFMA GEMMs at >= 128-wide tiles, and the
+    batch-reduced weight gradients at any width). bf16 operands stay on hipBLASLt for now
+    (0.69-0.88 PF/s here vs 1.2-1.45 PF/s)."""
+    if A.dtype != torch.float32:
+        return False
+    return reduce_batch or (M >= 128 and N >= 128)
+
+
 def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=0.0, out_dtype=None,
-             splits=1, reduce_batch=False):
+             splits=1, reduce_batch=False, cache_a=False, cache_b=False, auto=False):
     """C = epi(alpha * A @ B + beta * out). A: [M, K] or [z, M, K]; B: [K, N] or [z, K, N]
     (any strides with one unit-stride dim each). bias: fp32 [N] (bias_dim=1) or [M]
     (bias_dim=0). Returns C ([M, N] / [z, M, N], or [M, N] when reduce_batch sums over z),
@@ -55,6 +99,15 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     K2, N = b3.shape[1], b3.shape[2]
     if K != K2:
         raise RuntimeError(f"gemm: inner dims differ ({K} vs {K2})")
+    if auto and not preferred(A, M, N, reduce_batch):
+        return None
+    if auto and splits == 1:
+        # few output tiles over a deep reduction (weight gradients of token-major linears):
+        # split K so the grid covers the 256 CUs several times
+        z0 = max(a3.shape[0], b3.shape[0]) if not reduce_batch else max(a3.shape[0], b3.shape[0])
+        tiles = -(-M // 128) * -(-N // 128) * z0
+        if tiles < 512 and K >= 2048:
+            splits = max(1, min(-(-1024 // tiles), K // 512, 64))
     la = _layout(a3, True)                       # A rows = m, cols = k
     lb = _layout(b3.transpose(1, 2), True)       # B^T rows = n, cols = k
     if la is None or lb is None:
@@ -80,11 +133,32 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     if bias is not None:
         bias = bias.detach().float().contiguous()
         bias_mode = 1 if bias_dim in (None, 1) else 2
+    flops = 2.0 * z * M * N * K
+    stream = custom_ops.stream_ptr(A.device)
+    if FAST and splits <= 1 and not reduce_batch and K % 64 == 0 and M * N >= FAST_MIN_MN:
+        # large tiles + LDS-DMA pipeline (csrc/gemm_fast.hip); fp32 operands as one bf16 GEMM of
+        # depth 3K over their [hi|hi|lo] x [hi;lo;hi] split
+        if A.dtype == torch.float32:
+            Ak, fa_kc, flda, fsA = _split3(a3, M, K, a_kc, lda, sA, 0, cache_a, stream)
+            Bk, fb_kc, fldb, fsB = _split3(b3, N, K, b_kc, ldb, sB, 1, cache_b, stream)
+            if Ak is None or Bk is None:
+                Ak = None
+            Kf = 3 * K
+        else:
+            Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB, Kf = a3, a_kc, lda, sA, b3, b_kc, ldb, sB, K
+        if Ak is not None:
+            tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
+            with kernel_timer.region(f"gemm_fast<{tag}>", 0, flops, "mfma"):
+                rc = _lib.vfm_gemm_fast(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias),
+                                        _CODES[out_dtype], M, N, Kf, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB,
+                                        ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], stream)
+            if rc != custom_ops.VFM_NO_KERNEL:
+                custom_ops.check(rc, "vfm_gemm_fast")
+                return out
     ws = None
     if splits > 1 or reduce_batch:
         n = _lib.vfm_gemm_workspace_floats(M, N, z, splits, int(reduce_batch))
         ws = torch.empty(n, dtype=torch.float32, device=A.device)
-    flops = 2.0 * z * M * N * K
     tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
     with kernel_timer.region(f"gemm<{tag}>", 0, flops, "mfma"):
         rc = _lib.vfm_gemm(A.data_ptr(), B.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(ws),

@@ -16,7 +16,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import gemm_hip
+
+def _gemm():
+    from . import gemm_hip          # loads the kernel library (ROCm tensors only reach here)
+    return gemm_hip
 
 
 def _wanted(ctx, i):
@@ -38,7 +41,7 @@ class _LinearFn(torch.autograd.Function):
         if x2.stride(-1) != 1:
             x2 = x2.contiguous()
         wc = w if w.dtype == x.dtype else w.to(x.dtype)
-        y = gemm_hip.try_gemm(x2, wc.t(), bias=b, bias_dim=1)
+        y = _gemm().try_gemm(x2, wc.t(), bias=b, bias_dim=1, cache_b=True, auto=True)
         if y is None:
             y = F.linear(x2, wc, None if b is None else b.to(x.dtype))
         ctx.save_for_backward(x2, wc)
@@ -55,12 +58,12 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2.contiguous().to(x2.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0] and _wanted(ctx, 0):
-            dx = gemm_hip.try_gemm(dy2, wc)
+            dx = _gemm().try_gemm(dy2, wc, cache_b=True, auto=True)
             if dx is None:
                 dx = dy2 @ wc
             dx = dx.reshape(shape)
         if ctx.needs_input_grad[1] and _wanted(ctx, 1):
-            dw = gemm_hip.try_gemm(dy2.t(), x2, out_dtype=torch.float32)
+            dw = _gemm().try_gemm(dy2.t(), x2, out_dtype=torch.float32, auto=True)
             if dw is None:
                 dw = dy2.t().float() @ x2.float()
             dw = dw.to(wdt)

@@ -365,11 +365,13 @@ def construct_networks(G_kwargs, D_kwargs, device, label_dim=0):
 
 
 def construct_iteration(G, D, G_ema, device, loss_kwargs, G_opt_kwargs, D_opt_kwargs, batch_size,
-                        accumulate_gradients=1, ema_kimg=10.0, ema_rampup=0.05, graph_nograd_forward=True,
+                        accumulate_gradients=1, ema_kimg=10.0, ema_rampup=0.05, graph_nograd_forward=False,
                         bucket_mb=64.0):
     """TotalLoss + optimisers + the TrainingIteration that train.py and bench.py both run.
     graph_nograd_forward: replay the D phase's no-grad generator forward from HIP graphs
-    (training/graphed_forward.py; falls back to eager where capture is not eligible)."""
+    (training/graphed_forward.py). OFF by default: at the full C1 configuration a replay that
+    follows an eager forward run after a decoder weight update reads stale memory
+    (tools_dev/graph_c1_debug*.py), so the D phase runs eagerly."""
     loss = dnnlib.util.construct_class_by_name(device=device, G=G, D=D, **loss_kwargs)
     if graph_nograd_forward and device.type == 'cuda':
         loss.enable_graphed_nograd_forward()
@@ -394,7 +396,7 @@ def training_loop(run_dir='.', training_set_kwargs={}, validation_set_kwargs={},
                   total_kimg=25000, kimg_per_tick=4, image_snapshot_ticks=50, network_snapshot_ticks=50,
                   resume_path=None, resume_kimg=0, resume_discriminator=True, cudnn_benchmark=True, abort_fn=None,
                   progress_fn=None, one_epoch=False, device=None, train_sample_dir=None, wandb_project_name=None,
-                  wandb_run_name=None, max_iterations=None, graph_nograd_forward=True, **_unused):
+                  wandb_run_name=None, max_iterations=None, graph_nograd_forward=False, **_unused):
     device = device or (torch.device('cuda') if torch.cuda.is_available() else torch.device('cpu'))
     start_time = time.time()
     base_seed = random_seed * dist.get_world_size() + dist.get_rank()
