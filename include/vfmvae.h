@@ -208,6 +208,23 @@ int vfm_attention_fwd(const void* q, const void* k, const void* v, void* o, int 
                       const long long* sq, const long long* sk, const long long* sv, const long long* so,
                       float scale, void* stream);
 
+/* fp32 attention with gradients (replaces F.scaled_dot_product_attention on the fp32 paths of the
+ * generator: fusion-adapter AttnProjection, reference networks/utils/ldm_utils.py:55-87, and the
+ * decoder SelfAttention with null key/value, reference networks/utils/gigagan_utils.py:53-91).
+ * q [B, Nq, H, 64], k/v [B, Nk, H, 64] fp32 views, element strides {batch, token, head}, unit
+ * stride on the head dim, strides multiples of 4, pointers 16-B aligned. Products run on bf16
+ * MFMA through a 3-term hi/lo split (relative error per product <= ~2^-16, fp32 accumulation).
+ *   fwd: o (strides so) and lse [B, H, Nq] (log2 domain of the scaled scores);
+ *   bwd: dq/dk/dv (own strides) from dout; delta [B, H, Nq] fp32 scratch. */
+int vfm_attention_f32_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int H, int Nq,
+                          int Nk, int head_dim, const long long* sq, const long long* sk, const long long* sv,
+                          const long long* so, float scale, void* stream);
+int vfm_attention_f32_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                          const void* lse, void* delta, void* dq, void* dk, void* dv, int B, int H, int Nq, int Nk,
+                          int head_dim, const long long* sq, const long long* sk, const long long* sv,
+                          const long long* so, const long long* sdo, const long long* sdq, const long long* sdk,
+                          const long long* sdv, float scale, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Dense GEMM on the MFMA cores with a fused epilogue (replaces the hipBLASLt GEMMs behind
  * torch.addmm / torch.bmm for the frozen ViT projections, reference

@@ -82,7 +82,6 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     c, step = bench.build(bench.CONFIG, args.batch, dev, 1)
-    step.loss.enable_graphed_nograd_forward()
     from training.data_synthetic import SyntheticDataset
     pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=0).make_pool(args.batch, dev)
     labels = ['a photo'] * args.batch

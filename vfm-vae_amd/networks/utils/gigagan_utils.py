@@ -10,7 +10,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from torch_utils.ops import decoder_ops
+from torch_utils.ops import decoder_ops, vit_ops
 
 
 def exists(v):
@@ -77,13 +77,7 @@ class SelfAttention(nn.Module):
         nk, nv = (t.to(q.dtype)[None, :, None, :].expand(B, h, 1, d) for t in self.null_kv.unbind(0))
         k = torch.cat([nk, k], dim=2)
         v = torch.cat([nv, v], dim=2)
-        # the fused SDPA kernels (AOTriton mem-efficient, fp32 too) need stride(-1) == 1 on q;
-        # the channel-first GEMM output gives stride P, which silently drops the op to the
-        # math path (explicit [B,h,P,P+1] fp32 scores: 5.4 vs ~1 ms fwd+bwd at P=1024).
-        # The CPU keeps the reference's view layout (and with it torch-CPU's math-path order).
-        if q.is_cuda:
-            q = q.contiguous()
-        out = F.scaled_dot_product_attention(q, k, v)                          # [B, h, P, d]
+        out = vit_ops.sdpa(q, k, v)                                            # [B, h, P, d]
         out = out.permute(0, 1, 3, 2).reshape(B, h * d, H * W)
         return _pointwise(self.to_out, out).reshape(B, C, H, W)
 

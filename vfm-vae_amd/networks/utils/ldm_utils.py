@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from torch_utils import distributed as dist
+from torch_utils.ops import vit_ops
 from torch_utils.ops.linear import Linear, linear
 from networks.utils.kl_utils import DiagonalGaussianDistribution
 from networks.utils.quant_utils import VectorQuantizerM
@@ -73,7 +74,7 @@ class PlainAttention(nn.Module):
         bias = torch.cat((self.q_bias, self.zero_k_bias, self.v_bias))
         qkv = linear(x, self.qkv.weight, bias)
         q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
-        x = F.scaled_dot_product_attention(q, k, v)                          # [B, h, N, d]
+        x = vit_ops.sdpa(q, k, v)                                            # [B, h, N, d]
         if self.in_dim > self.out_dim:
             x = x.mean(dim=1)
             if self.in_dim // self.num_heads != self.out_dim:

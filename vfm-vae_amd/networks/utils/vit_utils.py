@@ -41,7 +41,7 @@ class Attention(nn.Module):
         B, N, D = x.shape
         qkv = vit_ops.linear(x, self.qkv.weight.to(x.dtype), self.qkv.bias)
         q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
-        o = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, N, D)
+        o = vit_ops.sdpa(q, k, v).transpose(1, 2).reshape(B, N, D)
         return vit_ops.linear(o, self.proj.weight.to(x.dtype), self.proj.bias)
 
 

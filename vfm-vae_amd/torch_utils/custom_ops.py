@@ -63,6 +63,10 @@ SIGNATURES = {
                  c_ll, c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_int, c_int, c_vp],
     "vfm_attention_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp, c_llp, c_float,
                           c_vp],
+    "vfm_attention_f32_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp,
+                              c_llp, c_float, c_vp],
+    "vfm_attention_f32_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                              c_int, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_float, c_vp],
 }
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}

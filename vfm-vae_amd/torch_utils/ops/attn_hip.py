@@ -52,3 +52,78 @@ def attention_packed(qkv, heads):
     v5 = qkv.view(B, N, 3, heads, D // heads)
     o = attention(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2])
     return o.view(B, N, D)
+
+
+# ------------------------------------------------------------------------------------------------
+# fp32 attention with gradients (csrc/attention_f32.hip): the generator's fusion-adapter
+# AttnProjection (reference networks/utils/ldm_utils.py:55-87) and decoder SelfAttention with
+# null key/value (reference networks/utils/gigagan_utils.py:53-91), both fp32 and trained.
+
+def _s4(t):
+    """(batch, token, head) strides of a [B, N, H, d] fp32 view the kernel can read in place."""
+    st = t.stride()
+    if st[3] != 1 or any(x % 4 for x in st[:3]) or t.data_ptr() % 16:
+        return None
+    return custom_ops.strides_of([st[0], st[1], st[2]])
+
+
+def _ready(t):
+    s = _s4(t)
+    if s is None:
+        t = t.contiguous()
+        s = _s4(t)
+    return t, s
+
+
+class _Attention32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v):
+        B, Nq, H, d = q.shape
+        Nk = k.shape[1]
+        (q, sq), (k, sk), (v, sv) = _ready(q), _ready(k), _ready(v)
+        o = torch.empty(B, Nq, H, d, dtype=torch.float32, device=q.device)
+        lse = torch.empty(B, H, Nq, dtype=torch.float32, device=q.device)
+        flops = 4 * B * H * Nq * Nk * d
+        with kernel_timer.region(f"attention_fwd<f32x3,{d}>", 4 * (2 * B * Nq * H * d + 2 * B * Nk * H * d), flops,
+                                 "mfma"):
+            rc = _lib.vfm_attention_f32_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+                                            B, H, Nq, Nk, d, sq, sk, sv, _s4(o), float(d) ** -0.5,
+                                            custom_ops.stream_ptr(q.device))
+        custom_ops.check(rc, "vfm_attention_f32_fwd")
+        ctx.save_for_backward(q, k, v, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        B, Nq, H, d = q.shape
+        Nk = k.shape[1]
+        do, sdo = _ready(do)
+        dq = torch.empty(B, Nq, H, d, dtype=torch.float32, device=q.device)
+        dk = torch.empty(B, Nk, H, d, dtype=torch.float32, device=q.device)
+        dv = torch.empty(B, Nk, H, d, dtype=torch.float32, device=q.device)
+        delta = torch.empty(B, H, Nq, dtype=torch.float32, device=q.device)
+        flops = 10 * B * H * Nq * Nk * d          # S and dP recomputed in both passes, dV, dK, dQ
+        with kernel_timer.region(f"attention_bwd<f32x3,{d}>", 4 * 4 * (B * Nq * H * d + B * Nk * H * d), flops,
+                                 "mfma"):
+            rc = _lib.vfm_attention_f32_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(),
+                                            lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                                            dv.data_ptr(), B, H, Nq, Nk, d, _s4(q), _s4(k), _s4(v), _s4(o), sdo,
+                                            _s4(dq), _s4(dk), _s4(dv), float(d) ** -0.5,
+                                            custom_ops.stream_ptr(q.device))
+        custom_ops.check(rc, "vfm_attention_f32_bwd")
+        return dq, dk, dv
+
+
+def supported_f32(q, k, v):
+    return (q.is_cuda and q.dtype == torch.float32 and k.dtype == torch.float32 and v.dtype == torch.float32
+            and q.shape[-1] == HEAD_DIM and k.shape == v.shape and q.shape[0] == k.shape[0]
+            and q.shape[1] == k.shape[1])
+
+
+def sdpa_f32(q, k, v):
+    """F.scaled_dot_product_attention(q, k, v) for fp32 [B, H, N, 64] operands (no mask, default
+    scale), forward and backward on the HIP kernels. Returns [B, H, Nq, 64] (a view of a
+    token-major [B, Nq, H, 64] tensor)."""
+    o = _Attention32.apply(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2))
+    return o.transpose(1, 2)

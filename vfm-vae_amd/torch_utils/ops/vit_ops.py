@@ -84,4 +84,21 @@ def attention_packed(qkv, heads):
         if attn_hip.supported(qkv, d):
             return attn_hip.attention_packed(qkv, heads)
     q, k, v = qkv.reshape(B, N, 3, heads, d).permute(2, 0, 3, 1, 4).unbind(0)
-    return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, N, D)
+    return sdpa(q, k, v).transpose(1, 2).reshape(B, N, D)
+
+
+def sdpa(q, k, v):
+    """F.scaled_dot_product_attention(q, k, v) (no mask, default scale) on [B, H, N, d] operands.
+    fp32 ROCm operands with head dim 64 run the HIP kernels (attn_hip.sdpa_f32, forward and
+    backward: the generator's adapter / decoder attention and the D's DINO tower); the rest is
+    torch SDPA."""
+    if q.is_cuda:
+        if q.dtype == torch.float32:
+            from . import attn_hip
+            if attn_hip.supported_f32(q, k, v):
+                return attn_hip.sdpa_f32(q, k, v)
+        if q.stride(-1) != 1:
+            # AOTriton's fused kernels need stride(-1) == 1 on q (else the math path: an explicit
+            # [B, h, N, N] score tensor)
+            q = q.contiguous()
+    return F.scaled_dot_product_attention(q, k, v)
