@@ -36,6 +36,7 @@ CONFIG = os.path.join(PKG, "configs", "vfm_vae_f16d32_siglip2_stage_0_synthetic.
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 BF16_PEAK_TFLOPS = 2500.0      # dense
+FLOP_TABLE = os.path.join(ROOT, "profiles", "r2_flops.json")
 
 
 def parse_args(argv=None):
@@ -110,6 +111,30 @@ def _log(rank, msg):
     """Progress on stderr (the JSON line is the only stdout output)."""
     if rank == 0:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def step_flops(draws, hits, batch, steps, value):
+    """Step-level MFMA fraction: the timed steps' matrix-work FLOPs (GEMM / conv / attention
+    products, per image, per equivariance outcome of each phase: profiles/r2_flops.json from
+    tools_dev/count_flops.py) x images/s / dense bf16 peak. Each step draws one outcome in its
+    D phase and one in its G phase; the G phase is priced with or without the VFM tower
+    depending on whether it reused the D phase's features."""
+    if not os.path.exists(FLOP_TABLE):
+        return None
+    tab = json.load(open(FLOP_TABLE))
+    if len(draws) != 2 * steps or len(hits) != steps:
+        return {"error": f"{len(draws)} equivariance draws / {len(hits)} steps (expected 2 per step)"}
+    key = lambda v: f"{float(v[0])},{int(bool(v[2]))}"
+    total = 0.0
+    for i in range(steps):
+        vd, vg = draws[2 * i], draws[2 * i + 1]
+        g = tab["G"][key(vg)]
+        total += tab["D"][key(vd)] + (g["1"] if hits[i] and g.get("1") is not None else g["0"])
+    per_img = total / steps
+    achieved = value * per_img / 1e12
+    return {"flops_per_img": round(per_img / 1e12, 4), "unit": "TFLOP/img", "achieved_tflops": round(achieved, 1),
+            "peak_tflops": BF16_PEAK_TFLOPS, "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+            "reuse_steps": int(sum(1 for h in hits if h)), "table": os.path.relpath(FLOP_TABLE, ROOT)}
 
 
 def cpu_baseline(cfg_path, threads):
@@ -194,10 +219,18 @@ def main(argv=None):
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    # equivariance outcomes drawn inside the timed region (+ VFM feature reuse per step), to price
+    # the timed steps from the FLOP table (profiles/r2_flops.json; host-side bookkeeping only)
+    draws, hits = [], []
+    eq_fwd = eqt.forward
+    eqt.forward = lambda *a, **k: draws.append(eq_fwd(*a, **k)) or draws[-1]
+    venc = step.G.vfm_encoder
     kernel_timer.enable(True)
     t0 = time.perf_counter()
     for i in range(args.steps):
+        h0 = getattr(venc, "reuse_hits", 0)
         one(args.warmup + i, cur)
+        hits.append(getattr(venc, "reuse_hits", 0) - h0)
         cur += args.batch * world
         if args.trace:                      # diagnostics only: per-step wall time (synchronising)
             torch.cuda.synchronize()
@@ -208,6 +241,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     kernel_timer.enable(False)
+    eqt.forward = eq_fwd
     _log(rank, f"timed {args.steps} steps: {dt:.2f}s")
     if args.trace:
         ms = torch.cuda.memory_stats(device)
@@ -228,6 +262,7 @@ def main(argv=None):
     roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table)
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
+    step_mfma = step_flops(draws, hits, args.batch, args.steps, value)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -250,6 +285,7 @@ def main(argv=None):
                        "d_phase_g_forward": "hip_graph" if args.graphs else "eager",
                        "gemm_table": tunable["table"] if tunable and tunable["mode"] == "use" else None},
             "roofline": roof,
+            "step_mfma": step_mfma,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -68,11 +68,13 @@ def test_lpips_head_only_target_grad_and_zero_pixel():
 
 @pytest.mark.gpu
 def test_lpips_module_hip_head_matches_torch_head():
-    """Whole LPIPS on cuda:0 with the HIP head vs the same module with the torch head (same
-    MIOpen VGG features, so only the head differs: value 1e-5; the input gradient then runs
-    13 fp32 MIOpen backward convolutions whose solver/accumulation order is not fixed between
-    calls — measured 1.6e-3 in a full-suite run — so 1e-2), and vs the CPU module (1e-4 / 1e-2).
-    The head's own gradient is checked at 1e-4 against fp64 in the tests above."""
+    """Whole LPIPS on cuda:0 with the HIP head vs the same module with the torch head. Both run
+    the same HIP VGG16 stack (torch_utils/ops/vgg_hip.py: fixed accumulation order, so the
+    features and the backward chain are identical) and only the head differs: value 1e-5,
+    input gradient 1e-4 of max. Against the CPU module: value 1e-4; the input gradient in
+    relative L2 norm (1e-2), since the GPU stack's ~2^-16 forward rounding flips the odd ReLU /
+    max-pool decision of the CPU's fp32 stack, which moves single gradient entries by O(their
+    size); the kernels themselves are checked through the same decisions in test_vgg_gpu.py."""
     from training.lpips import LPIPS
     torch.manual_seed(0)
     m = LPIPS().eval()
@@ -92,6 +94,7 @@ def test_lpips_module_hip_head_matches_torch_head():
         res[impl] = (out.detach().cpu(), bg.grad.cpu())
     md.head_impl = "cuda"
     assert _rel(res["cuda"][0], res["ref"][0]) < 1e-5
-    assert _rel(res["cuda"][1], res["ref"][1]) < 1e-2
+    assert _rel(res["cuda"][1], res["ref"][1]) < 1e-4
     assert _rel(res["cuda"][0], ref) < 1e-4
-    assert _rel(res["cuda"][1], bc.grad) < 1e-2
+    l2 = float((res["cuda"][1].double() - bc.grad.double()).norm() / bc.grad.double().norm())
+    assert l2 < 1e-2, l2

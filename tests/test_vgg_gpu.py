@@ -1,0 +1,86 @@
+"""LPIPS VGG16 stack on the HIP implicit-GEMM conv (csrc/conv.hip, torch_utils/ops/vgg_hip.py)
+against fp64 torch convolutions of the same weights: single conv3x3 layers (image layer with
+3 -> 4 padded channels, ragged spatial sizes, the fused ReLU-derivative mask) and the whole
+relu1_2..relu5_3 tap stack forward + input gradient (reference training/lpips.py:126-163).
+
+Tolerance: 3e-5 of max |ref| per conv layer, 2e-4 on the 13-layer taps and 1e-3 on the input
+gradient (the 3-term split carries ~2^-15.5 relative error per product; errors compound over
+the stack)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max())
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 3, 64), (2, 12, 20, 64, 64), (1, 7, 9, 128, 256),
+                                            (3, 8, 8, 512, 512), (2, 33, 5, 256, 128)])
+def test_conv3x3_layer(B, H, W, Cin, Cout):
+    from torch_utils.ops import vgg_hip
+    g = torch.Generator(device=DEV).manual_seed(H * W + Cin)
+    x = torch.randn(B, Cin, H, W, generator=g, device=DEV)
+    conv = torch.nn.Conv2d(Cin, Cout, 3, padding=1).to(DEV)
+    wf, wb, b, w = vgg_hip.prepare([conv])[0]
+    cp = wf.shape[1] // 9
+    xh = torch.zeros(B, H, W, cp, device=DEV)
+    xh[..., :Cin] = x.permute(0, 2, 3, 1)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).relu()
+    y = vgg_hip.conv3x3(xh, wf, b, relu=True)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 3e-5
+    if Cin >= 64:
+        # data gradient with the layer-below mask, as the backward runs it
+        dz = torch.randn(B, H, W, Cout, generator=g, device=DEV)
+        mask = torch.randn(B, H, W, Cin, generator=g, device=DEV)
+        gx = vgg_hip.conv3x3(dz, wb, None, relu=False, mask=mask)
+        ref = torch.nn.grad.conv2d_input((B, Cin, H, W), w.double(), dz.permute(0, 3, 1, 2).double(), padding=1)
+        ref = ref * (mask.permute(0, 3, 1, 2) > 0)
+        assert _rel(gx.permute(0, 3, 1, 2), ref) < 3e-5
+
+
+def _conv64(x, w, bias=None, relu=False, mask=None):
+    """fp64 torch stand-in for vgg_hip.conv3x3 (same NHWC / tap-major conventions)."""
+    B, H, W, Cin = x.shape
+    y = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double().reshape(w.shape[0], 3, 3, Cin).permute(0, 3, 1, 2),
+                 None if bias is None else bias.double(), padding=1)
+    y = (y.relu() if relu else y).permute(0, 2, 3, 1)
+    return (y * (mask > 0) if mask is not None else y).contiguous()
+
+
+@pytest.mark.parametrize("res", [64, 48])
+def test_vgg16_taps_forward_backward(res):
+    """Taps vs an independent fp64 stack; the input gradient vs the fp64 backward chain taken
+    through the same ReLU masks and pool choices (a 2^-16 forward difference flips the odd ReLU
+    or max-pool decision of an fp64 stack, which moves single gradient entries by O(1) of their
+    size -- that comparison is made in relative L2 norm instead)."""
+    from training.lpips import vgg16
+    from torch_utils.ops import vgg_hip
+    net = vgg16(pretrained=False).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(res)
+    x = torch.randn(2, 3, res, res, generator=g, device=DEV).requires_grad_(True)
+    outs = net(x)
+    gs = [torch.randn(o.shape, generator=g, device=DEV) for o in outs]
+    torch.autograd.backward(list(outs), gs)
+    ref_net = vgg16(pretrained=False).to(DEV).double()
+    ref_net.load_state_dict(net.state_dict())
+    xr = x.detach().double().requires_grad_(True)
+    h, refs = xr, []
+    for k in range(1, 6):
+        h = getattr(ref_net, f"slice{k}")(h)
+        refs.append(h)
+    torch.autograd.backward(refs, [t.double() for t in gs])
+    for o, r in zip(outs, refs):
+        assert o.shape == r.shape
+        assert _rel(o, r) < 2e-4
+    convs = [m for k in range(1, 6) for m in getattr(net, f"slice{k}") if isinstance(m, torch.nn.Conv2d)]
+    prep = vgg_hip.prepare(convs)
+    _, ys, pools = vgg_hip.forward_chain(x.detach(), prep)
+    gx = vgg_hip.backward_chain([y.double() for y in ys], pools, prep, x.shape, [t.double() for t in gs],
+                                conv=_conv64)
+    assert _rel(x.grad, gx) < 1e-4
+    l2 = float((x.grad.double() - xr.grad).norm() / xr.grad.norm())
+    assert l2 < 2e-2, l2

@@ -1,0 +1,242 @@
+// 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA cores, fp32 through the
+// 3-term bf16 split (the LPIPS VGG16 stack: reference training/lpips.py:126-163, run in fp32 by
+// the reference; MIOpen's fp32 Winograd was the single largest kernel of the training step).
+//
+//   out[p, n] = epi( sum_{tap, c} x[p + shift(tap), c] * w[n, tap, c] ),   p = (b, y, x) pixels,
+//   epi: + bias[n], ReLU, and/or x (mask[p, n] > 0) (the ReLU derivative of the layer below, for
+//   the data-gradient pass), fp32 out.
+//
+// Layout: activations NHWC fp32 ([B, H, W, C] contiguous: channels_last), weights [Cout][9][Cin]
+// fp32 (tap-major, channels contiguous). Cin is a power of two >= 4 (the 3-channel image is
+// padded to 4), Cout a multiple of 64. The data gradient of the same conv is this kernel with the
+// flipped, transposed weights w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
+//
+// GEMM view: M = B*H*W pixels, N = Cout, K = 9*Cin (tap-major). Tile 128 pixels x BN (128 or 64)
+// couts x 64 k, 4 waves (2 x 2), 32x32x16 bf16 MFMA, fp32 operands split into hi/lo images on
+// the way into LDS (gemm.hip's f32x3; error per product <= ~2^-15.5 relative). The A loader is
+// implicit: each thread owns 8 pixel rows and one 4-channel column of the tile; a k-tile (64
+// channels of one tap, or for Cin < 64 several taps) becomes one 16-B load per row at
+// (p + dy*W + dx)*Cin + c, zero outside the image. The 9 shifted reads of a pixel hit L2.
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 128, BK = 64, THREADS = 256;
+constexpr int IMG_A = BM * BK * 2;   // bytes of one bf16 image of the A tile
+
+struct ConvArgs {
+    const float* x;      // [B, H, W, Cin]
+    const float* w;      // [Cout, 9 * Cin]
+    const float* bias;   // [Cout] or null
+    const float* mask;   // [B, H, W, Cout] or null
+    float* out;          // [B, H, W, Cout]
+    int M, H, W, Cin, lc, Cout, K;
+    FastDiv fW, fH;
+    int relu;
+};
+
+__device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
+
+__device__ __forceinline__ uint32_t bf16_bits(float v) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(v));
+}
+__device__ __forceinline__ float bf16_val(uint32_t bits) { return __uint_as_float(bits << 16); }
+
+// 4 fp32 (one uint4) -> hi/lo halves of a 16-B image chunk
+__device__ __forceinline__ void put4(unsigned char* hi, unsigned char* lo, int off, uint4 r) {
+    const float x[4] = {__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z), __uint_as_float(r.w)};
+    uint32_t hb[4], lb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        hb[e] = bf16_bits(x[e]);
+        lb[e] = bf16_bits(x[e] - bf16_val(hb[e]));
+    }
+    *reinterpret_cast<uint2*>(hi + off) = make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
+    *reinterpret_cast<uint2*>(lo + off) = make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
+}
+
+// thread -> (row = tid/16 + 16u, 4-element column tid%16) of a [rows][64] fp32 tile
+struct StageA {
+    uint4 r[8];
+    int pm[8];    // pixel index (or -1)
+    int pyx[8];   // y << 16 | x
+    __device__ __forceinline__ void init(const ConvArgs& a, int m0, int tid) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int m = m0 + tid / 16 + 16 * u;
+            if (m < a.M) {
+                const uint32_t q = fdiv((uint32_t)m, a.fW);
+                const int xx = m - (int)q * a.W;
+                const int yy = (int)q - (int)fdiv(q, a.fH) * a.H;
+                pm[u] = m;
+                pyx[u] = (yy << 16) | xx;
+            } else {
+                pm[u] = -1;
+                pyx[u] = 0;
+            }
+        }
+    }
+    __device__ __forceinline__ void load(const ConvArgs& a, int k0, int tid) {
+        const int k = k0 + 4 * (tid & 15);
+        const int tap = k >> a.lc, c = k & (a.Cin - 1);
+        const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
+        const bool tap_ok = tap < 9;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int yy = (pyx[u] >> 16) + dy, xx = (pyx[u] & 0xffff) + dx;
+            const bool ok = tap_ok && pm[u] >= 0 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+            r[u] = ok ? *reinterpret_cast<const uint4*>(a.x + (long long)(pm[u] + dy * a.W + dx) * a.Cin + c)
+                      : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
+        const int cc = tid & 15;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) put4(hi, lo, kc_off(tid / 16 + 16 * u, cc >> 1) + 8 * (cc & 1), r[u]);
+    }
+};
+
+template <int ROWS>
+struct StageB {
+    static constexpr int PER = ROWS / 16;
+    uint4 r[PER];
+    __device__ __forceinline__ void load(const ConvArgs& a, int n0, int k0, int tid) {
+        const int k = k0 + 4 * (tid & 15);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int n = n0 + tid / 16 + 16 * u;
+            r[u] = (k < a.K && n < a.Cout) ? *reinterpret_cast<const uint4*>(a.w + (long long)n * a.K + k)
+                                           : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
+        const int cc = tid & 15;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) put4(hi, lo, kc_off(tid / 16 + 16 * u, cc >> 1) + 8 * (cc & 1), r[u]);
+    }
+};
+
+__device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int s, int lane) {
+    return *reinterpret_cast<const bf16x8*>(img + kc_off(32 * blk + (lane & 31), 2 * s + (lane >> 5)));
+}
+
+template <int BN>
+__global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
+    constexpr int NJ = BN / 64;                 // 32-col blocks per wave
+    constexpr int IMG_B = BN * BK * 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* a_hi = lds;
+    unsigned char* a_lo = lds + IMG_A;
+    unsigned char* b_hi = lds + 2 * IMG_A;
+    unsigned char* b_lo = lds + 2 * IMG_A + IMG_B;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int tiles_n = a.Cout / BN;
+    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+
+    StageA sa;
+    StageB<BN> sb;
+    sa.init(a, m0, tid);
+    f32x16 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
+
+    sa.load(a, 0, tid);
+    sb.load(a, n0, 0, tid);
+    for (int k0 = 0; k0 < a.K; k0 += BK) {
+        sa.store(a_hi, a_lo, tid);
+        sb.store(b_hi, b_lo, tid);
+        __syncthreads();
+        if (k0 + BK < a.K) {
+            sa.load(a, k0 + BK, tid);
+            sb.load(a, n0, k0 + BK, tid);
+        }
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {
+            bf16x8 ah[2], al[2], bh[NJ], bl[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ah[i] = frag(a_hi, 2 * wm + i, s, lane);
+                al[i] = frag(a_lo, 2 * wm + i, s, lane);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                bh[j] = frag(b_hi, NJ * wn + j, s, lane);
+                bl[j] = frag(b_lo, NJ * wn + j, s, lane);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+
+    // acc[i][j][e] = out[m][n], m = m0 + 64wm + 32i + (e&3) + 8(e>>2) + 4hh, n = n0 + 32(NJ wn + j) + r
+    const int r = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + 32 * (NJ * wn + j) + r;
+        const float bn = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m0 + 64 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * hh;
+                if (m >= a.M) continue;
+                const long long o = (long long)m * a.Cout + n;
+                float v = acc[i][j][e] + bn;
+                if (a.relu) v = fmaxf(v, 0.f);
+                if (a.mask && !(a.mask[o] > 0.f)) v = 0.f;
+                a.out[o] = v;
+            }
+    }
+}
+
+template <int BN>
+int launch(const ConvArgs& a, hipStream_t st) {
+    const size_t lds = 2 * IMG_A + 2 * BN * BK * 2;
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)conv3x3_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    const long long tiles = (long long)((a.M + BM - 1) / BM) * (a.Cout / BN);
+    if (tiles > 0x7fffffff) return VFM_ERR_ARGS;
+    hipLaunchKernelGGL(conv3x3_kernel<BN>, dim3((unsigned)tiles), dim3(THREADS), lds, st, a);
+    return launch_status();
+}
+
+}  // namespace
+
+extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const float* w, const float* bias, const float* mask, float* out,
+                                    int B, int H, int W, int Cin, int Cout, int relu, void* stream) {
+    if (!x || !w || !out || B <= 0 || H <= 0 || W <= 0 || H > 32767 || W > 32767) return VFM_ERR_ARGS;
+    if (Cin < 4 || (Cin & (Cin - 1)) || Cout <= 0 || Cout % 64) return VFM_NO_KERNEL;
+    if (((uintptr_t)x | (uintptr_t)w) % 16) return VFM_ERR_ARGS;
+    const long long M = (long long)B * H * W;
+    if (M * (long long)(Cin > Cout ? Cin : Cout) >= (1ll << 40) || M >= (1ll << 31) - 2 * (long long)W - 2)
+        return VFM_ERR_ARGS;
+    ConvArgs a;
+    a.x = x; a.w = w; a.bias = bias; a.mask = mask; a.out = out;
+    a.M = (int)M; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.K = 9 * Cin;
+    a.lc = 0;
+    while ((1 << a.lc) < Cin) ++a.lc;
+    a.fW = make_fastdiv((uint32_t)W);
+    a.fH = make_fastdiv((uint32_t)H);
+    a.relu = relu;
+    hipStream_t st = (hipStream_t)stream;
+    return (Cout % 128 == 0) ? launch<128>(a, st) : launch<64>(a, st);
+}

@@ -1,0 +1,168 @@
+"""LPIPS VGG16 feature stack on the HIP implicit-GEMM convolution (csrc/conv.hip).
+
+Replaces the torchvision `vgg16().features[:30]` forward/backward of the reference's LPIPS
+(training/lpips.py:126-163; MIOpen fp32 Winograd on ROCm) with 13 fused conv3x3 + bias + ReLU
+launches on NHWC fp32 activations (fp32 products through the 3-term bf16 split, error per
+product <= ~2^-15.5 relative), torch max-pool on the channels_last views, and a backward that
+runs the data gradients on the same kernel with flipped/transposed weights, the ReLU derivative
+of the layer below fused into the epilogue where no pool sits in between. VGG is frozen: no
+weight gradients.
+
+`vgg16_taps(x, convs)` returns the five LPIPS taps (relu1_2, relu2_2, relu3_3, relu4_3,
+relu5_3) as NCHW-shaped views of NHWC tensors.
+"""
+import torch
+import torch.nn.functional as F
+
+from .. import custom_ops
+from . import kernel_timer
+
+_lib = custom_ops.get_native()
+
+# torchvision vgg16 cfg D up to relu5_3: conv channels, 'M' pool; taps after these conv indices
+_CFG = [64, 64, 'M', 128, 128, 'M', 256, 256, 256, 'M', 512, 512, 512, 'M', 512, 512, 512]
+_TAPS = (1, 3, 6, 9, 12)          # conv ordinal (0-based) whose ReLU output is a tap
+
+
+def _plan():
+    ops, ci = [], 0
+    for v in _CFG:
+        if v == 'M':
+            ops.append(('pool',))
+        else:
+            ops.append(('conv', ci))
+            if ci in _TAPS:
+                ops.append(('tap', _TAPS.index(ci)))
+            ci += 1
+    return ops
+
+
+PLAN = _plan()
+
+
+def conv3x3(x, w, bias=None, relu=False, mask=None):
+    """x: NHWC fp32 [B, H, W, Cin] contiguous; w: [Cout, 9*Cin] fp32 (tap-major) -> [B, H, W, Cout]
+    = relu?(conv(x) + bias) (x (mask > 0) when given)."""
+    B, H, W, Cin = x.shape
+    Cout = w.shape[0]
+    if not x.is_contiguous() or w.shape[1] != 9 * Cin or (mask is not None and mask.shape != (B, H, W, Cout)):
+        raise RuntimeError("conv3x3: NHWC contiguous input, [Cout, 9*Cin] weights, mask of the output shape")
+    out = torch.empty(B, H, W, Cout, dtype=torch.float32, device=x.device)
+    flops = 2 * B * H * W * Cout * 9 * Cin
+    with kernel_timer.region(f"conv3x3_nhwc<f32x3,{Cin},{Cout}>", 4 * (x.numel() + out.numel() + w.numel()), flops,
+                             "mfma"):
+        rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), w.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(mask),
+                                       out.data_ptr(), B, H, W, Cin, Cout, int(relu), custom_ops.stream_ptr(x.device))
+    custom_ops.check(rc, "vfm_conv3x3_nhwc_f32")
+    return out
+
+
+def prepare(convs):
+    """Per nn.Conv2d: forward weights [Cout, 9*Cin'] (Cin' = Cin padded to 4 for the image layer),
+    data-gradient weights [Cin, 9*Cout] (flipped taps), bias; cached on the module until the
+    weight's version moves."""
+    out = []
+    for m in convs:
+        key = (m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version)
+        hit = getattr(m, "_vfm_vgg_prep", None)
+        if hit is None or hit[0] != key:
+            w = m.weight.detach().float()
+            Cout, Cin = w.shape[:2]
+            cp = max(Cin, 4)
+            wf = torch.zeros(Cout, 3, 3, cp, dtype=torch.float32, device=w.device)
+            wf[..., :Cin] = w.permute(0, 2, 3, 1)
+            wb = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9 * Cout).contiguous()
+            hit = (key, (wf.reshape(Cout, 9 * cp).contiguous(), wb, m.bias.detach().float().contiguous(), w))
+            m._vfm_vgg_prep = hit
+        out.append(hit[1])
+    return out
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2)
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def forward_chain(x, prep):
+    """(taps, ReLU outputs, pool indices) of the stack on x (NCHW fp32): taps / outputs NHWC."""
+    B, C, H, W = x.shape
+    h = torch.zeros(B, H, W, 4, dtype=torch.float32, device=x.device)
+    h[..., :C] = x.permute(0, 2, 3, 1)
+    ys, pools, taps = [], [], []
+    for op in PLAN:
+        if op[0] == 'conv':
+            wf, _, b, _ = prep[op[1]]
+            h = conv3x3(h, wf, b, relu=True)
+            ys.append(h)
+        elif op[0] == 'tap':
+            taps.append(h)
+        else:
+            p, idx = F.max_pool2d(_nchw(h), 2, 2, return_indices=True)
+            pools.append(idx)
+            h = _nhwc(p)
+    return taps, ys, pools
+
+
+class _VGG16Taps(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, prep):
+        taps, ys, pools = forward_chain(x, prep)
+        ctx.prep = prep
+        ctx.in_shape = x.shape
+        if ctx.needs_input_grad[0]:
+            ctx.save_for_backward(*ys, *pools)
+        return tuple(_nchw(t) for t in taps)
+
+    @staticmethod
+    def backward(ctx, *gtaps):
+        saved = ctx.saved_tensors
+        return backward_chain(saved[:13], saved[13:], ctx.prep, ctx.in_shape, gtaps), None
+
+
+def backward_chain(ys, pools, prep, in_shape, gtaps, conv=None):
+    """Input gradient of the tap stack from the saved ReLU outputs `ys`, pool indices and tap
+    gradients. `conv` (default conv3x3) runs every data-gradient conv; tests pass an fp64 torch
+    conv to check the kernels against the same ReLU / pool decisions."""
+    conv = conv or conv3x3
+    g = None           # gradient wrt the current NHWC activation (walking the plan backwards)
+    masked = False     # g already carries the ReLU derivative of the conv that produced it
+    pi = len(pools)
+    for at in range(len(PLAN) - 1, -1, -1):
+        op = PLAN[at]
+        if op[0] == 'tap':
+            gt = gtaps[op[1]]
+            if gt is not None:
+                gt = _nhwc(gt)
+                g = gt if g is None else g + gt
+                masked = False
+        elif op[0] == 'pool':
+            pi -= 1
+            g = _nhwc(torch.ops.aten.max_pool2d_with_indices_backward(
+                _nchw(g), _nchw(_pool_input(ys, pi)), [2, 2], [2, 2], [0, 0], [1, 1], False, pools[pi]))
+            masked = False
+        elif g is not None:
+            ci = op[1]
+            if not masked:
+                g = g * (ys[ci] > 0)
+            _, wb, _, w = prep[ci]
+            if ci == 0:
+                return torch.nn.grad.conv2d_input(in_shape, w.to(g.dtype), _nchw(g), padding=1)
+            # the op before is conv ci-1 (taps are always followed by a pool): fuse its ReLU derivative
+            fuse = PLAN[at - 1][0] == 'conv'
+            g = conv(g, wb, None, relu=False, mask=ys[ci - 1] if fuse else None)
+            masked = fuse
+    return None
+
+
+def _pool_input(ys, pool_index):
+    """NHWC input of the pool_index-th pool: the output of the conv right before it."""
+    convs_before = [1, 3, 6, 9][pool_index]
+    return ys[convs_before]
+
+
+def vgg16_taps(x, convs):
+    """x: fp32 NCHW (LPIPS-scaled) on ROCm; convs: the 13 nn.Conv2d of vgg16 features in order."""
+    return _VGG16Taps.apply(x, prepare(convs))

@@ -71,12 +71,20 @@ class vgg16(nn.Module):
             for p in self.parameters():
                 p.requires_grad = False
 
+    # 'hip': fp32 ROCm inputs run the fused NHWC stack (torch_utils/ops/vgg_hip.py); 'torch': MIOpen (A/B)
+    impl = os.environ.get('VFM_LPIPS_VGG', 'hip')
+
     def forward(self, X):
-        outs = []
-        h = X
-        for k in range(1, 6):
-            h = getattr(self, f"slice{k}")(h)
-            outs.append(h)
+        if X.is_cuda and X.dtype == torch.float32 and self.impl == 'hip':
+            from torch_utils.ops import vgg_hip
+            convs = [m for k in range(1, 6) for m in getattr(self, f"slice{k}") if isinstance(m, nn.Conv2d)]
+            outs = vgg_hip.vgg16_taps(X, convs)
+        else:
+            outs = []
+            h = X
+            for k in range(1, 6):
+                h = getattr(self, f"slice{k}")(h)
+                outs.append(h)
         return namedtuple("VggOutputs", ['relu1_2', 'relu2_2', 'relu3_3', 'relu4_3', 'relu5_3'])(*outs)
 
 
