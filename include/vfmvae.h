@@ -324,6 +324,12 @@ int vfm_lpips_head_fwd(const float* f0, const float* f1, const float* w, float* 
                        int B, int C, long long HW, void* stream);
 int vfm_lpips_head_bwd(const float* f0, const float* f1, const float* w, const float* n0, const float* n1,
                        const float* gs, float* g0, float* g1, int B, int C, long long HW, void* stream);
+/* Same head on NHWC (channels_last) taps [B, HW, C], C in {64, 128, 256, 512} (the HIP VGG16
+ * stack's layout; 16-B aligned); r / n0 / n1 / gs as above, g0 / g1 NHWC. */
+int vfm_lpips_head_fwd_nhwc(const float* f0, const float* f1, const float* w, float* r, float* n0, float* n1,
+                            int B, int C, long long HW, void* stream);
+int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, const float* n0, const float* n1,
+                            const float* gs, float* g0, float* g1, int B, int C, long long HW, void* stream);
 
 #ifdef __cplusplus
 }

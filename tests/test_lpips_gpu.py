@@ -23,16 +23,21 @@ def test_head_ref_is_the_reference_expression():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,C,H,W", [(3, 64, 33, 31), (2, 130, 16, 16), (4, 512, 16, 16), (2, 64, 256, 256)])
-def test_lpips_head_matches_reference(B, C, H, W):
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+@pytest.mark.parametrize("B,C,H,W", [(3, 64, 33, 31), (2, 130, 16, 16), (4, 512, 16, 16), (2, 64, 256, 256),
+                                     (2, 256, 9, 7)])
+def test_lpips_head_matches_reference(B, C, H, W, layout):
+    """nhwc: channels_last features (the HIP VGG16 stack's taps) run the NHWC kernels in place
+    (C = 130 is not covered and takes the NCHW kernel through a contiguous copy)."""
     dev = torch.device("cuda:0")
+    fmt = torch.channels_last if layout == "nhwc" else torch.contiguous_format
     g = torch.Generator().manual_seed(B * C + H)
     # ReLU-like features (non-negative, some exact zeros) as the VGG taps are
     f0 = torch.relu(torch.randn(B, C, H, W, generator=g))
     f1 = torch.relu(f0 + 0.3 * torch.randn(B, C, H, W, generator=g))
     w = torch.rand(C, generator=g) / C
-    x0 = f0.to(dev).requires_grad_(True)
-    x1 = f1.to(dev).requires_grad_(True)
+    x0 = f0.to(dev).to(memory_format=fmt).requires_grad_(True)
+    x1 = f1.to(dev).to(memory_format=fmt).requires_grad_(True)
     out = lpips_ops.lpips_head(x0, x1, w.to(dev))
     gout = torch.rand(B, 1, 1, 1, generator=g)
     out.backward(gout.to(dev))

@@ -128,7 +128,8 @@ def test_lpips_gpu(vgg, monkeypatch):
     assert _rel(v.detach().cpu(), _arr("L/val")) < 1e-5
     v.sum().backward()
     torch.cuda.synchronize()
-    _native_ran(kt, "lpips_head_fwd", "lpips_head_bwd", *(["conv3x3_nhwc"] if vgg == "hip" else []))
+    _native_ran(kt, *(["lpips_head_fwd_nhwc", "lpips_head_bwd_nhwc", "conv3x3_nhwc"] if vgg == "hip"
+                      else ["lpips_head_fwd", "lpips_head_bwd"]))
     kt.enable(False)
     if vgg == "hip":
         ref = torch.from_numpy(_arr("L/db")).double()
@@ -187,6 +188,8 @@ def test_total_loss_step_gpu(vfm_dir, graphed, gemm, monkeypatch):
     # tensor-valued gradient stays within 5e-3 of the reference.
     # element-wise, the same amplification reaches 1.4e-2 of max on the 64-px block's GroupNorm
     # weights (gemm='hip'); norms and sums stay within 5e-3
+    # gemm='torch': MIOpen picks its fp32 solvers per run (accumulation order not fixed), which
+    # moves the same scalars by up to 1.3e-2 between runs (measured)
     _check_grads("T/G", G2, norm_tol=5e-3, full_tol=2e-2 if gemm == "hip" else 1e-2, sum_tol=5e-3,
-                 scalar_tol=6e-2 if gemm == "hip" else None)
+                 scalar_tol=6e-2 if gemm == "hip" else 3e-2)
     assert loss._off_done

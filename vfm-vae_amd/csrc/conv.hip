@@ -210,7 +210,7 @@ int launch(const ConvArgs& a, hipStream_t st) {
     const size_t lds = 2 * IMG_A + 2 * BN * BK * 2;
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)conv3x3_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
     const long long tiles = (long long)((a.M + BM - 1) / BM) * (a.Cout / BN);

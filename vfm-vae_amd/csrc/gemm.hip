@@ -294,7 +294,7 @@ int launch(const GemmArgs& a, int batch, hipStream_t st) {
     const size_t lds = (F32 ? 4 : 2) * IMG;
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, F32, OUTF32>,
+        (void)hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, F32, OUTF32>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }

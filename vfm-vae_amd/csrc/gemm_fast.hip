@@ -218,7 +218,7 @@ int launch_fast(const FastArgs& a, int batch, hipStream_t st) {
     const int nwg = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)gemm_fast_kernel<AK, BKC, OUTF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)gemm_fast_kernel<AK, BKC, OUTF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             2 * FSTAGE);
         attr = true;
     }

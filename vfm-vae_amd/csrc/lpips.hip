@@ -117,6 +117,103 @@ __global__ __launch_bounds__(LP_NT) void lpips_head_bwd(const float* __restrict_
 
 int grid_of(long long total) { return (int)((total + LP_NT - 1) / LP_NT); }
 
+// ---------------------------------------------------------------------------------------------
+// NHWC (channels_last) features, as the HIP VGG16 stack produces them (torch_utils/ops/vgg_hip.py):
+// 16 lanes per pixel, lane j holds channels 4j + 64i (i < CH = C/64) as float4 -- each pixel's
+// channel vector is read once, coalesced, and kept in registers for the second pass; the
+// channel sums are 16-lane xor-shuffle reductions. Same arithmetic as the NCHW kernels above.
+template <int CH>
+__device__ __forceinline__ void lp_load(const float* p, int j, float4* v) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) v[i] = *reinterpret_cast<const float4*>(p + 64 * i + 4 * j);
+}
+__device__ __forceinline__ float lp_sum16(float s) {
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) s += __shfl_xor(s, m, 16);
+    return s;
+}
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+template <int CH>
+__global__ __launch_bounds__(LP_NT) void lpips_head_fwd_nhwc(const float* __restrict__ f0, const float* __restrict__ f1,
+                                                             const float* __restrict__ w, float* __restrict__ r,
+                                                             float* __restrict__ n0s, float* __restrict__ n1s,
+                                                             long long total) {
+    constexpr int C = 64 * CH;
+    const long long pix = (long long)blockIdx.x * (LP_NT / 16) + threadIdx.x / 16;
+    const int j = threadIdx.x & 15;
+    if (pix >= total) return;                          // uniform over the pixel's 16 lanes
+    float4 x[CH], y[CH];
+    lp_load<CH>(f0 + pix * C, j, x);
+    lp_load<CH>(f1 + pix * C, j, y);
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) { s0 += dot4(x[i], x[i]); s1 += dot4(y[i], y[i]); }
+    s0 = lp_sum16(s0);
+    s1 = lp_sum16(s1);
+    const float n0 = sqrtf(s0), n1 = sqrtf(s1);
+    const float n0e = n0 + LP_EPS, n1e = n1 + LP_EPS;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + 64 * i + 4 * j);
+        const float d0 = x[i].x / n0e - y[i].x / n1e, d1 = x[i].y / n0e - y[i].y / n1e;
+        const float d2 = x[i].z / n0e - y[i].z / n1e, d3 = x[i].w / n0e - y[i].w / n1e;
+        acc += wv.x * (d0 * d0) + wv.y * (d1 * d1) + wv.z * (d2 * d2) + wv.w * (d3 * d3);
+    }
+    acc = lp_sum16(acc);
+    if (j == 0) {
+        r[pix] = acc;
+        n0s[pix] = n0;
+        n1s[pix] = n1;
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(LP_NT) void lpips_head_bwd_nhwc(const float* __restrict__ f0, const float* __restrict__ f1,
+                                                             const float* __restrict__ w, const float* __restrict__ n0s,
+                                                             const float* __restrict__ n1s, const float* __restrict__ gs,
+                                                             float* __restrict__ g0, float* __restrict__ g1, long long HW,
+                                                             long long total) {
+    constexpr int C = 64 * CH;
+    const long long pix = (long long)blockIdx.x * (LP_NT / 16) + threadIdx.x / 16;
+    const int j = threadIdx.x & 15;
+    if (pix >= total) return;
+    float4 x[CH], y[CH], G[CH];
+    lp_load<CH>(f0 + pix * C, j, x);
+    lp_load<CH>(f1 + pix * C, j, y);
+    const float n0 = n0s[pix], n1 = n1s[pix];
+    const float n0e = n0 + LP_EPS, n1e = n1 + LP_EPS;
+    const float s2 = 2.f * gs[pix / HW];
+    float dot0 = 0.f, dot1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + 64 * i + 4 * j);
+        G[i].x = s2 * wv.x * (x[i].x / n0e - y[i].x / n1e);
+        G[i].y = s2 * wv.y * (x[i].y / n0e - y[i].y / n1e);
+        G[i].z = s2 * wv.z * (x[i].z / n0e - y[i].z / n1e);
+        G[i].w = s2 * wv.w * (x[i].w / n0e - y[i].w / n1e);
+        dot0 += dot4(G[i], x[i]);
+        dot1 += dot4(G[i], y[i]);
+    }
+    dot0 = lp_sum16(dot0);
+    dot1 = lp_sum16(dot1);
+    const float k0 = n0 > 0.f ? dot0 / (n0e * n0e * n0) : 0.f;
+    const float k1 = n1 > 0.f ? dot1 / (n1e * n1e * n1) : 0.f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+        const long long o = pix * C + 64 * i + 4 * j;
+        if (g0)
+            *reinterpret_cast<float4*>(g0 + o) = make_float4(G[i].x / n0e - x[i].x * k0, G[i].y / n0e - x[i].y * k0,
+                                                             G[i].z / n0e - x[i].z * k0, G[i].w / n0e - x[i].w * k0);
+        if (g1)
+            *reinterpret_cast<float4*>(g1 + o) = make_float4(-G[i].x / n1e + y[i].x * k1, -G[i].y / n1e + y[i].y * k1,
+                                                             -G[i].z / n1e + y[i].z * k1, -G[i].w / n1e + y[i].w * k1);
+    }
+}
+
+int nhwc_grid(long long pixels) { return (int)((pixels + LP_NT / 16 - 1) / (LP_NT / 16)); }
+
 }  // namespace
 
 extern "C" int vfm_lpips_head_fwd(const float* f0, const float* f1, const float* w, float* r, float* n0, float* n1,
@@ -140,5 +237,44 @@ extern "C" int vfm_lpips_head_bwd(const float* f0, const float* f1, const float*
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(lpips_head_bwd, dim3(grid_of(total)), dim3(LP_NT), 0, st, f0, f1, w, n0, n1, gs, g0, g1, C, HW,
                        total);
+    return (int)hipGetLastError();
+}
+
+extern "C" int vfm_lpips_head_fwd_nhwc(const float* f0, const float* f1, const float* w, float* r, float* n0, float* n1,
+                                       int B, int C, long long HW, void* stream) {
+    if (B < 0 || HW < 0) return VFM_ERR_ARGS;
+    if (C != 64 && C != 128 && C != 256 && C != 512) return VFM_NO_KERNEL;
+    const long long total = (long long)B * HW;
+    if (total == 0) return VFM_OK;
+    if (!f0 || !f1 || !w || !r || !n0 || !n1 || total > (1ll << 36)) return VFM_ERR_ARGS;
+    if (((uintptr_t)f0 | (uintptr_t)f1 | (uintptr_t)w) % 16) return VFM_ERR_ARGS;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 g(nhwc_grid(total)), b(LP_NT);
+    switch (C) {
+        case 64: hipLaunchKernelGGL(lpips_head_fwd_nhwc<1>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        case 128: hipLaunchKernelGGL(lpips_head_fwd_nhwc<2>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        case 256: hipLaunchKernelGGL(lpips_head_fwd_nhwc<4>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        default: hipLaunchKernelGGL(lpips_head_fwd_nhwc<8>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+    }
+    return (int)hipGetLastError();
+}
+
+extern "C" int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, const float* n0,
+                                       const float* n1, const float* gs, float* g0, float* g1, int B, int C, long long HW,
+                                       void* stream) {
+    if (B < 0 || HW < 0) return VFM_ERR_ARGS;
+    if (C != 64 && C != 128 && C != 256 && C != 512) return VFM_NO_KERNEL;
+    const long long total = (long long)B * HW;
+    if (total == 0 || (!g0 && !g1)) return VFM_OK;
+    if (!f0 || !f1 || !w || !n0 || !n1 || !gs || total > (1ll << 36)) return VFM_ERR_ARGS;
+    if (((uintptr_t)f0 | (uintptr_t)f1 | (uintptr_t)w | (uintptr_t)g0 | (uintptr_t)g1) % 16) return VFM_ERR_ARGS;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 g(nhwc_grid(total)), b(LP_NT);
+    switch (C) {
+        case 64: hipLaunchKernelGGL(lpips_head_bwd_nhwc<1>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        case 128: hipLaunchKernelGGL(lpips_head_bwd_nhwc<2>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        case 256: hipLaunchKernelGGL(lpips_head_bwd_nhwc<4>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        default: hipLaunchKernelGGL(lpips_head_bwd_nhwc<8>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+    }
     return (int)hipGetLastError();
 }

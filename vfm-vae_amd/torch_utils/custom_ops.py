@@ -55,6 +55,8 @@ SIGNATURES = {
                              c_int, c_vp],
     "vfm_lpips_head_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_lpips_head_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
+    "vfm_lpips_head_fwd_nhwc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
+    "vfm_lpips_head_bwd_nhwc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_gemm_fast": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
                       c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_split3": [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp],

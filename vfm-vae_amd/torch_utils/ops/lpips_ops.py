@@ -32,7 +32,12 @@ class _LpipsHead(torch.autograd.Function):
             raise RuntimeError(f"lpips head: feature shapes {tuple(f0.shape)} vs {tuple(f1.shape)}")
         B, C, H, W = f0.shape
         HW = H * W
-        f0c, f1c = f0.contiguous(), f1.contiguous()
+        # channels_last features (the HIP VGG16 stack) run the NHWC kernels in place
+        nhwc = C in (64, 128, 256, 512) and all(_is_nhwc(t) for t in (f0, f1))
+        if nhwc:
+            f0c, f1c = f0, f1
+        else:
+            f0c, f1c = f0.contiguous(), f1.contiguous()
         wc = w.detach().reshape(-1).float().contiguous()
         if wc.numel() != C or wc.device != f0.device:
             raise RuntimeError(f"lpips head: lin weight has {wc.numel()} entries for {C} channels")
@@ -40,12 +45,14 @@ class _LpipsHead(torch.autograd.Function):
         n0 = torch.empty_like(r)
         n1 = torch.empty_like(r)
         nb = 2 * 2 * B * C * HW * 4 + 3 * B * HW * 4
-        with kernel_timer.region('lpips_head_fwd', nb):
-            rc = lib.vfm_lpips_head_fwd(f0c.data_ptr(), f1c.data_ptr(), wc.data_ptr(), r.data_ptr(), n0.data_ptr(),
-                                        n1.data_ptr(), B, C, HW, custom_ops.stream_ptr(f0.device))
+        fn = lib.vfm_lpips_head_fwd_nhwc if nhwc else lib.vfm_lpips_head_fwd
+        with kernel_timer.region('lpips_head_fwd_nhwc' if nhwc else 'lpips_head_fwd', nb):
+            rc = fn(f0c.data_ptr(), f1c.data_ptr(), wc.data_ptr(), r.data_ptr(), n0.data_ptr(), n1.data_ptr(), B, C, HW,
+                    custom_ops.stream_ptr(f0.device))
         custom_ops.check(rc, "vfm_lpips_head_fwd")
         ctx.save_for_backward(f0c, f1c, wc, n0, n1)
         ctx.shape = (B, C, H, W)
+        ctx.nhwc = nhwc
         return r.mean(1).reshape(B, 1, 1, 1)
 
     @staticmethod
@@ -61,16 +68,20 @@ class _LpipsHead(torch.autograd.Function):
         if not (need0 or need1):
             return None, None, None
         gs = (gout.reshape(B).float() / HW).contiguous()
-        g0 = torch.empty_like(f0) if need0 else None
+        g0 = torch.empty_like(f0) if need0 else None          # same memory format as the features
         g1 = torch.empty_like(f1) if need1 else None
         nb = 2 * 2 * B * C * HW * 4 + (int(need0) + int(need1)) * B * C * HW * 4 + 2 * B * HW * 4
-        with kernel_timer.region('lpips_head_bwd', nb):
-            rc = lib.vfm_lpips_head_bwd(f0.data_ptr(), f1.data_ptr(), w.data_ptr(), n0.data_ptr(), n1.data_ptr(),
-                                        gs.data_ptr(), g0.data_ptr() if need0 else None,
-                                        g1.data_ptr() if need1 else None, B, C, HW,
-                                        custom_ops.stream_ptr(f0.device))
+        fn = lib.vfm_lpips_head_bwd_nhwc if ctx.nhwc else lib.vfm_lpips_head_bwd
+        with kernel_timer.region('lpips_head_bwd_nhwc' if ctx.nhwc else 'lpips_head_bwd', nb):
+            rc = fn(f0.data_ptr(), f1.data_ptr(), w.data_ptr(), n0.data_ptr(), n1.data_ptr(), gs.data_ptr(),
+                    g0.data_ptr() if need0 else None, g1.data_ptr() if need1 else None, B, C, HW,
+                    custom_ops.stream_ptr(f0.device))
         custom_ops.check(rc, "vfm_lpips_head_bwd")
         return g0, g1, None
+
+
+def _is_nhwc(t):
+    return t.dim() == 4 and t.permute(0, 2, 3, 1).is_contiguous() and t.data_ptr() % 16 == 0
 
 
 def lpips_head(f0, f1, w, impl='cuda'):
