@@ -239,3 +239,4 @@ def test_training_stats_reduce_over_ranks():
         assert out["num"] == 4 and abs(out["mean"] - 2.25) < 1e-12
         assert abs(out["std"] - float(vals.std(unbiased=False))) < 1e-12
         assert out["r0"] == (1.0, 5.0)
+

@@ -19,6 +19,13 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
+def _ours(stack):
+    """This package's frames of a profiler stack (relative paths; torch / builtin frames dropped)."""
+    return [f.split("vfm-vae_amd/")[-1] for f in stack
+            if not f.startswith(("torch/", "<built-in", "nn.Module", "contextlib")) and "kernel_timer" not in f
+            and "/torch/" not in f]
+
+
 def idle_by_stack(prof, path, min_gap_us=5.0):
     """GPU idle gaps attributed to the Python call site that launched the kernel after each
     gap (kernel -> runtime launch event by correlation id -> innermost op with a stack)."""
@@ -50,8 +57,7 @@ def idle_by_stack(prof, path, min_gap_us=5.0):
             i -= 1
         if best is None:
             return "(no op)"
-        frames = [f for f in best.stack if "vfm-vae_amd" in f or "bench.py" in f][:4]
-        return best.name + " <- " + " <- ".join(f.split("vfm-vae_amd/")[-1] for f in frames)
+        return best.name + " <- " + " <- ".join(_ours(best.stack)[:4])
 
     idle = defaultdict(float)
     cnt = defaultdict(int)
@@ -91,7 +97,8 @@ def main():
     step([pool[1].float() / 255.], [labels], 2 * args.batch)
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True) as prof:
+    cfg = torch._C._profiler._ExperimentalConfig(verbose=True)      # Python stacks need verbose on this torch
+    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True, experimental_config=cfg) as prof:
         step([pool[0].float() / 255.], [labels], 2 * args.batch)
         torch.cuda.synchronize()
     sort = "self_cuda_time_total"
@@ -129,7 +136,7 @@ def main():
     evs.sort(key=lambda e: -e.count)
     with open(os.path.join(args.out, "launch_sites.txt"), "w") as f:
         for e in evs[:150]:
-            fr = [x.split("vfm-vae_amd/")[-1] for x in e.stack if ("vfm-vae_amd" in x or "bench.py" in x) and "torch_utils/ops/kernel_timer" not in x][:5]
+            fr = _ours(e.stack)[:5]
             f.write(f"{e.count:6d} calls {e.self_device_time_total / 1e3:8.2f} ms  {e.key}  <- {' <- '.join(fr)}\n")
     open(os.path.join(args.out, "ops.txt"), "w").write(t1)
     open(os.path.join(args.out, "ops_shapes.txt"), "w").write(t2)

@@ -323,6 +323,8 @@ __device__ __forceinline__ void st4<float>(float* p, const float* v) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 // v[0 .. K+2]: the lane's 4 columns with PAD columns of left and K-1-PAD of right halo.
 template <int K>
 __device__ __forceinline__ void dwr_halo(const float* own, float* v, int q, int L) {
@@ -379,11 +381,9 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
     T* yp = reinterpret_cast<T*>(a.y) + ln.poff;
     const float* np = a.noise ? a.noise + 4 * q : nullptr;
 
-    float acc[K][4];
+    f2 acc2[K][2];
 #pragma unroll
-    for (int s = 0; s < K; ++s)
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) acc[s][c4] = 0.f;
+    for (int s = 0; s < K; ++s) acc2[s][0] = acc2[s][1] = f2{0.f, 0.f};
     const int nrows = a.BH + K - 1;
     float nxt[4] = {0.f, 0.f, 0.f, 0.f};
     if (live && y0 - PAD >= 0 && y0 - PAD < a.H) ld4(xp + (long long)(y0 - PAD) * a.W, nxt);
@@ -392,8 +392,7 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
         for (int u = 0; u < K; ++u) {
             const int jj = jj0 + u;
             if (jj < nrows) {
-#pragma unroll
-                for (int c4 = 0; c4 < 4; ++c4) acc[u][c4] = bias;      // output row jj starts here
+                acc2[u][0] = acc2[u][1] = f2{bias, bias};              // output row jj starts here
                 float own[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
                 const int iyn = y0 - PAD + jj + 1;                     // prefetch the next input row
 #pragma unroll
@@ -401,20 +400,30 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
                 if (live && jj + 1 < nrows && iyn >= 0 && iyn < a.H) ld4(xp + (long long)iyn * a.W, nxt);
                 float v[K + 3];
                 dwr_halo<K>(own, v, q, a.L);
+                // column pairs (2p, 2p+1) as packed fp32 (v_pk_fma_f32): the operand pair for tap kx
+                // is (v[2p+kx], v[2p+kx+1]) = ve[p + kx/2] (kx even) or vo[p + kx/2] (kx odd)
+                f2 ve[(K + 3) / 2], vo[(K + 2) / 2];
+#pragma unroll
+                for (int i = 0; i < (K + 3) / 2; ++i) ve[i] = f2{v[2 * i], v[2 * i + 1]};
+#pragma unroll
+                for (int i = 0; i < (K + 2) / 2; ++i) vo[i] = f2{v[2 * i + 1], v[2 * i + 2]};
 #pragma unroll
                 for (int ky = 0; ky < K; ++ky) {
                     const int sl = (u - ky + K) % K;                    // output row jj - ky
 #pragma unroll
-                    for (int c4 = 0; c4 < 4; ++c4)
+                    for (int p2 = 0; p2 < 2; ++p2)
 #pragma unroll
-                        for (int kx = 0; kx < K; ++kx) acc[sl][c4] = fmaf(v[c4 + kx], wk[ky * K + kx], acc[sl][c4]);
+                        for (int kx = 0; kx < K; ++kx) {
+                            const f2 xv = (kx & 1) ? vo[p2 + kx / 2] : ve[p2 + kx / 2];
+                            const float wv = wk[ky * K + kx];
+                            acc2[sl][p2] = __builtin_elementwise_fma(xv, f2{wv, wv}, acc2[sl][p2]);
+                        }
                 }
                 const int ob = jj - (K - 1);                           // completed output row
                 const int oy = y0 + ob;
                 if (live && ob >= 0 && ob < a.BH && oy < a.H) {
-                    float o[4];
-#pragma unroll
-                    for (int c4 = 0; c4 < 4; ++c4) o[c4] = acc[(u + 1) % K][c4];
+                    const f2 o0 = acc2[(u + 1) % K][0], o1 = acc2[(u + 1) % K][1];
+                    float o[4] = {o0.x, o0.y, o1.x, o1.y};
                     if (np) {
 #pragma unroll
                         for (int c4 = 0; c4 < 4; ++c4) o[c4] += np[oy * a.W + c4];
@@ -464,6 +473,8 @@ __global__ __launch_bounds__(NT) void dwr_bwd_w(DwRowArgs a) {
                 if (live && iy >= 0 && iy < a.H) ld4(xp + (long long)iy * a.W, own);
                 float v[K + 3];
                 dwr_halo<K>(own, v, q, a.L);
+                // scalar FMAs here: the packed form (v_pk_fma_f32 over column pairs) measured 13-18 %
+                // slower at 158 VGPRs (occupancy 3)
 #pragma unroll
                 for (int ky = 0; ky < K; ++ky) {
                     const int sl = (u - ky + K) % K;                    // dy row jj - ky
