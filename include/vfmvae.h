@@ -257,6 +257,10 @@ int vfm_attention_f32_bwd(const void* q, const void* k, const void* v, const voi
 int vfm_gemm_fast(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
                   int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
                   long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
+/* Same contract as vfm_gemm_fast on a 4-phase-per-K-tile LDS-DMA pipeline (csrc/gemm8.hip). */
+int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+              int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 /* fp32 -> bf16 3-term split of one GEMM operand along its reduction dimension K, so that the
  * fp32 product runs as ONE bf16 GEMM of depth 3K: role 0 (A) writes [hi | hi | lo], role 1 (B)
  * [hi ; lo ; hi]; kcont = 1: src [R][K] (row stride ld) -> dst [R][3K], kcont = 0: src [K][R]

@@ -131,12 +131,16 @@ def test_gemm_unsupported_shape_returns_none():
     assert gemm_hip.try_gemm(A, B) is None
 
 
+@pytest.mark.parametrize("kernel", ["gemm8", "gemm_fast"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
-@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128)])
-def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K):
-    """The 256-tile LDS-DMA kernel (csrc/gemm_fast.hip) and, for fp32, the [hi|hi|lo] split."""
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128), (256, 256, 64), (1000, 264, 704)])
+def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, kernel, monkeypatch):
+    """The 256-tile LDS-DMA kernels (csrc/gemm8.hip: 4-phase pipeline, the default; csrc/gemm_fast.hip)
+    and, for fp32, the [hi|hi|lo] split; K = 64 is the single-K-tile path of gemm8's schedule."""
     from torch_utils.ops import gemm_hip, kernel_timer
+    monkeypatch.setattr(gemm_hip, "GEMM8", kernel == "gemm8")
+    monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
     g = torch.Generator().manual_seed(M * 3 + N + K)
     A = _make((K, M) if a_t else (M, K), dtype, g)
     B = _make((N, K) if b_t else (K, N), dtype, g)
@@ -145,7 +149,7 @@ def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K):
     kernel_timer.enable(True)
     out = gemm_hip.gemm(Av, Bv, out_dtype=torch.float32)
     torch.cuda.synchronize()
-    assert any(k.startswith("gemm_fast") for k in kernel_timer.summary())
+    assert any(k.startswith(kernel + "<") for k in kernel_timer.summary())
     kernel_timer.enable(False)
     tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
     assert _rel(out, Av.float() @ Bv.float()) < tol

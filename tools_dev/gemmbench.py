@@ -25,14 +25,21 @@ def bench(fn, iters=10):
 
 
 def row(name, fl, fh, ft):
-    th, tt = bench(fh), bench(ft)
-    print(f"{name:34s} hip {th:7.3f} ms {fl / th / 1e9:7.1f} TF/s | torch {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF/s",
-          flush=True)
+    gemm_hip.GEMM8 = True
+    th8 = bench(fh)
+    gemm_hip.GEMM8 = False
+    th = bench(fh)
+    gemm_hip.GEMM8 = True
+    tt = bench(ft)
+    print(f"{name:34s} gemm8 {th8:7.3f} ms {fl / th8 / 1e9:7.1f} TF/s | fast {th:7.3f} ms {fl / th / 1e9:7.1f} TF/s"
+          f" | torch {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF/s", flush=True)
 
 
 dev = "cuda"
 for name, dt, M, N, K in [("siglip qkv bf16", torch.bfloat16, 32768, 3072, 1024),
+                          ("siglip fc1 bf16", torch.bfloat16, 32768, 4096, 1024),
                           ("siglip fc2 bf16", torch.bfloat16, 32768, 1024, 4096),
+                          ("square 8192 bf16", torch.bfloat16, 8192, 8192, 8192),
                           ("adapter qkv fp32", torch.float32, 32768, 3072, 1024)]:
     A = torch.randn(M, K, device=dev).to(dt)
     W = torch.randn(N, K, device=dev).to(dt)

@@ -1,0 +1,326 @@
+// 256 x 256 bf16 GEMM with a 4-phase-per-K-tile LDS-DMA pipeline (the products of csrc/gemm_fast.hip
+// -- frozen-ViT projections, fusion-adapter linears, decoder 1x1 convolutions at batch 32, fp32
+// operands pre-split into a depth-3K bf16 GEMM -- on a deeper schedule):
+//   C[z] = epi(alpha A[z] B[z] + beta C[z]), same contract / epilogue as vfm_gemm_fast.
+//
+// Schedule (cdna_hip_programming.md §5 "The 256² 8-phase template", T2-T5; written from its rules):
+//   * 8 waves as 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 blocks of v_mfma_f32_16x16x32_bf16;
+//     each K-tile (64) is computed in 4 phases, one C-quadrant (64 x 32, 16 MFMAs) each, in the
+//     order (Alo,Blo) (Alo,Bhi) (Ahi,Bhi) (Ahi,Blo): every fragment is read from LDS once per
+//     K-tile (A_lo p0, B_lo p0, B_hi p1, A_hi p2; 24 ds_read_b128 per wave) and kept in VGPRs;
+//   * each operand tile is staged as two half-tiles: A_lo = the first 64 rows of both wave-rows'
+//     128-row bands, A_hi the second 64; B_lo / B_hi the first / second 32 columns of each
+//     wave-column's 64. A half-tile is 16 KB = 2 LDS-DMA (global_load_lds_dwordx4) per thread;
+//   * phase p of K-tile t issues ONE half-tile of K-tile t+1 into the other LDS buffer (order
+//     A_lo, B_lo, B_hi, A_hi), reads its own fragments (made visible by the previous phase's
+//     counted wait + barrier), waits with a COUNTED s_waitcnt vmcnt for the next phase's
+//     half-tile only (4 DMA stay in flight across every barrier), raw s_barrier, lgkmcnt(0),
+//     then its 16 MFMAs under s_setprio(1);
+//   * two barriers per phase (after the reads, after the MFMAs) and the wm = 1 wave-row one
+//     barrier behind the wm = 0 row (one extra barrier before / after the loop): each row's MFMAs
+//     run while the other row issues its DMA and fragment reads (ping-pong);
+//   * RAW: the half-tile read in phase p is waited for (counted vmcnt, every wave) before the
+//     first barrier of phase p-1, which both rows pass before their phase-p reads;
+//   * WAR: with the rows one barrier apart, a half-tile is restaged >= 2 phases after its last
+//     read (A_lo: read p0, restaged next tile p0 = 4 phases; B_lo: p0 -> p1 = 5; B_hi: p1 -> p2 = 5;
+//     A_hi: p2 -> p3 = 5);
+//   * LDS images XOR-swizzled on the DMA source address (destination lane-linear): K-contiguous
+//     half-tiles [128 rows][64 k] (128-B rows, chunk ^= (row>>1)&7, ds_read_b128 fragments),
+//     MN-contiguous ones [64 k][128] (256-B rows, gemm.hip's 4x4 chunk swizzle, ds_read_b64_tr_b16);
+//   * XCD-aware bijective block -> tile remap; the epilogue is gemm_fast's (LDS-staged bf16 tile
+//     with 16-B stores when the tile is full).
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int HALF = 128 * 64 * 2;        // bytes of one half-tile image (16 KB)
+constexpr int BUF = 4 * HALF;             // A_lo, A_hi, B_lo, B_hi of one K-tile (64 KB)
+
+struct G8Args {
+    const __hip_bfloat16* A;
+    const __hip_bfloat16* B;
+    void* C;
+    const float* bias;
+    long long lda, ldb, ldc, sA, sB, sC;
+    int M, N, K;
+    float alpha, beta;
+    int bias_mode, act;
+};
+
+__device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
+__device__ __forceinline__ int mc_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int mc_off(int row, int ch) { return row * 256 + 16 * (ch ^ mc_swz(row)); }
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+    const float u = 0.7978845608028654f * fmaf(0.044715f * x, x * x, x);
+    const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * u);
+    return 0.5f * x * (2.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f));
+}
+
+// half-tile row / column r (0..127) -> tile row / column, q = lo (0) / hi (1) half
+__device__ __forceinline__ int a_outer(int r, int q) { return 128 * (r >> 6) + 64 * q + (r & 63); }
+__device__ __forceinline__ int b_outer(int r, int q) { return 64 * (r >> 5) + 32 * q + (r & 31); }
+
+// LDS offsets of the half-tiles inside one buffer
+constexpr int OFF_ALO = 0, OFF_AHI = HALF, OFF_BLO = 2 * HALF, OFF_BHI = 3 * HALF;
+
+// One LDS-DMA instruction (global_load_lds_dwordx4: lane l's 16 B land at lds_dst + 16 l). Issued
+// from inline asm so that hipcc's waitcnt pass does not see an LDS write in flight and drain it
+// with vmcnt(0) before every ds_read (which serialised the pipeline of the builtin form: see
+// gemm_fast.hip); the counted waits below are the only ones. m0 is set in the same statement.
+__device__ __forceinline__ void glds16(const void* g, const unsigned char* lds_dst) {
+    const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void*)lds_dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
+}
+
+// Issue the DMA of one half-tile (2 x 16 B per thread).
+template <bool KCONT, bool ISA>
+__device__ __forceinline__ void dma_half(unsigned char* img, const __hip_bfloat16* base, long long ld, int outer0,
+                                         int outer_n, int k0, int q, int tid) {
+    const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int cbase = wave * 64 + 512 * u;
+        const int ci = cbase + lane;
+        const __hip_bfloat16* src;
+        if (KCONT) {
+            const int row = ci >> 3, chs = (ci & 7) ^ ((row >> 1) & 7);
+            const int o = min(outer0 + (ISA ? a_outer(row, q) : b_outer(row, q)), outer_n - 1);
+            src = base + (long long)o * ld + k0 + 8 * chs;
+        } else {
+            const int row = ci >> 4, chs = (ci & 15) ^ mc_swz(row);
+            int o = outer0 + (ISA ? a_outer(8 * chs, q) : b_outer(8 * chs, q));
+            if (o >= outer_n) o = 0;                       // (outer_n % 8 == 0): a valid chunk, result unused
+            src = base + (long long)(k0 + row) * ld + o;
+        }
+        glds16(src, img + cbase * 16);
+    }
+}
+
+// 16x16x32 fragment of 16-row block `blk` of a half-tile image (blk 0..7), k32 step t
+template <bool KCONT>
+__device__ __forceinline__ bf16x8 frag16(const unsigned char* img, int blk, int t, int lane) {
+    if (KCONT) {
+        return *reinterpret_cast<const bf16x8*>(img + kc_off(16 * blk + (lane & 15), 4 * t + (lane >> 4)));
+    } else {
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int ch = 2 * blk + (p >> 1);
+        const int row = 32 * t + 8 * g + q;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + mc_off(row, ch) + 8 * (p & 1)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + mc_off(row + 4, ch) + 8 * (p & 1)));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+}
+
+#define VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+template <bool AK, bool BKC, bool OUTF32>
+__global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    // grouped order: consecutive tiles (the ~32 an XCD runs at once) cover GROUP tile-rows x 32/GROUP
+    // tile-columns, so the XCD's L2 holds GROUP A panels + 32/GROUP B panels instead of 1 + 32
+    constexpr int GROUP = 4;
+    const int gsz = GROUP * tiles_n, grp = tile / gsz, rem = tile - grp * gsz;
+    const int rows_g = min(GROUP, tiles_m - grp * GROUP);
+    const int tm = grp * GROUP + rem % rows_g, tn = rem / rows_g;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int z = blockIdx.y;
+    const __hip_bfloat16* Ab = a.A + (long long)z * a.sA;
+    const __hip_bfloat16* Bb = a.B + (long long)z * a.sB;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+    const int KT = a.K / BK;
+    // half-tile h of K-tile t into its buffer: h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi (issue order)
+    auto issue = [&](int t, int h) {
+        unsigned char* buf = lds + (t & 1) * BUF;
+        const int k0 = t * BK;
+        if (h == 0) dma_half<AK, true>(buf + OFF_ALO, Ab, a.lda, m0, a.M, k0, 0, tid);
+        else if (h == 1) dma_half<BKC, false>(buf + OFF_BLO, Bb, a.ldb, n0, a.N, k0, 0, tid);
+        else if (h == 2) dma_half<BKC, false>(buf + OFF_BHI, Bb, a.ldb, n0, a.N, k0, 1, tid);
+        else dma_half<AK, true>(buf + OFF_AHI, Ab, a.lda, m0, a.M, k0, 1, tid);
+    };
+    issue(0, 0);
+    issue(0, 1);
+    issue(0, 2);
+    issue(0, 3);
+    VMCNT(4);                                   // A_lo, B_lo of tile 0
+    __builtin_amdgcn_s_barrier();
+    // ping-pong: the wm = 1 wave-row runs one barrier behind (2 barriers per phase), so one
+    // wave-row's 16 MFMAs overlap the other's DMA issue + fragment reads (see the header)
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+
+    bf16x8 af[4][2], bl[2][2], bh[2][2];        // A quadrant rows; B_lo / B_hi columns (both kept)
+    for (int t = 0; t < KT; ++t) {
+        const unsigned char* buf = lds + (t & 1) * BUF;
+        const bool nxt = t + 1 < KT;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int qm = p >> 1;                          // 0 0 1 1
+            const int qn = (p == 1 || p == 2) ? 1 : 0;      // 0 1 1 0
+            if (nxt) issue(t + 1, p);
+            // this phase's fragments (A every second phase)
+            if (p == 0 || p == 2) {
+                const unsigned char* ai = buf + (qm ? OFF_AHI : OFF_ALO);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) af[i][s] = frag16<AK>(ai, 4 * wm + i, s, lane);
+            }
+            if (p == 0 || p == 1) {                         // B_lo read once (p0, reused p3), B_hi once (p1, reused p2)
+                const unsigned char* bi = buf + (p ? OFF_BHI : OFF_BLO);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        if (p == 0) bl[j][s] = frag16<BKC>(bi, 2 * wn + j, s, lane);
+                        else bh[j][s] = frag16<BKC>(bi, 2 * wn + j, s, lane);
+                    }
+            }
+            // wait for the NEXT phase's half-tile (see the header), then the phase barrier
+            if (nxt) {
+                if (p == 0 || p == 1 || p == 3) VMCNT(4);
+            } else {
+                if (p == 0) VMCNT(2);
+                else if (p == 1) VMCNT(0);
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+                        acc[4 * qm + i][2 * qn + j] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], qn ? bh[j][s] : bl[j][s],
+                                                                    acc[4 * qm + i][2 * qn + j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    VMCNT(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // epilogue: acc[i][j][r] = C[m0 + 128wm + 16i + 4(l>>4) + r][n0 + 64wn + 16j + (l&15)]
+    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
+    TC* Cb = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
+    const int cl = lane & 15, rq = 4 * (lane >> 4);
+    if (!OUTF32 && a.beta == 0.f && m0 + BM <= a.M && n0 + BN <= a.N && (a.ldc % 8) == 0 &&
+        (reinterpret_cast<uintptr_t>(a.C) % 16) == 0 && (a.sC % 8) == 0) {
+        unsigned short* wl = reinterpret_cast<unsigned short*>(lds + wave * 128 * 128);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int nl = 16 * j + cl;
+            const int n = n0 + 64 * wn + nl;
+            const float bcol = (a.bias_mode == 1) ? a.bias[n] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ml = 16 * i + rq + r;
+                    float v = a.alpha * acc[i][j][r];
+                    v += (a.bias_mode == 2) ? a.bias[m0 + 128 * wm + ml] : bcol;
+                    if (a.act == 1) v = gelu_tanh(v);
+                    else if (a.act == 2) v = v * gelu_parts(v).cdf;
+                    const int ch = (nl >> 3) ^ (ml & 7);
+                    wl[ml * 64 + ch * 8 + (nl & 7)] = __builtin_bit_cast(unsigned short, __float2bfloat16(v));
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        __hip_bfloat16* crow = reinterpret_cast<__hip_bfloat16*>(a.C) + (long long)z * a.sC +
+                               (long long)(m0 + 128 * wm) * a.ldc + n0 + 64 * wn;
+#pragma unroll 4
+        for (int c = lane; c < 128 * 8; c += 64) {
+            const int ml = c >> 3, chl = c & 7;
+            const uint4 v = *reinterpret_cast<const uint4*>(wl + ml * 64 + 8 * (chl ^ (ml & 7)));
+            *reinterpret_cast<uint4*>(crow + (long long)ml * a.ldc + 8 * chl) = v;
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = n0 + 64 * wn + 16 * j + cl;
+        if (n >= a.N) continue;
+        const float bcol = (a.bias_mode == 1) ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + 128 * wm + 16 * i + rq + r;
+                if (m >= a.M) continue;
+                TC* cp = Cb + (long long)m * a.ldc + n;
+                float v = a.alpha * acc[i][j][r];
+                if (a.beta != 0.f) v = fmaf(a.beta, ld(cp), v);
+                v += (a.bias_mode == 2) ? a.bias[m] : bcol;
+                if (a.act == 1) v = gelu_tanh(v);
+                else if (a.act == 2) v = v * gelu_parts(v).cdf;
+                st(cp, v);
+            }
+    }
+}
+
+template <bool AK, bool BKC, bool OUTF32>
+int launch8(const G8Args& a, int batch, hipStream_t st) {
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
+        attr = true;
+    }
+    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32>), dim3(nwg, batch), dim3(THREADS), 2 * BUF, st, a);
+    return launch_status();
+}
+
+}  // namespace
+
+extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+                         int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream) {
+    if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
+    if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
+    if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
+    if (K % BK) return VFM_NO_KERNEL;
+    const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
+    if (a_c % 8 || b_c % 8 || lda % 8 || ldb % 8 || sA % 8 || sB % 8) return VFM_NO_KERNEL;
+    if (((uintptr_t)A | (uintptr_t)B) % 16) return VFM_NO_KERNEL;
+    if (lda < (a_kcont ? K : M) || ldb < (b_kcont ? K : N) || ldc < N) return VFM_ERR_ARGS;
+    const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
+    G8Args a;
+    a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
+    a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
+    a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
+    hipStream_t st = (hipStream_t)stream;
+    const bool of32 = out_dtype == VFM_F32;
+#define VFM_G8(AK, BK_) return of32 ? launch8<AK, BK_, true>(a, batch, st) : launch8<AK, BK_, false>(a, batch, st)
+    if (a_kcont && b_kcont) VFM_G8(true, true);
+    if (a_kcont && !b_kcont) VFM_G8(true, false);
+    if (!a_kcont && b_kcont) VFM_G8(false, true);
+    VFM_G8(false, false);
+#undef VFM_G8
+}

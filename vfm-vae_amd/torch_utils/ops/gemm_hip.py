@@ -39,6 +39,8 @@ def _layout(t, kdim_last):
 
 
 FAST = True                 # large-tile LDS-DMA kernel where it applies
+# the 4-phase pipelined form of the large-tile kernel (csrc/gemm8.hip); VFM_GEMM8=0 -> gemm_fast.hip
+GEMM8 = __import__("os").environ.get("VFM_GEMM8", "1") == "1"
 FAST_MIN_MN = 1 << 18       # below ~256k outputs the 128-tile kernel fills the chip better
 
 
@@ -148,10 +150,11 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB, Kf = a3, a_kc, lda, sA, b3, b_kc, ldb, sB, K
         if Ak is not None:
             tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
-            with kernel_timer.region(f"gemm_fast<{tag}>", 0, flops, "mfma"):
-                rc = _lib.vfm_gemm_fast(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias),
-                                        _CODES[out_dtype], M, N, Kf, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB,
-                                        ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], stream)
+            fn, kname = (_lib.vfm_gemm8, "gemm8") if GEMM8 else (_lib.vfm_gemm_fast, "gemm_fast")
+            with kernel_timer.region(f"{kname}<{tag}>", 0, flops, "mfma"):
+                rc = fn(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype], M, N,
+                        Kf, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta),
+                        bias_mode, ACTS[act], stream)
             if rc != custom_ops.VFM_NO_KERNEL:
                 custom_ops.check(rc, "vfm_gemm_fast")
                 return out
