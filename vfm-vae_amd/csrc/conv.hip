@@ -138,7 +138,12 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
     const int tiles_n = a.Cout / BN;
-    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+    // XCD-aware bijective remap: the blocks b, b+8, b+16, ... (one XCD, one L2) take consecutive
+    // tiles, i.e. all Cout tiles of neighbouring pixel rows, which share the same input rows
+    // (9 taps x Cout/BN reads of every input pixel then hit that XCD's L2)
+    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
     StageA sa;
     StageB<BN> sb;

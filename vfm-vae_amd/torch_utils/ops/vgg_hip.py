@@ -49,8 +49,10 @@ def conv3x3(x, w, bias=None, relu=False, mask=None):
         raise RuntimeError("conv3x3: NHWC contiguous input, [Cout, 9*Cin] weights, mask of the output shape")
     out = torch.empty(B, H, W, Cout, dtype=torch.float32, device=x.device)
     flops = 2 * B * H * W * Cout * 9 * Cin
-    with kernel_timer.region(f"conv3x3_nhwc<f32x3,{Cin},{Cout}>", 4 * (x.numel() + out.numel() + w.numel()), flops,
-                             "mfma"):
+    # one timer region per kernel instantiation (BN = 128 / 64 output channels per tile), as
+    # rocprofv3 names them: conv3x3_kernel<128> / <64>
+    with kernel_timer.region(f"conv3x3_nhwc<f32x3,{128 if Cout % 128 == 0 else 64}>",
+                             4 * (x.numel() + out.numel() + w.numel()), flops, "mfma"):
         rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), w.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(mask),
                                        out.data_ptr(), B, H, W, Cin, Cout, int(relu), custom_ops.stream_ptr(x.device))
     custom_ops.check(rc, "vfm_conv3x3_nhwc_f32")
