@@ -211,10 +211,12 @@ int vfm_attention_fwd(const void* q, const void* k, const void* v, void* o, int 
 /* 3x3 / stride 1 / pad 1 convolution, NHWC fp32, implicit GEMM on bf16 MFMA through the 3-term
  * split (replaces the MIOpen fp32 convolutions of the LPIPS VGG16 stack, reference
  * training/lpips.py:126-163, forward and data gradient). x [B, H, W, Cin] (Cin a power of two
- * >= 4), w [Cout][9][Cin] (tap-major, Cout % 64 == 0), out [B, H, W, Cout] = relu?(conv + bias),
+ * >= 4), w [Cout][9][Cin] (tap-major, Cout % 64 == 0) given as bf16 hi = bf16(w) and
+ * lo = bf16(w - hi) arrays [Cout][ldw] (rows zero-padded to ldw, a multiple of 64 >= 9*Cin),
+ * out [B, H, W, Cout] = relu?(conv + bias),
  * zeroed where mask [B, H, W, Cout] <= 0 when mask is given (bias / mask may be null). */
-int vfm_conv3x3_nhwc_f32(const float* x, const float* w, const float* bias, const float* mask, float* out, int B,
-                         int H, int W, int Cin, int Cout, int relu, void* stream);
+int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void* w_lo, int ldw, const float* bias,
+                         const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int relu, void* stream);
 
 /* fp32 attention with gradients (replaces F.scaled_dot_product_attention on the fp32 paths of the
  * generator: fusion-adapter AttnProjection, reference networks/utils/ldm_utils.py:55-87, and the

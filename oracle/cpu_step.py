@@ -16,7 +16,8 @@ import torch
 import yaml
 
 
-def time_iteration(cfg_path, batch=1, threads=0, iters=1):
+def time_iteration(cfg_path, batch=1, threads=0, iters=5, warmup=2):
+    """`warmup` untimed iterations, then the median of `iters` timed ones."""
     import dnnlib
     from train import resolve_config
     from torch_utils.ops import decoder_ops
@@ -38,11 +39,17 @@ def time_iteration(cfg_path, batch=1, threads=0, iters=1):
     res = c.training_set_kwargs.get("resolution", 256)
     g = torch.Generator().manual_seed(0)
     img = torch.randint(0, 256, (batch, 3, res, res), dtype=torch.uint8, generator=g).float() / 255.
-    t0 = time.perf_counter()
-    for i in range(iters):
+    for i in range(warmup):
         it([img], [["a photo"] * batch], i * batch)
-    dt = time.perf_counter() - t0
+    times = []
+    for i in range(iters):
+        t0 = time.perf_counter()
+        it([img], [["a photo"] * batch], (warmup + i) * batch)
+        times.append(time.perf_counter() - t0)
     decoder_ops.set_force_ref(False)
-    return {"value": round(batch * iters / dt, 5), "unit": "images/sec", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"{iters} full stage-0 iteration(s) (D+G+Adam+EMA) at batch {batch}, "
-                                      f"{res}px, same architectures, fp32 torch CPU ops; {dt:.1f} s"}
+    dt = float(np.median(times))
+    return {"value": round(batch / dt, 5), "unit": "images/sec", "cores": torch.get_num_threads(),
+            "host_cpus": os.cpu_count(), "kind": "port",
+            "sample": f"median of {iters} full stage-0 iterations (D+G+Adam+EMA) after {warmup} warm-up, batch "
+                      f"{batch}, {res}px, same architectures, fp32 torch CPU ops; {dt:.2f} s per iteration "
+                      f"(min {min(times):.2f}, max {max(times):.2f})"}

@@ -26,7 +26,7 @@ def test_conv3x3_layer(B, H, W, Cin, Cout):
     x = torch.randn(B, Cin, H, W, generator=g, device=DEV)
     conv = torch.nn.Conv2d(Cin, Cout, 3, padding=1).to(DEV)
     wf, wb, b, w = vgg_hip.prepare([conv])[0]
-    cp = wf.shape[1] // 9
+    cp = max(Cin, 4)
     xh = torch.zeros(B, H, W, cp, device=DEV)
     xh[..., :Cin] = x.permute(0, 2, 3, 1)
     ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).relu()
@@ -43,9 +43,10 @@ def test_conv3x3_layer(B, H, W, Cin, Cout):
 
 
 def _conv64(x, w, bias=None, relu=False, mask=None):
-    """fp64 torch stand-in for vgg_hip.conv3x3 (same NHWC / tap-major conventions)."""
+    """fp64 torch stand-in for vgg_hip.conv3x3 (same NHWC / tap-major conventions; w = (hi, lo))."""
     B, H, W, Cin = x.shape
-    y = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double().reshape(w.shape[0], 3, 3, Cin).permute(0, 3, 1, 2),
+    w = (w[0].double() + w[1].double())[:, :9 * Cin]
+    y = F.conv2d(x.permute(0, 3, 1, 2).double(), w.reshape(w.shape[0], 3, 3, Cin).permute(0, 3, 1, 2),
                  None if bias is None else bias.double(), padding=1)
     y = (y.relu() if relu else y).permute(0, 2, 3, 1)
     return (y * (mask > 0) if mask is not None else y).contiguous()

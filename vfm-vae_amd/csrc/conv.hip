@@ -7,7 +7,7 @@
 //   the data-gradient pass), fp32 out.
 //
 // Layout: activations NHWC fp32 ([B, H, W, C] contiguous: channels_last), weights [Cout][9][Cin]
-// fp32 (tap-major, channels contiguous). Cin is a power of two >= 4 (the 3-channel image is
+// (tap-major, channels contiguous) pre-split into bf16 hi / lo arrays with rows padded to ldw. Cin is a power of two >= 4 (the 3-channel image is
 // padded to 4), Cout a multiple of 64. The data gradient of the same conv is this kernel with the
 // flipped, transposed weights w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
 //
@@ -31,7 +31,9 @@ constexpr int IMG_A = BM * BK * 2;   // bytes of one bf16 image of the A tile
 
 struct ConvArgs {
     const float* x;      // [B, H, W, Cin]
-    const float* w;      // [Cout, 9 * Cin]
+    const __hip_bfloat16* wh;   // [Cout, ldw] hi = bf16(w), tap-major k, zero-padded to ldw
+    const __hip_bfloat16* wl;   // [Cout, ldw] lo = bf16(w - hi)
+    int ldw;
     const float* bias;   // [Cout] or null
     const float* mask;   // [B, H, W, Cout] or null
     float* out;          // [B, H, W, Cout]
@@ -101,23 +103,29 @@ struct StageA {
     }
 };
 
+// weights arrive pre-split (hi / lo bf16, split once per weight version on the host side):
+// thread -> 16-B chunks (8 k) c = tid + 256u of a [ROWS][64] tile, copied as-is into both images
 template <int ROWS>
 struct StageB {
-    static constexpr int PER = ROWS / 16;
-    uint4 r[PER];
+    static constexpr int PER = ROWS * 8 / THREADS;
+    uint4 h[PER], l[PER];
     __device__ __forceinline__ void load(const ConvArgs& a, int n0, int k0, int tid) {
-        const int k = k0 + 4 * (tid & 15);
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int n = n0 + tid / 16 + 16 * u;
-            r[u] = (k < a.K && n < a.Cout) ? *reinterpret_cast<const uint4*>(a.w + (long long)n * a.K + k)
-                                           : make_uint4(0, 0, 0, 0);
+            const int c = tid + THREADS * u, row = c >> 3, k = k0 + 8 * (c & 7), n = n0 + row;
+            const bool ok = k < a.ldw && n < a.Cout;
+            const long long o = (long long)n * a.ldw + k;
+            h[u] = ok ? *reinterpret_cast<const uint4*>(a.wh + o) : make_uint4(0, 0, 0, 0);
+            l[u] = ok ? *reinterpret_cast<const uint4*>(a.wl + o) : make_uint4(0, 0, 0, 0);
         }
     }
     __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
-        const int cc = tid & 15;
 #pragma unroll
-        for (int u = 0; u < PER; ++u) put4(hi, lo, kc_off(tid / 16 + 16 * u, cc >> 1) + 8 * (cc & 1), r[u]);
+        for (int u = 0; u < PER; ++u) {
+            const int c = tid + THREADS * u, off = kc_off(c >> 3, c & 7);
+            *reinterpret_cast<uint4*>(hi + off) = h[u];
+            *reinterpret_cast<uint4*>(lo + off) = l[u];
+        }
     }
 };
 
@@ -226,16 +234,19 @@ int launch(const ConvArgs& a, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const float* w, const float* bias, const float* mask, float* out,
-                                    int B, int H, int W, int Cin, int Cout, int relu, void* stream) {
-    if (!x || !w || !out || B <= 0 || H <= 0 || W <= 0 || H > 32767 || W > 32767) return VFM_ERR_ARGS;
+extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void* w_lo, int ldw, const float* bias,
+                                    const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int relu,
+                                    void* stream) {
+    if (!x || !w_hi || !w_lo || !out || B <= 0 || H <= 0 || W <= 0 || H > 32767 || W > 32767) return VFM_ERR_ARGS;
     if (Cin < 4 || (Cin & (Cin - 1)) || Cout <= 0 || Cout % 64) return VFM_NO_KERNEL;
-    if (((uintptr_t)x | (uintptr_t)w) % 16) return VFM_ERR_ARGS;
+    if (ldw < 9 * Cin || ldw % 64) return VFM_ERR_ARGS;
+    if (((uintptr_t)x | (uintptr_t)w_hi | (uintptr_t)w_lo) % 16) return VFM_ERR_ARGS;
     const long long M = (long long)B * H * W;
     if (M * (long long)(Cin > Cout ? Cin : Cout) >= (1ll << 40) || M >= (1ll << 31) - 2 * (long long)W - 2)
         return VFM_ERR_ARGS;
     ConvArgs a;
-    a.x = x; a.w = w; a.bias = bias; a.mask = mask; a.out = out;
+    a.x = x; a.wh = (const __hip_bfloat16*)w_hi; a.wl = (const __hip_bfloat16*)w_lo; a.ldw = ldw;
+    a.bias = bias; a.mask = mask; a.out = out;
     a.M = (int)M; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.K = 9 * Cin;
     a.lc = 0;
     while ((1 << a.lc) < Cin) ++a.lc;

@@ -40,29 +40,43 @@ def _plan():
 PLAN = _plan()
 
 
+def split_weight(w2d):
+    """fp32 [Cout, K] tap-major weights -> (hi, lo) bf16 [Cout, Kp] (Kp = K rounded up to 64, zero
+    padded): hi = bf16(w), lo = bf16(w - hi), round-to-nearest as the kernels' own split."""
+    Cout, K = w2d.shape
+    Kp = -(-K // 64) * 64
+    wp = torch.zeros(Cout, Kp, dtype=torch.float32, device=w2d.device)
+    wp[:, :K] = w2d
+    hi = wp.to(torch.bfloat16)
+    lo = (wp - hi.float()).to(torch.bfloat16)
+    return hi.contiguous(), lo.contiguous()
+
+
 def conv3x3(x, w, bias=None, relu=False, mask=None):
-    """x: NHWC fp32 [B, H, W, Cin] contiguous; w: [Cout, 9*Cin] fp32 (tap-major) -> [B, H, W, Cout]
-    = relu?(conv(x) + bias) (x (mask > 0) when given)."""
+    """x: NHWC fp32 [B, H, W, Cin] contiguous; w: (hi, lo) from split_weight of the [Cout, 9*Cin]
+    tap-major weights -> [B, H, W, Cout] = relu?(conv(x) + bias) (x (mask > 0) when given)."""
     B, H, W, Cin = x.shape
-    Cout = w.shape[0]
-    if not x.is_contiguous() or w.shape[1] != 9 * Cin or (mask is not None and mask.shape != (B, H, W, Cout)):
-        raise RuntimeError("conv3x3: NHWC contiguous input, [Cout, 9*Cin] weights, mask of the output shape")
+    wh, wl = w
+    Cout = wh.shape[0]
+    if not x.is_contiguous() or wh.shape[1] < 9 * Cin or (mask is not None and mask.shape != (B, H, W, Cout)):
+        raise RuntimeError("conv3x3: NHWC contiguous input, split [Cout, >= 9*Cin] weights, mask of the output shape")
     out = torch.empty(B, H, W, Cout, dtype=torch.float32, device=x.device)
     flops = 2 * B * H * W * Cout * 9 * Cin
     # one timer region per kernel instantiation (BN = 128 / 64 output channels per tile), as
     # rocprofv3 names them: conv3x3_kernel<128> / <64>
     with kernel_timer.region(f"conv3x3_nhwc<f32x3,{128 if Cout % 128 == 0 else 64}>",
-                             4 * (x.numel() + out.numel() + w.numel()), flops, "mfma"):
-        rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), w.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(mask),
-                                       out.data_ptr(), B, H, W, Cin, Cout, int(relu), custom_ops.stream_ptr(x.device))
+                             4 * (x.numel() + out.numel() + Cout * 9 * Cin), flops, "mfma"):
+        rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), wh.data_ptr(), wl.data_ptr(), wh.shape[1], custom_ops.ptr(bias),
+                                       custom_ops.ptr(mask), out.data_ptr(), B, H, W, Cin, Cout, int(relu),
+                                       custom_ops.stream_ptr(x.device))
     custom_ops.check(rc, "vfm_conv3x3_nhwc_f32")
     return out
 
 
 def prepare(convs):
     """Per nn.Conv2d: forward weights [Cout, 9*Cin'] (Cin' = Cin padded to 4 for the image layer),
-    data-gradient weights [Cin, 9*Cout] (flipped taps), bias; cached on the module until the
-    weight's version moves."""
+    data-gradient weights [Cin, 9*Cout] (flipped taps) -- both as split_weight (hi, lo) pairs --, bias
+    and the fp32 weight; cached on the module until the weight's version moves."""
     out = []
     for m in convs:
         key = (m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version)
@@ -74,7 +88,8 @@ def prepare(convs):
             wf = torch.zeros(Cout, 3, 3, cp, dtype=torch.float32, device=w.device)
             wf[..., :Cin] = w.permute(0, 2, 3, 1)
             wb = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9 * Cout).contiguous()
-            hit = (key, (wf.reshape(Cout, 9 * cp).contiguous(), wb, m.bias.detach().float().contiguous(), w))
+            hit = (key, (split_weight(wf.reshape(Cout, 9 * cp)), split_weight(wb), m.bias.detach().float().contiguous(),
+                         w))
             m._vfm_vgg_prep = hit
         out.append(hit[1])
     return out
