@@ -14,9 +14,10 @@ for s in "$@"; do
     bench)   timeout -k 10 900 python bench.py > $out/bench.log 2>&1 ;;
     benchq)  timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench.log 2>&1 ;;
     benchref) timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline --force-ref-ops > $out/bench_ref.log 2>&1 ;;
-    prof)    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 \
-               && python tools_dev/prof_summary.py $(find $out/prof -name '*kernel_trace.csv' | head -1) 3 \
-                    $(sed -n 's/.*timed 3 steps: \([0-9.]*\)s.*/\1/p' $out/prof.log) > $out/prof_summary.txt \
+    prof)    ps=${PROF_STEPS:-20}
+             timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps $ps --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 \
+               && python tools_dev/prof_summary.py $(find $out/prof -name '*kernel_trace.csv' | head -1) $ps \
+                    $(sed -n "s/.*timed $ps steps: \([0-9.]*\)s.*/\1/p" $out/prof.log) > $out/prof_summary.txt \
                && find $out/prof -name '*kernel_trace.csv' -delete ;;
     pmc)     re=${PMC_RE:-gelu_bwd}
              timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" -d $out/pmc_f -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_f.log 2>&1 \

@@ -151,7 +151,10 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         if Ak is not None:
             tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
             fn, kname = (_lib.vfm_gemm8, "gemm8") if GEMM8 else (_lib.vfm_gemm_fast, "gemm_fast")
-            with kernel_timer.region(f"{kname}<{tag}>", 0, flops, "mfma"):
+            tb = lambda v: "true" if v else "false"
+            # one timer region per kernel instantiation (rocprof: gemm8_kernel<AK, BK, OUTF32>)
+            region = f"{kname}<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
+            with kernel_timer.region(region, 0, flops, "mfma"):
                 rc = fn(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype], M, N,
                         Kf, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta),
                         bias_mode, ACTS[act], stream)

@@ -101,6 +101,8 @@ def rocprof_name(region):
     """'scale_bias_gelu_bwd<bf16>' -> 'gelu_bwd<__hip_bfloat16>' (a prefix of the rocprof name)."""
     base, _, args = region.partition("<")
     args = args.rstrip(">").split(",") if args else []
+    if base in ("gemm8", "gemm_fast") and len(args) == 4:      # <tag, AK, BK, OUTF32>
+        return f"{base}_kernel<{args[1]}, {args[2]}, {args[3]}>"
     pat = _ROC.get(base)
     if pat is None:
         return None
