@@ -259,10 +259,16 @@ int vfm_attention_f32_bwd(const void* q, const void* k, const void* v, const voi
 int vfm_gemm_fast(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
                   int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
                   long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
-/* Same contract as vfm_gemm_fast on a 4-phase-per-K-tile LDS-DMA pipeline (csrc/gemm8.hip). */
+/* Same contract as vfm_gemm_fast on a 4-phase-per-K-tile LDS-DMA pipeline (csrc/gemm8.hip), plus
+ * split-K: the K-tiles of each output (of every batch concatenated when reduce_batch: C = sum_z
+ * A[z] B[z]) are cut into chunks of kchunk tiles (<= 0: no split); the splits write fp32 partials
+ * to workspace (vfm_gemm8_workspace_floats floats) and a reduce pass applies the epilogue in a
+ * fixed order. */
 int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
               int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
+              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
+              int kchunk, int reduce_batch, void* stream);
+int vfm_gemm8_workspace_floats(int M, int N, int K, int batch, int kchunk, int reduce_batch);  /* -1: too large */
 /* fp32 -> bf16 3-term split of one GEMM operand along its reduction dimension K, so that the
  * fp32 product runs as ONE bf16 GEMM of depth 3K: role 0 (A) writes [hi | hi | lo], role 1 (B)
  * [hi ; lo ; hi]; kcont = 1: src [R][K] (row stride ld) -> dst [R][3K], kcont = 0: src [K][R]

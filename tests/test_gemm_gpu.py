@@ -182,3 +182,41 @@ def test_gemm_generic_path_when_fast_off(monkeypatch):
     A = _make((512, 256), torch.float32, g)
     B = _make((256, 768), torch.float32, g)
     assert _rel(gemm_hip.gemm(A, B), A @ B) < 5e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("O,I,P,Bn", [(512, 256, 1024, 6), (304, 264, 320, 3)])
+def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, monkeypatch):
+    """sum_b dy[b] . x[b]^T on gemm8's split-K over the batch-concatenated K (opt-in path,
+    VFM_GEMM8_SPLIT=1): fp32 partials + fixed-order reduce; every operand layout; ragged M/N."""
+    from torch_utils.ops import gemm_hip, kernel_timer
+    monkeypatch.setattr(gemm_hip, "SPLIT8", True)
+    g = torch.Generator().manual_seed(O + I + P)
+    dy = _make((Bn, O, P), dtype, g)
+    x = _make((Bn, I, P), dtype, g)
+    A = dy if a_kc else dy.transpose(1, 2).contiguous().transpose(1, 2)
+    Bm = x.transpose(1, 2) if b_kc else x.transpose(1, 2).contiguous()
+    kernel_timer.enable(True)
+    dW = gemm_hip.gemm(A, Bm, out_dtype=torch.float32, reduce_batch=True)
+    torch.cuda.synchronize()
+    assert any(k.startswith("gemm8<") for k in kernel_timer.summary())
+    kernel_timer.enable(False)
+    ref = (dy.double() @ x.double().transpose(1, 2)).sum(0)
+    assert _rel(dW, ref) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+    assert torch.equal(dW, gemm_hip.gemm(A, Bm, out_dtype=torch.float32, reduce_batch=True))   # deterministic
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 512, 8192), (256, 300, 2048)])
+def test_gemm8_split_k(M, N, K, monkeypatch):
+    """Few output tiles over a deep K (the adapter's weight gradients): split-K on gemm8 with a bias
+    epilogue in the reduce pass."""
+    from torch_utils.ops import gemm_hip
+    monkeypatch.setattr(gemm_hip, "SPLIT8", True)
+    g = torch.Generator().manual_seed(M + K)
+    A = _make((M, K), torch.float32, g)
+    B = _make((K, N), torch.float32, g)
+    bias = torch.randn(N, generator=g).to(DEV)
+    out = gemm_hip.gemm(A, B, bias=bias, splits=4)
+    ref = A.double() @ B.double() + bias.double()
+    assert _rel(out, ref) < 5e-5

@@ -54,6 +54,11 @@ struct G8Args {
     int M, N, K;
     float alpha, beta;
     int bias_mode, act;
+    // split-K over "virtual" K-tiles: per output batch (reduce = 0) or over the concatenation of
+    // every batch's K (reduce = 1: C = sum_z A[z] B[z]); S = ceil(V / kchunk) splits write fp32
+    // partials to ws, gemm8_reduce applies the epilogue. ws == null: direct epilogue.
+    float* ws;
+    int kchunk, S, reduce, Z;
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -139,9 +144,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     const int rows_g = min(GROUP, tiles_m - grp * GROUP);
     const int tm = grp * GROUP + rem % rows_g, tn = rem / rows_g;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int z = blockIdx.y;
-    const __hip_bfloat16* Ab = a.A + (long long)z * a.sA;
-    const __hip_bfloat16* Bb = a.B + (long long)z * a.sB;
+    const int KTz = a.K / BK;                          // K-tiles per batch
+    const int zo = a.reduce ? 0 : (int)blockIdx.y / a.S, sp = (int)blockIdx.y - zo * a.S;
+    const int V = a.reduce ? a.Z * KTz : KTz;          // virtual K-tiles of this output
+    const int v0 = sp * a.kchunk;
+    const int KT = min(V, v0 + a.kchunk) - v0;         // >= 1 by construction of S on the host
+    const int z = zo;                                  // output batch
 
     f32x4 acc[8][4];
 #pragma unroll
@@ -149,11 +157,13 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
 
-    const int KT = a.K / BK;
-    // half-tile h of K-tile t into its buffer: h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi (issue order)
+    // half-tile h of local K-tile t into its buffer: h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi (issue order)
     auto issue = [&](int t, int h) {
         unsigned char* buf = lds + (t & 1) * BUF;
-        const int k0 = t * BK;
+        const int v = v0 + t;
+        const int zt = a.reduce ? v / KTz : zo, k0 = (a.reduce ? v - zt * KTz : v) * BK;
+        const __hip_bfloat16* Ab = a.A + (long long)zt * a.sA;
+        const __hip_bfloat16* Bb = a.B + (long long)zt * a.sB;
         if (h == 0) dma_half<AK, true>(buf + OFF_ALO, Ab, a.lda, m0, a.M, k0, 0, tid);
         else if (h == 1) dma_half<BKC, false>(buf + OFF_BLO, Bb, a.ldb, n0, a.N, k0, 0, tid);
         else if (h == 2) dma_half<BKC, false>(buf + OFF_BHI, Bb, a.ldb, n0, a.N, k0, 1, tid);
@@ -225,9 +235,25 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     __builtin_amdgcn_s_barrier();
 
     // epilogue: acc[i][j][r] = C[m0 + 128wm + 16i + 4(l>>4) + r][n0 + 64wn + 16j + (l&15)]
+    const int cl = lane & 15, rq = 4 * (lane >> 4);
+    if (a.ws) {                                        // split-K partial, raw fp32
+        float* w = a.ws + (long long)blockIdx.y * a.M * a.N;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + 64 * wn + 16 * j + cl;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + 128 * wm + 16 * i + rq + r;
+                    if (m < a.M) w[(long long)m * a.N + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
     typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
     TC* Cb = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
-    const int cl = lane & 15, rq = 4 * (lane >> 4);
     if (!OUTF32 && a.beta == 0.f && m0 + BM <= a.M && n0 + BN <= a.N && (a.ldc % 8) == 0 &&
         (reinterpret_cast<uintptr_t>(a.C) % 16) == 0 && (a.sC % 8) == 0) {
         unsigned short* wl = reinterpret_cast<unsigned short*>(lds + wave * 128 * 128);
@@ -283,6 +309,27 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     }
 }
 
+// C[zo] = epi(alpha * sum_s ws[zo * S + s] + beta * C[zo]), fixed summation order (deterministic)
+template <bool OUTF32>
+__global__ __launch_bounds__(256) void gemm8_reduce(G8Args a) {
+    const long long MN = (long long)a.M * a.N;
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int zo = blockIdx.y;
+    if (i >= MN) return;
+    const float* w = a.ws + (long long)zo * a.S * MN + i;
+    float v = 0.f;
+    for (int s = 0; s < a.S; ++s) v += w[s * MN];
+    const int m = (int)(i / a.N), n = (int)(i - (long long)m * a.N);
+    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
+    TC* cp = reinterpret_cast<TC*>(a.C) + (long long)zo * a.sC + (long long)m * a.ldc + n;
+    v *= a.alpha;
+    if (a.beta != 0.f) v = fmaf(a.beta, ld(cp), v);
+    v += a.bias_mode == 1 ? a.bias[n] : (a.bias_mode == 2 ? a.bias[m] : 0.f);
+    if (a.act == 1) v = gelu_tanh(v);
+    else if (a.act == 2) v = v * gelu_parts(v).cdf;
+    st(cp, v);
+}
+
 template <bool AK, bool BKC, bool OUTF32>
 int launch8(const G8Args& a, int batch, hipStream_t st) {
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -292,7 +339,12 @@ int launch8(const G8Args& a, int batch, hipStream_t st) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32>), dim3(nwg, batch), dim3(THREADS), 2 * BUF, st, a);
+    const int zo = a.reduce ? 1 : batch;
+    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32>), dim3(nwg, zo * a.S), dim3(THREADS), 2 * BUF, st, a);
+    if (a.ws) {
+        const long long MN = (long long)a.M * a.N;
+        hipLaunchKernelGGL(gemm8_reduce<OUTF32>, dim3((unsigned)((MN + 255) / 256), zo), dim3(256), 0, st, a);
+    }
     return launch_status();
 }
 
@@ -300,7 +352,8 @@ int launch8(const G8Args& a, int batch, hipStream_t st) {
 
 extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
                          int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream) {
+                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
+                         int kchunk, int reduce_batch, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
     if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
     if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
@@ -315,6 +368,15 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
     a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
+    // virtual K-tiles V per output; S = ceil(V / kchunk) splits (kchunk <= 0: one split)
+    const int V = (reduce_batch ? batch : 1) * (K / BK);
+    a.Z = batch;
+    a.reduce = reduce_batch ? 1 : 0;
+    a.kchunk = (kchunk <= 0 || kchunk > V) ? V : kchunk;
+    a.S = (V + a.kchunk - 1) / a.kchunk;
+    a.ws = (a.S > 1 || a.reduce) ? workspace : nullptr;
+    if ((a.S > 1 || a.reduce) && !workspace) return VFM_ERR_ARGS;
+    if ((long long)(a.reduce ? 1 : batch) * a.S > 65535) return VFM_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;
     const bool of32 = out_dtype == VFM_F32;
 #define VFM_G8(AK, BK_) return of32 ? launch8<AK, BK_, true>(a, batch, st) : launch8<AK, BK_, false>(a, batch, st)
@@ -323,4 +385,15 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
     if (!a_kcont && b_kcont) VFM_G8(false, true);
     VFM_G8(false, false);
 #undef VFM_G8
+}
+
+// fp32 workspace floats vfm_gemm8 needs for (M, N, K, batch, kchunk, reduce_batch); 0 = none
+extern "C" int vfm_gemm8_workspace_floats(int M, int N, int K, int batch, int kchunk, int reduce_batch) {
+    if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || K % BK) return -1;
+    const int V = (reduce_batch ? batch : 1) * (K / BK);
+    const int kc = (kchunk <= 0 || kchunk > V) ? V : kchunk;
+    const int S = (V + kc - 1) / kc;
+    if (S <= 1 && !reduce_batch) return 0;
+    const long long n = (long long)M * N * S * (reduce_batch ? 1 : batch);
+    return n > 0x7fffffffLL ? -1 : (int)n;
 }

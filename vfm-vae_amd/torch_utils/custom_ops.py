@@ -60,7 +60,8 @@ SIGNATURES = {
     "vfm_gemm_fast": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
                       c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
-                      c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
+                      c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    "vfm_gemm8_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_split3": [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp],
     "vfm_gemm_workspace_floats": [c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int,

@@ -41,6 +41,7 @@ def _layout(t, kdim_last):
 FAST = True                 # large-tile LDS-DMA kernel where it applies
 # the 4-phase pipelined form of the large-tile kernel (csrc/gemm8.hip); VFM_GEMM8=0 -> gemm_fast.hip
 GEMM8 = __import__("os").environ.get("VFM_GEMM8", "1") == "1"
+SPLIT8 = __import__("os").environ.get("VFM_GEMM8_SPLIT", "0") == "1"
 FAST_MIN_MN = 1 << 18       # below ~256k outputs the 128-tile kernel fills the chip better
 
 
@@ -137,7 +138,14 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         bias_mode = 1 if bias_dim in (None, 1) else 2
     flops = 2.0 * z * M * N * K
     stream = custom_ops.stream_ptr(A.device)
-    if FAST and splits <= 1 and not reduce_batch and K % 64 == 0 and M * N >= FAST_MIN_MN:
+    # split-K / batch-reduced products on the large-tile kernel (weight gradients: few output
+    # tiles over a deep reduction): chunks of >= 4 K-tiles, ~512 workgroups. Opt-in: for the
+    # decoder's batch-reduced weight gradients the 128-tile kernel, which splits fp32 operands in
+    # registers, measured faster (0.35 vs 0.40 ms at 2048x512x32x1024: the depth-3K copies cost
+    # ~1 GB of HBM traffic per product, tools_dev/gemmbench.py)
+    split8 = (FAST and GEMM8 and SPLIT8 and K % 64 == 0 and min(M, N) >= 256
+              and (reduce_batch or splits > 1 or (auto and -(-M // 256) * -(-N // 256) * z < 256 and K >= 1024)))
+    if split8 or (FAST and splits <= 1 and not reduce_batch and K % 64 == 0 and M * N >= FAST_MIN_MN):
         # large tiles + LDS-DMA pipeline (csrc/gemm_fast.hip); fp32 operands as one bf16 GEMM of
         # depth 3K over their [hi|hi|lo] x [hi;lo;hi] split
         if A.dtype == torch.float32:
@@ -150,14 +158,32 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB, Kf = a3, a_kc, lda, sA, b3, b_kc, ldb, sB, K
         if Ak is not None:
             tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
-            fn, kname = (_lib.vfm_gemm8, "gemm8") if GEMM8 else (_lib.vfm_gemm_fast, "gemm_fast")
             tb = lambda v: "true" if v else "false"
+            args = (Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype], M, N, Kf,
+                    z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta), bias_mode,
+                    ACTS[act])
+            if split8:
+                zo = 1 if reduce_batch else z
+                V = (z if reduce_batch else 1) * (Kf // 64)
+                S0 = max(1, -(-512 // (-(-M // 256) * -(-N // 256) * zo)))
+                kchunk = max(4, -(-V // S0))
+                n = _lib.vfm_gemm8_workspace_floats(M, N, Kf, z, kchunk, int(reduce_batch))
+                ws = torch.empty(max(n, 0), dtype=torch.float32, device=A.device) if n > 0 else None
+                region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
+                with kernel_timer.region(region, 0, flops, "mfma"):
+                    rc = _lib.vfm_gemm8(*args, custom_ops.ptr(ws), kchunk, int(reduce_batch), stream)
+                if rc != custom_ops.VFM_NO_KERNEL:
+                    custom_ops.check(rc, "vfm_gemm8")
+                    return out
+        if Ak is not None and not split8:
             # one timer region per kernel instantiation (rocprof: gemm8_kernel<AK, BK, OUTF32>)
+            kname = "gemm8" if GEMM8 else "gemm_fast"
             region = f"{kname}<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
             with kernel_timer.region(region, 0, flops, "mfma"):
-                rc = fn(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype], M, N,
-                        Kf, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta),
-                        bias_mode, ACTS[act], stream)
+                if GEMM8:
+                    rc = _lib.vfm_gemm8(*args, None, 0, 0, stream)
+                else:
+                    rc = _lib.vfm_gemm_fast(*args, stream)
             if rc != custom_ops.VFM_NO_KERNEL:
                 custom_ops.check(rc, "vfm_gemm_fast")
                 return out
