@@ -343,6 +343,49 @@ int vfm_lpips_head_fwd_nhwc(const float* f0, const float* f1, const float* w, fl
 int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, const float* n0, const float* n1,
                             const float* gs, float* g0, float* g1, int B, int C, long long HW, void* stream);
 
+/* ---- ToRGB: modulated 1x1 (no demodulation) to O <= 4 image channels ----------------------
+ * Replaces networks/utils/convnext_utils.py:145-187 (ConvNeXtToRGBLayer.forward: x * style, 1x1
+ * conv, + bias) in both directions as one HBM pass.
+ *   x: [B, C, P] (dtype VFM_F32 / VFM_BF16, P % 8 == 0, 16-B aligned); wm: fp32 [B, O, C] =
+ *   weight[o, c] * style[b, c]; bias fp32 [O]; y fp32 [B, O, P] = round_x(sum_c wm x) + bias
+ *   (round_x: to bf16 when x is bf16, the reference's bf16 product before the fp32 bias).
+ * bwd: dy fp32 [B, O, P] -> dx [B, C, P] (x's dtype) = sum_o wm dy, and per pixel split s the
+ *   partial tpart[b, s, o, c] = sum_{p in split s} x[b, c, p] dy[b, o, p] (C % 16 == 0;
+ *   S from vfm_torgb_bwd_splits; tpart holds B * S * O * C floats). */
+int vfm_torgb_fwd(const void* x, const float* wm, const float* bias, float* y, int dtype, int B, int O, int C,
+                  int P, void* stream);
+int vfm_torgb_bwd_splits(int B, int C, int P);
+int vfm_torgb_bwd(const void* x, const float* dy, const float* wm, void* dx, float* tpart, int dtype, int B, int O,
+                  int C, int P, int S, void* stream);
+
+/* ---- Multi-scale PatchGAN (stage 3), fp32 NHWC ----------------------------------------------
+ * Replace networks/discriminator.py:180-228 (NLayerDiscriminator's nn.Conv2d k4 s2/s1 p2 layers,
+ * run by the reference on cuDNN) around our MFMA GEMM, and :75-99 (BatchNormLocal2d) + LeakyReLU.
+ * im2col: A[m, (ky k + kx) C + c] = x[b, s oy - pad + ky, s ox - pad + kx, c] (0 outside), m =
+ *   (b Ho + oy) Wo + ox, x NHWC [B, H, W, C], A row stride ldA >= k k C.
+ * col2im: dX[b, iy, ix, c] = sum of dA[m, tap C + c] over the taps that read (iy, ix); with dy1
+ *   ([M]) and w1 ([k k C]) instead of dA: dA[m, j] = dy1[m] w1[j] (the 1-channel layer).
+ * rowdot: y[m] = sum_k A[m, k] w[k] (+ bias[0]); coldot: part[s, k] = sum_{m in split s} A[m, k] v[m]
+ *   (S from vfm_coldot_splits; part holds S * K floats).
+ * bnl_lrelu: x NHWC [B, P = H W, C] in G virtual batches of B / G samples; per (g, c) mean / rstd
+ *   over (samples, P); y = lrelu((x - mean) rstd w + b, slope) (w / b may be NULL); bwd writes dx
+ *   and dw / db (summed over groups; may be NULL). C % 4 == 0 and 256 % (C / 4) == 0; ws holds
+ *   vfm_bnl_workspace_floats floats; deterministic (fixed-order partial sums). */
+int vfm_im2col_nhwc_f32(const float* x, float* A, long long ldA, int B, int H, int W, int C, int Ho, int Wo, int k,
+                        int stride, int pad, void* stream);
+int vfm_col2im_nhwc_f32(const float* dA, long long ldA, const float* dy1, const float* w1, float* dX, int B, int H,
+                        int W, int C, int Ho, int Wo, int k, int stride, int pad, void* stream);
+int vfm_rowdot_f32(const float* A, long long ldA, const float* w, const float* bias, float* y, int M, int K,
+                   void* stream);
+int vfm_coldot_splits(int M, int K);
+int vfm_coldot_f32(const float* A, long long ldA, const float* v, float* part, int M, int K, int S, void* stream);
+long long vfm_bnl_workspace_floats(int B, int P, int C, int G);
+int vfm_bnl_lrelu_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd, float* ws,
+                      int B, int P, int C, int G, float eps, float slope, void* stream);
+int vfm_bnl_lrelu_bwd(const float* x, const float* dy, const float* w, const float* b, const float* mean,
+                      const float* rstd, float* dx, float* dw, float* db, float* ws, int B, int P, int C, int G,
+                      float slope, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

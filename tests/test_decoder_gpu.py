@@ -266,3 +266,23 @@ def test_input_only_grad_skips_parameter_work():
     (y * r).sum().backward()
     assert _rel(gx, x.grad) == 0.0
     assert layer.dwconv.weight.grad is not None and layer.pwconv1.weight.grad is not None
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,H,W,O", [(4, 128, 16, 16, 3), (2, 512, 8, 8, 3), (3, 256, 32, 24, 1), (2, 16, 4, 2, 4)])
+def test_torgb(dt, B, C, H, W, O):
+    """ToRGB (csrc/torgb.hip) vs (W @ (style * x)) + bias in fp32: output, dx, dstyle, dweight, dbias."""
+    ops, _ = _ops()
+    g = torch.Generator().manual_seed(B * C + H)
+    x = torch.randn(B, C, H, W, generator=g).to(dt).float().requires_grad_()
+    w2 = (0.1 * torch.randn(O, C, generator=g)).requires_grad_()
+    st = (1 + 0.3 * torch.randn(B, C, generator=g)).requires_grad_()
+    bias = torch.randn(1, O, 1, 1, generator=g).requires_grad_()
+
+    def hip(x, w2, st, bias):
+        return ops.torgb(x.to(dt), w2, st, bias)
+
+    def ref(x, w2, st, bias):
+        return torch.einsum('oc,bchw->bohw', w2, x * st[:, :, None, None]) + bias
+
+    _run(hip, ref, [x, w2, st, bias], dt, ['torgb_fwd', 'torgb_bwd'])

@@ -149,6 +149,9 @@ def test_total_loss_step_gpu(vfm_dir, graphed, gemm, monkeypatch):
     from training.lpips import vgg16
     monkeypatch.setattr(decoder_hip, "_USE_HIP_GEMM", gemm == "hip")
     monkeypatch.setattr(vgg16, "impl", "hip" if gemm == "hip" else "torch")
+    if gemm == "torch":                 # vendor fp32 PatchGAN convolutions (MIOpen) as well
+        from torch_utils.ops import patchgan_hip
+        monkeypatch.setattr(patchgan_hip, "supported", lambda x: False)
     from networks.generator import Generator
     from networks.discriminator import ProjectedDiscriminator
     from training.loss import TotalLoss

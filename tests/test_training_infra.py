@@ -117,3 +117,14 @@ def test_vfm_feature_reuse_is_exact(tmp_path, outcomes, hit):
     assert grads[True].keys() == grads[False].keys() and grads[True]
     for n in grads[True]:
         assert torch.equal(grads[True][n], grads[False][n]), n
+
+
+def test_kernel_timer_rocprof_names():
+    """Timer regions map onto the kernel names rocprofv3 prints, so the bench's roofline
+    average can be checked against the committed profile."""
+    from torch_utils.ops import kernel_timer as kt
+    assert kt.rocprof_name("gemm<f32x3,true,false,true>") == "gemm_kernel<true, false, true, true>"
+    assert kt.rocprof_name("gemm<bf16,false,true,false>[4x8x16x1]") == "gemm_kernel<false, true, false, false>"
+    assert kt.rocprof_name("gemm8<f32x3,true,true,true>") == "gemm8_kernel<true, true, true>"
+    assert kt.rocprof_name("dwconv2d_fwd<bf16,7>") == "dwr_fwd<__hip_bfloat16, 7>"
+    assert kt.rocprof_name("gemm_ws<f32x3,true,true,true>") is None

@@ -173,6 +173,58 @@ def weights_init(m):
         m.bias.data.fill_(0)
 
 
+class PatchBlock(nn.Sequential):
+    """nn.Sequential of the PatchGAN's Conv2d / BatchNormLocal2d / LeakyReLU (same state-dict keys).
+    ROCm fp32 inputs run the HIP path (torch_utils/ops/patchgan_hip.py): NHWC activations, k4 convs
+    as im2col + MFMA GEMM, BatchNormLocal2d + LeakyReLU fused; outputs are NCHW views of the NHWC
+    results (channels_last memory)."""
+
+    def forward(self, x):
+        from torch_utils.ops import patchgan_hip
+        mods = list(self)
+        if not patchgan_hip.supported(x) or not self._hip_ok(mods, x.shape[0]):
+            return super().forward(x)
+        h = x.permute(0, 2, 3, 1)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            if isinstance(m, nn.Conv2d):
+                fuse = isinstance(nxt, nn.LeakyReLU) and m.bias is not None
+                h = patchgan_hip.conv_nhwc(h, m.weight, None if fuse else m.bias, m.stride[0], m.padding[0])
+                if fuse:
+                    h = patchgan_hip.bias_lrelu(h, m.bias, nxt.negative_slope)
+                    i += 1
+            elif isinstance(m, BatchNormLocal2d):
+                G = int(np.ceil(h.shape[0] / m.virtual_bs))
+                if isinstance(nxt, nn.LeakyReLU):
+                    slope, i = nxt.negative_slope, i + 1
+                else:
+                    slope = 1.0
+                h = patchgan_hip.bn_local_lrelu(h, m.weight if m.affine else None, m.bias if m.affine else None, G,
+                                                m.eps, slope)
+            elif isinstance(m, nn.LeakyReLU):
+                h = patchgan_hip.bias_lrelu(h, None, m.negative_slope)
+            else:
+                h = m(h.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+            i += 1
+        return h.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def _hip_ok(mods, B):
+        for m in mods:
+            if isinstance(m, nn.Conv2d):
+                if m.groups != 1 or m.dilation != (1, 1) or m.padding_mode != 'zeros' or m.stride[0] != m.stride[1] \
+                        or m.padding[0] != m.padding[1] or m.kernel_size[0] != m.kernel_size[1]:
+                    return False
+            elif isinstance(m, BatchNormLocal2d):
+                G = int(np.ceil(B / m.virtual_bs))
+                C = m.weight.shape[0] if m.affine else 0
+                if B % G or (m.affine and (C % 4 or 256 % (C // 4))):
+                    return False
+        return True
+
+
 class NLayerDiscriminator(nn.Module):
     def __init__(self, input_nc, ndf=64, n_layers=3, norm_layer=BatchNormLocal2d, use_sigmoid=False,
                  get_interm_feat=False):
@@ -192,9 +244,9 @@ class NLayerDiscriminator(nn.Module):
             seq += [[nn.Sigmoid()]]
         if get_interm_feat:
             for n, layers in enumerate(seq):
-                setattr(self, f'model{n}', nn.Sequential(*layers))
+                setattr(self, f'model{n}', PatchBlock(*layers))
         else:
-            self.model = nn.Sequential(*[m for layers in seq for m in layers])
+            self.model = PatchBlock(*[m for layers in seq for m in layers])
 
     def forward(self, x):
         if self.get_interm_feat:

@@ -32,6 +32,7 @@ from torch_utils import misc
 from torch_utils import distributed as dist
 from torch_utils.ops import upfirdn2d, conv2d_resample, bias_act, fma
 from networks.utils.shared import FullyConnectedLayer, MLP, GroupNorm32, StyleSplit, ScaleAdaptiveAvgPool2d
+from networks.utils.shared import DepthwiseConv2d, Conv1x1, LeakyReLU
 from networks.utils.ldm_utils import LDMAdapter, EquivarianceTransform
 from networks.utils.gigagan_utils import SelfAttentionBlock, CrossAttentionBlock
 from networks.utils.convnext_utils import ConvNeXtSynthesisLayer, ConvNeXtToRGBLayer, SeparableUpsampleWithFixedBlur
@@ -483,16 +484,17 @@ class SynthesisNetwork(nn.Module):
             self.blocks[f"{idx:01d}"] = block
 
     def _make_3x3_conv(self, cin, cout, activation='gelu', use_activation=True):
-        layers = [nn.Conv2d(cin, cin, 3, padding=1, groups=cin, bias=False), nn.Conv2d(cin, cout, 1, bias=False),
+        # HIP depthwise / 1x1 GEMM / GroupNorm / LReLU (same modules and state-dict keys as nn.*)
+        layers = [DepthwiseConv2d(cin, cin, 3, padding=1, groups=cin, bias=False), Conv1x1(cin, cout, 1, bias=False),
                   GroupNorm32(min(32, cout), cout)]
         if use_activation:
-            layers += [{'lrelu': lambda: nn.LeakyReLU(negative_slope=0.2), 'silu': nn.SiLU, 'gelu': nn.GELU}[activation]()]
+            layers += [{'lrelu': lambda: LeakyReLU(negative_slope=0.2), 'silu': nn.SiLU, 'gelu': nn.GELU}[activation]()]
         return nn.Sequential(*layers)
 
     def _make_1x1_conv(self, cin, cout, activation='gelu', use_activation=True):
-        layers = [nn.Conv2d(cin, cout, 1, bias=False), GroupNorm32(min(32, cout), cout)]
+        layers = [Conv1x1(cin, cout, 1, bias=False), GroupNorm32(min(32, cout), cout)]
         if use_activation:
-            layers += [{'lrelu': lambda: nn.LeakyReLU(negative_slope=0.2), 'silu': nn.SiLU, 'gelu': nn.GELU}[activation]()]
+            layers += [{'lrelu': lambda: LeakyReLU(negative_slope=0.2), 'silu': nn.SiLU, 'gelu': nn.GELU}[activation]()]
         return nn.Sequential(*layers)
 
     def forward(self, z, ws, text, text_mask, **block_kwargs):

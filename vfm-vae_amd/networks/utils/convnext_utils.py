@@ -132,9 +132,7 @@ class ConvNeXtToRGBLayer(nn.Module):
         B, C, H, W = x.shape
         style = self.affine(w) * self.weight_gain                              # [B, C]
         if self.kernel_size == 1:
-            xm = x * style.to(x.dtype)[:, :, None, None]
-            y = decoder_ops.pointwise(self.weight.reshape(self.out_channels, C), xm.reshape(B, C, H * W))
-            y = y.reshape(B, self.out_channels, H, W)
+            return decoder_ops.torgb(x, self.weight.reshape(self.out_channels, C), style, self.bias)
         else:
             w_mod = (self.weight[None] * style.reshape(B, 1, -1, 1, 1)).reshape(B * self.out_channels, C,
                                                                                self.kernel_size, self.kernel_size)

@@ -47,6 +47,11 @@ class FullyConnectedLayer(nn.Module):
         if self.activation == 'linear':
             return torch.addmm(b.unsqueeze(0), x, w.t()) if b is not None else x.matmul(w.t())
         y = x.matmul(w.t())
+        if self.activation in ('relu', 'lrelu') and y.is_cuda:
+            # bias + activation in one HIP bias_act pass (gain 1: F.relu / F.leaky_relu(0.2) semantics)
+            from torch_utils.ops import bias_act
+            return bias_act.bias_act(y, b, act=self.activation, alpha=0.2 if self.activation == 'lrelu' else None,
+                                     gain=1.0)
         if b is not None:
             y = y + b
         if self.activation == 'relu':
@@ -90,6 +95,49 @@ class GroupNorm32(nn.GroupNorm):
     def forward(self, x):
         from torch_utils.ops import decoder_ops
         return decoder_ops.group_norm(x, self.num_groups, self.weight, self.bias, self.eps, out_dtype=x.dtype)
+
+
+def _conv_dtype(x):
+    """The dtype nn.Conv2d would compute in: autocast's dtype inside a CUDA autocast region."""
+    if x.is_cuda and torch.is_autocast_enabled('cuda'):
+        return torch.get_autocast_dtype('cuda')
+    return x.dtype
+
+
+class DepthwiseConv2d(nn.Conv2d):
+    """nn.Conv2d(C, C, k, padding=p, groups=C) (same parameters / state-dict keys) on the HIP
+    depthwise kernel (decoder_ops.dwconv2d); the z-conv stems' 3x3 (reference generator.py:839-868)."""
+
+    def forward(self, x):
+        if not x.is_cuda or self.groups != x.shape[1] or self.stride != (1, 1) or self.dilation != (1, 1) \
+                or self.padding_mode != 'zeros' or self.padding[0] != self.padding[1]:
+            return super().forward(x)
+        from torch_utils.ops import decoder_ops
+        return decoder_ops.dwconv2d(x.to(_conv_dtype(x)), self.weight, self.bias, self.padding[0])
+
+
+class Conv1x1(nn.Conv2d):
+    """nn.Conv2d(I, O, 1) as the decoder's 1x1 GEMM (decoder_ops.pointwise: HIP f32x3 / bf16 MFMA GEMM
+    forward, data and weight gradient)."""
+
+    def forward(self, x):
+        if not x.is_cuda or self.kernel_size != (1, 1) or self.stride != (1, 1) or self.groups != 1 \
+                or self.padding != (0, 0):
+            return super().forward(x)
+        from torch_utils.ops import decoder_ops
+        B, C, H, W = x.shape
+        x = x.to(_conv_dtype(x))
+        y = decoder_ops.pointwise(self.weight.reshape(self.out_channels, C), x.reshape(B, C, H * W))
+        y = y.reshape(B, self.out_channels, H, W)
+        return y + self.bias.to(y.dtype)[None, :, None, None] if self.bias is not None else y
+
+
+class LeakyReLU(nn.LeakyReLU):
+    """nn.LeakyReLU on the HIP bias_act kernel (gain 1)."""
+
+    def forward(self, x):
+        from torch_utils.ops import bias_act
+        return bias_act.bias_act(x, act='lrelu', alpha=self.negative_slope, gain=1.0)
 
 
 class StyleSplit(nn.Module):

@@ -62,6 +62,20 @@ SIGNATURES = {
     "vfm_gemm8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
                       c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "vfm_gemm8_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "vfm_im2col_nhwc_f32": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_col2im_nhwc_f32": [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                            c_int, c_vp],
+    "vfm_rowdot_f32": [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
+    "vfm_coldot_splits": [c_int, c_int],
+    "vfm_coldot_f32": [c_vp, c_ll, c_vp, c_vp, c_int, c_int, c_int, c_vp],
+    "vfm_bnl_workspace_floats": [c_int, c_int, c_int, c_int],
+    "vfm_bnl_lrelu_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_float,
+                          c_vp],
+    "vfm_bnl_lrelu_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                          c_float, c_vp],
+    "vfm_torgb_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_torgb_bwd_splits": [c_int, c_int, c_int],
+    "vfm_torgb_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_split3": [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp],
     "vfm_gemm_workspace_floats": [c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int,
@@ -105,6 +119,7 @@ def get_native():
                 fn.argtypes = argtypes
                 fn.restype = c_int
             lib.vfm_version.restype = ctypes.c_char_p
+            lib.vfm_bnl_workspace_floats.restype = c_ll
             _lib = lib
     return _lib
 

@@ -577,3 +577,64 @@ def shuffle_blur(x, blur1d, upscale):
 
 def blur_replicate(x, blur1d):
     return _ShuffleBlur.apply(x, tuple(blur1d), 1)
+
+
+# ---------------------------------------------------------------------------
+# ToRGB: modulated 1x1 to O <= 4 channels + bias (reference convnext_utils.py:145-187), one
+# HBM pass per direction (csrc/torgb.hip); dstyle / dweight / dbias from the kernel's [B, O, C]
+# partials on the host side (tiny).
+
+
+class _ToRGB(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w2, style, bias):
+        _edges(ctx, x, w2, style, bias)
+        B, C, H, W = x.shape
+        O, P = w2.shape[0], H * W
+        x = _c(x)
+        s32, w32 = style.detach().float(), w2.detach().float()
+        wm = (w32[None] * s32[:, None, :]).contiguous()                      # [B, O, C]
+        b32 = bias.detach().reshape(-1).float().contiguous()
+        y = torch.empty([B, O, H, W], dtype=torch.float32, device=x.device)
+        with kernel_timer.region(_rn('torgb_fwd', x), _nb(x, y)):
+            _check(_lib.vfm_torgb_fwd(x.data_ptr(), wm.data_ptr(), b32.data_ptr(), y.data_ptr(), _code(x), B, O, C, P,
+                                      _stream()), 'vfm_torgb_fwd')
+        ctx.save_for_backward(x, wm, s32, w32)
+        ctx.meta = (w2.dtype, style.dtype, bias.dtype, bias.shape)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x, wm, s32, w32 = ctx.saved_tensors
+        wdt, sdt, bdt, bshape = ctx.meta
+        B, C, H, W = x.shape
+        O, P = wm.shape[1], H * W
+        dy = _c(dy.float())
+        dx = dw = ds = db = None
+        S = _lib.vfm_torgb_bwd_splits(B, C, P)
+        dxt = torch.empty_like(x)
+        tpart = torch.empty([B, S, O, C], dtype=torch.float32, device=x.device)
+        with kernel_timer.region(_rn('torgb_bwd', x), _nb(x, dy, dxt)):
+            _check(_lib.vfm_torgb_bwd(x.data_ptr(), dy.data_ptr(), wm.data_ptr(), dxt.data_ptr(), tpart.data_ptr(),
+                                      _code(x), B, O, C, P, S, _stream()), 'vfm_torgb_bwd')
+        T = tpart.sum(1)                                                        # [B, O, C]
+        if _wanted(ctx, 0):
+            dx = dxt
+        if _wanted(ctx, 1):
+            dw = (T * s32[:, None, :]).sum(0).to(wdt)
+        if _wanted(ctx, 2):
+            ds = (T * w32[None]).sum(1).to(sdt)
+        if _wanted(ctx, 3):
+            db = dy.sum((0, 2, 3)).reshape(bshape).to(bdt)
+        return dx, dw, ds, db
+
+
+def torgb_supported(x, O):
+    B, C, H, W = x.shape
+    return x.dtype in (torch.float32, torch.bfloat16) and 1 <= O <= 4 and (H * W) % 8 == 0 and C % 16 == 0
+
+
+def torgb(x, w2, style, bias):
+    """y = (w2 @ (style * x)) + bias in fp32: x [B, C, H, W], w2 [O, C], style [B, C], bias [1, O, 1, 1]."""
+    return _ToRGB.apply(x, w2, style, bias)

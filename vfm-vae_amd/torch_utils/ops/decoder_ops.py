@@ -155,6 +155,20 @@ def blur_replicate(x, blur1d, impl='cuda'):
     return F.conv2d(F.pad(x, pad, mode='replicate'), w, groups=c)
 
 
+def torgb(x, weight2d, style, bias, impl='cuda'):
+    """Modulated (no demodulation) 1x1 conv to the image channels + bias, fp32 result:
+    (W @ (style * x)) + bias (reference convnext_utils.py:145-187). ROCm tensors run the fused
+    HIP kernels (csrc/torgb.hip); elsewhere the torch formulation."""
+    if impl == 'cuda' and x.is_cuda and not _FORCE_REF:
+        from . import decoder_hip
+        if decoder_hip.torgb_supported(x, weight2d.shape[0]):
+            return decoder_hip.torgb(x, weight2d, style, bias)
+    B, C, H, W = x.shape
+    xm = x * style.to(x.dtype)[:, :, None, None]
+    y = pointwise(weight2d, xm.reshape(B, C, H * W), impl=impl).reshape(B, -1, H, W)
+    return y + bias
+
+
 def convnext_mlp_fusable(m, C, P, x_in):
     """True when the layer's pointwise -> GELU -> pointwise -> residual chain can run as
     one forward kernel (with or without autograd): ROCm bf16 activations, a supported

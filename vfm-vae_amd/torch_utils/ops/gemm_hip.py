@@ -170,6 +170,8 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
                 n = _lib.vfm_gemm8_workspace_floats(M, N, Kf, z, kchunk, int(reduce_batch))
                 ws = torch.empty(max(n, 0), dtype=torch.float32, device=A.device) if n > 0 else None
                 region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
+                if kernel_timer.SHAPES:
+                    region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}k{kchunk}]"
                 with kernel_timer.region(region, 0, flops, "mfma"):
                     rc = _lib.vfm_gemm8(*args, custom_ops.ptr(ws), kchunk, int(reduce_batch), stream)
                 if rc != custom_ops.VFM_NO_KERNEL:
@@ -179,6 +181,8 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             # one timer region per kernel instantiation (rocprof: gemm8_kernel<AK, BK, OUTF32>)
             kname = "gemm8" if GEMM8 else "gemm_fast"
             region = f"{kname}<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
+            if kernel_timer.SHAPES:
+                region += f"[{M}x{N}x{K}x{z}]"
             with kernel_timer.region(region, 0, flops, "mfma"):
                 if GEMM8:
                     rc = _lib.vfm_gemm8(*args, None, 0, 0, stream)
@@ -192,7 +196,14 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         n = _lib.vfm_gemm_workspace_floats(M, N, z, splits, int(reduce_batch))
         ws = torch.empty(n, dtype=torch.float32, device=A.device)
     tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
-    with kernel_timer.region(f"gemm<{tag}>", 0, flops, "mfma"):
+    tb = lambda v: "true" if v else "false"
+    # one region per gemm_kernel<AK, BK, F32, OUTF32> instantiation; split-K / batch-reduced
+    # launches (kernel + gemm_reduce_kernel) are their own region
+    kname = "gemm_ws" if ws is not None else "gemm"
+    region = f"{kname}<{tag},{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
+    if kernel_timer.SHAPES:
+        region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
+    with kernel_timer.region(region, 0, flops, "mfma"):
         rc = _lib.vfm_gemm(A.data_ptr(), B.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(ws),
                            _CODES[A.dtype], _CODES[out_dtype], M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB,
                            ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], int(splits), int(reduce_batch),

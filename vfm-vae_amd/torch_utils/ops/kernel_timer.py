@@ -8,8 +8,13 @@ the kernel with the largest total time and returns the bench.py `roofline`
 object (achieved = algorithmic bytes or flops per launch / average launch time).
 """
 import contextlib
+import os
 
 import torch
+
+# VFM_TIMER_SHAPES=1: GEMM regions carry their [MxNxKxz] shape (a breakdown for tuning; the
+# bench line's roofline then ranks per shape)
+SHAPES = os.environ.get("VFM_TIMER_SHAPES", "0") == "1"
 
 _enabled = False
 _records = {}      # name -> list of (start_event, end_event, bytes, flops, bound)
@@ -99,10 +104,14 @@ _TNAME = {"f32": "float", "bf16": "__hip_bfloat16", "f16": "__half", "f64": "dou
 
 def rocprof_name(region):
     """'scale_bias_gelu_bwd<bf16>' -> 'gelu_bwd<__hip_bfloat16>' (a prefix of the rocprof name)."""
+    region = region.split("[", 1)[0]
     base, _, args = region.partition("<")
     args = args.rstrip(">").split(",") if args else []
     if base in ("gemm8", "gemm_fast") and len(args) == 4:      # <tag, AK, BK, OUTF32>
         return f"{base}_kernel<{args[1]}, {args[2]}, {args[3]}>"
+    if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, F32, OUTF32>
+        f32 = "true" if args[0] == "f32x3" else "false"
+        return f"gemm_kernel<{args[1]}, {args[2]}, {f32}, {args[3]}>"
     pat = _ROC.get(base)
     if pat is None:
         return None

@@ -1,0 +1,179 @@
+"""Multi-scale PatchGAN discriminator on the gfx950 kernels (stage 3; reference
+networks/discriminator.py:75-99 BatchNormLocal2d, :180-228 NLayerDiscriminator).
+
+Activations are NHWC fp32 (channels_last views of the reference's NCHW tensors). A k4 conv is
+im2col (csrc/patchgan.hip) + our MFMA GEMM (gemm_hip, fp32 through the 3-term bf16 split) with the
+bias fused into the GEMM epilogue; its weight gradient is the same GEMM (split-K over the pixels) and
+its data gradient a GEMM followed by the col2im gather. The 1-channel logit layer uses a row dot /
+column dot instead of a 1-wide GEMM. BatchNormLocal2d + LeakyReLU(0.2) run as one fused forward and
+one fused backward (virtual-batch statistics, deterministic partial sums). Layer 0's bias + LeakyReLU
+is the HIP bias_act kernel.
+
+Only reached for ROCm fp32 tensors (`supported`); a missing kernel library raises.
+"""
+import torch
+
+from .. import custom_ops
+from . import kernel_timer
+
+_lib = custom_ops.get_native()
+
+
+def _stream():
+    return custom_ops.stream_ptr()
+
+
+def _check(rc, name):
+    custom_ops.check(rc, name)
+
+
+def _c16(t):
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def _gemm(A, B, **kw):
+    from . import gemm_hip
+    return gemm_hip.gemm(A, B, out_dtype=torch.float32, **kw)
+
+
+def _splits(M, N, K):
+    tiles = -(-M // 128) * -(-N // 128)
+    return max(1, min(-(-1024 // tiles), K // 512, 64))
+
+
+def _im2col(xh, k, stride, pad, Ho, Wo):
+    B, H, W, C = xh.shape
+    K = k * k * C
+    A = torch.empty([B * Ho * Wo, K], dtype=torch.float32, device=xh.device)
+    with kernel_timer.region("im2col_nhwc<f32>", 4 * (xh.numel() + A.numel())):
+        _check(_lib.vfm_im2col_nhwc_f32(xh.data_ptr(), A.data_ptr(), K, B, H, W, C, Ho, Wo, k, stride, pad, _stream()),
+               "vfm_im2col_nhwc_f32")
+    return A
+
+
+class _ConvNHWC(torch.autograd.Function):
+    """y[b, oy, ox, o] = sum_{ky, kx, c} x[b, s oy - p + ky, s ox - p + kx, c] w[o, c, ky, kx] (+ bias[o])."""
+
+    @staticmethod
+    def forward(ctx, xh, weight, bias, stride, pad):
+        B, H, W, C = xh.shape
+        O, _, k, _ = weight.shape
+        Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        xh = _c16(xh)
+        A = _im2col(xh, k, stride, pad, Ho, Wo)
+        Wm = weight.detach().permute(0, 2, 3, 1).reshape(O, k * k * C).float().contiguous()   # [O, K] tap-major
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        M = B * Ho * Wo
+        if O == 1:
+            y = torch.empty([M], dtype=torch.float32, device=xh.device)
+            with kernel_timer.region("rowdot<f32>", 4 * (A.numel() + M), flops=2.0 * A.numel(), bound="hbm"):
+                _check(_lib.vfm_rowdot_f32(A.data_ptr(), A.shape[1], Wm.data_ptr(), custom_ops.ptr(b32), y.data_ptr(),
+                                           M, A.shape[1], _stream()), "vfm_rowdot_f32")
+        else:
+            y = _gemm(A, Wm.t(), bias=b32, bias_dim=1)
+        ctx.save_for_backward(A, Wm)
+        ctx.geo = (B, H, W, C, Ho, Wo, k, stride, pad, O)
+        ctx.meta = (weight.dtype, None if bias is None else bias.dtype)
+        ctx.needs = (ctx.needs_input_grad[0], ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2])
+        return y.reshape(B, Ho, Wo, O)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        A, Wm = ctx.saved_tensors
+        B, H, W, C, Ho, Wo, k, stride, pad, O = ctx.geo
+        wdt, bdt = ctx.meta
+        nx, nw, nb = ctx.needs
+        M, K = A.shape
+        dy = _c16(dy.float().reshape(M, O))
+        dx = dw = db = None
+        if nb:
+            db = dy.sum(0).to(bdt)
+        if nw:
+            if O == 1:
+                S = _lib.vfm_coldot_splits(M, K)
+                part = torch.empty([S, K], dtype=torch.float32, device=dy.device)
+                with kernel_timer.region("coldot<f32>", 4 * (A.numel() + M + part.numel()), flops=2.0 * A.numel()):
+                    _check(_lib.vfm_coldot_f32(A.data_ptr(), K, dy.data_ptr(), part.data_ptr(), M, K, S, _stream()),
+                           "vfm_coldot_f32")
+                dWm = part.sum(0, keepdim=True)
+            else:
+                dWm = _gemm(dy.t(), A, splits=_splits(O, K, M))
+            dw = dWm.reshape(O, k, k, C).permute(0, 3, 1, 2).contiguous().to(wdt)
+        if nx:
+            dX = torch.empty([B, H, W, C], dtype=torch.float32, device=dy.device)
+            if O == 1:
+                dA, dy1, w1 = None, dy, Wm
+            else:
+                dA, dy1, w1 = _gemm(dy, Wm), None, None
+            with kernel_timer.region("col2im_nhwc<f32>", 4 * (dX.numel() + (dA.numel() if dA is not None else M))):
+                _check(_lib.vfm_col2im_nhwc_f32(custom_ops.ptr(dA), K, custom_ops.ptr(dy1), custom_ops.ptr(w1),
+                                                dX.data_ptr(), B, H, W, C, Ho, Wo, k, stride, pad, _stream()),
+                       "vfm_col2im_nhwc_f32")
+            dx = dX
+        return dx, dw, db, None, None
+
+
+class _BnLocalLReLU(torch.autograd.Function):
+    """lrelu(BatchNormLocal2d(x)) over NHWC x [B, H, W, C], G virtual batches."""
+
+    @staticmethod
+    def forward(ctx, xh, weight, bias, G, eps, slope):
+        B, H, W, C = xh.shape
+        P = H * W
+        xh = _c16(xh)
+        w32 = None if weight is None else weight.detach().float().contiguous()
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        n = _lib.vfm_bnl_workspace_floats(B, P, C, G)
+        ws = torch.empty([n], dtype=torch.float32, device=xh.device)
+        mean = torch.empty([G, C], dtype=torch.float32, device=xh.device)
+        rstd = torch.empty_like(mean)
+        y = torch.empty_like(xh)
+        with kernel_timer.region("bnl_lrelu_fwd<f32>", 4 * 4 * xh.numel()):
+            _check(_lib.vfm_bnl_lrelu_fwd(xh.data_ptr(), custom_ops.ptr(w32), custom_ops.ptr(b32), y.data_ptr(),
+                                          mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), B, P, C, G, float(eps),
+                                          float(slope), _stream()), "vfm_bnl_lrelu_fwd")
+        ctx.save_for_backward(xh, w32, b32, mean, rstd)
+        ctx.cfg = (G, slope, None if weight is None else weight.dtype, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        xh, w32, b32, mean, rstd = ctx.saved_tensors
+        G, slope, wdt, bdt = ctx.cfg
+        B, H, W, C = xh.shape
+        P = H * W
+        dy = _c16(dy.float())
+        n = _lib.vfm_bnl_workspace_floats(B, P, C, G)
+        ws = torch.empty([n], dtype=torch.float32, device=xh.device)
+        dx = torch.empty_like(xh)
+        dw = torch.empty([C], dtype=torch.float32, device=xh.device) if w32 is not None else None
+        db = torch.empty([C], dtype=torch.float32, device=xh.device) if b32 is not None else None
+        with kernel_timer.region("bnl_lrelu_bwd<f32>", 4 * 4 * xh.numel()):
+            _check(_lib.vfm_bnl_lrelu_bwd(xh.data_ptr(), dy.data_ptr(), custom_ops.ptr(w32), custom_ops.ptr(b32),
+                                          mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), custom_ops.ptr(dw),
+                                          custom_ops.ptr(db), ws.data_ptr(), B, P, C, G, float(slope), _stream()),
+                   "vfm_bnl_lrelu_bwd")
+        return (dx, None if dw is None else dw.to(wdt), None if db is None else db.to(bdt), None, None, None)
+
+
+def supported(x):
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+
+
+def conv_nhwc(xh, weight, bias, stride, pad):
+    return _ConvNHWC.apply(xh, weight, bias, int(stride), int(pad))
+
+
+def bn_local_lrelu(xh, weight, bias, groups, eps, slope):
+    return _BnLocalLReLU.apply(xh, weight, bias, int(groups), float(eps), float(slope))
+
+
+def bias_lrelu(yh, bias, slope):
+    """lrelu(y + bias[c]) over NHWC y (HIP bias_act, gain 1)."""
+    from . import bias_act
+    C = yh.shape[-1]
+    y2 = bias_act.bias_act(yh.reshape(-1, C), bias, dim=1, act='lrelu', alpha=slope, gain=1.0)
+    return y2.reshape(yh.shape)
