@@ -343,6 +343,15 @@ int vfm_lpips_head_fwd_nhwc(const float* f0, const float* f1, const float* w, fl
 int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, const float* n0, const float* n1,
                             const float* gs, float* g0, float* g1, int B, int C, long long HW, void* stream);
 
+/* Depthwise K x K conv (K in {3, 5, 7}, pad (K-1)/2, stride 1) of bf16 NCHW planes on the MFMA
+ * cores (banded-matrix form, csrc/dwconv_mfma.hip); same contract as vfm_dwconv2d_fwd (noise: fp32
+ * [H, W] added to every channel, or NULL), taps w fp32 [C, K, K] rounded to bf16 (the reference's
+ * autocast conv: replaces convnext_utils.py:121-124 / :243 nn.Conv2d(groups=C) for the bf16 blocks,
+ * and its data gradient with the rotated taps). W % 16 == 0, 16-B aligned x / y / noise;
+ * VFM_NO_KERNEL otherwise. */
+int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise, void* y, int B,
+                          int C, int H, int W, int K, int pad, void* stream);
+
 /* ---- ToRGB: modulated 1x1 (no demodulation) to O <= 4 image channels ----------------------
  * Replaces networks/utils/convnext_utils.py:145-187 (ConvNeXtToRGBLayer.forward: x * style, 1x1
  * conv, + bias) in both directions as one HBM pass.
@@ -357,6 +366,16 @@ int vfm_torgb_fwd(const void* x, const float* wm, const float* bias, float* y, i
 int vfm_torgb_bwd_splits(int B, int C, int P);
 int vfm_torgb_bwd(const void* x, const float* dy, const float* wm, void* dx, float* tpart, int dtype, int B, int O,
                   int C, int P, int S, void* stream);
+
+/* ---- Latent posterior (replaces networks/utils/kl_utils.py:30-56 DiagonalGaussianDistribution's
+ * sample() and kl() on the continuous latent): params fp32 [B, 2C, P] (mean | logvar channels),
+ * eps fp32 [B, C, P] (drawn by the caller as the reference does); z = mean + exp(clamp(logvar,
+ * -30, 20) / 2) eps, kl[b] = 0.5 sum_{c,p}(mean^2 + exp(lv) - 1 - lv) (z or kl may be NULL).
+ * bwd: dz [B, C, P] and dkl [B] (either may be NULL) -> dparams [B, 2C, P]. Deterministic. */
+int vfm_posterior_fwd(const float* params, const float* eps, float* z, float* kl, int B, int C, long long P,
+                      void* stream);
+int vfm_posterior_bwd(const float* params, const float* eps, const float* dz, const float* dkl, float* dparams,
+                      int B, int C, long long P, void* stream);
 
 /* ---- Multi-scale PatchGAN (stage 3), fp32 NHWC ----------------------------------------------
  * Replace networks/discriminator.py:180-228 (NLayerDiscriminator's nn.Conv2d k4 s2/s1 p2 layers,

@@ -43,7 +43,8 @@ def _run(fn_hip, fn_ref, inputs, dt, names, out_grad_seed=0):
     torch.cuda.synchronize()
     recorded = set(kt.summary())
     kt.enable(False)
-    base = {r.split('<')[0] for r in recorded}        # region names carry <dtype,taps>
+    # region names carry <dtype,taps>; the banded-MFMA dwconv (bf16) counts as the dwconv op
+    base = {r.split('<')[0].replace('dwconv2d_mfma', 'dwconv2d') for r in recorded}
     for n in names:
         assert n in base, (n, recorded)
     ref_in = [None if t is None else t.detach().to(DEV).double().float().requires_grad_(t.requires_grad)
@@ -80,6 +81,28 @@ def test_dwconv2d(case, dt):
     hip = lambda x, w, b, n: ops.dwconv2d(x.to(dt), w, b, K // 2, noise=n)
     ref = lambda x, w, b, n: ops.dwconv2d(x, w, b, K // 2, noise=n, impl='ref')
     _run(hip, ref, [x, w, b, noise], dt, ["dwconv2d_fwd", "dwconv2d_bwd_data", "dwconv2d_bwd_weight"])
+
+
+@pytest.mark.parametrize("case", [(2, 8, 16, 16, 3), (2, 6, 16, 16, 5), (2, 5, 20, 64, 7), (1, 3, 64, 256, 7),
+                                  (3, 4, 37, 48, 7), (2, 3, 8, 128, 5), (1, 2, 5, 32, 3)])
+def test_dwconv2d_mfma(case):
+    """The banded-MFMA depthwise kernel (csrc/dwconv_mfma.hip): bf16 planes, no noise, forward and
+    data gradient (both on MFMA; the weight gradient stays on the row kernel) vs the fp32 torch
+    formulation with the taps rounded to bf16, as the reference's autocast conv uses them."""
+    ops, kt = _ops()
+    B, C, H, W, K = case
+    torch.manual_seed(2)
+    x = torch.randn(B, C, H, W).to(torch.bfloat16).float().requires_grad_(True)
+    w = (torch.randn(C, 1, K, K) * 0.2).to(torch.bfloat16).float().requires_grad_(True)
+    b = (torch.randn(C) * 0.1).requires_grad_(True)
+    hip = lambda x, w, b: ops.dwconv2d(x.to(torch.bfloat16), w, b, K // 2)
+    ref = lambda x, w, b: ops.dwconv2d(x, w, b, K // 2, impl='ref')
+    _run(hip, ref, [x, w, b], torch.bfloat16, ["dwconv2d_fwd", "dwconv2d_bwd_data", "dwconv2d_bwd_weight"])
+    kt.enable(True)
+    ops.dwconv2d(x.detach().to(DEV, torch.bfloat16), w.detach().to(DEV), b.detach().to(DEV), K // 2)
+    torch.cuda.synchronize()
+    assert any(n.startswith("dwconv2d_mfma_fwd") for n in kt.summary()), kt.summary()
+    kt.enable(False)
 
 
 def test_dwconv2d_no_bias_valid_padding():
@@ -286,3 +309,39 @@ def test_torgb(dt, B, C, H, W, O):
         return torch.einsum('oc,bchw->bohw', w2, x * st[:, :, None, None]) + bias
 
     _run(hip, ref, [x, w2, st, bias], dt, ['torgb_fwd', 'torgb_bwd'])
+
+
+@pytest.mark.parametrize("B,C,H", [(4, 32, 16), (3, 8, 5)])
+def test_posterior_sample_kl(B, C, H):
+    """Fused posterior sample + KL (csrc/posterior.hip) vs DiagonalGaussianDistribution's torch ops
+    (reference kl_utils.py:30-56) on the same epsilon: z, kl, and the moment gradients of a loss on
+    both outputs (logvar values beyond the clamp included, whose gradient is zero)."""
+    from networks.utils import kl_utils
+    _, kt = _ops()
+    g = torch.Generator().manual_seed(B * C + H)
+    params = torch.randn(B, 2 * C, H, H, generator=g)
+    params[:, C:, 0, 0] = 25.0              # clamped above
+    params[:, C:, 1, 0] = -35.0             # clamped below
+    eps = torch.randn(B, C, H, H, generator=g)
+    wz = torch.randn(B, C, H, H, generator=g)
+    wk = torch.randn(B, generator=g)
+    kl_utils.set_noise_source(lambda shape: eps.clone())
+    try:
+        pg = params.to(DEV).requires_grad_()
+        kt.enable(True)
+        z, kl = kl_utils.sample_and_kl(pg)
+        ((z * wz.to(DEV)).sum() + (kl * wk.to(DEV)).sum()).backward()
+        torch.cuda.synchronize()
+        names = set(kt.summary())
+        kt.enable(False)
+        assert "posterior_fwd<f32>" in names and "posterior_bwd<f32>" in names, names
+        pr = params.double().requires_grad_()
+        post = kl_utils.DiagonalGaussianDistribution(pr)
+        zr = post.sample()
+        klr = post.kl()
+        ((zr * wz.double()).sum() + (klr * wk.double()).sum()).backward()
+    finally:
+        kl_utils.set_noise_source(None)
+    assert _rel(z, zr) < 1e-6
+    assert _rel(kl, klr) < 1e-6
+    assert _rel(pg.grad, pr.grad) < 1e-5

@@ -48,6 +48,7 @@ for s in "$@"; do
     bsteps)  timeout -k 10 900 python bench.py --steps 6 --warmup 2 --trace --no-cpu-baseline > $out/bsteps.log 2>&1 ;;
     bstepsng) timeout -k 10 900 python bench.py --steps 6 --warmup 2 --trace --no-cpu-baseline --no-gc-freeze > $out/bstepsng.log 2>&1 ;;
     tprof)   timeout -k 10 600 python tools_dev/torchprof.py --out $out/tp > $out/tprof.log 2>&1 ;;
+    gemmbench8) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;
     ptest)   timeout -k 10 ${PT_TIMEOUT:-900} python -u -m pytest $PT -m gpu -v --timeout ${PT_CASE:-240} --timeout-method thread > $out/ptest.log 2>&1 ;;
     attnbench) timeout -k 10 300 python tools_dev/attnbench.py > $out/attnbench.log 2>&1 ;;
     gc1)     REUSE=1 timeout -k 10 400 python tools_dev/graph_c1_debug.py > $out/gc1.log 2>&1; REUSE=0 timeout -k 10 400 python tools_dev/graph_c1_debug.py >> $out/gc1.log 2>&1 ;;

@@ -8,7 +8,7 @@ for i in 1 2 3 4; do
   rc=$?
   if [ $rc -eq 3 ] || grep -q "status=transient" "$log"; then
     echo "[retry] transient infrastructure failure ($i), waiting" >> "$log.retries"
-    sleep 90
+    sleep 200
     continue
   fi
   exit $rc

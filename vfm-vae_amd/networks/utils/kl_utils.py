@@ -72,6 +72,27 @@ class DiagonalGaussianDistribution(object):
         return self.mean
 
 
+def _draw_eps(shape, device, dtype):
+    """The noise DiagonalGaussianDistribution.sample() draws (same source, shape and order)."""
+    eps = _noise_source(tuple(shape)) if _noise_source is not None else torch.randn(shape)
+    return eps.to(device=device, dtype=dtype)
+
+
+def sample_and_kl(parameters, need_kl=True):
+    """(DiagonalGaussianDistribution(parameters).sample(), .kl() or None). fp32 ROCm moments run
+    the fused HIP kernel (torch_utils/ops/posterior_hip.py: one forward and one backward launch
+    instead of the ~12 elementwise / reduction kernels below); elsewhere the class itself."""
+    if parameters.is_cuda and parameters.dtype == torch.float32 and parameters.dim() >= 3:
+        from torch_utils.ops import posterior_hip
+        B, C2 = parameters.shape[:2]
+        eps = _draw_eps((B, C2 // 2) + tuple(parameters.shape[2:]), parameters.device, torch.float32)
+        z, kl = posterior_hip.sample_kl(parameters, eps)
+        return z, (kl if need_kl else None)
+    post = DiagonalGaussianDistribution(parameters)
+    z = post.sample()
+    return z, (post.kl() if need_kl else None)
+
+
 def normal_kl(mean1, logvar1, mean2, logvar2):
     ref = next(o for o in (mean1, logvar1, mean2, logvar2) if isinstance(o, torch.Tensor))
     logvar1, logvar2 = [t if isinstance(t, torch.Tensor) else torch.tensor(t).to(ref) for t in (logvar1, logvar2)]

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 from torch_utils import distributed as dist
 from torch_utils.ops import vit_ops
 from torch_utils.ops.linear import Linear, linear
+from networks.utils import kl_utils
 from networks.utils.kl_utils import DiagonalGaussianDistribution
 from networks.utils.quant_utils import VectorQuantizerM
 from networks.utils.dataclasses import EncodeOutput
@@ -289,10 +290,9 @@ class LDMAdapter(nn.Module):
         vq_loss = entropy_loss = usages = kl_loss = 0.0
         z_before_quantize = x
         if self.compression_mode == 'continuous':
-            posterior = DiagonalGaussianDistribution(x)
-            z = posterior.sample()
+            z, kl = kl_utils.sample_and_kl(x, need_kl=self.use_kl_loss)     # posterior sample (+ KL)
             if self.use_kl_loss:
-                kl_loss = posterior.kl().mean()
+                kl_loss = kl.mean()
         else:
             z_tokens, vq_loss, entropy_loss, usages = self.quantizer(_map_to_tokens(x))
             z = _tokens_to_map(z_tokens)

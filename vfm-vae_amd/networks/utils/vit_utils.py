@@ -19,16 +19,6 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from torch_utils.ops import vit_ops
-from torch_utils.ops import linear as hip_linear
-
-
-def _linear(x, lin):
-    """fp32 ROCm tokens (the discriminator's DINO tower): the HIP GEMM with autograd (f32x3,
-    torch_utils/ops/linear.py: forward, and the input gradient the frozen tower passes back to the
-    image); otherwise vit_ops.linear (bf16 towers, CPU)."""
-    if x.is_cuda and x.dtype == torch.float32:
-        return hip_linear.linear(x, lin.weight, lin.bias)
-    return vit_ops.linear(x, lin.weight.to(x.dtype), lin.bias)
 
 
 class PatchEmbed(nn.Module):
@@ -49,10 +39,10 @@ class Attention(nn.Module):
 
     def forward(self, x):
         B, N, D = x.shape
-        qkv = _linear(x, self.qkv)
+        qkv = vit_ops.linear(x, self.qkv.weight.to(x.dtype), self.qkv.bias)
         q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
         o = vit_ops.sdpa(q, k, v).transpose(1, 2).reshape(B, N, D)
-        return _linear(o, self.proj)
+        return vit_ops.linear(o, self.proj.weight.to(x.dtype), self.proj.bias)
 
 
 class Mlp(nn.Module):
@@ -62,8 +52,8 @@ class Mlp(nn.Module):
         self.fc2 = nn.Linear(hidden, dim)
 
     def forward(self, x):
-        h = F.gelu(_linear(x, self.fc1))
-        return _linear(h, self.fc2)
+        h = F.gelu(vit_ops.linear(x, self.fc1.weight.to(x.dtype), self.fc1.bias))
+        return vit_ops.linear(h, self.fc2.weight.to(x.dtype), self.fc2.bias)
 
 
 class Block(nn.Module):

@@ -73,6 +73,9 @@ SIGNATURES = {
                           c_vp],
     "vfm_bnl_lrelu_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                           c_float, c_vp],
+    "vfm_dwconv2d_fwd_mfma": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_posterior_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
+    "vfm_posterior_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_torgb_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_torgb_bwd_splits": [c_int, c_int, c_int],
     "vfm_torgb_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],

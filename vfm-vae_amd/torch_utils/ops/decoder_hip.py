@@ -208,11 +208,23 @@ def pointwise(w, x):
 # Depthwise conv (reference convnext_utils.py:121-124 / :243: nn.Conv2d(groups=C)).
 
 
+DW_MFMA = os.environ.get("VFM_DW_MFMA", "1") == "1"      # A/B switch for the banded-MFMA dwconv
+
+
 def _dw_fwd(x, w3, bias, noise, pad, name):
     B, C, H, W = x.shape
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
     y = torch.empty([B, C, Ho, Wo], dtype=x.dtype, device=x.device)
+    if DW_MFMA and x.dtype == torch.bfloat16 and 2 * pad == K - 1:
+        # bf16 planes: the banded-MFMA kernel (csrc/dwconv_mfma.hip); taps rounded to bf16 as
+        # the reference's autocast conv does
+        with kernel_timer.region(_rn(name.replace('dwconv2d', 'dwconv2d_mfma'), x, K), _nb(x, y)):
+            rc = _lib.vfm_dwconv2d_fwd_mfma(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), B, C, H,
+                                            W, K, pad, _stream())
+        if rc != custom_ops.VFM_NO_KERNEL:
+            _check(rc, name)
+            return y
     with kernel_timer.region(_rn(name, x, K), _nb(x, y)):
         _check(_lib.vfm_dwconv2d_fwd(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
                                      B, C, H, W, K, pad, _stream()), name)

@@ -45,10 +45,14 @@ from torch_utils.ops import conv2d_gradfix
 class FlatGradSync:
     """Owns the .grad storage of the trainable parameters of one phase."""
 
-    def __init__(self, module: nn.Module, bucket_mb: float = 64.0):
+    def __init__(self, module: nn.Module, bucket_mb: float = 64.0, collective: Optional[bool] = None):
         self.module = module
         self.bucket_mb = bucket_mb
         self.world = dist.get_world_size()
+        # collective=True runs the bucketed all-reduce path (comm stream, hooks, agreement check)
+        # even at world size 1 (an initialised 1-rank process group): how the RCCL path is
+        # exercised on a single GPU (tests/test_distributed_gpu.py)
+        self.collective = self.world > 1 if collective is None else bool(collective)
         self.params = []
         self.key = None
         self.hooks = []
@@ -82,7 +86,7 @@ class FlatGradSync:
                 start, n, cnt = start + n, 0, 0
         if cnt:
             self.buckets.append((start, start + n, cnt))
-        if dev.type == 'cuda' and self.world > 1:
+        if dev.type == 'cuda' and self.collective:
             self.comm_stream = torch.cuda.Stream(device=dev)
         for p in params:
             self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -141,7 +145,7 @@ class FlatGradSync:
 
     def _on_grad(self, p):
         self.seen.add(id(p))
-        if not self.last_microbatch or self.world <= 1:
+        if not self.last_microbatch or not self.collective:
             return
         bi = self.bucket_of[id(p)]
         if bi in self.pending:              # a second backward touched a bucket already in flight
@@ -165,7 +169,7 @@ class FlatGradSync:
         """Complete the reduction: flat = nan_to_num(sum_ranks / world * gain)."""
         if not self.params:
             return
-        if self.world > 1:
+        if self.collective:
             for bi in range(len(self.buckets)):
                 if bi not in self.pending:
                     self._launch(bi)
