@@ -351,6 +351,13 @@ int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, co
  * VFM_NO_KERNEL otherwise. */
 int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise, void* y, int B,
                           int C, int H, int W, int K, int pad, void* stream);
+/* Weight (and bias) gradient of the same conv on MFMA: partial[t, c, 0 .. K*K-1] = per-wave sums of
+ * dW[c][ky][kx] = sum dy[b,c,y,x] x[b,c,y+ky-pad,x+kx-pad], partial[t, c, K*K] = sum dy; t < tiles
+ * = vfm_dwconv2d_bwd_weight_mfma_tiles(...) (same partial layout as vfm_dwconv2d_bwd_weight; the
+ * caller sums over t in a fixed order). bf16 x / dy, W % 16 == 0. */
+int vfm_dwconv2d_bwd_weight_mfma_tiles(int B, int C, int H, int W, int K, int pad);
+int vfm_dwconv2d_bwd_weight_mfma(const void* x, const void* dy, float* partial, int B, int C, int H, int W, int K,
+                                 int pad, void* stream);
 
 /* ---- ToRGB: modulated 1x1 (no demodulation) to O <= 4 image channels ----------------------
  * Replaces networks/utils/convnext_utils.py:145-187 (ConvNeXtToRGBLayer.forward: x * style, 1x1

@@ -103,6 +103,22 @@ def test_dwconv2d_mfma(case):
     torch.cuda.synchronize()
     assert any(n.startswith("dwconv2d_mfma_fwd") for n in kt.summary()), kt.summary()
     kt.enable(False)
+    # the weight gradient on MFMA as well (bf16 x / dy)
+    kt.enable(True)
+    xg = x.detach().to(DEV, torch.bfloat16).requires_grad_(False)
+    wg = w.detach().to(DEV).requires_grad_(True)
+    bg = b.detach().to(DEV).requires_grad_(True)
+    dyg = torch.randn(B, C, H, W).to(DEV, torch.bfloat16)
+    ops.dwconv2d(xg, wg, bg, K // 2).backward(dyg)
+    torch.cuda.synchronize()
+    assert any(n.startswith("dwconv2d_mfma_bwd_weight") for n in kt.summary()), kt.summary()
+    kt.enable(False)
+    xr = x.detach().double().requires_grad_(False)
+    wr = w.detach().double().requires_grad_(True)
+    br = b.detach().double().requires_grad_(True)
+    torch.nn.functional.conv2d(xr, wr, br, padding=K // 2, groups=C).backward(dyg.double().cpu())
+    assert _rel(wg.grad, wr.grad) < 1e-5, _rel(wg.grad, wr.grad)
+    assert _rel(bg.grad, br.grad) < 1e-5
 
 
 def test_dwconv2d_no_bias_valid_padding():

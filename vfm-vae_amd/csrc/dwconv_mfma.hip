@@ -156,6 +156,171 @@ int dwm_launch(DwmArgs& a, hipStream_t st) {
     return launch_status();
 }
 
+
+// ---- weight gradient -------------------------------------------------------------------------
+//   dW[ky][kx] = sum_{b, y, x} dY[y][x] X[y + ky - P][x + kx - P],   db = sum dY
+// per 32-row x 16-column dY tile and kernel row ky, with j over the 32 input columns x0 - 8 + j:
+//   T_ky[i][j] = sum_{n < 32} dY[y0 + n][x0 + i] X[y0 + n + ky - P][x0 - 8 + j]   (one MFMA per j-half)
+//   dW[ky][kx] = sum_i T_ky[i][i + kx + 8 - P]                                     (diagonals, once per wave)
+// Both operands run along the rows (the MFMA k dimension), i.e. against the memory layout: the
+// fragments come from the LDS images with ds_read_b64_tr_b16 (the hardware transpose read). T_ky
+// accumulates in registers over all tiles of the wave's bands; at the end the accumulators go to LDS
+// and 49 lanes sum the diagonals. One fp32 partial [K K + 1] per wave (host sums in a fixed order).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct DwmBwArgs {
+    const __hip_bfloat16* x;
+    const __hip_bfloat16* dy;
+    float* partial;                       // [tiles, C, K K + 1]
+    int B, C, H, W, nyb, nxs, tiles, per; // per: bands per wave; bands per channel = B nyb nxs
+};
+
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned char* lo, const unsigned char* hi) {
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo);
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int K, int XW>
+__global__ __launch_bounds__(64 * 2) void dwm_bwd_w(DwmBwArgs a) {
+    constexpr int P = (K - 1) / 2;
+    constexpr int RSD = ((XW * 2 / 16) | 1) * 16;           // dY image row stride (bytes)
+    constexpr int NQX = XW / 8 + 2;
+    constexpr int RSX = ((NQX * 16 / 16) | 1) * 16;         // X image row stride
+    constexpr int NRX = 32 + K - 1;
+    constexpr int QD = 32 * XW / 8, QX = NRX * NQX;          // 16-B chunks per band
+    constexpr int LD = (QD + 63) / 64, LX = (QX + 63) / 64;
+    constexpr int IMG = 32 * RSD + NRX * RSX;
+    constexpr int SCR = K * 16 * 32 * 4;                     // diagonal scratch (end of the wave)
+    constexpr int AREA = ((IMG > SCR ? IMG : SCR) + 15) / 16 * 16;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2][AREA];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long wg = (long long)blockIdx.x * 2 + wave;
+    if (wg >= (long long)a.C * a.tiles) return;             // wave-uniform
+    const int c = (int)(wg / a.tiles), tile = (int)(wg - (long long)c * a.tiles);
+    unsigned char* dimg = lds[wave];
+    unsigned char* ximg = dimg + 32 * RSD;
+    const int nbands = a.B * a.nyb * a.nxs;
+    const int band0 = tile * a.per, band1 = min(nbands, band0 + a.per);
+
+    uint4 sd[LD], sx[LX];
+    auto fetch = [&](int band) {
+        const int xs = band % a.nxs;
+        const int t = band / a.nxs;
+        const int yb = t % a.nyb, b = t / a.nyb;
+        const int x0 = xs * XW, y0 = yb * 32;
+        const long long plane = ((long long)b * a.C + c) * a.H * a.W;
+#pragma unroll
+        for (int u = 0; u < LD; ++u) {
+            const int q = lane + 64 * u, r = q / (XW / 8), ch = q - r * (XW / 8);
+            sd[u] = make_uint4(0, 0, 0, 0);
+            if (q < QD && y0 + r < a.H)
+                sd[u] = *reinterpret_cast<const uint4*>(a.dy + plane + (long long)(y0 + r) * a.W + x0 + 8 * ch);
+        }
+#pragma unroll
+        for (int u = 0; u < LX; ++u) {
+            const int q = lane + 64 * u, r = q / NQX, ch = q - r * NQX;
+            const int yy = y0 - P + r, xx = x0 - 8 + 8 * ch;
+            sx[u] = make_uint4(0, 0, 0, 0);
+            if (q < QX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+                sx[u] = *reinterpret_cast<const uint4*>(a.x + plane + (long long)yy * a.W + xx);
+        }
+    };
+    float dbs = 0.f;
+    auto put = [&]() {
+#pragma unroll
+        for (int u = 0; u < LD; ++u) {
+            const int q = lane + 64 * u, r = q / (XW / 8), ch = q - r * (XW / 8);
+            if (q < QD) {
+                *reinterpret_cast<uint4*>(dimg + r * RSD + 16 * ch) = sd[u];
+                const uint32_t w4[4] = {sd[u].x, sd[u].y, sd[u].z, sd[u].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dbs += __uint_as_float(w4[e] << 16) + __uint_as_float(w4[e] & 0xffff0000u);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < LX; ++u) {
+            const int q = lane + 64 * u, r = q / NQX, ch = q - r * NQX;
+            if (q < QX) *reinterpret_cast<uint4*>(ximg + r * RSX + 16 * ch) = sx[u];
+        }
+    };
+
+    f32x4 acc[K][2];
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) acc[ky][0] = acc[ky][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    if (band0 < band1) fetch(band0);
+    for (int band = band0; band < band1; ++band) {
+        put();                                              // after the previous band's fragment reads
+        if (band + 1 < band1) fetch(band + 1);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int s = 0; s < XW / 16; ++s) {
+            // A[i][n] = dY[n][16 s + i]: image rows 8 g + q4 (+4), columns 16 s + 4 p4
+            const bf16x8 af = tr_frag(dimg + (8 * g + q4) * RSD + 2 * (16 * s + 4 * p4),
+                                      dimg + (8 * g + 4 + q4) * RSD + 2 * (16 * s + 4 * p4));
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb) {
+                    const int col = 2 * (16 * s + 16 * jb + 4 * p4);
+                    const bf16x8 bfr = tr_frag(ximg + (ky + 8 * g + q4) * RSX + col,
+                                               ximg + (ky + 8 * g + 4 + q4) * RSX + col);
+                    acc[ky][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[ky][jb], 0, 0, 0);
+                }
+        }
+    }
+    // diagonals: lane holds T_ky[i = 4 g + r][j = 16 jb + (l & 15)]
+    __builtin_amdgcn_wave_barrier();
+    float* scr = reinterpret_cast<float*>(lds[wave]);       // [K][16][32]
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) scr[(ky * 16 + 4 * g + r) * 32 + 16 * jb + (lane & 15)] = acc[ky][jb][r];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dbs += __shfl_xor(dbs, o, 64);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float* out = a.partial + ((long long)tile * a.C + c) * (K * K + 1);
+    if (lane < K * K) {
+        const int ky = lane / K, kx = lane - ky * K;
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t += scr[(ky * 16 + i) * 32 + i + kx + 8 - P];
+        out[lane] = t;
+    } else if (lane == K * K) {
+        out[lane] = dbs;
+    }
+}
+
+template <int K>
+int dwm_bw_launch(DwmBwArgs& a, int XW, hipStream_t st) {
+    const long long waves = (long long)a.C * a.tiles;
+    const long long blocks = (waves + 1) / 2;
+    if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
+    if (XW == 64) hipLaunchKernelGGL((dwm_bwd_w<K, 64>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+    else hipLaunchKernelGGL((dwm_bwd_w<K, 16>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+    return launch_status();
+}
+
+// bands per channel and bands per wave: ~16k waves over the whole grid
+bool dwm_bw_plan(DwmBwArgs& a, int B, int C, int H, int W, int& XW) {
+    XW = W % 64 == 0 ? 64 : 16;
+    a.B = B; a.C = C; a.H = H; a.W = W;
+    a.nyb = (H + 31) / 32;
+    a.nxs = W / XW;
+    const long long nb = (long long)B * a.nyb * a.nxs;
+    if (nb > 0x7fffffffLL) return false;
+    long long want = (16384 + C - 1) / C;                   // waves per channel
+    if (want > nb) want = nb;
+    a.per = (int)((nb + want - 1) / want);
+    a.tiles = (int)((nb + a.per - 1) / a.per);
+    return true;
+}
+
 }  // namespace
 
 // y = dwconv(x, w) + bias on bf16 NCHW planes via MFMA (see the header). VFM_NO_KERNEL for shapes it
@@ -180,5 +345,33 @@ extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float*
     case 3: return dwm_launch<3>(a, st);
     case 5: return dwm_launch<5>(a, st);
     default: return dwm_launch<7>(a, st);
+    }
+}
+
+// tiles (rows of the partial buffer) of vfm_dwconv2d_bwd_weight_mfma; VFM_NO_KERNEL if not covered
+extern "C" int vfm_dwconv2d_bwd_weight_mfma_tiles(int B, int C, int H, int W, int K, int pad) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
+    if ((K != 3 && K != 5 && K != 7) || pad != (K - 1) / 2 || W % 16) return VFM_NO_KERNEL;
+    DwmBwArgs a{};
+    int XW;
+    if (!dwm_bw_plan(a, B, C, H, W, XW)) return VFM_NO_KERNEL;
+    return a.tiles;
+}
+
+// partial[t, c, :] (t < tiles): per-wave sums of dW[c] (K K taps) and db[c] over bf16 NCHW x / dy
+extern "C" int vfm_dwconv2d_bwd_weight_mfma(const void* x, const void* dy, float* partial, int B, int C, int H, int W,
+                                           int K, int pad, void* stream) {
+    if (!x || !dy || !partial || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
+    if ((K != 3 && K != 5 && K != 7) || pad != (K - 1) / 2 || W % 16) return VFM_NO_KERNEL;
+    if (((uintptr_t)x | (uintptr_t)dy) % 16) return VFM_NO_KERNEL;
+    DwmBwArgs a{};
+    int XW;
+    if (!dwm_bw_plan(a, B, C, H, W, XW)) return VFM_NO_KERNEL;
+    a.x = (const __hip_bfloat16*)x; a.dy = (const __hip_bfloat16*)dy; a.partial = partial;
+    hipStream_t st = (hipStream_t)stream;
+    switch (K) {
+    case 3: return dwm_bw_launch<3>(a, XW, st);
+    case 5: return dwm_bw_launch<5>(a, XW, st);
+    default: return dwm_bw_launch<7>(a, XW, st);
     }
 }

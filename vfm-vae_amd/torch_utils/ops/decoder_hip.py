@@ -260,7 +260,20 @@ class _DwConv2d(torch.autograd.Function):
         want_w, want_b = _wanted(ctx, 1), _wanted(ctx, 2)
         if _wanted(ctx, 0):
             dx = _dw_fwd(dy, torch.flip(w3, [1, 2]).contiguous(), None, None, K - 1 - pad, 'dwconv2d_bwd_data')
-        if want_w or want_b:
+        if (want_w or want_b) and DW_MFMA and x.dtype == torch.bfloat16 and \
+                _lib.vfm_dwconv2d_bwd_weight_mfma_tiles(B, C, H, W, K, pad) > 0:
+            # bf16 planes: the weight gradient as banded MFMA products (csrc/dwconv_mfma.hip)
+            tiles = _lib.vfm_dwconv2d_bwd_weight_mfma_tiles(B, C, H, W, K, pad)
+            part = torch.empty([tiles, C, K * K + 1], dtype=torch.float32, device=x.device)
+            with kernel_timer.region(_rn('dwconv2d_mfma_bwd_weight', x, K), _nb(x, dy)):
+                _check(_lib.vfm_dwconv2d_bwd_weight_mfma(x.data_ptr(), dy.data_ptr(), part.data_ptr(), B, C, H, W, K,
+                                                         pad, _stream()), 'vfm_dwconv2d_bwd_weight_mfma')
+            s = part.sum(0)
+            if want_w:
+                dw = s[:, :K * K].reshape(wshape).to(wdt)
+            if want_b:
+                db = s[:, K * K].to(bdt)
+        elif want_w or want_b:
             tiles = _lib.vfm_dwconv2d_bwd_weight_tiles(B, C, H, W, K, pad)
             if tiles <= 0:
                 raise custom_ops.NativeError(f"vfm_dwconv2d_bwd_weight_tiles failed with code {tiles}")

@@ -95,6 +95,7 @@ _ROC = {
     "dwconv2d_fwd": "dwr_fwd<{T}, {K}>", "dwconv2d_bwd_data": "dwr_fwd<{T}, {K}>",
     "dwconv2d_bwd_weight": "dwr_bwd_w<{T}, {K}>",
     "dwconv2d_mfma_fwd": "dwm_fwd<{K}, ", "dwconv2d_mfma_bwd_data": "dwm_fwd<{K}, ",
+    "dwconv2d_mfma_bwd_weight": "dwm_bwd_w<{K}, ",
     "shuffle_blur_fwd": "blur_fwd<{T}, 2, {K}>", "shuffle_blur_bwd": "blur_bwd<{T}, 2, {K}>",
     "residual_layer_norm": "ln_rows<", "codebook_argmax": "codebook_argmax_kernel<",
     "convnext_mlp_fwd": "mlp_fwd<", "pw_gemm_gelu_bwd": "pw_gemm_gelu<1, ",
