@@ -77,15 +77,22 @@ class FlatGradSync:
         self.buckets = []                           # (start, end, n_params)
         start, n, cnt = 0, 0, 0
         self.bucket_of = {}
+        self.bucket_params = [[]]
         for p in order:
             self.bucket_of[id(p)] = len(self.buckets)
+            self.bucket_params[-1].append(p)
             n += p.numel()
             cnt += 1
             if n >= limit:
                 self.buckets.append((start, start + n, cnt))
+                self.bucket_params.append([])
                 start, n, cnt = start + n, 0, 0
         if cnt:
             self.buckets.append((start, start + n, cnt))
+        else:
+            self.bucket_params.pop()
+        self.views = {id(p): self.flat[self.offsets[id(p)][0]:self.offsets[id(p)][0] + p.numel()].view_as(p)
+                      for p in params}
         if dev.type == 'cuda' and self.collective:
             self.comm_stream = torch.cuda.Stream(device=dev)
         for p in params:
@@ -100,9 +107,12 @@ class FlatGradSync:
         if tuple(id(p) for p in params) != self.key:
             self._build(params)
         self.flat.zero_()
+        # grads start as None: the autograd engine then hands each parameter its gradient tensor
+        # without a kernel (AccumulateGrad "steals" it), and the grads move into the flat buffer
+        # with one multi-tensor copy per bucket (or per phase at world size 1) instead of one
+        # accumulate kernel per parameter
         for p in self.params:
-            off, n = self.offsets[id(p)]
-            p.grad = self.flat[off:off + n].view_as(p)
+            p.grad = None
         self.seen = set()
         self.ready = [0] * len(self.buckets)
         self.pending = {}
@@ -155,7 +165,24 @@ class FlatGradSync:
         if self.ready[bi] == self.buckets[bi][2]:
             self._launch(bi)
 
+    def _gather(self, plist):
+        """Move the stolen gradients of `plist` into their flat-buffer views (one multi-tensor copy)
+        and point .grad at the views."""
+        dst, src = [], []
+        for p in plist:
+            g, v = p.grad, self.views[id(p)]
+            if g is None or g.data_ptr() == v.data_ptr():
+                continue
+            dst.append(v)
+            src.append(g)
+        if dst:
+            torch._foreach_copy_(dst, src)
+            for p in plist:
+                if p.grad is not None:
+                    p.grad = self.views[id(p)]
+
     def _launch(self, bi):
+        self._gather(self.bucket_params[bi])
         s, e, _ = self.buckets[bi]
         view = self.flat[s:e]
         if self.comm_stream is not None:
@@ -182,6 +209,8 @@ class FlatGradSync:
                 torch.cuda.current_stream(self.flat.device).wait_stream(self.comm_stream)
             self._launch_agreement()
             self.flat.mul_(1.0 / self.world)
+        else:
+            self._gather(self.params)
         if gain is not None and gain != 1:
             self.flat.mul_(gain)
         torch.nan_to_num_(self.flat, nan=0, posinf=1e5, neginf=-1e5)
