@@ -32,6 +32,7 @@ for s in "$@"; do
     benchab) VFM_LPIPS_VGG=torch timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_a.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_b.log 2>&1 && VFM_LPIPS_VGG=torch timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_c.log 2>&1 ;;
     convpmc) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex conv3x3_kernel -d $out/convpmc -o run --output-format csv -- python3 tools_dev/vggbench.py > $out/convpmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-include-regex conv3x3_kernel -d $out/convpmc2 -o run --output-format csv -- python3 tools_dev/vggbench.py > $out/convpmc2.log 2>&1 ;;
     dwpmc) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex "dwr_fwd|blur_fwd" -d $out/dwpmc -o run --output-format csv -- python3 tools_dev/decbench.py --only dw,blur > $out/dwpmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM --kernel-include-regex "dwr_fwd|blur_fwd" -d $out/dwpmc2 -o run --output-format csv -- python3 tools_dev/decbench.py --only dw,blur > $out/dwpmc2.log 2>&1 ;;
+    mlppmc) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex mlp_fwd -d $out/mlppmc -o run --output-format csv -- python3 tools_dev/pwbench.py > $out/mlppmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM --kernel-include-regex mlp_fwd -d $out/mlppmc2 -o run --output-format csv -- python3 tools_dev/pwbench.py > $out/mlppmc2.log 2>&1 ;;
     gdebug)  timeout -k 10 300 python tools_dev/graph_debug.py > $out/gdebug.log 2>&1 ;;
     benchfind) MIOPEN_FIND_MODE=NORMAL VFM_CUDNN_BENCHMARK=1 timeout -k 10 900 python bench.py --no-cpu-baseline > $out/benchfind.log 2>&1 ;;
     tune)    ( while sleep 30; do echo "tick $(date +%T)"; done ) & tk=$!

@@ -69,6 +69,13 @@ def main():
             tm = timeit(lambda: lib.vfm_convnext_mlp_fwd(A.data_ptr(), X.data_ptr(), s.data_ptr(), bias.data_ptr(),
                                                          W2.data_ptr(), b2.data_ptr(), gam.data_ptr(), xin.data_ptr(),
                                                          outm.data_ptr(), None, None, None, B, C, N, st))
+            ym = torch.empty_like(xin)
+            tmg = timeit(lambda: lib.vfm_convnext_mlp_fwd(A.data_ptr(), X.data_ptr(), s.data_ptr(), bias.data_ptr(),
+                                                          W2.data_ptr(), b2.data_ptr(), gam.data_ptr(), xin.data_ptr(),
+                                                          outm.data_ptr(), h.data_ptr(), g.data_ptr(), ym.data_ptr(),
+                                                          B, C, N, st))
+            print(f"{name}: whole MLP fwd saving h/g/y {tmg:8.1f} us {(4 * ux + 2 * uh) / tmg / 1e3:6.0f} GB/s",
+                  flush=True)
         t4 = timeit(unfused_fwd)
         t5 = timeit(lambda: torch.bmm(A.expand(B, M, K), X))
         print(f"{name}: fused fwd(h+g) {t1:8.1f} us {(ux + 2 * uh) / t1 / 1e3:7.0f} GB/s | fwd(g) {t2:8.1f} us "
