@@ -111,24 +111,6 @@ __device__ __forceinline__ f2 gelu2(f2 z) {
     return z * cdf;
 }
 
-// GELU'(z) = Phi(z) + z phi(z) for two values, the same operations as gelu_parts (cdf + zpdf)
-__device__ __forceinline__ f2 gelu2_grad(f2 z) {
-    const f2 x = z * 0.70710678118654752f;
-    const f2 ax = {fabsf(x.x), fabsf(x.y)};
-    const f2 d = __builtin_elementwise_fma(ax, f2{0.3275911f, 0.3275911f}, f2{1.f, 1.f});
-    const f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    f2 p = __builtin_elementwise_fma(t, f2{1.061405429f, 1.061405429f}, f2{-1.453152027f, -1.453152027f});
-    p = __builtin_elementwise_fma(p, t, f2{1.421413741f, 1.421413741f});
-    p = __builtin_elementwise_fma(p, t, f2{-0.284496736f, -0.284496736f});
-    p = __builtin_elementwise_fma(p, t, f2{0.254829592f, 0.254829592f});
-    const f2 arg = -(x * x) * 1.4426950408889634f;
-    const f2 e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
-    const f2 q = (0.5f * (p * t)) * e;
-    const f2 cdf = {x.x < 0.f ? q.x : 1.f - q.x, x.y < 0.f ? q.y : 1.f - q.y};
-    const f2 zpdf = z * 0.39894228040143268f * e;
-    return cdf + zpdf;
-}
-
 // packed bf16 pair (round to nearest even) and its two values back as fp32
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
@@ -201,17 +183,16 @@ __global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
             }
         }
 
-        // mode 1: this lane's h values (rows of registers i, column r of each 32-column block), all
-        // 16-bit loads issued together right after the MFMAs
-        uint16_t hraw[MODE == 1 ? 16 : 1][NBW];
+        const bool odd = r & 1;
+        uint32_t hraw[MODE == 1 ? 8 : 1][NBW];     // packed pairs, see pair_pack
         if (MODE == 1) {
-            const __hip_bfloat16* hb = a.h + (long long)b * M * N + n0 + 64 * cw + r;
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
+            for (int i = 0; i < 16; i += 2)
 #pragma unroll
                 for (int nb = 0; nb < NBW; ++nb) {
-                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                    hraw[i][nb] = *reinterpret_cast<const uint16_t*>(hb + (unsigned)(m * N + 32 * nb));
+                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh + (odd ? 1 : 0);
+                    hraw[i / 2][nb] = *reinterpret_cast<const uint32_t*>(a.h + outb - (odd ? 1 : 0) +
+                                                                         (long long)m * N + 32 * nb);
                 }
         }
         // epilogue: register i of acc[nb] is row m0 + (i&3) + 8(i>>2) + 4hh, column n0 + 32nb + r
@@ -236,38 +217,46 @@ __global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
                 }
             }
         } else {
-            __hip_bfloat16* dhb = a.out0 + (long long)b * M * N + n0 + 64 * cw + r;
 #pragma unroll
             for (int i = 0; i < 16; i += 2) {
                 const int mA = m0 + (i & 3) + 8 * (i >> 2) + 4 * hh;      // row of register i; i+1 is mA+1
-                const f2 sc = {s_sc[mA], s_sc[mA + 1]};
-                const f2 bi = {s_bi[mA], s_bi[mA + 1]};
-                f2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
+                float s0[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f};
 #pragma unroll
                 for (int nb = 0; nb < NBW; ++nb) {
-                    const f2 hv = unpk_bf16((uint32_t)hraw[i][nb] | ((uint32_t)hraw[i + 1][nb] << 16));
-                    const f2 dg = unpk_bf16(pk_bf16(acc[nb][i], acc[nb][i + 1]));
-                    const f2 dz = dg * gelu2_grad(__builtin_elementwise_fma(hv, sc, bi));
-                    const uint32_t dp = pk_bf16(dz.x * sc.x, dz.y * sc.y);
-                    const unsigned o = (unsigned)(mA * N + 32 * nb);
-                    *reinterpret_cast<uint16_t*>(dhb + o) = (uint16_t)dp;
-                    *reinterpret_cast<uint16_t*>(dhb + o + (unsigned)N) = (uint16_t)(dp >> 16);
-                    s0 = __builtin_elementwise_fma(dz, hv, s0);
-                    s1 = s1 + dz;
+                    // unpack this lane's h for rows mA, mA+1 (column r)
+                    const uint32_t own = hraw[i / 2][nb];
+                    const uint32_t x = (uint32_t)__shfl_xor((int)(odd ? (own & 0xffffu) : (own >> 16)), 1);
+                    const uint32_t hb0 = odd ? x : (own & 0xffffu);
+                    const uint32_t hb1 = odd ? (own >> 16) : x;
+                    float dhv[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int m = mA + t;
+                        const float sc = s_sc[m];
+                        const float bi = s_bi[m];
+                        const float hv = __uint_as_float((t ? hb1 : hb0) << 16);
+                        const float dg = bf16_round(acc[nb][i + t]);
+                        const GeluParts gp = gelu_parts(fmaf(hv, sc, bi));
+                        const float dz = dg * (gp.cdf + gp.zpdf);
+                        dhv[t] = dz * sc;
+                        s0[t] = fmaf(dz, hv, s0[t]);
+                        s1[t] += dz;
+                    }
+                    const uint32_t pk = pair_pack(dhv[0], dhv[1], odd);
+                    *reinterpret_cast<uint32_t*>(a.out0 + outb - (odd ? 1 : 0) + (long long)(mA + (odd ? 1 : 0)) * N +
+                                                 32 * nb) = pk;
                 }
-                const float s0v[2] = {s0.x, s0.y}, s1v[2] = {s1.x, s1.y};
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
-                    float u0 = s0v[t], u1 = s1v[t];
 #pragma unroll
                     for (int off = 16; off >= 1; off >>= 1) {     // sum over the 32 columns of this half
-                        u0 += __shfl_xor(u0, off);
-                        u1 += __shfl_xor(u1, off);
+                        s0[t] += __shfl_xor(s0[t], off);
+                        s1[t] += __shfl_xor(s1[t], off);
                     }
                     if (r == 0) {
                         const long long pi = ((long long)b * a.ntiles + 2 * tile + cw) * M + mA + t;
-                        a.part0[pi] = u0;
-                        a.part1[pi] = u1;
+                        a.part0[pi] = s0[t];
+                        a.part1[pi] = s1[t];
                     }
                 }
             }
