@@ -347,10 +347,11 @@ int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, co
  * cores (banded-matrix form, csrc/dwconv_mfma.hip); same contract as vfm_dwconv2d_fwd (noise: fp32
  * [H, W] added to every channel, or NULL), taps w fp32 [C, K, K] rounded to bf16 (the reference's
  * autocast conv: replaces convnext_utils.py:121-124 / :243 nn.Conv2d(groups=C) for the bf16 blocks,
- * and its data gradient with the rotated taps). W % 16 == 0, 16-B aligned x / y / noise;
- * VFM_NO_KERNEL otherwise. */
-int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise, void* y, int B,
-                          int C, int H, int W, int K, int pad, void* stream);
+ * and its data gradient with the rotated taps). res: bf16 [B, C, H, W] added to the fp32 result before
+ * the output rounding (the residual branch's gradient of the same input), or NULL. W % 16 == 0,
+ * 16-B aligned x / y / noise / res; VFM_NO_KERNEL otherwise. */
+int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise, const void* res,
+                          void* y, int B, int C, int H, int W, int K, int pad, void* stream);
 /* Weight (and bias) gradient of the same conv on MFMA: partial[t, c, 0 .. K*K-1] = per-wave sums of
  * dW[c][ky][kx] = sum dy[b,c,y,x] x[b,c,y+ky-pad,x+kx-pad], partial[t, c, K*K] = sum dy; t < tiles
  * = vfm_dwconv2d_bwd_weight_mfma_tiles(...) (same partial layout as vfm_dwconv2d_bwd_weight; the

@@ -19,7 +19,8 @@
 // and runs XW / 16 tiles x K MFMAs; a wave walks up to 4 such row blocks down the plane with the next
 // block's loads in flight during the current block's MFMAs. Output: lane l holds
 // out[y0 + (l & 15)][x0 + 16 s + 4 (l >> 4) + r], r < 4 -> one 8-B store per tile (+ the fp32 noise
-// plane of the legacy noise path when given).
+// plane of the legacy noise path, and / or a residual tensor (the data gradient's other branch),
+// when given).
 #include "vfm_common.h"
 
 namespace {
@@ -37,6 +38,7 @@ struct DwmArgs {
     const float* w;                       // [C, K, K] fp32 (rounded to bf16 here, as autocast does)
     const float* bias;                    // [C] or null
     const float* noise;                   // [H, W] fp32 added to every channel (legacy noise) or null
+    const __hip_bfloat16* res;            // [B, C, H, W] bf16 added before the output rounding, or null
     __hip_bfloat16* y;
     int B, C, H, W, XW, nyb, nxs, rb;     // rb: 16-row blocks per wave
     long long units;
@@ -126,6 +128,7 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
         const int oy = y0 + n;
         __hip_bfloat16* yp = a.y + plane + (long long)oy * a.W + x0 + 4 * g;
         const float* np = a.noise ? a.noise + (long long)oy * a.W + x0 + 4 * g : nullptr;
+        const __hip_bfloat16* rp = a.res ? a.res + plane + (long long)oy * a.W + x0 + 4 * g : nullptr;
 #pragma unroll
         for (int s = 0; s < XW / 16; ++s) {
             f32x4 acc = {bias, bias, bias, bias};
@@ -137,6 +140,11 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
             for (int ky = 0; ky < K; ++ky) {
                 const bf16x8 b = *reinterpret_cast<const bf16x8*>(img + (n + ky) * RS + 16 * (2 * s + g));
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky], b, acc, 0, 0, 0);
+            }
+            if (rp && oy < a.H) {          // residual-branch gradient (the layer's other use of x)
+                const uint2 rv = *reinterpret_cast<const uint2*>(rp + 16 * s);
+                acc[0] += __uint_as_float(rv.x << 16); acc[1] += __uint_as_float(rv.x & 0xffff0000u);
+                acc[2] += __uint_as_float(rv.y << 16); acc[3] += __uint_as_float(rv.y & 0xffff0000u);
             }
             if (oy < a.H) {
                 const uint2 o = make_uint2((uint32_t)bf16_bits(acc[0]) | ((uint32_t)bf16_bits(acc[1]) << 16),
@@ -326,13 +334,15 @@ bool dwm_bw_plan(DwmBwArgs& a, int B, int C, int H, int W, int& XW) {
 // y = dwconv(x, w) + bias on bf16 NCHW planes via MFMA (see the header). VFM_NO_KERNEL for shapes it
 // does not cover (W % 16, pad != (K - 1) / 2, K not in {3, 5, 7}, misaligned pointers): the caller
 // then uses vfm_dwconv2d_fwd.
-extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise, void* y,
-                                     int B, int C, int H, int W, int K, int pad, void* stream) {
+extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise,
+                                     const void* res, void* y, int B, int C, int H, int W, int K, int pad,
+                                     void* stream) {
     if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
     if ((K != 3 && K != 5 && K != 7) || pad != (K - 1) / 2 || W % 16) return VFM_NO_KERNEL;
-    if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)noise) % 16) return VFM_NO_KERNEL;
+    if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)noise | (uintptr_t)res) % 16) return VFM_NO_KERNEL;
     DwmArgs a;
     a.x = (const __hip_bfloat16*)x; a.w = w; a.bias = bias; a.noise = noise; a.y = (__hip_bfloat16*)y;
+    a.res = (const __hip_bfloat16*)res;
     a.B = B; a.C = C; a.H = H; a.W = W;
     a.XW = W % 64 == 0 ? 64 : 16;
     const int rows16 = (H + 15) / 16;

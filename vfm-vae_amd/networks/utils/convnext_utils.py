@@ -93,8 +93,14 @@ class ConvNeXtSynthesisLayer(nn.Module):
         x_in = x
         B, C, H, W = x.shape
         style = self.affine_pw1(w).float()                                     # [B, C]
+        # x feeds the dwconv and the residual: on the HIP path the residual's gradient is added in the
+        # dwconv data-gradient kernel instead of by autograd (decoder_hip.ResidualSlot)
+        slot = None
+        if x.is_cuda and x.dtype == cdt and x.requires_grad and torch.is_grad_enabled():
+            from torch_utils.ops import decoder_hip
+            slot = decoder_hip.ResidualSlot()
         d = decoder_ops.dwconv2d(x.to(cdt), self.dwconv.weight, self.dwconv.bias, self.kernel_size // 2,
-                                 noise=self._noise(H, W))
+                                 noise=self._noise(H, W), slot=slot)
         m = decoder_ops.group_norm(d, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps,
                                    out_dtype=cdt, style=style)                 # GN(d) * s_b
         w1 = self.pwconv1.weight.reshape(4 * C, C)
@@ -104,12 +110,12 @@ class ConvNeXtSynthesisLayer(nn.Module):
             # the whole MLP forward in one kernel (hidden 4C tensor on chip without autograd)
             out = decoder_ops.convnext_mlp_nograd(m.reshape(B, C, H * W), w1, dcoef, self.pwconv1.bias.reshape(-1),
                                                   self.pwconv2.weight.reshape(C, 4 * C), self.pwconv2.bias, gamma,
-                                                  x_in.reshape(B, C, H * W))
+                                                  x_in.reshape(B, C, H * W), slot=slot)
             return out.reshape(B, C, H, W)
         h = decoder_ops.pointwise(w1, m.reshape(B, C, H * W))                    # [B, 4C, HW]
         g = decoder_ops.scale_bias_gelu(h, dcoef, self.pwconv1.bias.reshape(-1))
         y = decoder_ops.pointwise(self.pwconv2.weight.reshape(C, 4 * C), g)     # [B, C, HW]
-        out = decoder_ops.layer_scale_residual(y, self.pwconv2.bias, gamma, x_in.reshape(B, C, H * W))
+        out = decoder_ops.layer_scale_residual(y, self.pwconv2.bias, gamma, x_in.reshape(B, C, H * W), slot=slot)
         return out.reshape(B, C, H, W)
 
 

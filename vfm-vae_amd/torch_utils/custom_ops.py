@@ -73,7 +73,7 @@ SIGNATURES = {
                           c_vp],
     "vfm_bnl_lrelu_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                           c_float, c_vp],
-    "vfm_dwconv2d_fwd_mfma": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_dwconv2d_fwd_mfma": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_posterior_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_posterior_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_dwconv2d_bwd_weight_mfma_tiles": [c_int, c_int, c_int, c_int, c_int, c_int],

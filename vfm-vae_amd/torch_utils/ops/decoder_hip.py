@@ -211,7 +211,9 @@ def pointwise(w, x):
 DW_MFMA = os.environ.get("VFM_DW_MFMA", "1") == "1"      # A/B switch for the banded-MFMA dwconv
 
 
-def _dw_fwd(x, w3, bias, noise, pad, name):
+def _dw_fwd(x, w3, bias, noise, pad, name, res=None):
+    """y = dwconv(x) (+ bias, + noise plane) (+ res, a tensor of y's shape: the residual-branch
+    gradient added in the MFMA kernel's epilogue, else by a torch add)."""
     B, C, H, W = x.shape
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -219,22 +221,50 @@ def _dw_fwd(x, w3, bias, noise, pad, name):
     if DW_MFMA and x.dtype == torch.bfloat16 and 2 * pad == K - 1:
         # bf16 planes: the banded-MFMA kernel (csrc/dwconv_mfma.hip); taps rounded to bf16 as
         # the reference's autocast conv does
-        with kernel_timer.region(_rn(name.replace('dwconv2d', 'dwconv2d_mfma'), x, K), _nb(x, y)):
-            rc = _lib.vfm_dwconv2d_fwd_mfma(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), B, C, H,
-                                            W, K, pad, _stream())
+        r = None if res is None else _c(res.to(torch.bfloat16))
+        with kernel_timer.region(_rn(name.replace('dwconv2d', 'dwconv2d_mfma'), x, K), _nb(x, y, r)):
+            rc = _lib.vfm_dwconv2d_fwd_mfma(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), _p(r), y.data_ptr(), B,
+                                            C, H, W, K, pad, _stream())
         if rc != custom_ops.VFM_NO_KERNEL:
             _check(rc, name)
             return y
     with kernel_timer.region(_rn(name, x, K), _nb(x, y)):
         _check(_lib.vfm_dwconv2d_fwd(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
                                      B, C, H, W, K, pad, _stream()), name)
-    return y
+    return y if res is None else y.add_(res.to(y.dtype))
+
+
+class ResidualSlot:
+    """Hands a ConvNeXt layer's residual-branch gradient (d out / d x_in = d out) from the layer-scale
+    residual's backward to the backward of the layer's depthwise conv, whose data-gradient kernel
+    adds it in its epilogue: x feeds both the dwconv and the residual, and autograd would otherwise
+    sum the two gradients in a separate full-tensor add. Used only when the dwconv input IS x_in
+    (no cast in between) and the dwconv's backward node will run in the same engine pass."""
+    __slots__ = ("node", "grad")
+
+    def __init__(self):
+        self.node = None
+        self.grad = None
+
+
+def _stash_residual(slot, dout):
+    """True when the residual gradient was handed to the dwconv backward (return None for x_in)."""
+    if slot is None or slot.node is None:
+        return False
+    try:
+        if not torch._C._will_engine_execute_node(slot.node):
+            return False
+    except RuntimeError:
+        return False
+    slot.grad = dout
+    return True
 
 
 class _DwConv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, noise, pad):
-        _edges(ctx, x, weight, bias, noise, pad)
+    def forward(ctx, x, weight, bias, noise, pad, slot):
+        _edges(ctx, x, weight, bias, noise, pad, slot)
+        ctx.slot = slot
         x = _c(x)
         C, K = weight.shape[0], weight.shape[-1]
         w3 = weight.detach().reshape(C, K, K).float().contiguous()
@@ -258,8 +288,12 @@ class _DwConv2d(torch.autograd.Function):
         K = w3.shape[-1]
         dx = dw = db = dn = None
         want_w, want_b = _wanted(ctx, 1), _wanted(ctx, 2)
+        res = None
+        if ctx.slot is not None and ctx.slot.grad is not None:
+            res, ctx.slot.grad = ctx.slot.grad, None
         if _wanted(ctx, 0):
-            dx = _dw_fwd(dy, torch.flip(w3, [1, 2]).contiguous(), None, None, K - 1 - pad, 'dwconv2d_bwd_data')
+            dx = _dw_fwd(dy, torch.flip(w3, [1, 2]).contiguous(), None, None, K - 1 - pad, 'dwconv2d_bwd_data', res)
+        # (res unused when dx is not wanted: then nothing consumes x's gradient in this pass)
         if (want_w or want_b) and DW_MFMA and x.dtype == torch.bfloat16 and \
                 _lib.vfm_dwconv2d_bwd_weight_mfma_tiles(B, C, H, W, K, pad) > 0:
             # bf16 planes: the weight gradient as banded MFMA products (csrc/dwconv_mfma.hip)
@@ -288,11 +322,14 @@ class _DwConv2d(torch.autograd.Function):
                 db = s[:, K * K].to(bdt)
         if _wanted(ctx, 3):
             dn = dy.float().sum(dim=(0, 1)).to(ndt)
-        return dx, dw, db, dn, None
+        return dx, dw, db, dn, None, None
 
 
-def dwconv2d(x, weight, bias, padding, noise):
-    return _DwConv2d.apply(x, weight, bias, noise, int(padding))
+def dwconv2d(x, weight, bias, padding, noise, slot=None):
+    y = _DwConv2d.apply(x, weight, bias, noise, int(padding), slot)
+    if slot is not None:
+        slot.node = y.grad_fn
+    return y
 
 
 # ---------------------------------------------------------------------------
@@ -400,8 +437,9 @@ def scale_bias_gelu(h, scale, bias):
 
 class _LayerScaleResidual(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, bias, gamma, x_in):
-        _edges(ctx, y, bias, gamma, x_in)
+    def forward(ctx, y, bias, gamma, x_in, slot=None):
+        _edges(ctx, y, bias, gamma, x_in, slot)
+        ctx.slot = slot
         y, x_in = _c(y), _c(x_in)
         B, C = y.shape[:2]
         P = y[0, 0].numel()
@@ -436,15 +474,16 @@ class _LayerScaleResidual(torch.autograd.Function):
             db = (s1 * g if g is not None else s1).to(bdt)
         if g is not None and _wanted(ctx, 2):
             dg = r0.view(B, C).sum(0).to(gdt)
-        return (dy if ctx.needs_input_grad[0] else None), db, dg, (dout if ctx.needs_input_grad[3] else None)
+        dx = dout if ctx.needs_input_grad[3] and not _stash_residual(ctx.slot, dout) else None
+        return (dy if ctx.needs_input_grad[0] else None), db, dg, dx, None
 
 
-def layer_scale_residual(y, bias, gamma, x_in):
+def layer_scale_residual(y, bias, gamma, x_in, slot=None):
     if bias is not None:
         bias = bias.reshape(-1)
     if gamma is not None:
         gamma = gamma.reshape(-1)
-    return _LayerScaleResidual.apply(y, bias, gamma, x_in)
+    return _LayerScaleResidual.apply(y, bias, gamma, x_in, slot)
 
 
 # ---------------------------------------------------------------------------
@@ -467,8 +506,9 @@ class _ConvNeXtMLP(torch.autograd.Function):
     and dm; the same arithmetic as the unfused Functions above (bf16 roundings included)."""
 
     @staticmethod
-    def forward(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in):
-        _edges(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in)
+    def forward(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in, slot=None):
+        _edges(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in, slot)
+        ctx.slot = slot
         m, x_in = _c(m), _c(x_in)
         B, C, P = m.shape
         w1c = _cast_cached(w1, torch.bfloat16).contiguous()
@@ -532,13 +572,13 @@ class _ConvNeXtMLP(torch.autograd.Function):
             dm = _gemm(w1c.t(), dh)
             if dm is None:
                 dm = torch.bmm(w1c.t().expand(B, C, O), dh)
-        dx = dout if ctx.needs_input_grad[7] else None
-        return dm, dw1, ds, db1, dw2, db2, dgm, dx
+        dx = dout if ctx.needs_input_grad[7] and not _stash_residual(ctx.slot, dout) else None
+        return dm, dw1, ds, db1, dw2, db2, dgm, dx, None
 
 
-def convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in):
+def convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot=None):
     """Autograd form of the fused MLP (same arguments as convnext_mlp_nograd)."""
-    return _ConvNeXtMLP.apply(m, w1, dcoef, b1, w2, b2, gamma, x_in)
+    return _ConvNeXtMLP.apply(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot)
 
 
 def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):

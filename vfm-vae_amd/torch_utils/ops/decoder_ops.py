@@ -78,12 +78,13 @@ def pointwise(weight, x, impl='cuda'):
 # Depthwise k x k convolution (+bias, + optional additive [H, W] plane).
 
 
-def dwconv2d(x, weight, bias=None, padding=0, noise=None, impl='cuda'):
+def dwconv2d(x, weight, bias=None, padding=0, noise=None, impl='cuda', slot=None):
     """Depthwise conv: weight [C, 1, k, k], zero padding `padding`, stride 1.
-    `noise` ([H_out, W_out], fp32) is added to every channel (legacy noise path)."""
+    `noise` ([H_out, W_out], fp32) is added to every channel (legacy noise path). `slot`
+    (decoder_hip.ResidualSlot, HIP path only) receives the layer's residual gradient."""
     if _use_hip('dwconv2d', x, impl, k=weight.shape[-1]):
         from . import decoder_hip
-        return decoder_hip.dwconv2d(x, weight, bias, padding, noise)
+        return decoder_hip.dwconv2d(x, weight, bias, padding, noise, slot)
     y = F.conv2d(x, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None, padding=padding,
                  groups=x.shape[1])
     if noise is not None:
@@ -112,11 +113,11 @@ def scale_bias_gelu(h, scale=None, bias=None, impl='cuda'):
 # Residual with layer scale: x_in + gamma[c] * (y + b[c]).
 
 
-def layer_scale_residual(y, bias, gamma, x_in, impl='cuda'):
+def layer_scale_residual(y, bias, gamma, x_in, impl='cuda', slot=None):
     """y: [B, C, P] (or [B, C, H, W]); bias, gamma: [C]; x_in like y. Output dtype = x_in.dtype."""
     if _use_hip('layer_scale_residual', y, impl):
         from . import decoder_hip
-        return decoder_hip.layer_scale_residual(y, bias, gamma, x_in)
+        return decoder_hip.layer_scale_residual(y, bias, gamma, x_in, slot)
     shape = [1, -1] + [1] * (y.ndim - 2)
     z = y.float()
     if bias is not None:
@@ -179,10 +180,10 @@ def convnext_mlp_fusable(m, C, P, x_in):
     return decoder_hip.convnext_mlp_supported(m, C, P)
 
 
-def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
+def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot=None):
     from . import decoder_hip
     if torch.is_grad_enabled():
-        return decoder_hip.convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in)
+        return decoder_hip.convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot)
     return decoder_hip.convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in)
 
 
