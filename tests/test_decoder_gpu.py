@@ -361,3 +361,34 @@ def test_posterior_sample_kl(B, C, H):
     assert _rel(z, zr) < 1e-6
     assert _rel(kl, klr) < 1e-6
     assert _rel(pg.grad, pr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("C,res", [(128, 32), (64, 48)])
+def test_convnext_layer_residual_fusion(C, res, monkeypatch):
+    """The residual-branch gradient handed to the dwconv data-gradient kernel (decoder_hip.ResidualSlot)
+    gives the layer the same input / parameter gradients as autograd's separate add (bf16 layer:
+    one rounding of the sum instead of two, hence 1e-2 of max)."""
+    from networks.utils.convnext_utils import ConvNeXtSynthesisLayer
+    from torch_utils.ops import decoder_hip
+    _, kt = _ops()
+    torch.manual_seed(C + res)
+    layer = ConvNeXtSynthesisLayer(C, 32, 7, layer_scale_init=0.5).to(DEV)
+    x0 = torch.randn(2, C, res, res, device=DEV).to(torch.bfloat16)
+    w = torch.randn(2, 32, device=DEV)
+    r = torch.randn(2, C, res, res, device=DEV)
+    grads = []
+    for fused in (True, False):
+        monkeypatch.setattr(decoder_hip, "RESIDUAL_FUSION", fused)
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        kt.enable(True)
+        y = layer(x, w, compute_dtype=torch.bfloat16)
+        (y.float() * r).sum().backward()
+        torch.cuda.synchronize()
+        names = set(kt.summary())
+        kt.enable(False)
+        assert any(n.startswith("dwconv2d_mfma_bwd_data") for n in names), names
+        grads.append([x.grad.float()] + [p.grad.float() for p in layer.parameters() if p.grad is not None])
+    assert len(grads[0]) == len(grads[1])
+    for a, b in zip(*grads):
+        assert _rel(a, b) < 1e-2, _rel(a, b)

@@ -98,7 +98,7 @@ class ConvNeXtSynthesisLayer(nn.Module):
         slot = None
         if x.is_cuda and x.dtype == cdt and x.requires_grad and torch.is_grad_enabled():
             from torch_utils.ops import decoder_hip
-            slot = decoder_hip.ResidualSlot()
+            slot = decoder_hip.ResidualSlot() if decoder_hip.RESIDUAL_FUSION else None
         d = decoder_ops.dwconv2d(x.to(cdt), self.dwconv.weight, self.dwconv.bias, self.kernel_size // 2,
                                  noise=self._noise(H, W), slot=slot)
         m = decoder_ops.group_norm(d, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps,

@@ -218,6 +218,8 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None):
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
     y = torch.empty([B, C, Ho, Wo], dtype=x.dtype, device=x.device)
+    if res is not None:
+        res = res.reshape(y.shape)            # handed over as the residual's [B, C, P] view
     if DW_MFMA and x.dtype == torch.bfloat16 and 2 * pad == K - 1:
         # bf16 planes: the banded-MFMA kernel (csrc/dwconv_mfma.hip); taps rounded to bf16 as
         # the reference's autocast conv does
@@ -232,6 +234,9 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None):
         _check(_lib.vfm_dwconv2d_fwd(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
                                      B, C, H, W, K, pad, _stream()), name)
     return y if res is None else y.add_(res.to(y.dtype))
+
+
+RESIDUAL_FUSION = os.environ.get("VFM_RESIDUAL_FUSION", "1") == "1"     # A/B switch (tests, benches)
 
 
 class ResidualSlot:
