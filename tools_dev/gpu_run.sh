@@ -13,6 +13,8 @@ for s in "$@"; do
     testsk)  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 ;;
     bench)   timeout -k 10 900 python bench.py > $out/bench.log 2>&1 ;;
     benchshape) VFM_TIMER_SHAPES=1 timeout -k 10 600 python bench.py --steps 6 --warmup 2 --no-cpu-baseline > $out/benchshape.log 2>&1 ;;
+    benchres) VFM_RESIDUAL_FUSION=0 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_r0.log 2>&1 && VFM_RESIDUAL_FUSION=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_r1.log 2>&1 && VFM_RESIDUAL_FUSION=0 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_r2.log 2>&1 && VFM_RESIDUAL_FUSION=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_r3.log 2>&1 ;;
+    benchkt) timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_kt1.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline --no-kernel-timer > $out/bench_kt0.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_kt3.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline --no-kernel-timer > $out/bench_kt2.log 2>&1 ;;
     benchq)  timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench.log 2>&1 ;;
     benchref) timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline --force-ref-ops > $out/bench_ref.log 2>&1 ;;
     prof)    ps=${PROF_STEPS:-20}

@@ -27,6 +27,13 @@ def enable(flag: bool):
         _records.clear()
 
 
+def set_active(flag: bool):
+    """Pause / resume recording without clearing what was recorded (bench.py samples every n-th
+    timed step: the two events per launch cost host time that the unsampled steps do not pay)."""
+    global _enabled
+    _enabled = bool(flag)
+
+
 def is_enabled():
     return _enabled
 
