@@ -52,8 +52,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
     ap.add_argument("--timer-every", type=int, default=4,
-                    help="per-launch HIP events on every n-th timed step (1 = all; they cost ~5 %% of the "
-                         "step in host time when on every launch)")
+                    help="per-launch HIP events on every n-th launch of each kernel region (1 = all; on every "
+                         "launch they cost ~5 %% of the step in host time)")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", action="store_true",
                     help="experimental: replay the D-phase generator forward from HIP graphs (off: see DESIGN.md)")
@@ -230,14 +230,10 @@ def main(argv=None):
     eq_fwd = eqt.forward
     eqt.forward = lambda *a, **k: draws.append(eq_fwd(*a, **k)) or draws[-1]
     venc = step.G.vfm_encoder
-    kernel_timer.enable(not args.no_kernel_timer)
     every = max(1, args.timer_every)
-    sampled = 0
+    kernel_timer.enable(not args.no_kernel_timer, every)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if not args.no_kernel_timer:
-            kernel_timer.set_active(i % every == 0)
-            sampled += i % every == 0
         h0 = getattr(venc, "reuse_hits", 0)
         one(args.warmup + i, cur)
         hits.append(getattr(venc, "reuse_hits", 0) - h0)
@@ -272,7 +268,7 @@ def main(argv=None):
     roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table)
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
-        roof["timed_steps_sampled"] = f"{sampled} of {args.steps} (every {every})"
+        roof["timer_sampling"] = f"every {every}-th launch of each kernel region over all {args.steps} timed steps"
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

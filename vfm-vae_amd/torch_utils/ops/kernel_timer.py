@@ -18,20 +18,17 @@ SHAPES = os.environ.get("VFM_TIMER_SHAPES", "0") == "1"
 
 _enabled = False
 _records = {}      # name -> list of (start_event, end_event, bytes, flops, bound)
+_counts = {}       # name -> launches seen while enabled (timed or not)
+_every = 1         # time every n-th launch of each region (the events cost host time per launch)
 
 
-def enable(flag: bool):
-    global _enabled
+def enable(flag: bool, every: int = 1):
+    global _enabled, _every
     _enabled = bool(flag)
     if flag:
         _records.clear()
-
-
-def set_active(flag: bool):
-    """Pause / resume recording without clearing what was recorded (bench.py samples every n-th
-    timed step: the two events per launch cost host time that the unsampled steps do not pay)."""
-    global _enabled
-    _enabled = bool(flag)
+        _counts.clear()
+        _every = max(1, int(every))
 
 
 def is_enabled():
@@ -79,6 +76,10 @@ def region(name, nbytes=0, flops=0, bound="hbm"):
     (this is on every launch's host path)."""
     if not _enabled:
         return _NULL
+    c = _counts.get(name, 0)
+    _counts[name] = c + 1
+    if c % _every:
+        return _NULL
     return _timed(name, nbytes, flops, bound)
 
 
@@ -87,8 +88,11 @@ def summary():
     out = {}
     for name, recs in _records.items():
         ms = sum(s.elapsed_time(e) for s, e, *_ in recs)
-        out[name] = dict(launches=len(recs), total_ms=ms, bytes=sum(r[2] for r in recs),
-                         flops=sum(r[3] for r in recs), bound=recs[0][4])
+        n = _counts.get(name, len(recs))
+        scale = n / len(recs)               # every n-th launch timed: totals extrapolated to all launches
+        out[name] = dict(launches=n, timed_launches=len(recs), total_ms=ms * scale,
+                         bytes=sum(r[2] for r in recs) * scale, flops=sum(r[3] for r in recs) * scale,
+                         bound=recs[0][4])
     return out
 
 
@@ -158,7 +162,7 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None):
     return {"bound": r["bound"], "achieved": round(achieved, 1), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": name, "rocprof_kernel": roc,
             "peak_note": note,
-            "launches": r["launches"],
+            "launches": r["launches"], "timed_launches": r["timed_launches"],
             "avg_us": round(r["total_ms"] * 1e3 / r["launches"], 2),
             "bytes_per_launch": int(r["bytes"] / r["launches"]),
             "all_kernels": {k: {"ms": round(v["total_ms"], 3), "launches": v["launches"],

@@ -114,6 +114,7 @@ class FlatGradSync:
         for p in self.params:
             p.grad = None
         self.seen = set()
+        self.staged = []
         self.ready = [0] * len(self.buckets)
         self.pending = {}
         self.last_microbatch = True
@@ -155,7 +156,15 @@ class FlatGradSync:
 
     def _on_grad(self, p):
         self.seen.add(id(p))
-        if not self.last_microbatch or not self.collective:
+        if not self.collective:
+            # world size 1: gather in chunks while the backward is still running (host work and the
+            # multi-tensor copies overlap the GPU instead of trailing it in finish())
+            self.staged.append(p)
+            if len(self.staged) >= 64:
+                self._gather(self.staged)
+                self.staged = []
+            return
+        if not self.last_microbatch:
             return
         bi = self.bucket_of[id(p)]
         if bi in self.pending:              # a second backward touched a bucket already in flight
@@ -210,7 +219,8 @@ class FlatGradSync:
             self._launch_agreement()
             self.flat.mul_(1.0 / self.world)
         else:
-            self._gather(self.params)
+            self._gather(self.staged)
+            self.staged = []
         if gain is not None and gain != 1:
             self.flat.mul_(gain)
         torch.nan_to_num_(self.flat, nan=0, posinf=1e5, neginf=-1e5)
