@@ -52,7 +52,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
     ap.add_argument("--timer-every", type=int, default=4,
-                    help="per-launch HIP events on every n-th launch of each kernel region (1 = all; on every "
+                    help="per-launch HIP events on 1/n of each kernel region's launches (1 = all; on every "
                          "launch they cost ~5 %% of the step in host time)")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", action="store_true",
@@ -268,7 +268,8 @@ def main(argv=None):
     roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table)
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
-        roof["timer_sampling"] = f"every {every}-th launch of each kernel region over all {args.steps} timed steps"
+        roof["timer_sampling"] = (f"1/{every} of each kernel region's launches (pseudo-random by launch index) over all "
+                                  f"{args.steps} timed steps")
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

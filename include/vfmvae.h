@@ -385,6 +385,17 @@ int vfm_posterior_fwd(const float* params, const float* eps, float* z, float* kl
 int vfm_posterior_bwd(const float* params, const float* eps, const float* dz, const float* dkl, float* dparams,
                       int B, int C, long long P, void* stream);
 
+/* ---- BatchNormLocal (1-d) + LeakyReLU of the projected discriminator's heads (replaces
+ * networks/discriminator.py:45-71 + the head blocks' nn.LeakyReLU(0.2), :102-109): x fp32 [B, C, L] in
+ * G virtual batches (B % G == 0), statistics per (group, channel) over the group's samples and L;
+ * y = lrelu((x - mean) rstd w + b, slope), mean / rstd [G, C] saved. bwd: dx and part [2, G, C] =
+ * per-group (sum dz xhat, sum dz) for dw / db (the caller sums over G). w / b may be NULL. */
+int vfm_bnl1d_lrelu_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd, int B,
+                        int C, int L, int G, float eps, float slope, void* stream);
+int vfm_bnl1d_lrelu_bwd(const float* x, const float* dy, const float* w, const float* b, const float* mean,
+                        const float* rstd, float* dx, float* part, int B, int C, int L, int G, float slope,
+                        void* stream);
+
 /* ---- Multi-scale PatchGAN (stage 3), fp32 NHWC ----------------------------------------------
  * Replace networks/discriminator.py:180-228 (NLayerDiscriminator's nn.Conv2d k4 s2/s1 p2 layers,
  * run by the reference on cuDNN) around our MFMA GEMM, and :75-99 (BatchNormLocal2d) + LeakyReLU.

@@ -125,3 +125,40 @@ def test_bn_local_lrelu_kernel():
     assert _rel(xg.grad, xd.grad) < 2e-5
     assert _rel(wg.grad, wd.grad) < 2e-5
     assert _rel(bg.grad, bd.grad) < 2e-5
+
+
+@pytest.mark.parametrize("B,C,L,k", [(16, 384, 196, 9), (2, 384, 197, 1), (8, 64, 33, 9)])
+def test_head_block_fused_bn_lrelu(B, C, L, k):
+    """The projected discriminator's head block (SpectralConv1d -> BatchNormLocal -> LeakyReLU) with
+    the fused HIP BatchNormLocal + LeakyReLU (csrc/patchgan.hip bn1d_*) vs the same module's torch
+    formulation in fp64: output, input and parameter gradients."""
+    from networks.discriminator import make_block
+    from torch_utils.ops import kernel_timer
+    torch.manual_seed(B + L)
+    blk = make_block(C, k)
+    blk[1].weight.data.normal_(1.0, 0.2)
+    blk[1].bias.data.normal_(0.0, 0.2)
+    x = torch.randn(B, C, L)
+    r = torch.randn(B, C, L)
+    # eval(): the spectral norm uses its stored power-iteration vectors without updating them (so both
+    # copies normalise the same weight); BatchNormLocal always normalises with the batch statistics
+    state = {kk: v.detach().clone().double() for kk, v in blk.state_dict().items()}
+    bg = blk.cuda().eval()
+    xg = x.cuda().requires_grad_()
+    kernel_timer.enable(True)
+    y = bg(xg)
+    (y * r.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    names = set(kernel_timer.summary())
+    kernel_timer.enable(False)
+    assert "bnl1d_lrelu_fwd<f32>" in names and "bnl1d_lrelu_bwd<f32>" in names, names
+    bc = make_block(C, k).double().eval()
+    bc.load_state_dict(state)
+    xc = x.double().requires_grad_()
+    yc = torch.nn.Sequential.forward(bc, xc)
+    (yc * r.double()).sum().backward()
+    assert _rel(y, yc) < 1e-5, _rel(y, yc)
+    assert _rel2(xg.grad, xc.grad) < 1e-3, _rel2(xg.grad, xc.grad)
+    for (n, p), (_, q) in zip(bg.named_parameters(), bc.named_parameters()):
+        if p.grad is not None:
+            assert _rel2(p.grad, q.grad) < 1e-3, (n, _rel2(p.grad, q.grad))

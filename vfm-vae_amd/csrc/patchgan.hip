@@ -277,6 +277,87 @@ __global__ __launch_bounds__(256) void bn_apply(BnArgs a, const float* __restric
     *reinterpret_cast<float4*>(a.out + 4 * i) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+
+// ---- BatchNormLocal (1-d, the projected discriminator's heads) + LeakyReLU over [B, C, L] -----------
+// reference networks/discriminator.py:45-71 (BatchNormLocal over virtual batches of 8: statistics per
+// (group, channel) over the group's samples and L) and the head blocks' LeakyReLU(0.2) (:102-109).
+// One block per (group, channel): the n * L values (<= 8 x 200 here) are reduced in two passes
+// (mean, then centred variance), fixed-order block reductions; backward: sum dz, sum dz xhat, dx.
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void bn1d_fwd(const float* __restrict__ x, const float* __restrict__ w,
+                                                const float* __restrict__ b, float* __restrict__ y,
+                                                float* __restrict__ mean, float* __restrict__ rstd, int C, int L,
+                                                int n, float eps, float slope) {
+    __shared__ float red[4];
+    const int g = blockIdx.y, c = blockIdx.x;
+    const int cnt = n * L;
+    auto at = [&](int i) -> long long { const int s = i / L; return ((long long)(g * n + s) * C + c) * L + (i - s * L); };
+    float s1 = 0.f;
+    for (int i = threadIdx.x; i < cnt; i += 256) s1 += x[at(i)];
+    const float mu = block_sum256(s1, red) / (float)cnt;
+    float s2 = 0.f;
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+        const float d = x[at(i)] - mu;
+        s2 = fmaf(d, d, s2);
+    }
+    const float rs = 1.f / sqrtf(block_sum256(s2, red) / (float)cnt + eps);
+    const float wc = w ? w[c] : 1.f, bc = b ? b[c] : 0.f;
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+        const long long o = at(i);
+        const float z = fmaf((x[o] - mu) * rs, wc, bc);
+        y[o] = z > 0.f ? z : z * slope;
+    }
+    if (threadIdx.x == 0) {
+        mean[g * C + c] = mu;
+        rstd[g * C + c] = rs;
+    }
+}
+
+__global__ __launch_bounds__(256) void bn1d_bwd(const float* __restrict__ x, const float* __restrict__ dy,
+                                                const float* __restrict__ w, const float* __restrict__ b,
+                                                const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                float* __restrict__ dx, float* __restrict__ part, int C, int L, int n,
+                                                float slope) {
+    __shared__ float red[4];
+    const int g = blockIdx.y, c = blockIdx.x, G = gridDim.y;
+    const int cnt = n * L;
+    auto at = [&](int i) -> long long { const int s = i / L; return ((long long)(g * n + s) * C + c) * L + (i - s * L); };
+    const float mu = mean[g * C + c], rs = rstd[g * C + c];
+    const float wc = w ? w[c] : 1.f, bc = b ? b[c] : 0.f;
+    float a0 = 0.f, a1 = 0.f;
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+        const long long o = at(i);
+        const float h = (x[o] - mu) * rs;
+        const float z = fmaf(h, wc, bc);
+        const float dz = z > 0.f ? dy[o] : dy[o] * slope;
+        a0 += dz;
+        a1 = fmaf(dz, h, a1);
+    }
+    const float S1 = block_sum256(a0, red);
+    const float S2 = block_sum256(a1, red);
+    const float m1 = S1 / (float)cnt, m2 = S2 / (float)cnt;
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+        const long long o = at(i);
+        const float h = (x[o] - mu) * rs;
+        const float z = fmaf(h, wc, bc);
+        const float dz = z > 0.f ? dy[o] : dy[o] * slope;
+        dx[o] = rs * wc * (dz - m1 - h * m2);
+    }
+    if (threadIdx.x == 0) {                 // per-group partials of dw (sum dz xhat) and db (sum dz)
+        part[(long long)g * C + c] = S2;
+        part[((long long)G + g) * C + c] = S1;
+    }
+}
+
 int bn_setup(BnArgs& a, int B, int P, int C, int G) {
     if (B <= 0 || P <= 0 || C < 4 || C % 4 || C > 1024 || 256 % (C / 4) || G <= 0 || B % G) return VFM_ERR_ARGS;
     a.B = B; a.P = P; a.C = C; a.G = G; a.n = B / G;
@@ -412,5 +493,28 @@ extern "C" int vfm_bnl_lrelu_bwd(const float* x, const float* dy, const float* w
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
     hipLaunchKernelGGL(bn_apply<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, (const float*)c0,
                        (const float*)c1, total4);
+    return launch_status();
+}
+
+// BatchNormLocal (1-d) + LeakyReLU over x [B, C, L] fp32 in G virtual batches (B % G == 0); mean / rstd
+// [G, C] saved for the backward. bwd: dx, and part [2, G, C] = per-group (sum dz xhat, sum dz).
+extern "C" int vfm_bnl1d_lrelu_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+                                   int B, int C, int L, int G, float eps, float slope, void* stream) {
+    if (!x || !y || !mean || !rstd || B <= 0 || C <= 0 || L <= 0 || G <= 0 || B % G || C > 65535 || G > 65535)
+        return VFM_ERR_ARGS;
+    if ((long long)(B / G) * L > 0x7fffffffLL) return VFM_ERR_ARGS;
+    hipLaunchKernelGGL(bn1d_fwd, dim3(C, G), dim3(256), 0, (hipStream_t)stream, x, w, b, y, mean, rstd, C, L, B / G,
+                       eps, slope);
+    return launch_status();
+}
+
+extern "C" int vfm_bnl1d_lrelu_bwd(const float* x, const float* dy, const float* w, const float* b, const float* mean,
+                                   const float* rstd, float* dx, float* part, int B, int C, int L, int G, float slope,
+                                   void* stream) {
+    if (!x || !dy || !dx || !part || !mean || !rstd || B <= 0 || C <= 0 || L <= 0 || G <= 0 || B % G ||
+        C > 65535 || G > 65535)
+        return VFM_ERR_ARGS;
+    hipLaunchKernelGGL(bn1d_bwd, dim3(C, G), dim3(256), 0, (hipStream_t)stream, x, dy, w, b, mean, rstd, dx, part, C,
+                       L, B / G, slope);
     return launch_status();
 }

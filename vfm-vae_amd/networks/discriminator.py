@@ -112,8 +112,26 @@ class BatchNormLocal2d(nn.Module):
         return x.view(shape)
 
 
+class HeadBlock(nn.Sequential):
+    """SpectralConv1d -> BatchNormLocal -> LeakyReLU(0.2) (same modules / state-dict keys as the
+    reference's nn.Sequential). On ROCm fp32 inputs the BatchNormLocal + LeakyReLU pair runs as one
+    fused HIP kernel per direction (patchgan_hip.bn_local1d_lrelu); the conv stays exact fp32."""
+
+    def forward(self, x):
+        conv, bn, act = self[0], self[1], self[2]
+        if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3):
+            return super().forward(x)
+        h = conv(x)
+        G = int(np.ceil(h.shape[0] / bn.virtual_bs))
+        if h.shape[0] % G:
+            return act(bn(h))
+        from torch_utils.ops import patchgan_hip
+        return patchgan_hip.bn_local1d_lrelu(h, bn.weight if bn.affine else None, bn.bias if bn.affine else None, G,
+                                            bn.eps, act.negative_slope)
+
+
 def make_block(channels, kernel_size):
-    return nn.Sequential(
+    return HeadBlock(
         SpectralConv1d(channels, channels, kernel_size=kernel_size, padding=kernel_size // 2, padding_mode='circular'),
         BatchNormLocal(channels),
         nn.LeakyReLU(0.2, True),

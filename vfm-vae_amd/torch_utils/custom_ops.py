@@ -78,6 +78,8 @@ SIGNATURES = {
     "vfm_posterior_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_dwconv2d_bwd_weight_mfma_tiles": [c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_dwconv2d_bwd_weight_mfma": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_bnl1d_lrelu_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_vp],
+    "vfm_bnl1d_lrelu_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_vp],
     "vfm_torgb_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_torgb_bwd_splits": [c_int, c_int, c_int],
     "vfm_torgb_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],

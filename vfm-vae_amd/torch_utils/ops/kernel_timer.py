@@ -19,7 +19,7 @@ SHAPES = os.environ.get("VFM_TIMER_SHAPES", "0") == "1"
 _enabled = False
 _records = {}      # name -> list of (start_event, end_event, bytes, flops, bound)
 _counts = {}       # name -> launches seen while enabled (timed or not)
-_every = 1         # time every n-th launch of each region (the events cost host time per launch)
+_every = 1         # time ~1/n of each region's launches (the events cost host time per launch)
 
 
 def enable(flag: bool, every: int = 1):
@@ -71,6 +71,15 @@ def suspended():
         _enabled = prev
 
 
+def _mix(c):
+    """32-bit integer hash (murmur3 finaliser) of a launch index."""
+    x = (c + 0x9E3779B9) & 0xFFFFFFFF
+    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
+    return x ^ (x >> 16)
+
+
 def region(name, nbytes=0, flops=0, bound="hbm"):
     """Context manager around one native launch; a shared no-op object when timing is off
     (this is on every launch's host path)."""
@@ -78,7 +87,9 @@ def region(name, nbytes=0, flops=0, bound="hbm"):
         return _NULL
     c = _counts.get(name, 0)
     _counts[name] = c + 1
-    if c % _every:
+    # a pseudo-random 1/_every of each region's launches (integer hash of the launch index): a plain
+    # stride aliases with the region's launches per step (every 4th of 10 per step = even ones only)
+    if _every > 1 and _mix(c) % _every:
         return _NULL
     return _timed(name, nbytes, flops, bound)
 

@@ -159,6 +159,48 @@ class _BnLocalLReLU(torch.autograd.Function):
         return (dx, None if dw is None else dw.to(wdt), None if db is None else db.to(bdt), None, None, None)
 
 
+class _BnLocal1dLReLU(torch.autograd.Function):
+    """lrelu(BatchNormLocal(x)) over [B, C, L] fp32, G virtual batches (the D heads' blocks)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, G, eps, slope):
+        B, C, L = x.shape
+        x = x.contiguous()
+        w32 = None if weight is None else weight.detach().float().contiguous()
+        b32 = None if bias is None else bias.detach().float().contiguous()
+        mean = torch.empty([G, C], dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        y = torch.empty_like(x)
+        with kernel_timer.region("bnl1d_lrelu_fwd<f32>", 4 * 3 * x.numel()):
+            _check(_lib.vfm_bnl1d_lrelu_fwd(x.data_ptr(), custom_ops.ptr(w32), custom_ops.ptr(b32), y.data_ptr(),
+                                            mean.data_ptr(), rstd.data_ptr(), B, C, L, G, float(eps), float(slope),
+                                            _stream()), "vfm_bnl1d_lrelu_fwd")
+        ctx.save_for_backward(x, w32, b32, mean, rstd)
+        ctx.cfg = (G, slope, None if weight is None else weight.dtype, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x, w32, b32, mean, rstd = ctx.saved_tensors
+        G, slope, wdt, bdt = ctx.cfg
+        B, C, L = x.shape
+        dy = dy.float().contiguous()
+        dx = torch.empty_like(x)
+        part = torch.empty([2, G, C], dtype=torch.float32, device=x.device)
+        with kernel_timer.region("bnl1d_lrelu_bwd<f32>", 4 * 4 * x.numel()):
+            _check(_lib.vfm_bnl1d_lrelu_bwd(x.data_ptr(), dy.data_ptr(), custom_ops.ptr(w32), custom_ops.ptr(b32),
+                                            mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), B, C, L,
+                                            G, float(slope), _stream()), "vfm_bnl1d_lrelu_bwd")
+        dw = None if w32 is None else part[0].sum(0).to(wdt)
+        db = None if b32 is None else part[1].sum(0).to(bdt)
+        return dx, dw, db, None, None, None
+
+
+def bn_local1d_lrelu(x, weight, bias, groups, eps, slope):
+    return _BnLocal1dLReLU.apply(x, weight, bias, int(groups), float(eps), float(slope))
+
+
 def supported(x):
     return x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
 
