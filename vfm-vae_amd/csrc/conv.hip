@@ -96,6 +96,33 @@ struct StageA {
                       : make_uint4(0, 0, 0, 0);
         }
     }
+    // Cin >= 64: a K-tile is 64 channels of ONE tap, so the 8 rows' validity and 32-bit element offsets
+    // (pixel + tap shift, times Cin) change only with the tap; per K-tile only the channel offset moves
+    int off[8];
+    unsigned okm;
+    int cur_tap;
+    __device__ __forceinline__ void tap_setup(const ConvArgs& a, int tap) {
+        const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
+        okm = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int yy = (pyx[u] >> 16) + dy, xx = (pyx[u] & 0xffff) + dx;
+            const bool ok = pm[u] >= 0 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+            okm |= (unsigned)ok << u;
+            off[u] = ok ? (pm[u] + dy * a.W + dx) * a.Cin : 0;
+        }
+        cur_tap = tap;
+    }
+    __device__ __forceinline__ void load_wide(const ConvArgs& a, int k0, int tid) {
+        const int tap = k0 >> a.lc;                      // uniform
+        if (tap != cur_tap) tap_setup(a, tap);
+        const int c = (k0 & (a.Cin - 1)) + 4 * (tid & 15);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            r[u] = ((okm >> u) & 1)
+                       ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.x) + (unsigned)(off[u] + c) * 4u)
+                       : make_uint4(0, 0, 0, 0);
+    }
     __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
         const int cc = tid & 15;
 #pragma unroll
@@ -114,9 +141,9 @@ struct StageB {
         for (int u = 0; u < PER; ++u) {
             const int c = tid + THREADS * u, row = c >> 3, k = k0 + 8 * (c & 7), n = n0 + row;
             const bool ok = k < a.ldw && n < a.Cout;
-            const long long o = (long long)n * a.ldw + k;
-            h[u] = ok ? *reinterpret_cast<const uint4*>(a.wh + o) : make_uint4(0, 0, 0, 0);
-            l[u] = ok ? *reinterpret_cast<const uint4*>(a.wl + o) : make_uint4(0, 0, 0, 0);
+            const unsigned o = (unsigned)(n * a.ldw + k) * 2u;          // byte offset (host: Cout * ldw < 2^30)
+            h[u] = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.wh) + o) : make_uint4(0, 0, 0, 0);
+            l[u] = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.wl) + o) : make_uint4(0, 0, 0, 0);
         }
     }
     __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
@@ -156,20 +183,24 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
     StageA sa;
     StageB<BN> sb;
     sa.init(a, m0, tid);
+    sa.cur_tap = -1;
+    const bool wide = a.lc >= 6;                        // Cin >= 64 (uniform)
     f32x16 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
 
-    sa.load(a, 0, tid);
+    if (wide) sa.load_wide(a, 0, tid);
+    else sa.load(a, 0, tid);
     sb.load(a, n0, 0, tid);
     for (int k0 = 0; k0 < a.K; k0 += BK) {
         sa.store(a_hi, a_lo, tid);
         sb.store(b_hi, b_lo, tid);
         __syncthreads();
         if (k0 + BK < a.K) {
-            sa.load(a, k0 + BK, tid);
+            if (wide) sa.load_wide(a, k0 + BK, tid);
+            else sa.load(a, k0 + BK, tid);
             sb.load(a, n0, k0 + BK, tid);
         }
 #pragma unroll
@@ -209,11 +240,11 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
             for (int e = 0; e < 16; ++e) {
                 const int m = m0 + 64 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * hh;
                 if (m >= a.M) continue;
-                const long long o = (long long)m * a.Cout + n;
+                const unsigned o = (unsigned)(m * a.Cout + n) * 4u;     // byte offset (host: M * Cout < 2^30)
                 float v = acc[i][j][e] + bn;
                 if (a.relu) v = fmaxf(v, 0.f);
-                if (a.mask && !(a.mask[o] > 0.f)) v = 0.f;
-                a.out[o] = v;
+                if (a.mask && !(*reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.mask) + o) > 0.f)) v = 0.f;
+                *reinterpret_cast<float*>(reinterpret_cast<char*>(a.out) + o) = v;
             }
     }
 }
@@ -244,6 +275,9 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void
     const long long M = (long long)B * H * W;
     if (M * (long long)(Cin > Cout ? Cin : Cout) >= (1ll << 40) || M >= (1ll << 31) - 2 * (long long)W - 2)
         return VFM_ERR_ARGS;
+    // 32-bit byte offsets in the loaders / epilogue
+    if (Cin >= 64 && (M + 2 * (long long)W + 2) * Cin >= (1ll << 30)) return VFM_ERR_ARGS;
+    if (M * (long long)Cout >= (1ll << 30) || (long long)Cout * ldw >= (1ll << 30)) return VFM_ERR_ARGS;
     ConvArgs a;
     a.x = x; a.wh = (const __hip_bfloat16*)w_hi; a.wl = (const __hip_bfloat16*)w_lo; a.ldw = ldw;
     a.bias = bias; a.mask = mask; a.out = out;
