@@ -128,3 +128,5 @@ def test_kernel_timer_rocprof_names():
     assert kt.rocprof_name("gemm8<f32x3,true,true,true>") == "gemm8_kernel<true, true, true>"
     assert kt.rocprof_name("dwconv2d_fwd<bf16,7>") == "dwr_fwd<__hip_bfloat16, 7>"
     assert kt.rocprof_name("gemm_ws<f32x3,true,true,true>") is None
+    assert kt.rocprof_name("convnext_mlp_fwd<bf16,128,true>") == "mlp_fwd<128, true>"
+    assert kt.rocprof_name("dwconv2d_mfma_bwd_weight<bf16,7>") == "dwm_bwd_w<7, "

@@ -303,7 +303,9 @@ struct MlpArgs {
     int N;
 };
 
-template <int C>
+// SAVE: the autograd forward, which also writes h and g for the backward (a separate instantiation,
+// so the no-grad launches carry no dead stores and rocprofv3 reports the two apart)
+template <int C, bool SAVE>
 __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
     constexpr int M = 4 * C;
     constexpr int YB = C / 128;                 // 32-row output blocks per wave (1 or 2)
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
         // GELU epilogue into the g image (row = hidden row within the chunk, column = pixel): registers
         // i, i+1 are rows lr, lr+1 of column col = 64 cw + 32 nb + r, processed as a packed pair;
         // 16-bit LDS / global writes per row (no lane-pair exchange)
-        __hip_bfloat16* hb = a.hout ? a.hout + ((long long)b * M + mc) * N + n0 : nullptr;   // block-uniform
+        __hip_bfloat16* hb = SAVE ? a.hout + ((long long)b * M + mc) * N + n0 : nullptr;
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
             const int lr = 32 * rw + (i & 3) + 8 * (i >> 2) + 4 * hh;     // chunk-local row of register i
@@ -398,7 +400,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
                 const int o1 = swz(lr + 1, col >> 3) + 2 * (col & 7);
                 *reinterpret_cast<uint16_t*>(gimg + o) = (uint16_t)gp;
                 *reinterpret_cast<uint16_t*>(gimg + o1) = (uint16_t)(gp >> 16);
-                if (hb) {           // saved for the backward (autograd pass); g goes out below
+                if constexpr (SAVE) {   // saved for the backward; g goes out below
                     const unsigned ho = (unsigned)(lr * N + col);               // uniform base + 32-bit offset
                     *reinterpret_cast<uint16_t*>(hb + ho) = (uint16_t)hp;
                     *reinterpret_cast<uint16_t*>(hb + ho + (unsigned)N) = (uint16_t)(hp >> 16);
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
             }
         }
         __syncthreads();
-        if (a.gout) {
+        if constexpr (SAVE) {
             // g for the backward straight from the LDS image: 16-B chunks, whole 256-B rows per
             // 16 threads (the register layout would need 4-B stores of lane pairs)
 #pragma unroll
@@ -475,6 +477,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
         }
     }
 }
+template <int C, bool SAVE>
+void launch_mlp(const MlpArgs& a, int B, size_t lds, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)mlp_fwd<C, SAVE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL((mlp_fwd<C, SAVE>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
+}
 }  // namespace
 
 extern "C" int vfm_pw_gemm_gelu(const void* A, const void* X, const float* scale, const float* bias,
@@ -537,20 +548,13 @@ extern "C" int vfm_convnext_mlp_fwd(const void* W1, const void* m, const float* 
     a.N = N;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t lds = (size_t)C * 256 + 128 * 256 + 8 * 4 * (size_t)C + 8 * (size_t)C;
+    const bool save = hout != nullptr;
     if (C == 128) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)mlp_fwd<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL((mlp_fwd<128>), dim3(N / NT, B), dim3(64 * WAVES), lds, st, a);
+        if (save) launch_mlp<128, true>(a, B, lds, st);
+        else launch_mlp<128, false>(a, B, lds, st);
     } else {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)mlp_fwd<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL((mlp_fwd<256>), dim3(N / NT, B), dim3(64 * WAVES), lds, st, a);
+        if (save) launch_mlp<256, true>(a, B, lds, st);
+        else launch_mlp<256, false>(a, B, lds, st);
     }
     return launch_status();
 }

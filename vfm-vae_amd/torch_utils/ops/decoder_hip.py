@@ -524,7 +524,7 @@ class _ConvNeXtMLP(torch.autograd.Function):
         h = torch.empty([B, 4 * C, P], dtype=torch.bfloat16, device=m.device)
         g = torch.empty_like(h)
         y = torch.empty_like(m)
-        with kernel_timer.region(_rn('convnext_mlp_fwd', m), _nb(m, x_in, out, h, g, y)):
+        with kernel_timer.region(_rn('convnext_mlp_fwd', m, C, 'true'), _nb(m, x_in, out, h, g, y)):
             _check(_lib.vfm_convnext_mlp_fwd(w1c.data_ptr(), m.data_ptr(), _p(s), _p(fb1), w2c.data_ptr(), _p(fb2),
                                              _p(fg), x_in.data_ptr(), out.data_ptr(), h.data_ptr(), g.data_ptr(),
                                              y.data_ptr(), B, C, P, _stream()), 'vfm_convnext_mlp_fwd')
@@ -595,7 +595,7 @@ def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
     w2c = _cast_cached(w2, torch.bfloat16).contiguous()
     s = None if dcoef is None else dcoef.detach().float().contiguous()
     out = torch.empty_like(x_in)
-    with kernel_timer.region(_rn('convnext_mlp_fwd', m), _nb(m, x_in, out), flops=4.0 * B * P * C * 4 * C,
+    with kernel_timer.region(_rn('convnext_mlp_fwd', m, C, 'false'), _nb(m, x_in, out), flops=4.0 * B * P * C * 4 * C,
                              bound="hbm"):
         _check(_lib.vfm_convnext_mlp_fwd(w1c.data_ptr(), m.data_ptr(), _p(s), _p(_f32(b1)), w2c.data_ptr(),
                                          _p(_f32(b2)), _p(_f32(gamma)), x_in.data_ptr(), out.data_ptr(), None, None, None, B, C, P,

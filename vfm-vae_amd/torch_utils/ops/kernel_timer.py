@@ -136,6 +136,8 @@ def rocprof_name(region):
     if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, F32, OUTF32>
         f32 = "true" if args[0] == "f32x3" else "false"
         return f"gemm_kernel<{args[1]}, {args[2]}, {f32}, {args[3]}>"
+    if base == "convnext_mlp_fwd" and len(args) == 3:          # mlp_fwd<C, SAVE>
+        return f"mlp_fwd<{args[1]}, {args[2]}>"
     pat = _ROC.get(base)
     if pat is None:
         return None
