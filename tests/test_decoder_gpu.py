@@ -130,7 +130,10 @@ def test_dwconv2d_no_bias_valid_padding():
          [x, w], torch.float32, ["dwconv2d_fwd"])
 
 
-GN_CASES = [(2, 64, 16, 16, 16), (2, 12, 5, 7, 3), (3, 32, 8, 8, 32), (1, 256, 32, 32, 32), (2, 8, 1, 1, 2)]
+GN_CASES = [(2, 64, 16, 16, 16), (2, 12, 5, 7, 3), (3, 32, 8, 8, 32), (1, 256, 32, 32, 32), (2, 8, 1, 1, 2),
+            # flat forms: 2-lane channel segments, channels spanning many chunk rounds; channel-loop
+            # fallbacks: HW / 8 not a power of two, more than 128 channels per group
+            (2, 8, 4, 4, 1), (2, 64, 128, 128, 32), (1, 16, 24, 24, 4), (1, 512, 16, 16, 2)]
 
 
 @pytest.mark.parametrize("dt_in,dt_out", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
@@ -194,9 +197,11 @@ def test_layer_scale_residual(shape, dt_y, dt_x):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("taps", [[1, 2, 1], [1, 3, 3, 1], [1, 4, 6, 4, 1]])
+@pytest.mark.parametrize("taps", [[1, 1], [1, 2, 1], [1, 3, 3, 1], [1, 4, 6, 4, 1], [1, 7, 21, 35, 35, 21, 7, 1]])
 @pytest.mark.parametrize("shape,r", [((2, 16, 8, 8), 2), ((1, 12, 5, 7), 2), ((2, 4, 9, 6), 1), ((1, 4, 1, 1), 2),
-                                     ((1, 2, 16, 32), 1), ((1, 8, 40, 70), 2), ((1, 3, 70, 130), 1)])
+                                     ((1, 2, 16, 32), 1), ((1, 8, 40, 70), 2), ((1, 3, 70, 130), 1),
+                                     # 16-B vector forms (W % 8 == 0) with partial edge tiles
+                                     ((2, 8, 40, 48), 2), ((1, 3, 72, 136), 1), ((1, 4, 3, 8), 2)])
 def test_shuffle_blur(shape, r, taps, dt):
     ops, _ = _ops()
     torch.manual_seed(7)

@@ -632,6 +632,11 @@ struct GnArgs {
     float eps;
 };
 
+// Flat forms (8 | HW, HW / 8 a power of two, at most GN_FLAT_MAX channels per group): the
+// group is walked as one run of 8-element chunks by all threads instead of channel by channel
+// (which left most threads idle on planes under 2048 elements and cost two barriers per channel).
+constexpr int GN_FLAT_MAX = 128;
+
 template <class TI, class TO>
 __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
     __shared__ float scratch[8];
@@ -671,6 +676,36 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
         a.rstd[bg] = rstd;
     }
     TO* yp = reinterpret_cast<TO*>(a.y) + (long long)bg * n;
+    const int cpc = a.HW >> 3;                     // 8-element chunks per channel
+    if (vec && cpg <= GN_FLAT_MAX && (cpc & (cpc - 1)) == 0) {
+        // flat form: every thread walks the whole group in chunks, so small planes (8x8 ..
+        // 32x32 in the fp32 blocks) keep all 256 threads busy; per-channel affine from LDS
+        __shared__ float s_sc[GN_FLAT_MAX], s_sh[GN_FLAT_MAX];
+        for (int cl = threadIdx.x; cl < cpg; cl += NT) {
+            const int c = g * cpg + cl;
+            float sc = rstd * (a.w ? a.w[c] : 1.f);
+            float sh = (a.b ? a.b[c] : 0.f) - mean * sc;
+            if (a.s) {
+                const float m = a.s[bidx * a.C + c];
+                sc *= m;
+                sh *= m;
+            }
+            s_sc[cl] = sc;
+            s_sh[cl] = sh;
+        }
+        __syncthreads();
+        const int lg = __builtin_ctz(cpc);
+        for (long long i = threadIdx.x; i < nv; i += NT) {
+            const int cl = (int)(i >> lg);
+            const float sc = s_sc[cl], sh = s_sh[cl];
+            float v[8];
+            load8(xp + i * 8, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sc, sh);
+            store8(yp + i * 8, v);
+        }
+        return;
+    }
     for (int cl = 0; cl < cpg; ++cl) {
         const int c = g * cpg + cl;
         float sc = rstd * (a.w ? a.w[c] : 1.f);
@@ -711,6 +746,85 @@ struct GnBwdArgs {
     int B, C, G, HW;
 };
 
+// Flat backward. Pass 1: per-channel sums A_c = sum dy*xhat, B_c = sum dy with the group
+// walked in chunks by all threads; a thread's partial sums are reduced over the lanes that share
+// its channel (an aligned segment of min(HW/8, 64) lanes) whenever the wave moves to the next
+// channel, and each wave stores its channel partial in its own LDS slot: every (wave, channel)
+// slot has one writer, and the 4 wave slots are added in a fixed order -- deterministic.
+template <class TX, class TY>
+__device__ __forceinline__ void gn_bwd_flat(const GnBwdArgs& a, int bg, int bidx, int g, int cpg, int cpc,
+                                            const TX* xp, const TY* gp, float mean, float rstd) {
+    __shared__ float s_pa[4][GN_FLAT_MAX], s_pb[4][GN_FLAT_MAX], s_k[GN_FLAT_MAX];
+    __shared__ float scratch[8];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lg = __builtin_ctz(cpc);
+    const long long nch = (long long)cpg * cpc;
+    for (int i = threadIdx.x; i < 4 * GN_FLAT_MAX; i += NT) {
+        (&s_pa[0][0])[i] = 0.f;
+        (&s_pb[0][0])[i] = 0.f;
+    }
+    __syncthreads();
+    const int seg = cpc < 64 ? cpc : 64;
+    float sa = 0.f, sb = 0.f;
+    for (long long base = 0; base < nch; base += NT) {
+        const long long i = base + threadIdx.x;
+        if (i < nch) {
+            float xv[8], gv[8];
+            load8(xp + i * 8, xv);
+            load8(gp + i * 8, gv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                sa = fmaf(gv[k], (xv[k] - mean) * rstd, sa);
+                sb += gv[k];
+            }
+        }
+        const long long w0 = base + 64 * wave;        // this wave's first chunk
+        const bool flush = cpc < 64 || w0 + NT >= nch || ((w0 + NT) >> lg) != (w0 >> lg);
+        if (flush) {                                  // wave-uniform
+            for (int off = seg >> 1; off >= 1; off >>= 1) {
+                sa += __shfl_xor(sa, off);
+                sb += __shfl_xor(sb, off);
+            }
+            if ((lane & (seg - 1)) == 0 && i < nch) {
+                const int cl = (int)(i >> lg);
+                s_pa[wave][cl] = sa;
+                s_pb[wave][cl] = sb;
+            }
+            sa = sb = 0.f;
+        }
+    }
+    __syncthreads();
+    float cx = 0.f, cxx = 0.f;
+    for (int cl = threadIdx.x; cl < cpg; cl += NT) {
+        const float A = (s_pa[0][cl] + s_pa[1][cl]) + (s_pa[2][cl] + s_pa[3][cl]);
+        const float Bs = (s_pb[0][cl] + s_pb[1][cl]) + (s_pb[2][cl] + s_pb[3][cl]);
+        const int c = g * cpg + cl;
+        const float wc = a.w ? a.w[c] : 1.f;
+        const float sc = a.s ? a.s[bidx * a.C + c] : 1.f;
+        cx += sc * wc * Bs;
+        cxx += sc * wc * A;
+        s_k[cl] = wc * sc;
+        a.dw_part[bidx * a.C + c] = sc * A;
+        a.db_part[bidx * a.C + c] = sc * Bs;
+        if (a.ds) a.ds[bidx * a.C + c] = wc * A + (a.b ? a.b[c] : 0.f) * Bs;
+    }
+    const float n = (float)nch * 8.f;
+    const float m1 = block_sum(cx, scratch) / n, m2 = block_sum(cxx, scratch + 4) / n;
+    TX* dxp = reinterpret_cast<TX*>(a.dx) + (long long)bg * nch * 8;
+    for (long long i = threadIdx.x; i < nch; i += NT) {
+        const float k = s_k[(int)(i >> lg)];
+        float xv[8], gv[8], o[8];
+        load8(xp + i * 8, xv);
+        load8(gp + i * 8, gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float xh = (xv[j] - mean) * rstd;
+            o[j] = rstd * (gv[j] * k - m1 - xh * m2);
+        }
+        store8(dxp + i * 8, o);
+    }
+}
+
 // Per (sample, group) workgroup. Pass 1: per-channel sums A_c = sum dy*xhat, B_c = sum dy
 // (channel loop, one workgroup reduction per channel). Pass 2: dx.
 template <class TX, class TY>
@@ -724,6 +838,11 @@ __global__ __launch_bounds__(NT) void gn_bwd(GnBwdArgs a) {
     const TY* gp = reinterpret_cast<const TY*>(a.dy) + (long long)bg * n;
     const float mean = a.mean[bg], rstd = a.rstd[bg];
     const bool vec = (a.HW % 8) == 0;
+    const int cpc = a.HW >> 3;
+    if (vec && cpg <= GN_FLAT_MAX && (cpc & (cpc - 1)) == 0) {
+        gn_bwd_flat<TX, TY>(a, bg, bidx, g, cpg, cpc, xp, gp, mean, rstd);
+        return;
+    }
     float sum_dxhat = 0.f, sum_dxhat_xhat = 0.f;   // group sums (block-uniform)
     for (int cl = 0; cl < cpg; ++cl) {
         const TX* xc = xp + (long long)cl * a.HW;
@@ -947,7 +1066,16 @@ struct BlurArgs {
 // Tiled forms: one workgroup = one (sample, channel) plane x a 64 x 32 tile of the
 // (shuffled, full-resolution) image. The separable blur runs as a row pass then a column
 // pass through LDS, so every input element is read from HBM once per tile (plus halo).
+//
+// Vector form (source width W % 8 == 0, every shape of the decoder): global memory is touched
+// only in 8-element chunks (16 B for 16-bit types): the staged rows are whole chunks, and the
+// column pass gives each thread one row x 8 consecutive destination elements, stored with one
+// 16-B store. In the backward the destination is the pre-shuffle layout, so the row pass writes
+// its result de-interleaved by sub-pixel column (R = 2: [even X | odd X]) and a thread's 8
+// outputs are contiguous in both LDS and its source plane. The scalar form (2-byte accesses)
+// remains for other widths.
 constexpr int BTW = 64, BTH = 32;
+constexpr int SBW = BTW + 4;          // padded LDS row stride of the row-pass result
 
 // R (shuffle factor) is a template constant: the sub-pixel plane / low-res coordinate of a
 // full-resolution (Y, X) are shifts and masks, not integer divisions.
@@ -955,8 +1083,12 @@ template <class T, int R, int K>
 __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
     constexpr int P = (K - 1) / 2;
     constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
+    constexpr int SC = BTW / R + 16;                 // source columns kept per plane (vector form)
+    constexpr int NB = LH * R * SC > LH * SBW ? LH * R * SC : LH * SBW;
     __shared__ float sA[LH * LW];
-    __shared__ float sB[LH * BTW];
+    __shared__ __attribute__((aligned(16))) float sBuf[NB];   // staged source rows, then the row pass
+    float* sS = sBuf;
+    float* sB = sBuf;
     const int Ho = a.H * R, Wo = a.W * R;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
@@ -971,30 +1103,27 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
     float k[K];
 #pragma unroll
     for (int t = 0; t < K; ++t) k[t] = a.k[t];
-    if (R == 2 && (a.W & 7) == 0) {
-        // Vector staging (R = 2): the window's source columns of both sub-pixel planes of each
-        // staged row as 8-element chunks (16-B loads for 16-bit types) into sS, then the
-        // replicate-clamped, shuffled window gathered from LDS -- 8x fewer memory instructions
-        // than one 2-byte load per window element (the kernel was load-latency bound, PMC).
-        constexpr int SC = BTW / 2 + 16;                 // source columns kept per plane
-        __shared__ float sS[LH * 2 * SC];
-        const int c_lo = max(0, X0 / 2 - 8), c_hi = min(a.W, X0 / 2 + BTW / 2 + 8);
+    const bool vec = (a.W & 7) == 0;
+    if (vec) {
+        // the window's source columns of the R sub-pixel planes of each staged row, as chunks
+        const int c_lo = max(0, X0 / R - 8), c_hi = min(a.W, X0 / R + BTW / R + 8);
         const int nch = (c_hi - c_lo) >> 3;
-        for (int i = threadIdx.x; i < LH * 2 * nch; i += NT) {
-            const int ry = i / (2 * nch), rem = i - ry * 2 * nch, pp = rem / nch, ch = rem - pp * nch;
+        for (int i = threadIdx.x; i < LH * R * nch; i += NT) {
+            const int ry = i / (R * nch), rem = i - ry * R * nch, pp = rem / nch, ch = rem - pp * nch;
             const int Y = min(max(Y0 + ry - P, 0), Ho - 1);
-            const T* src = xb + ((Y & 1) * 2 + pp) * plane + (long long)(Y >> 1) * a.W + c_lo + 8 * ch;
+            const T* src = xb + ((Y % R) * R + pp) * plane + (long long)(Y / R) * a.W + c_lo + 8 * ch;
             float v[8];
             load8(src, v);
-            float* d = sS + (ry * 2 + pp) * SC + 8 * ch;
+            float* d = sS + (ry * R + pp) * SC + 8 * ch;
 #pragma unroll
             for (int e = 0; e < 8; ++e) d[e] = v[e];
         }
         __syncthreads();
+        // the replicate-clamped, shuffled window gathered from LDS
         for (int i = threadIdx.x; i < LH * LW; i += NT) {
             const int ry = i / LW, rx = i - ry * LW;
             const int X = min(max(X0 + rx - P, 0), Wo - 1);
-            sA[i] = sS[(ry * 2 + (X & 1)) * SC + (X >> 1) - c_lo];
+            sA[i] = sS[(ry * R + X % R) * SC + X / R - c_lo];
         }
     } else {
         // Stage the replicate-clamped source window, one row per wave-iteration.
@@ -1012,12 +1141,29 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
         float acc = 0.f;
 #pragma unroll
         for (int t = 0; t < K; ++t) acc = fmaf(k[t], sA[r * LW + lane + t], acc);
-        sB[r * BTW + lane] = acc;
+        sB[r * SBW + lane] = acc;
     }
     __syncthreads();
+    T* yb = reinterpret_cast<T*>(a.y) + ((long long)b * a.C + c) * Ho * Wo;
+    if (vec) {
+        const int ry = threadIdx.x >> 3, cx = 8 * (threadIdx.x & 7);
+        const int Y = Y0 + ry, X = X0 + cx;
+        if (Y < Ho && X < Wo) {
+            float o[8] = {};
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+                const float4 u0 = *reinterpret_cast<const float4*>(sB + (ry + t) * SBW + cx);
+                const float4 u1 = *reinterpret_cast<const float4*>(sB + (ry + t) * SBW + cx + 4);
+                const float u[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = fmaf(k[t], u[e], o[e]);
+            }
+            store8(yb + (long long)Y * Wo + X, o);
+        }
+        return;
+    }
     const int X = X0 + lane;
     if (X >= Wo) return;
-    T* yp = reinterpret_cast<T*>(a.y) + ((long long)b * a.C + c) * Ho * Wo + X;
 #pragma unroll
     for (int i = 0; i < BTH / 4; ++i) {
         const int ry = wave * (BTH / 4) + i;
@@ -1025,8 +1171,8 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
         if (Y < Ho) {
             float acc = 0.f;
 #pragma unroll
-            for (int t = 0; t < K; ++t) acc = fmaf(k[t], sB[(ry + t) * BTW + lane], acc);
-            st(yp + (long long)Y * Wo, acc);
+            for (int t = 0; t < K; ++t) acc = fmaf(k[t], sB[(ry + t) * SBW + lane], acc);
+            st(yb + (long long)Y * Wo + X, acc);
         }
     }
 }
@@ -1037,9 +1183,10 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
 template <class T, int R, int K>
 __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, void* dx) {
     constexpr int P = (K - 1) / 2, Q = K - 1 - P;
-    constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
-    __shared__ float sA[LH * LW];
-    __shared__ float sB[LH * BTW];
+    constexpr int LH = BTH + K - 1;
+    constexpr int SW = BTW + 16;       // staged dout columns X0 - 8 .. X0 + BTW + 8 (K <= 8: Q <= 4, P <= 3)
+    __shared__ __attribute__((aligned(16))) float sA[LH * SW];
+    __shared__ __attribute__((aligned(16))) float sB[LH * SBW];
     const int Ho = a.H * R, Wo = a.W * R;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
@@ -1049,13 +1196,33 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
     const int X0 = tx * BTW, Y0 = ty * BTH;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const T* gp = reinterpret_cast<const T*>(dout) + ((long long)b * a.C + c) * Ho * Wo;
-    // window row ry / column rx <-> dout (Y0 - Q + ry, X0 - Q + rx), zero outside the image
-    for (int ry = wave; ry < LH; ry += 4) {
-        const int y = Y0 + ry - Q;
-        const bool yok = y >= 0 && y < Ho;
-        for (int rx = lane; rx < LW; rx += 64) {
-            const int x = X0 + rx - Q;
-            sA[ry * LW + rx] = (yok && x >= 0 && x < Wo) ? ld(gp + (long long)y * Wo + x) : 0.f;
+    const bool vec = (a.W & 7) == 0;
+    // sA row ry, column 8 - Q + rx <-> dout (Y0 - Q + ry, X0 - Q + rx), zero outside the image
+    if (vec) {
+        constexpr int NCH = SW / 8;
+        for (int i = threadIdx.x; i < LH * NCH; i += NT) {
+            const int ry = i / NCH, ch = i - ry * NCH;
+            const int y = Y0 + ry - Q, x = X0 - 8 + 8 * ch;
+            float v[8];
+            if (y >= 0 && y < Ho && x >= 0 && x < Wo) {
+                load8(gp + (long long)y * Wo + x, v);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = 0.f;
+            }
+            float* d = sA + ry * SW + 8 * ch;
+            *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    } else {
+        constexpr int LW = BTW + K - 1;
+        for (int ry = wave; ry < LH; ry += 4) {
+            const int y = Y0 + ry - Q;
+            const bool yok = y >= 0 && y < Ho;
+            for (int rx = lane; rx < LW; rx += 64) {
+                const int x = X0 + rx - Q;
+                sA[ry * SW + 8 - Q + rx] = (yok && x >= 0 && x < Wo) ? ld(gp + (long long)y * Wo + x) : 0.f;
+            }
         }
     }
     __syncthreads();
@@ -1063,8 +1230,10 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
 #pragma unroll
     for (int j = 0; j < K; ++j) kr[j] = a.k[K - 1 - j];
     const int X = X0 + lane;
+    // vector form, R = 2: row-pass column of X is [X even | X odd] de-interleaved
+    const int bcol = (vec && R == 2) ? ((lane & 1) * (BTW / 2) + (lane >> 1)) : lane;
     for (int r = wave; r < LH; r += 4) {
-        const float* row = sA + r * LW;
+        const float* row = sA + r * SW + 8 - Q;
         float acc = 0.f;
 #pragma unroll
         for (int j = 0; j < K; ++j) acc = fmaf(kr[j], row[lane + j], acc);
@@ -1072,23 +1241,48 @@ __global__ __launch_bounds__(NT) void blur_bwd(BlurArgs a, const void* dout, voi
             for (int o = 0; o < P && o < Wo; ++o) acc = fmaf(a.clo[o], row[o + Q], acc);
         if (X == Wo - 1)
             for (int m = 0; m < Q && m < Wo; ++m) acc = fmaf(a.chi[m], row[lane - m + Q], acc);
-        sB[r * BTW + lane] = acc;
+        sB[r * SBW + bcol] = acc;
     }
     __syncthreads();
-    if (X >= Wo) return;
     const long long plane = (long long)a.H * a.W;
-    T* dxb = reinterpret_cast<T*>(dx) + ((long long)b * a.C + c) * (R * R) * plane + (X % R) * plane + X / R;
+    T* dxc = reinterpret_cast<T*>(dx) + ((long long)b * a.C + c) * (R * R) * plane;
+    if (vec) {
+        const int ry = threadIdx.x >> 3, ch = threadIdx.x & 7;
+        const int Y = Y0 + ry;
+        // destination: 8 consecutive source-plane columns of sub-pixel column pp
+        const int pp = R == 2 ? ch >> 2 : 0;
+        const int col = R == 2 ? X0 / 2 + 8 * (ch & 3) : X0 + 8 * ch;
+        if (Y >= Ho || col >= a.W) return;
+        float o[8] = {};
+        auto fma_row = [&](float w, int rr) {
+            const float4 u0 = *reinterpret_cast<const float4*>(sB + rr * SBW + 8 * ch);
+            const float4 u1 = *reinterpret_cast<const float4*>(sB + rr * SBW + 8 * ch + 4);
+            const float u[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = fmaf(w, u[e], o[e]);
+        };
+#pragma unroll
+        for (int j = 0; j < K; ++j) fma_row(kr[j], ry + j);
+        if (Y == 0)
+            for (int q = 0; q < P && q < Ho; ++q) fma_row(a.clo[q], q + Q);
+        if (Y == Ho - 1)
+            for (int m = 0; m < Q && m < Ho; ++m) fma_row(a.chi[m], ry - m + Q);
+        store8(dxc + ((Y % R) * R + pp) * plane + (long long)(Y / R) * a.W + col, o);
+        return;
+    }
+    if (X >= Wo) return;
+    T* dxb = dxc + (X % R) * plane + X / R;
     for (int i = 0; i < BTH / 4; ++i) {
         const int ry = wave * (BTH / 4) + i;
         const int Y = Y0 + ry;
         if (Y >= Ho) break;
         float acc = 0.f;
 #pragma unroll
-        for (int j = 0; j < K; ++j) acc = fmaf(kr[j], sB[(ry + j) * BTW + lane], acc);
+        for (int j = 0; j < K; ++j) acc = fmaf(kr[j], sB[(ry + j) * SBW + lane], acc);
         if (Y == 0)
-            for (int o = 0; o < P && o < Ho; ++o) acc = fmaf(a.clo[o], sB[(o + Q) * BTW + lane], acc);
+            for (int o = 0; o < P && o < Ho; ++o) acc = fmaf(a.clo[o], sB[(o + Q) * SBW + lane], acc);
         if (Y == Ho - 1)
-            for (int m = 0; m < Q && m < Ho; ++m) acc = fmaf(a.chi[m], sB[(ry - m + Q) * BTW + lane], acc);
+            for (int m = 0; m < Q && m < Ho; ++m) acc = fmaf(a.chi[m], sB[(ry - m + Q) * SBW + lane], acc);
         st(dxb + (Y % R) * R * plane + (long long)(Y / R) * a.W, acc);
     }
 }
