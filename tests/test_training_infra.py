@@ -130,3 +130,37 @@ def test_kernel_timer_rocprof_names():
     assert kt.rocprof_name("gemm_ws<f32x3,true,true,true>") is None
     assert kt.rocprof_name("convnext_mlp_fwd<bf16,128,true>") == "mlp_fwd<128, true>"
     assert kt.rocprof_name("dwconv2d_mfma_bwd_weight<bf16,7>") == "dwm_bwd_w<7, "
+
+
+def test_ema_copies_buffers_only_when_changed():
+    """update_ema lerps the trainable parameters and copies a G buffer into G_ema only when
+    the buffer changed since its last copy (reference training_loop.py:730-742 copies all)."""
+    import copy
+    from training.training_loop import TrainingIteration
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(4, 4)
+            self.register_buffer('const', torch.arange(4.0))
+            self.trainable_layers = ['lin']
+
+    G = Net()
+    G_ema = copy.deepcopy(G)
+    it = TrainingIteration.__new__(TrainingIteration)
+    it.G, it.G_ema, it.batch_size, it.ema_kimg, it.ema_rampup, it._ema_pairs = G, G_ema, 4, 10.0, None, None
+    with torch.no_grad():
+        G.const.add_(1.0)
+        G.lin.weight.add_(1.0)
+    it.update_ema(1000)
+    assert torch.equal(G_ema.const, G.const)
+    v = G_ema.const._version
+    it.update_ema(1000)                           # unchanged source: no copy
+    assert G_ema.const._version == v
+    with torch.no_grad():
+        G.const.mul_(2.0)
+    it.update_ema(1000)
+    assert torch.equal(G_ema.const, G.const) and G_ema.const._version != v
+    beta = 0.5 ** (4 / 10000.0)
+    assert not torch.equal(G_ema.lin.weight, G.lin.weight)
+    assert torch.isfinite(G_ema.lin.weight).all() and beta < 1

@@ -313,9 +313,21 @@ class TrainingIteration:
         if dst:
             # p_ema <- p.lerp(p_ema, beta) == p_ema + (1 - beta) * (p - p_ema)
             torch._foreach_lerp_(dst, src, 1.0 - beta)
-        bufs = [(be, b) for be, b in zip(self.G_ema.buffers(), self.G.buffers()) if be.data_ptr() != b.data_ptr()]
+        # buffers are copied only when the source changed since the last copy (version counter):
+        # the generator's buffers are constants (noise planes, filters), and copying ~60 of them
+        # every step was ~60 launches of nothing
+        seen = self.__dict__.setdefault('_ema_buf_versions', {})
+        bufs = []
+        for be, b in zip(self.G_ema.buffers(), self.G.buffers()):
+            if be.data_ptr() == b.data_ptr():
+                continue
+            key = (be.data_ptr(), b.data_ptr())
+            if seen.get(key) != (b._version, be._version):
+                bufs.append((be, b))
         if bufs:
             torch._foreach_copy_([be for be, _ in bufs], [b for _, b in bufs])
+            for be, b in bufs:
+                seen[(be.data_ptr(), b.data_ptr())] = (b._version, be._version)
 
     def __call__(self, phase_real_img, phase_real_c, cur_nimg):
         if self.trace is None:
