@@ -175,6 +175,26 @@ def test_gemm_fast_epilogue_batched(dtype):
     assert _rel(y3, ref3) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("act", [None, "gelu_tanh"])
+@pytest.mark.parametrize("bias_dim", [None, 1, 0])
+def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch):
+    """gemm8's fp32-output epilogue: full 256 x 256 tiles go through the LDS-staged 16-B store form
+    (alpha, row / column bias, GELU), the ragged last tiles through the per-element form."""
+    from torch_utils.ops import gemm_hip
+    monkeypatch.setattr(gemm_hip, "GEMM8", True)
+    monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
+    g = torch.Generator().manual_seed(11)
+    Bn, M, N, K = 2, 512, 776, 192
+    A = _make((M, K), dtype, g)
+    x = _make((Bn, K, N), dtype, g)
+    bias = None if bias_dim is None else torch.randn(N if bias_dim == 1 else M, generator=g).to(DEV)
+    y = gemm_hip.gemm(A, x, bias=bias, bias_dim=bias_dim, act=act, alpha=0.75, out_dtype=torch.float32,
+                      cache_a=True)
+    ref = _ref_epi(0.75 * (A.float() @ x.float()), bias, bias_dim if bias_dim is not None else 1, act)
+    assert _rel(y, ref) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+
+
 def test_gemm_generic_path_when_fast_off(monkeypatch):
     from torch_utils.ops import gemm_hip
     monkeypatch.setattr(gemm_hip, "FAST", False)

@@ -287,6 +287,46 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
         }
         return;
     }
+    if (OUTF32 && a.beta == 0.f && m0 + BM <= a.M && n0 + BN <= a.N && (a.ldc % 4) == 0 &&
+        (reinterpret_cast<uintptr_t>(a.C) % 16) == 0 && (a.sC % 4) == 0) {
+        // fp32 tile through LDS in two 64-row halves per wave (16 KB each, the wave's share of the
+        // operand buffers): 16-B stores of whole 256-B row segments instead of 4-B stores with
+        // per-element address arithmetic. 16-B chunk c of row ml sits at chunk c ^ (ml & 15), so
+        // both the row-group writes of the accumulator layout and the row reads are conflict-free.
+        float* wl = reinterpret_cast<float*>(lds + wave * 128 * 128);
+        float* crow0 = reinterpret_cast<float*>(a.C) + (long long)z * a.sC + (long long)(m0 + 128 * wm) * a.ldc +
+                       n0 + 64 * wn;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            if (hf) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int nl = 16 * j + cl;
+                const float bcol = (a.bias_mode == 1) ? a.bias[n0 + 64 * wn + nl] : 0.f;
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ml = 16 * ii + rq + r;
+                        float v = a.alpha * acc[4 * hf + ii][j][r];
+                        v += (a.bias_mode == 2) ? a.bias[m0 + 128 * wm + 64 * hf + ml] : bcol;
+                        if (a.act == 1) v = gelu_tanh(v);
+                        else if (a.act == 2) v = v * gelu_parts(v).cdf;
+                        wl[ml * 64 + (((nl >> 2) ^ (ml & 15)) << 2) + (nl & 3)] = v;
+                    }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            float* crow = crow0 + (long long)(64 * hf) * a.ldc;
+#pragma unroll 4
+            for (int c = lane; c < 64 * 16; c += 64) {
+                const int ml = c >> 4, ch = c & 15;
+                const float4 v = *reinterpret_cast<const float4*>(wl + ml * 64 + ((ch ^ (ml & 15)) << 2));
+                *reinterpret_cast<float4*>(crow + (long long)ml * a.ldc + 4 * ch) = v;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int n = n0 + 64 * wn + 16 * j + cl;
