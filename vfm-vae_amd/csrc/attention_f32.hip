@@ -62,16 +62,8 @@ struct Args {
 
 __device__ __forceinline__ int kv_off(int row, int ch) { return row * ROWB + 16 * (ch ^ ((row >> 1) & 7)); }
 
-__device__ __forceinline__ uint32_t bf_bits(float x) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(x));
-}
-
 // hi/lo bf16 pairs of two floats, packed
-__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t& h, uint32_t& l) {
-    const __hip_bfloat16 h0 = __float2bfloat16(x0), h1 = __float2bfloat16(x1);
-    h = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-    l = bf_bits(x0 - __bfloat162float(h0)) | (bf_bits(x1 - __bfloat162float(h1)) << 16);
-}
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t& h, uint32_t& l) { split2_bf16(x0, x1, h, l); }
 
 __device__ __forceinline__ void split8(const float* x, bf16x8& h, bf16x8& l) {
     uint4 hv, lv;
@@ -292,7 +284,7 @@ __global__ __launch_bounds__(256) void attn32_delta(Args a, int rows) {
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * WAVES, 1) void attn32_dq(Args a) {
+__global__ __launch_bounds__(64 * WAVES, 2) void attn32_dq(Args a) {   // 2 waves per SIMD (the register budget the kernel was tuned to)
     __shared__ __attribute__((aligned(16))) unsigned char lds[4 * IMG];
     unsigned char *khi = lds, *klo = lds + IMG, *vhi = lds + 2 * IMG, *vlo = lds + 3 * IMG;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -44,22 +44,13 @@ struct ConvArgs {
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
 
-__device__ __forceinline__ uint32_t bf16_bits(float v) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(v));
-}
-__device__ __forceinline__ float bf16_val(uint32_t bits) { return __uint_as_float(bits << 16); }
-
 // 4 fp32 (one uint4) -> hi/lo halves of a 16-B image chunk
 __device__ __forceinline__ void put4(unsigned char* hi, unsigned char* lo, int off, uint4 r) {
-    const float x[4] = {__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z), __uint_as_float(r.w)};
-    uint32_t hb[4], lb[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        hb[e] = bf16_bits(x[e]);
-        lb[e] = bf16_bits(x[e] - bf16_val(hb[e]));
-    }
-    *reinterpret_cast<uint2*>(hi + off) = make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
-    *reinterpret_cast<uint2*>(lo + off) = make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
+    uint32_t h01, l01, h23, l23;
+    split2_bf16(__uint_as_float(r.x), __uint_as_float(r.y), h01, l01);
+    split2_bf16(__uint_as_float(r.z), __uint_as_float(r.w), h23, l23);
+    *reinterpret_cast<uint2*>(hi + off) = make_uint2(h01, h23);
+    *reinterpret_cast<uint2*>(lo + off) = make_uint2(l01, l23);
 }
 
 // thread -> (row = tid/16 + 16u, 4-element column tid%16) of a [rows][64] fp32 tile

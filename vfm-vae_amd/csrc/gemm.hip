@@ -67,10 +67,6 @@ __device__ __forceinline__ int mc_off(int row, int ch) {
     return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
-__device__ __forceinline__ uint32_t bf16_bits(float v) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(v));
-}
-__device__ __forceinline__ float bf16_val(uint32_t bits) { return __uint_as_float(bits << 16); }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
     const float u = 0.7978845608028654f * fmaf(0.044715f * x, x * x, x);
@@ -123,16 +119,11 @@ struct Stage {
                 // 4 fp32 -> 4 bf16 hi + 4 bf16 lo (8 B each), half of a 16-B image chunk
                 const int ch = cc >> 1, half = cc & 1;
                 const int off = (KCONT ? kc_off(row, ch) : mc_off(row, ch)) + 8 * half;
-                const float x[4] = {__uint_as_float(r[u].x), __uint_as_float(r[u].y), __uint_as_float(r[u].z),
-                                    __uint_as_float(r[u].w)};
-                uint32_t hb[4], lb[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    hb[e] = bf16_bits(x[e]);
-                    lb[e] = bf16_bits(x[e] - bf16_val(hb[e]));
-                }
-                *reinterpret_cast<uint2*>(hi + off) = make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
-                *reinterpret_cast<uint2*>(lo + off) = make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
+                uint32_t h01, l01, h23, l23;
+                split2_bf16(__uint_as_float(r[u].x), __uint_as_float(r[u].y), h01, l01);
+                split2_bf16(__uint_as_float(r[u].z), __uint_as_float(r[u].w), h23, l23);
+                *reinterpret_cast<uint2*>(hi + off) = make_uint2(h01, h23);
+                *reinterpret_cast<uint2*>(lo + off) = make_uint2(l01, l23);
             }
         }
     }

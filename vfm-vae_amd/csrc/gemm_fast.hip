@@ -242,16 +242,11 @@ __global__ void split3_kernel(const float* __restrict__ src, __hip_bfloat16* __r
     if (kcont) { r = idx4 / K; c = idx4 % K; inner = K; }
     else       { r = idx4 / R; c = idx4 % R; inner = R; }   // r = k row, c = column
     const float4 v = *reinterpret_cast<const float4*>(s + r * lds_ + c);
-    const float x[4] = {v.x, v.y, v.z, v.w};
-    uint32_t hb[4], lb[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        hb[e] = (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(x[e]));
-        const float hv = __uint_as_float(hb[e] << 16);
-        lb[e] = (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(x[e] - hv));
-    }
-    const uint2 H = make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
-    const uint2 L = make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
+    uint32_t h01, l01, h23, l23;
+    split2_bf16(v.x, v.y, h01, l01);
+    split2_bf16(v.z, v.w, h23, l23);
+    const uint2 H = make_uint2(h01, h23);
+    const uint2 L = make_uint2(l01, l23);
     const uint2 parts[3] = {H, role == 0 ? H : L, role == 0 ? L : H};
 #pragma unroll
     for (int p = 0; p < 3; ++p) {

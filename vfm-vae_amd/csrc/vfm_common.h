@@ -27,6 +27,19 @@ __device__ __forceinline__ void st(double* p, double v) { *p = v; }
 __device__ __forceinline__ void st(__half* p, float v) { *p = __float2half(v); }
 __device__ __forceinline__ void st(__hip_bfloat16* p, float v) { *p = __float2bfloat16(v); }
 
+// fp32 pair -> packed bf16 hi pair and packed bf16 lo pair (lo = bf16(x - hi)), element 0 in the
+// low half: the 3-term split of the f32x3 products. One v_cvt_pk_bf16_f32 per packed pair and a
+// packed subtract, instead of a conversion per element plus shifts / ORs to pack; the roundings
+// (RNE) and the subtraction are the same IEEE operations, so the result is bit-identical.
+typedef float vfm_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 vfm_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2_bf16(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+    const vfm_f2 x = {x0, x1};
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, vfm_bf16x2));
+    const vfm_f2 h = {__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(x - h, vfm_bf16x2));
+}
+
 // floor(a / b) for b > 0 and any sign of a.
 __device__ __host__ __forceinline__ int floor_div(int a, int b) {
     int q = a / b;
