@@ -326,7 +326,7 @@ class _DwConv2d(torch.autograd.Function):
             if want_b:
                 db = s[:, K * K].to(bdt)
         if _wanted(ctx, 3):
-            dn = dy.float().sum(dim=(0, 1)).to(ndt)
+            dn = dy.sum(dim=(0, 1), dtype=torch.float32).to(ndt)       # fp32 accumulation, no fp32 copy of dy
         return dx, dw, db, dn, None, None
 
 

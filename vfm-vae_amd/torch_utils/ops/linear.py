@@ -68,7 +68,7 @@ class _LinearFn(torch.autograd.Function):
                 dw = dy2.t().float() @ x2.float()
             dw = dw.to(wdt)
         if bdt is not None and ctx.needs_input_grad[2] and _wanted(ctx, 2):
-            db = dy2.float().sum(0).to(bdt)
+            db = dy2.sum(0, dtype=torch.float32).to(bdt)
         return dx, dw, db
 
 
