@@ -246,18 +246,27 @@ __global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
                     *reinterpret_cast<uint32_t*>(a.out0 + outb - (odd ? 1 : 0) + (long long)(mA + (odd ? 1 : 0)) * N +
                                                  32 * nb) = pk;
                 }
+                // sums of the 4 values (s0, s1) x (rows mA, mA+1) over the 32 columns of this half:
+                // two halving butterfly steps (lanes keep / send opposite halves of the set) leave
+                // one value per lane, value q = 2 * bit4(r) + bit3(r), then three plain xor steps;
+                // 4 lanes per half hold the totals (12 shuffles instead of 20, one store)
+                float v0, v1;
+                {
+                    const bool up = r & 16;
+                    const float k0 = up ? s1[0] : s0[0], k1 = up ? s1[1] : s0[1];
+                    const float d0 = up ? s0[0] : s1[0], d1 = up ? s0[1] : s1[1];
+                    v0 = k0 + __shfl_xor(d0, 16);
+                    v1 = k1 + __shfl_xor(d1, 16);
+                }
+                {
+                    const bool up = r & 8;
+                    v0 = (up ? v1 : v0) + __shfl_xor(up ? v0 : v1, 8);
+                }
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
-#pragma unroll
-                    for (int off = 16; off >= 1; off >>= 1) {     // sum over the 32 columns of this half
-                        s0[t] += __shfl_xor(s0[t], off);
-                        s1[t] += __shfl_xor(s1[t], off);
-                    }
-                    if (r == 0) {
-                        const long long pi = ((long long)b * a.ntiles + 2 * tile + cw) * M + mA + t;
-                        a.part0[pi] = s0[t];
-                        a.part1[pi] = s1[t];
-                    }
+                for (int off = 4; off >= 1; off >>= 1) v0 += __shfl_xor(v0, off);
+                if ((r & 7) == 0) {
+                    const long long pi = ((long long)b * a.ntiles + 2 * tile + cw) * M + mA + ((r >> 3) & 1);
+                    ((r & 16) ? a.part1 : a.part0)[pi] = v0;
                 }
             }
         }
