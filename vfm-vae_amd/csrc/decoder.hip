@@ -599,10 +599,10 @@ __device__ __forceinline__ void store8(T* p, const float* v) {
 }
 template <>
 __device__ __forceinline__ void store8<__hip_bfloat16>(__hip_bfloat16* p, const float* v) {
-    __hip_bfloat16 t[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = __float2bfloat16(v[i]);
-    *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(t);
+    typedef float f8 __attribute__((ext_vector_type(8)));
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    const f8 x = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, __builtin_convertvector(x, b8));   // 4 v_cvt_pk_bf16_f32
 }
 template <>
 __device__ __forceinline__ void store8<__half>(__half* p, const float* v) {

@@ -45,6 +45,10 @@ struct DwmArgs {
 };
 
 __device__ __forceinline__ uint16_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, __float2bfloat16(v)); }
+// two floats -> packed bf16 pair (RNE, element 0 low), one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pk_bf16(float a0, float a1) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(vfm_f2{a0, a1}, vfm_bf16x2));
+}
 
 template <int K, int XW>
 __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
@@ -147,8 +151,7 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
                 acc[2] += __uint_as_float(rv.y << 16); acc[3] += __uint_as_float(rv.y & 0xffff0000u);
             }
             if (oy < a.H) {
-                const uint2 o = make_uint2((uint32_t)bf16_bits(acc[0]) | ((uint32_t)bf16_bits(acc[1]) << 16),
-                                           (uint32_t)bf16_bits(acc[2]) | ((uint32_t)bf16_bits(acc[3]) << 16));
+                const uint2 o = make_uint2(pk_bf16(acc[0], acc[1]), pk_bf16(acc[2], acc[3]));   // 2 v_cvt_pk_bf16_f32
                 *reinterpret_cast<uint2*>(yp + 16 * s) = o;
             }
         }
