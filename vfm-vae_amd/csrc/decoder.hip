@@ -1084,11 +1084,13 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
     constexpr int P = (K - 1) / 2;
     constexpr int LW = BTW + K - 1, LH = BTH + K - 1;
     constexpr int SC = BTW / R + 16;                 // source columns kept per plane (vector form)
-    constexpr int NB = LH * R * SC > LH * SBW ? LH * R * SC : LH * SBW;
-    __shared__ float sA[LH * LW];
-    __shared__ __attribute__((aligned(16))) float sBuf[NB];   // staged source rows, then the row pass
-    float* sS = sBuf;
-    float* sB = sBuf;
+    constexpr int NS = LH * R * SC > LH * LW ? LH * R * SC : LH * LW;
+    // staged source: the vector form's raw chunks of the R sub-pixel planes (sS) or the scalar
+    // form's clamped, shuffled window (sA); the row pass writes sB
+    __shared__ __attribute__((aligned(16))) float sStage[NS];
+    __shared__ __attribute__((aligned(16))) float sB[LH * SBW];
+    float* sS = sStage;
+    float* sA = sStage;
     const int Ho = a.H * R, Wo = a.W * R;
     const int tilesX = (Wo + BTW - 1) / BTW, tilesY = (Ho + BTH - 1) / BTH;
     int bid = blockIdx.x;
@@ -1119,11 +1121,20 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
             for (int e = 0; e < 8; ++e) d[e] = v[e];
         }
         __syncthreads();
-        // the replicate-clamped, shuffled window gathered from LDS
-        for (int i = threadIdx.x; i < LH * LW; i += NT) {
-            const int ry = i / LW, rx = i - ry * LW;
-            const int X = min(max(X0 + rx - P, 0), Wo - 1);
-            sA[i] = sS[(ry * R + X % R) * SC + X / R - c_lo];
+        // row pass straight from the raw chunks: tap t of output column X0 + lane reads source
+        // column clamp(X0 + lane + t - P) of its sub-pixel plane (offsets fixed per lane)
+        int idx[K];
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+            const int X = min(max(X0 + lane + t - P, 0), Wo - 1);
+            idx[t] = (X % R) * SC + X / R - c_lo;
+        }
+        for (int r = wave; r < LH; r += 4) {
+            const float* row = sS + r * R * SC;
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < K; ++t) acc = fmaf(k[t], row[idx[t]], acc);
+            sB[r * SBW + lane] = acc;
         }
     } else {
         // Stage the replicate-clamped source window, one row per wave-iteration.
@@ -1135,13 +1146,13 @@ __global__ __launch_bounds__(NT) void blur_fwd(BlurArgs a) {
                 sA[ry * LW + rx] = ld(src + (X % R) * plane + X / R);
             }
         }
-    }
-    __syncthreads();
-    for (int r = wave; r < LH; r += 4) {
-        float acc = 0.f;
+        __syncthreads();
+        for (int r = wave; r < LH; r += 4) {
+            float acc = 0.f;
 #pragma unroll
-        for (int t = 0; t < K; ++t) acc = fmaf(k[t], sA[r * LW + lane + t], acc);
-        sB[r * SBW + lane] = acc;
+            for (int t = 0; t < K; ++t) acc = fmaf(k[t], sA[r * LW + lane + t], acc);
+            sB[r * SBW + lane] = acc;
+        }
     }
     __syncthreads();
     T* yb = reinterpret_cast<T*>(a.y) + ((long long)b * a.C + c) * Ho * Wo;
