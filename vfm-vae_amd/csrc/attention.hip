@@ -56,10 +56,9 @@ struct AttnArgs {
 // byte offset of 16-B chunk `ch` (0..7) of key row `key` in a [64][64 x bf16] tile image
 __device__ __forceinline__ int kv_off(int key, int ch) { return key * ROWB + 16 * (ch ^ ((key >> 1) & 7)); }
 
+// (lo, hi) -> packed bf16 pair, RNE: one v_cvt_pk_bf16_f32
 __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-    const uint32_t a = (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(lo));
-    const uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(hi));
-    return a | (b << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(vfm_f2{lo, hi}, vfm_bf16x2));
 }
 
 __device__ __forceinline__ float xchg32(float v) {
