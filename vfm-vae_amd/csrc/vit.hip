@@ -104,12 +104,14 @@ __global__ __launch_bounds__(256) void ln_rows(LnArgs a) {
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
         const int c0 = (j * 64 + lane) * 4;
+        // affine parameters as 16-B loads (c0 is a multiple of 4; host: D % 256 == 0)
+        const float4 wv = a.w ? *reinterpret_cast<const float4*>(a.w + c0) : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 bv = a.b ? *reinterpret_cast<const float4*>(a.b + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
         float o[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float wv = a.w ? a.w[c0 + i] : 1.f, bv = a.b ? a.b[c0 + i] : 0.f;
-            o[i] = fmaf((v[j][i] - mean) * rstd, wv, bv);
-        }
+        o[0] = fmaf((v[j][0] - mean) * rstd, wv.x, bv.x);
+        o[1] = fmaf((v[j][1] - mean) * rstd, wv.y, bv.y);
+        o[2] = fmaf((v[j][2] - mean) * rstd, wv.z, bv.z);
+        o[3] = fmaf((v[j][3] - mean) * rstd, wv.w, bv.w);
         st4v(yp + c0, o);
     }
 }
@@ -136,6 +138,7 @@ extern "C" int vfm_residual_layer_norm(const float* h, const void* delta, float*
                                        const float* b, void* y, int dtype_delta, int dtype_out, int rows, int D,
                                        float eps, void* stream) {
     if (!h || !y || rows < 0 || D <= 0) return VFM_ERR_ARGS;
+    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) % 16) return VFM_ERR_ARGS;   // 16-B vector loads
     if (D % 256 || D > 2048) return VFM_NO_KERNEL;
     if (rows == 0) return VFM_OK;
     LnArgs a{h, delta, h_out, w, b, y, rows, D, eps};

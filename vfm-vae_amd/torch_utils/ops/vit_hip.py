@@ -34,6 +34,9 @@ def residual_layer_norm(h, delta, ln, out_dtype, write_h=True):
             h_out = torch.empty_like(h)
     w = ln.weight.detach().float().contiguous() if ln.weight is not None else None
     b = ln.bias.detach().float().contiguous() if ln.bias is not None else None
+    # the kernel reads the affine parameters as 16-B vectors
+    w = w.clone() if w is not None and w.data_ptr() % 16 else w
+    b = b.clone() if b is not None and b.data_ptr() % 16 else b
     es = 0 if delta is None else delta.element_size()
     nbytes = rows * D * (4 + es + y.element_size() + (4 if h_out is not None else 0))
     with kernel_timer.region('residual_layer_norm', nbytes):
