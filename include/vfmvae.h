@@ -34,6 +34,11 @@ enum {
     VFM_F16 = 1,
     VFM_BF16 = 2,
     VFM_F64 = 3,
+    /* Precision code of the fp32 MFMA paths only (GEMM / conv / fp32 attention): fp32 operands as
+     * the opt-in 3-term bf16 split (hi.hi + hi.lo + lo.hi, ~2^-15.5 relative per product). VFM_F32
+     * on those paths is the fp32-equivalent 6-term split (three exact bf16 pieces per operand, the
+     * six products of order >= 2^-16; dropped terms <= ~2^-23 relative, fp32 accumulation). */
+    VFM_F32X3 = 4,
 };
 
 enum {
@@ -208,44 +213,47 @@ int vfm_attention_fwd(const void* q, const void* k, const void* v, void* o, int 
                       const long long* sq, const long long* sk, const long long* sv, const long long* so,
                       float scale, void* stream);
 
-/* 3x3 / stride 1 / pad 1 convolution, NHWC fp32, implicit GEMM on bf16 MFMA through the 3-term
- * split (replaces the MIOpen fp32 convolutions of the LPIPS VGG16 stack, reference
- * training/lpips.py:126-163, forward and data gradient). x [B, H, W, Cin] (Cin a power of two
- * >= 4), w [Cout][9][Cin] (tap-major, Cout % 64 == 0) given as bf16 hi = bf16(w) and
- * lo = bf16(w - hi) arrays [Cout][ldw] (rows zero-padded to ldw, a multiple of 64 >= 9*Cin),
- * out [B, H, W, Cout] = relu?(conv + bias),
- * zeroed where mask [B, H, W, Cout] <= 0 when mask is given (bias / mask may be null). */
-int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void* w_lo, int ldw, const float* bias,
+/* 3x3 / stride 1 / pad 1 convolution, NHWC fp32, implicit GEMM on bf16 MFMA with fp32-equivalent
+ * products (precision VFM_F32: the 6-term split; VFM_F32X3: the opt-in 3-term one). Replaces the
+ * MIOpen fp32 convolutions of the LPIPS VGG16 stack, reference training/lpips.py:126-163, forward
+ * and data gradient. x [B, H, W, Cin] (Cin a power of two >= 4), w [Cout][9][Cin] (tap-major,
+ * Cout % 64 == 0) given as its bf16 pieces w_pieces [np][Cout][ldw] (np = 3: hi = bf16(w),
+ * mid = bf16(w - hi), lo = bf16(w - hi - mid); np = 2: hi, lo; rows zero-padded to ldw, a multiple
+ * of 64 >= 9*Cin), out [B, H, W, Cout] = relu?(conv + bias), zeroed where mask [B, H, W, Cout] <= 0
+ * when mask is given (bias / mask may be null). */
+int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int precision, int ldw, const float* bias,
                          const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int relu, void* stream);
 
 /* fp32 attention with gradients (replaces F.scaled_dot_product_attention on the fp32 paths of the
- * generator: fusion-adapter AttnProjection, reference networks/utils/ldm_utils.py:55-87, and the
- * decoder SelfAttention with null key/value, reference networks/utils/gigagan_utils.py:53-91).
- * q [B, Nq, H, 64], k/v [B, Nk, H, 64] fp32 views, element strides {batch, token, head}, unit
- * stride on the head dim, strides multiples of 4, pointers 16-B aligned. Products run on bf16
- * MFMA through a 3-term hi/lo split (relative error per product <= ~2^-16, fp32 accumulation).
+ * generator: fusion-adapter AttnProjection, reference networks/utils/ldm_utils.py:55-93 (encode,
+ * 64-dim heads; decode post_quant, 32-dim heads), the decoder SelfAttention with null key/value,
+ * reference networks/utils/gigagan_utils.py:53-91, and the DINO discriminator tower).
+ * q [B, Nq, H, d], k/v [B, Nk, H, d] fp32 views, d in {32, 64}, element strides {batch, token,
+ * head}, unit stride on the head dim, strides multiples of 4, pointers 16-B aligned. Products run on
+ * bf16 MFMA with fp32-equivalent products (precision VFM_F32: 6-term split; VFM_F32X3: opt-in 3-term),
+ * fp32 accumulation and softmax.
  *   fwd: o (strides so) and lse [B, H, Nq] (log2 domain of the scaled scores);
  *   bwd: dq/dk/dv (own strides) from dout; delta [B, H, Nq] fp32 scratch. */
 int vfm_attention_f32_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int H, int Nq,
                           int Nk, int head_dim, const long long* sq, const long long* sk, const long long* sv,
-                          const long long* so, float scale, void* stream);
+                          const long long* so, float scale, int precision, void* stream);
 int vfm_attention_f32_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                           const void* lse, void* delta, void* dq, void* dk, void* dv, int B, int H, int Nq, int Nk,
                           int head_dim, const long long* sq, const long long* sk, const long long* sv,
                           const long long* so, const long long* sdo, const long long* sdq, const long long* sdk,
-                          const long long* sdv, float scale, void* stream);
+                          const long long* sdv, float scale, int precision, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Dense GEMM on the MFMA cores with a fused epilogue (replaces the hipBLASLt GEMMs behind
  * torch.addmm / torch.bmm for the frozen ViT projections, reference
  * networks/utils/vfms/siglip2_utils.py:121 (HF SiglipEncoderLayer q/k/v/o, fc1 + gelu_tanh,
- * fc2), the fusion adapter (ldm_utils.py:55-166) and the decoder's 1x1 convolutions
- * (convnext_utils.py:36-142, gigagan_utils.py:53-185)):
+ * fc2), the fusion adapter (ldm_utils.py:55-166), the decoder's 1x1 convolutions
+ * (convnext_utils.py:36-142, gigagan_utils.py:53-185) and the discriminators' linears / convs):
  *   C[z] = epi(alpha * A[z] . B[z] + beta * C[z]), A: M x K, B: K x N, z < batch,
  *   epi = (+ bias[n] if bias_mode 1 | + bias[m] if bias_mode 2), then GELU (act 1 tanh,
  *   act 2 erf); fp32 accumulation.
- *   in_dtype VFM_BF16: bf16 operands; VFM_F32: fp32 operands evaluated as three bf16 MFMA
- *   products of a hi/lo split (relative error per product <= ~2^-15.5; see csrc/gemm.hip).
+ *   in_dtype VFM_BF16: bf16 operands; VFM_F32: fp32 operands, fp32-equivalent products (the 6-term
+ *   bf16 split, see VFM_F32X3 above); VFM_F32X3: fp32 operands on the opt-in 3-term split.
  *   out_dtype VFM_BF16 / VFM_F32. Operand layouts: a_kcont = 1: A is [M][K] (row stride lda),
  *   0: A is [K][M]; b_kcont = 1: B is [N][K], 0: B is [K][N]; C is [M][N] (row stride ldc);
  *   sA/sB/sC = element batch strides (0 = shared operand). The contiguous extents, lda/ldb
@@ -254,32 +262,33 @@ int vfm_attention_f32_bwd(const void* q, const void* k, const void* v, const voi
  *   vfm_gemm_workspace_floats(...) elements) and are summed in a fixed order by a second
  *   kernel that applies the epilogue. reduce_batch = 1: C (single matrix) = epi(sum over z)
  *   -- the weight gradient of a batched 1x1 convolution. */
-/* Large-tile bf16 form of vfm_gemm (csrc/gemm_fast.hip: 256 x 256 tiles, LDS-DMA double
- * buffer): same arguments without precision / split-K; K % 64 == 0 (else VFM_NO_KERNEL). */
-int vfm_gemm_fast(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
-                  int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-                  long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
-/* Same contract as vfm_gemm_fast on a 4-phase-per-K-tile LDS-DMA pipeline (csrc/gemm8.hip), plus
- * split-K: the K-tiles of each output (of every batch concatenated when reduce_batch: C = sum_z
- * A[z] B[z]) are cut into chunks of kchunk tiles (<= 0: no split); the splits write fp32 partials
- * to workspace (vfm_gemm8_workspace_floats floats) and a reduce pass applies the epilogue in a
- * fixed order. */
-int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
-              int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
-              int kchunk, int reduce_batch, void* stream);
-int vfm_gemm8_workspace_floats(int M, int N, int K, int batch, int kchunk, int reduce_batch);  /* -1: too large */
-/* fp32 -> bf16 3-term split of one GEMM operand along its reduction dimension K, so that the
- * fp32 product runs as ONE bf16 GEMM of depth 3K: role 0 (A) writes [hi | hi | lo], role 1 (B)
- * [hi ; lo ; hi]; kcont = 1: src [R][K] (row stride ld) -> dst [R][3K], kcont = 0: src [K][R]
- * -> dst [3K][R]; batch strides sb (src) / db (dst) in elements. */
-int vfm_split3(const float* src, void* dst, int R, int K, long long ld, long long sb, long long db, int batch,
-               int role, int kcont, void* stream);
 int vfm_gemm_workspace_floats(int M, int N, int batch, int splits, int reduce_batch);
 int vfm_gemm(const void* A, const void* B, void* C, const float* bias, float* workspace, int in_dtype,
              int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,
              int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
              int bias_mode, int act, int splits, int reduce_batch, void* stream);
+
+/* Large-tile form (csrc/gemm8.hip: 256 x 256 tiles, 4-phase LDS-DMA pipeline) of the same contract,
+ * K % 64 == 0 (else VFM_NO_KERNEL). precision VFM_BF16: A / B are bf16 matrices as above. precision
+ * VFM_F32 / VFM_F32X3: A / B hold the bf16 pieces of fp32 operands from vfm_split_f32 (3 pieces:
+ * hi | mid | lo, or 2: hi | lo), stacked along K: K-contiguous [R][np K] (lda >= np K), MN-contiguous
+ * [np K][R]; K is the fp32 depth, and the kernel accumulates the 6 (3) piece products of each
+ * K-tile in fp32. Split-K: the virtual K-tiles of each output (terms x K/64, of every batch when
+ * reduce_batch: C = sum_z A[z] B[z]) are cut into chunks of kchunk tiles (<= 0: no split); the
+ * splits write fp32 partials to workspace (vfm_gemm8_workspace_floats floats) and a reduce pass
+ * applies the epilogue in a fixed order. */
+int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype, int M, int N,
+              int K, int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
+              int kchunk, int reduce_batch, void* stream);
+int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
+                               int reduce_batch);  /* -1: too large */
+/* fp32 -> bf16 pieces of one GEMM operand along its reduction dimension K (precision VFM_F32: 3
+ * pieces hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid), x = hi + mid + lo exactly;
+ * VFM_F32X3: 2 pieces hi, lo). kcont = 1: src [R][K] (row stride ld) -> dst [R][np K];
+ * kcont = 0: src [K][R] -> dst [np K][R]; batch strides sb (src) / db (dst) in elements. */
+int vfm_split_f32(const float* src, void* dst, int R, int K, long long ld, long long sb, long long db, int batch,
+                  int precision, int kcont, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Discrete latent: codebook lookup of VectorQuantizer (replaces the

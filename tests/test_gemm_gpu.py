@@ -3,9 +3,12 @@
 Tolerances (max |err| / max |ref|):
   bf16 operands, fp32 accumulation: 1e-5 for fp32 output (same products, other summation
   order), 8e-3 for bf16 output (one output rounding);
-  f32x3 (fp32 operands as three bf16 products of a hi/lo split): 5e-5 -- the split's error
-  bound is ~2^-15.5 per product, far below the 2^-10 of TF32 (which the reference disables)
-  and above fp32's 2^-24.
+  fp32 operands (the default f32x6 mode: three exact bf16 pieces per operand, six piece
+  products, dropped terms <= ~2^-23 per product, fp32 accumulation): 2e-6 against the fp32
+  hipBLASLt product -- the size of fp32 accumulation differences at these depths, the
+  reference's precision (TF32 off, training_loop.py:504-505); test_gemm_f32x6_matches_fp32
+  additionally bounds the error against fp64 by twice hipBLASLt's own fp32 error;
+  the opt-in f32x3 mode (hi / lo, three products, ~2^-15.5 per product): F32_TOL.
 Layouts: every (A, B) contiguity combination, batched with shared and per-batch operands,
 ragged M/N/K (tails inside a tile), bias per row / per column, tanh/erf GELU, alpha/beta
 accumulation, split-K and the batch-reducing form used for 1x1-conv weight gradients."""
@@ -16,6 +19,10 @@ import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+
+
+F32_TOL = 2e-6
+F32X3_TOL = 5e-5
 
 
 def _rel(a, b):
@@ -49,7 +56,7 @@ def test_gemm_layouts(dtype, a_t, b_t, M, N, K):
     Bv = B.t() if b_t else B
     out = gemm_hip.gemm(Av, Bv, out_dtype=torch.float32)
     ref = Av.float() @ Bv.float()
-    tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
+    tol = 1e-5 if dtype == torch.bfloat16 else F32_TOL
     assert _rel(out, ref) < tol
 
 
@@ -77,7 +84,7 @@ def test_gemm_alpha_beta_accumulate():
     C = _make((96, 72), torch.float32, g)
     ref = 0.5 * (A @ B) + 2.0 * C
     gemm_hip.gemm(A, B, out=C, alpha=0.5, beta=2.0)
-    assert _rel(C, ref) < 5e-5
+    assert _rel(C, ref) < F32_TOL
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -90,7 +97,7 @@ def test_gemm_batched_1x1_conv_forms(dtype):
     W = _make((O, I), dtype, g)
     x = _make((Bn, I, P), dtype, g)
     dy = _make((Bn, O, P), dtype, g)
-    tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
+    tol = 1e-5 if dtype == torch.bfloat16 else F32_TOL
     y = gemm_hip.gemm(W, x, out_dtype=torch.float32)
     assert y.shape == (Bn, O, P) and _rel(y, W.float() @ x.float()) < tol
     dx = gemm_hip.gemm(W.t(), dy, out_dtype=torch.float32)
@@ -109,19 +116,46 @@ def test_gemm_split_k_deterministic():
     o1 = gemm_hip.gemm(A, B, splits=8)
     o2 = gemm_hip.gemm(A, B, splits=8)
     assert torch.equal(o1, o2)
-    assert _rel(o1, A @ B) < 5e-5
+    assert _rel(o1, A @ B) < F32_TOL
 
 
-def test_gemm_f32x3_accuracy_bound():
-    """The hi/lo split's error stays within its analytic bound relative to sum |a||b|."""
+@pytest.mark.parametrize("K", [64, 1024, 4096])
+def test_gemm_f32x6_matches_fp32(K, monkeypatch):
+    """fp32-equivalence of the default split on both kernels: error vs the fp64 product within its
+    analytic bound (dropped terms 2^-22 + fp32 accumulation K 2^-24, relative to |A||B|) and, in
+    norm, within twice the error of hipBLASLt's exact-fp32 GEMM on the same operands."""
     from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(7 + K)
+    A = torch.randn(512, K, generator=g, dtype=torch.float64).float()
+    B = torch.randn(K, 512, generator=g, dtype=torch.float64).float()
+    exact = A.double() @ B.double()
+    blas = (A.to(DEV) @ B.to(DEV)).double().cpu()
+    eb = float((blas - exact).norm())
+    for fast in (True, False):
+        monkeypatch.setattr(gemm_hip, "FAST", fast)
+        monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
+        out = gemm_hip.gemm(A.to(DEV), B.to(DEV)).double().cpu()
+        bound = (A.double().abs() @ B.double().abs()) * (2.0 ** -22 + K * 2.0 ** -24)
+        assert bool(((out - exact).abs() <= bound).all())
+        assert float((out - exact).norm()) <= 2.0 * eb + 1e-30, (fast, float((out - exact).norm()), eb)
+
+
+def test_gemm_f32x3_opt_in(monkeypatch):
+    """The opt-in 3-term split (VFM_F32_PRODUCTS=f32x3): within its ~2^-15.5-per-product bound."""
+    from torch_utils import custom_ops
+    from torch_utils.ops import gemm_hip
+    monkeypatch.setattr(custom_ops, "F32_PRODUCTS", "f32x3")
     g = torch.Generator().manual_seed(7)
     A = torch.randn(256, 1024, generator=g, dtype=torch.float64)
     B = torch.randn(1024, 256, generator=g, dtype=torch.float64)
-    out = gemm_hip.gemm(A.float().to(DEV), B.float().to(DEV)).double().cpu()
-    exact = A.float().double() @ B.float().double()
-    bound = (A.abs() @ B.abs()) * 2.0 ** -15.5 + 1024 * 2.0 ** -24 * (A.abs() @ B.abs())
-    assert bool(((out - exact).abs() <= bound).all())
+    for fast in (True, False):
+        monkeypatch.setattr(gemm_hip, "FAST", fast)
+        monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
+        out = gemm_hip.gemm(A.float().to(DEV), B.float().to(DEV)).double().cpu()
+        exact = A.float().double() @ B.float().double()
+        bound = (A.abs() @ B.abs()) * 2.0 ** -15.5 + 1024 * 2.0 ** -24 * (A.abs() @ B.abs())
+        assert bool(((out - exact).abs() <= bound).all())
+        assert _rel(out, exact) < F32X3_TOL
 
 
 def test_gemm_unsupported_shape_returns_none():
@@ -131,15 +165,14 @@ def test_gemm_unsupported_shape_returns_none():
     assert gemm_hip.try_gemm(A, B) is None
 
 
-@pytest.mark.parametrize("kernel", ["gemm8", "gemm_fast"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128), (256, 256, 64), (1000, 264, 704)])
-def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, kernel, monkeypatch):
-    """The 256-tile LDS-DMA kernels (csrc/gemm8.hip: 4-phase pipeline, the default; csrc/gemm_fast.hip)
-    and, for fp32, the [hi|hi|lo] split; K = 64 is the single-K-tile path of gemm8's schedule."""
+def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, monkeypatch):
+    """The 256-tile LDS-DMA kernel (csrc/gemm8.hip, 4-phase pipeline) and, for fp32, the piece split
+    walked as 6 product terms; K = 64 is the single-K-tile-per-term path of gemm8's schedule."""
     from torch_utils.ops import gemm_hip, kernel_timer
-    monkeypatch.setattr(gemm_hip, "GEMM8", kernel == "gemm8")
+    kernel = "gemm8"
     monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
     g = torch.Generator().manual_seed(M * 3 + N + K)
     A = _make((K, M) if a_t else (M, K), dtype, g)
@@ -151,7 +184,7 @@ def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, kernel, monkeypatch):
     torch.cuda.synchronize()
     assert any(k.startswith(kernel + "<") for k in kernel_timer.summary())
     kernel_timer.enable(False)
-    tol = 1e-5 if dtype == torch.bfloat16 else 5e-5
+    tol = 1e-5 if dtype == torch.bfloat16 else F32_TOL
     assert _rel(out, Av.float() @ Bv.float()) < tol
 
 
@@ -165,14 +198,14 @@ def test_gemm_fast_epilogue_batched(dtype):
     bias = torch.randn(O, generator=g).to(DEV)
     y = gemm_hip.gemm(W, x, bias=bias, bias_dim=0, act="gelu", out_dtype=torch.float32, cache_a=True)
     ref = torch.nn.functional.gelu(W.float() @ x.float() + bias[:, None])
-    assert _rel(y, ref) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+    assert _rel(y, ref) < (1e-5 if dtype == torch.bfloat16 else F32_TOL)
     y2 = gemm_hip.gemm(W, x, bias=bias, bias_dim=0, act="gelu", out_dtype=torch.float32, cache_a=True)
     assert torch.equal(y, y2)                                   # cached weight split reused
     with torch.no_grad():
         W.mul_(2.0)                                             # version bump invalidates the cache
     y3 = gemm_hip.gemm(W, x, bias=bias, bias_dim=0, act="gelu", out_dtype=torch.float32, cache_a=True)
     ref3 = torch.nn.functional.gelu(W.float() @ x.float() + bias[:, None])
-    assert _rel(y3, ref3) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+    assert _rel(y3, ref3) < (1e-5 if dtype == torch.bfloat16 else F32_TOL)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -182,7 +215,6 @@ def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch):
     """gemm8's fp32-output epilogue: full 256 x 256 tiles go through the LDS-staged 16-B store form
     (alpha, row / column bias, GELU), the ragged last tiles through the per-element form."""
     from torch_utils.ops import gemm_hip
-    monkeypatch.setattr(gemm_hip, "GEMM8", True)
     monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
     g = torch.Generator().manual_seed(11)
     Bn, M, N, K = 2, 512, 776, 192
@@ -192,7 +224,7 @@ def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch):
     y = gemm_hip.gemm(A, x, bias=bias, bias_dim=bias_dim, act=act, alpha=0.75, out_dtype=torch.float32,
                       cache_a=True)
     ref = _ref_epi(0.75 * (A.float() @ x.float()), bias, bias_dim if bias_dim is not None else 1, act)
-    assert _rel(y, ref) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+    assert _rel(y, ref) < (1e-5 if dtype == torch.bfloat16 else F32_TOL)
 
 
 def test_gemm_generic_path_when_fast_off(monkeypatch):
@@ -201,7 +233,7 @@ def test_gemm_generic_path_when_fast_off(monkeypatch):
     g = torch.Generator().manual_seed(10)
     A = _make((512, 256), torch.float32, g)
     B = _make((256, 768), torch.float32, g)
-    assert _rel(gemm_hip.gemm(A, B), A @ B) < 5e-5
+    assert _rel(gemm_hip.gemm(A, B), A @ B) < F32_TOL
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -223,7 +255,7 @@ def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, mon
     assert any(k.startswith("gemm8<") for k in kernel_timer.summary())
     kernel_timer.enable(False)
     ref = (dy.double() @ x.double().transpose(1, 2)).sum(0)
-    assert _rel(dW, ref) < (1e-5 if dtype == torch.bfloat16 else 5e-5)
+    assert _rel(dW, ref) < (1e-5 if dtype == torch.bfloat16 else F32_TOL)
     assert torch.equal(dW, gemm_hip.gemm(A, Bm, out_dtype=torch.float32, reduce_batch=True))   # deterministic
 
 
@@ -239,4 +271,4 @@ def test_gemm8_split_k(M, N, K, monkeypatch):
     bias = torch.randn(N, generator=g).to(DEV)
     out = gemm_hip.gemm(A, B, bias=bias, splits=4)
     ref = A.double() @ B.double() + bias.double()
-    assert _rel(out, ref) < 5e-5
+    assert _rel(out, ref) < F32_TOL

@@ -1,4 +1,6 @@
-// fp32 multi-head attention, forward + backward, on bf16 MFMA through a 3-term hi/lo split.
+// fp32 multi-head attention, forward + backward, on bf16 MFMA with fp32-equivalent products (the
+// f32x6 split of vfm_common.h: three exact bf16 pieces per operand, six piece products; the 3-term
+// f32x3 split is an opt-in precision code).
 //
 // Replaces `F.scaled_dot_product_attention(q, k, v)` on the fp32, gradient-carrying paths of
 // the generator:
@@ -7,16 +9,17 @@
 //   * the decoder's SelfAttention with its learned null key/value (reference
 //     networks/utils/gigagan_utils.py:53-91): 8 heads x 64, 1024 queries / 1025 keys, in the
 //     fp32 blocks (indices 0-2 < num_fp16_res boundary).
-// Both run forward and backward every G phase. AOTriton's fp32 kernels reach ~60-70 TF/s on
-// these shapes; here every fp32 product a*b is evaluated as hi(a)hi(b) + hi(a)lo(b) +
-// lo(a)hi(b) on v_mfma_f32_32x32x16_bf16 (hi = bf16(x), lo = bf16(x - hi); the dropped lo*lo
-// term and the rounding of lo bound the relative error of each product by ~2^-16, fp32
-// accumulation; gemm.hip's header has the derivation).
+//   * the decode-side AttnProjection (post_quant, ldm_utils.py:480-488): 16 heads x 32;
+//   * the DINO ViT-S discriminator tower (6 heads x 64, 197 tokens).
+// Both generator paths run forward and backward every G phase. Every fp32 product a*b is evaluated
+// as the Terms<NP> piece products on v_mfma_f32_32x32x16_bf16 (NP = 3: hi, mid, lo with
+// x = hi + mid + lo exactly; the dropped products total <= ~2^-23 |a b|), fp32 accumulation.
 //
-// Layout: q/k/v/o and their gradients are [B, N, H, 64] views with element strides
-// (batch, token, head) and unit stride along the head dim (so the adapter's packed qkv GEMM
-// output and the decoder's [B, h, P, d] tensors are read in place). lse / delta are [B, H, Nq]
-// fp32, lse in the base-2 domain of the scaled scores (m + log2 l).
+// Layout: q/k/v/o and their gradients are [B, N, H, d] views (d = 64, or 32: staged into the same
+// 64-wide images with zeros in d >= 32, so the products are unchanged and only d < 32 is stored)
+// with element strides (batch, token, head) and unit stride along the head dim (so the adapter's
+// packed qkv GEMM output and the decoder's [B, h, P, d] tensors are read in place). lse / delta are
+// [B, H, Nq] fp32, lse in the base-2 domain of the scaled scores (m + log2 l).
 //
 // Kernels (flash-attention-2 structure, workgroup = 4 waves x 32 rows):
 //   attn32_fwd   : queries on lanes (S^T = K Q^T, swapped), online softmax, O^T = V^T P^T with
@@ -26,9 +29,9 @@
 //                  dQ^T += K^T dS^T;
 //   attn32_dkdv  : keys on lanes; per 64-query tile recomputes S = Q K^T, P, dP = dO V^T,
 //                  dS, then dV^T += dO^T P and dK^T += Q^T dS (no atomics: dQ has its own pass).
-// K/V (or Q/dO) tiles are staged fp32 -> split -> LDS as two bf16 images (128-B rows, 16-B
-// chunks XOR-swizzled by (row>>1)&7, as attention.hip), next tile prefetched into registers
-// during the current tile's math.
+// K/V (or Q/dO) tiles are staged fp32 -> split -> LDS as NP bf16 images (128-B rows, 16-B chunks
+// XOR-swizzled by (row>>1)&7, as attention.hip), next tile prefetched into registers during the
+// current tile's math.
 #include "vfm_common.h"
 
 namespace {
@@ -56,47 +59,58 @@ struct Args {
     float *out, *lse, *delta, *dq, *dk, *dv;
     Strides sq, sk, sv, so, sdo, sdq, sdk, sdv;
     int Nq, Nk, H;
+    int hd;       // head dim of the tensors: 64, or 32 (zero-extended to 64 on chip)
     float c;      // scale * log2(e)
     float scale;
 };
 
 __device__ __forceinline__ int kv_off(int row, int ch) { return row * ROWB + 16 * (ch ^ ((row >> 1) & 7)); }
 
-// hi/lo bf16 pairs of two floats, packed
-__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t& h, uint32_t& l) { split2_bf16(x0, x1, h, l); }
+// one operand fragment as its NP bf16 pieces
+template <int NP>
+struct Frag {
+    bf16x8 p[NP];
+};
 
-__device__ __forceinline__ void split8(const float* x, bf16x8& h, bf16x8& l) {
-    uint4 hv, lv;
-    split_pair(x[0], x[1], hv.x, lv.x);
-    split_pair(x[2], x[3], hv.y, lv.y);
-    split_pair(x[4], x[5], hv.z, lv.z);
-    split_pair(x[6], x[7], hv.w, lv.w);
-    h = __builtin_bit_cast(bf16x8, hv);
-    l = __builtin_bit_cast(bf16x8, lv);
+// 8 floats -> NP bf16x8 pieces
+template <int NP>
+__device__ __forceinline__ Frag<NP> split8(const float* x) {
+    uint32_t q[4][NP];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pieces<NP>(x[2 * j], x[2 * j + 1], q[j]);
+    Frag<NP> f;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) f.p[p] = __builtin_bit_cast(bf16x8, make_uint4(q[0][p], q[1][p], q[2][p], q[3][p]));
+    return f;
 }
 
 // B-operand fragments (k step s of a 32-row accumulator block): elements 8s .. 8s+7
-template <int S>
-__device__ __forceinline__ void split_acc(const f32x16& a, bf16x8& h, bf16x8& l) {
+template <int NP, int S>
+__device__ __forceinline__ Frag<NP> split_acc(const f32x16& a) {
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = a[8 * S + j];
-    split8(x, h, l);
+    return split8<NP>(x);
 }
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-// c += a * b with a = ah + al, b = bh + bl (lo * lo dropped)
-__device__ __forceinline__ f32x16 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 c) {
-    c = mfma(al, bh, c);
-    c = mfma(ah, bl, c);
-    return mfma(ah, bh, c);
+// c += a * b over the piece products (Terms<NP>, smallest first)
+template <int NP>
+__device__ __forceinline__ f32x16 mfmaN(const Frag<NP>& a, const Frag<NP>& b, f32x16 c) {
+#pragma unroll
+    for (int t = 0; t < Terms<NP>::N; ++t) c = mfma(a.p[Terms<NP>::a(t)], b.p[Terms<NP>::b(t)], c);
+    return c;
 }
 
-// A operand, rows of the tile image: row `row`, k = d = 16s + 8hh .. +7
-__device__ __forceinline__ bf16x8 rd_row(const unsigned char* img, int row, int s, int hh) {
-    return *reinterpret_cast<const bf16x8*>(img + kv_off(row, 2 * s + hh));
+// A operand, rows of the tile images (piece p at img + p IMG): row `row`, k = d = 16s + 8hh .. +7
+template <int NP>
+__device__ __forceinline__ Frag<NP> rd_row(const unsigned char* img, int row, int s, int hh) {
+    Frag<NP> f;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) f.p[p] = *reinterpret_cast<const bf16x8*>(img + p * IMG + kv_off(row, 2 * s + hh));
+    return f;
 }
 
 // A operand, transposed: rows = d of block db, k = tile rows of 32-row block blk, step s, in the
@@ -104,23 +118,31 @@ __device__ __forceinline__ bf16x8 rd_row(const unsigned char* img, int row, int 
 struct TrLane {
     int g1, tq, tp, hh;
 };
-__device__ __forceinline__ bf16x8 rd_tr(const unsigned char* img, const TrLane& t, int blk, int s, int db) {
+template <int NP>
+__device__ __forceinline__ Frag<NP> rd_tr(const unsigned char* img, const TrLane& t, int blk, int s, int db) {
     const int d = 32 * db + 16 * t.g1 + 4 * t.tp;
     const int r0 = 32 * blk + 16 * s + 4 * t.hh + t.tq;
     const int o0 = kv_off(r0, d >> 3) + 8 * (t.tp & 1);
     const int o1 = kv_off(r0 + 8, d >> 3) + 8 * (t.tp & 1);
-    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
-    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+    Frag<NP> f;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + p * IMG + o0));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + p * IMG + o1));
+        f.p[p] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+    return f;
 }
 
 // register staging of one 64 x 64 fp32 tile: thread t holds row t>>2, d = 16 (t&3) .. +15
+// (zeros for d >= hd)
 struct Stage {
     float4 v[4];
 };
-__device__ __forceinline__ void stage_load(Stage& s, const float* base, long long sn, int row, int nrows, int tid) {
+__device__ __forceinline__ void stage_load(Stage& s, const float* base, long long sn, int row, int nrows, int hd,
+                                           int tid) {
     const int r = tid >> 2, d0 = 16 * (tid & 3);
-    if (row + r < nrows) {
+    if (row + r < nrows && d0 < hd) {
         const float4* p = reinterpret_cast<const float4*>(base + (long long)(row + r) * sn + d0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) s.v[u] = p[u];
@@ -129,28 +151,30 @@ __device__ __forceinline__ void stage_load(Stage& s, const float* base, long lon
         for (int u = 0; u < 4; ++u) s.v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
-__device__ __forceinline__ void stage_store(const Stage& s, unsigned char* hi, unsigned char* lo, int tid) {
+template <int NP>
+__device__ __forceinline__ void stage_store(const Stage& s, unsigned char* img, int tid) {
     const int r = tid >> 2, q = tid & 3;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const float x[8] = {s.v[2 * c].x, s.v[2 * c].y, s.v[2 * c].z, s.v[2 * c].w,
                             s.v[2 * c + 1].x, s.v[2 * c + 1].y, s.v[2 * c + 1].z, s.v[2 * c + 1].w};
-        bf16x8 h, l;
-        split8(x, h, l);
-        *reinterpret_cast<bf16x8*>(hi + kv_off(r, 2 * q + c)) = h;
-        *reinterpret_cast<bf16x8*>(lo + kv_off(r, 2 * q + c)) = l;
+        const Frag<NP> f = split8<NP>(x);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<bf16x8*>(img + p * IMG + kv_off(r, 2 * q + c)) = f.p[p];
     }
 }
 
-// fixed per-lane operand: row `row` of a [N, 64] fp32 matrix, d = 16s + 8hh .. +7, split
-__device__ __forceinline__ void load_fixed(const float* base, long long sn, int row, int nrows, int hh, bf16x8* h,
-                                           bf16x8* l) {
+// fixed per-lane operand: row `row` of a [N, hd] fp32 matrix, d = 16s + 8hh .. +7 (zero for
+// d >= hd), split into pieces
+template <int NP>
+__device__ __forceinline__ void load_fixed(const float* base, long long sn, int row, int nrows, int hd, int hh,
+                                           Frag<NP>* f) {
     const bool ok = row < nrows;
     const float* p = base + (long long)(ok ? row : 0) * sn + 8 * hh;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         float x[8];
-        if (ok) {
+        if (ok && 16 * s < hd) {
             const float4 a = *reinterpret_cast<const float4*>(p + 16 * s);
             const float4 b = *reinterpret_cast<const float4*>(p + 16 * s + 4);
             x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
@@ -159,14 +183,15 @@ __device__ __forceinline__ void load_fixed(const float* base, long long sn, int 
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = 0.f;
         }
-        split8(x, h[s], l[s]);
+        f[s] = split8<NP>(x);
     }
 }
 
-// store a transposed accumulator pair (rows d, lane = row of the output): out[row][d] = f * acc
-__device__ __forceinline__ void store_tr(float* p, const f32x16* acc, int hh, float f) {
+// store a transposed accumulator pair (rows d, lane = row of the output): out[row][d] = f * acc, d < hd
+__device__ __forceinline__ void store_tr(float* p, const f32x16* acc, int hh, float f, int hd) {
 #pragma unroll
     for (int db = 0; db < 2; ++db)
+        if (32 * db < hd)
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi)
             *reinterpret_cast<float4*>(p + 32 * db + 8 * gi + 4 * hh) =
@@ -176,44 +201,43 @@ __device__ __forceinline__ void store_tr(float* p, const f32x16* acc, int hh, fl
 __device__ __forceinline__ float xchg32(float v) { return __int_as_float(__shfl_xor(__float_as_int(v), 32)); }
 
 // ---------------------------------------------------------------------------------------------
+template <int NP>
 __global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[4 * IMG];
-    unsigned char *khi = lds, *klo = lds + IMG, *vhi = lds + 2 * IMG, *vlo = lds + 3 * IMG;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG];
+    unsigned char *kimg = lds, *vimg = lds + NP * IMG;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
     const int h = blockIdx.y, b = blockIdx.z;
-    const int Nq = a.Nq, Nk = a.Nk;
+    const int Nq = a.Nq, Nk = a.Nk, hd = a.hd;
     const int q_row = blockIdx.x * RB + 32 * wave + r;
     const TrLane tl{(lane >> 4) & 1, (lane >> 2) & 3, lane & 3, hh};
 
     const float* kb = a.k + (long long)b * a.sk.b + (long long)h * a.sk.h;
     const float* vb = a.v + (long long)b * a.sv.b + (long long)h * a.sv.h;
-    bf16x8 qh[4], ql[4];
-    load_fixed(a.q + (long long)b * a.sq.b + (long long)h * a.sq.h, a.sq.n, q_row, Nq, hh, qh, ql);
+    Frag<NP> qf[4];
+    load_fixed<NP>(a.q + (long long)b * a.sq.b + (long long)h * a.sq.h, a.sq.n, q_row, Nq, hd, hh, qf);
 
     Stage sk, sv;
     f32x16 oacc[2] = {f32x16{}, f32x16{}};
     float m_run = -INFINITY, l_run = 0.f;
     const float c = a.c;
     const int T = (Nk + TT - 1) / TT;
-    stage_load(sk, kb, a.sk.n, 0, Nk, tid);
-    stage_load(sv, vb, a.sv.n, 0, Nk, tid);
+    stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
+    stage_load(sv, vb, a.sv.n, 0, Nk, hd, tid);
     for (int t = 0; t < T; ++t) {
-        stage_store(sk, khi, klo, tid);
-        stage_store(sv, vhi, vlo, tid);
+        stage_store<NP>(sk, kimg, tid);
+        stage_store<NP>(sv, vimg, tid);
         __syncthreads();
         if (t + 1 < T) {
-            stage_load(sk, kb, a.sk.n, (t + 1) * TT, Nk, tid);
-            stage_load(sv, vb, a.sv.n, (t + 1) * TT, Nk, tid);
+            stage_load(sk, kb, a.sk.n, (t + 1) * TT, Nk, hd, tid);
+            stage_load(sv, vb, a.sv.n, (t + 1) * TT, Nk, hd, tid);
         }
         f32x16 sacc[2];
 #pragma unroll
         for (int kbk = 0; kbk < 2; ++kbk) {
             sacc[kbk] = f32x16{};
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-                sacc[kbk] = mfma3(rd_row(khi, 32 * kbk + r, s, hh), rd_row(klo, 32 * kbk + r, s, hh), qh[s], ql[s],
-                                  sacc[kbk]);
+            for (int s = 0; s < 4; ++s) sacc[kbk] = mfmaN<NP>(rd_row<NP>(kimg, 32 * kbk + r, s, hh), qf[s], sacc[kbk]);
         }
         const int kbase = t * TT;
         if (kbase + TT > Nk) {
@@ -249,56 +273,58 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
         }
 #pragma unroll
         for (int kbk = 0; kbk < 2; ++kbk) {
-            bf16x8 ph[2], pl[2];
-            split_acc<0>(sacc[kbk], ph[0], pl[0]);
-            split_acc<1>(sacc[kbk], ph[1], pl[1]);
+            const Frag<NP> pf[2] = {split_acc<NP, 0>(sacc[kbk]), split_acc<NP, 1>(sacc[kbk])};
 #pragma unroll
             for (int s = 0; s < 2; ++s)
 #pragma unroll
-                for (int db = 0; db < 2; ++db)
-                    oacc[db] = mfma3(rd_tr(vhi, tl, kbk, s, db), rd_tr(vlo, tl, kbk, s, db), ph[s], pl[s], oacc[db]);
+                for (int db = 0; db < 2; ++db) oacc[db] = mfmaN<NP>(rd_tr<NP>(vimg, tl, kbk, s, db), pf[s], oacc[db]);
         }
         __syncthreads();
     }
     const float l = l_run + xchg32(l_run);
     if (q_row < Nq) {
-        store_tr(a.out + (long long)b * a.so.b + (long long)q_row * a.so.n + (long long)h * a.so.h, oacc, hh, 1.f / l);
+        store_tr(a.out + (long long)b * a.so.b + (long long)q_row * a.so.n + (long long)h * a.so.h, oacc, hh, 1.f / l,
+                 hd);
         if (hh == 0) a.lse[((long long)b * a.H + h) * Nq + q_row] = m_run + __log2f(l);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]; one 16-lane group per row
+// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]; one 16-lane group per row (4 floats a lane)
 __global__ __launch_bounds__(256) void attn32_delta(Args a, int rows) {
     const int g = (blockIdx.x * 256 + threadIdx.x) >> 4, j = threadIdx.x & 15;
     if (g >= rows) return;
     const int q = g % a.Nq, bh = g / a.Nq, h = bh % a.H, b = bh / a.H;
-    const float4 o = *reinterpret_cast<const float4*>(a.o + (long long)b * a.so.b + (long long)q * a.so.n +
-                                                      (long long)h * a.so.h + 4 * j);
-    const float4 d = *reinterpret_cast<const float4*>(a.dout + (long long)b * a.sdo.b + (long long)q * a.sdo.n +
-                                                      (long long)h * a.sdo.h + 4 * j);
-    float s = o.x * d.x + o.y * d.y + o.z * d.z + o.w * d.w;
+    float s = 0.f;
+    if (4 * j < a.hd) {
+        const float4 o = *reinterpret_cast<const float4*>(a.o + (long long)b * a.so.b + (long long)q * a.so.n +
+                                                          (long long)h * a.so.h + 4 * j);
+        const float4 d = *reinterpret_cast<const float4*>(a.dout + (long long)b * a.sdo.b + (long long)q * a.sdo.n +
+                                                          (long long)h * a.sdo.h + 4 * j);
+        s = o.x * d.x + o.y * d.y + o.z * d.z + o.w * d.w;
+    }
 #pragma unroll
     for (int m = 8; m >= 1; m >>= 1) s += __shfl_xor(s, m);
     if (j == 0) a.delta[g] = s;
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * WAVES, 2) void attn32_dq(Args a) {   // 2 waves per SIMD (the register budget the kernel was tuned to)
-    __shared__ __attribute__((aligned(16))) unsigned char lds[4 * IMG];
-    unsigned char *khi = lds, *klo = lds + IMG, *vhi = lds + 2 * IMG, *vlo = lds + 3 * IMG;
+template <int NP>
+__global__ __launch_bounds__(64 * WAVES, NP == 3 ? 1 : 2) void attn32_dq(Args a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG];
+    unsigned char *kimg = lds, *vimg = lds + NP * IMG;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
     const int h = blockIdx.y, b = blockIdx.z;
-    const int Nq = a.Nq, Nk = a.Nk;
+    const int Nq = a.Nq, Nk = a.Nk, hd = a.hd;
     const int q_row = blockIdx.x * RB + 32 * wave + r;
     const TrLane tl{(lane >> 4) & 1, (lane >> 2) & 3, lane & 3, hh};
 
     const float* kb = a.k + (long long)b * a.sk.b + (long long)h * a.sk.h;
     const float* vb = a.v + (long long)b * a.sv.b + (long long)h * a.sv.h;
-    bf16x8 qh[4], ql[4], oh[4], ol[4];
-    load_fixed(a.q + (long long)b * a.sq.b + (long long)h * a.sq.h, a.sq.n, q_row, Nq, hh, qh, ql);
-    load_fixed(a.dout + (long long)b * a.sdo.b + (long long)h * a.sdo.h, a.sdo.n, q_row, Nq, hh, oh, ol);
+    Frag<NP> qf[4], of[4];
+    load_fixed<NP>(a.q + (long long)b * a.sq.b + (long long)h * a.sq.h, a.sq.n, q_row, Nq, hd, hh, qf);
+    load_fixed<NP>(a.dout + (long long)b * a.sdo.b + (long long)h * a.sdo.h, a.sdo.n, q_row, Nq, hd, hh, of);
     const long long rix = ((long long)b * a.H + h) * Nq + (q_row < Nq ? q_row : 0);
     const float lse = q_row < Nq ? a.lse[rix] : INFINITY;
     const float dlt = q_row < Nq ? a.delta[rix] : 0.f;
@@ -307,15 +333,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void attn32_dq(Args a) {   // 2 wave
     f32x16 dq[2] = {f32x16{}, f32x16{}};
     const float c = a.c;
     const int T = (Nk + TT - 1) / TT;
-    stage_load(sk, kb, a.sk.n, 0, Nk, tid);
-    stage_load(sv, vb, a.sv.n, 0, Nk, tid);
+    stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
+    stage_load(sv, vb, a.sv.n, 0, Nk, hd, tid);
     for (int t = 0; t < T; ++t) {
-        stage_store(sk, khi, klo, tid);
-        stage_store(sv, vhi, vlo, tid);
+        stage_store<NP>(sk, kimg, tid);
+        stage_store<NP>(sv, vimg, tid);
         __syncthreads();
         if (t + 1 < T) {
-            stage_load(sk, kb, a.sk.n, (t + 1) * TT, Nk, tid);
-            stage_load(sv, vb, a.sv.n, (t + 1) * TT, Nk, tid);
+            stage_load(sk, kb, a.sk.n, (t + 1) * TT, Nk, hd, tid);
+            stage_load(sv, vb, a.sv.n, (t + 1) * TT, Nk, hd, tid);
         }
         const int kbase = t * TT;
 #pragma unroll
@@ -323,8 +349,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void attn32_dq(Args a) {   // 2 wave
             f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
-                s = mfma3(rd_row(khi, 32 * kbk + r, st, hh), rd_row(klo, 32 * kbk + r, st, hh), qh[st], ql[st], s);
-                dp = mfma3(rd_row(vhi, 32 * kbk + r, st, hh), rd_row(vlo, 32 * kbk + r, st, hh), oh[st], ol[st], dp);
+                s = mfmaN<NP>(rd_row<NP>(kimg, 32 * kbk + r, st, hh), qf[st], s);
+                dp = mfmaN<NP>(rd_row<NP>(vimg, 32 * kbk + r, st, hh), of[st], dp);
             }
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -332,31 +358,30 @@ __global__ __launch_bounds__(64 * WAVES, 2) void attn32_dq(Args a) {   // 2 wave
                 const float p = key < Nk ? __builtin_amdgcn_exp2f(fmaf(s[i], c, -lse)) : 0.f;
                 s[i] = p * (dp[i] - dlt);
             }
-            bf16x8 dh[2], dl[2];
-            split_acc<0>(s, dh[0], dl[0]);
-            split_acc<1>(s, dh[1], dl[1]);
+            const Frag<NP> df[2] = {split_acc<NP, 0>(s), split_acc<NP, 1>(s)};
 #pragma unroll
             for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int db = 0; db < 2; ++db)
-                    dq[db] = mfma3(rd_tr(khi, tl, kbk, st, db), rd_tr(klo, tl, kbk, st, db), dh[st], dl[st], dq[db]);
+                for (int db = 0; db < 2; ++db) dq[db] = mfmaN<NP>(rd_tr<NP>(kimg, tl, kbk, st, db), df[st], dq[db]);
         }
         __syncthreads();
     }
     if (q_row < Nq)
-        store_tr(a.dq + (long long)b * a.sdq.b + (long long)q_row * a.sdq.n + (long long)h * a.sdq.h, dq, hh, a.scale);
+        store_tr(a.dq + (long long)b * a.sdq.b + (long long)q_row * a.sdq.n + (long long)h * a.sdq.h, dq, hh, a.scale,
+                 hd);
 }
 
 // ---------------------------------------------------------------------------------------------
+template <int NP>
 __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[4 * IMG + 2 * TT * 4];
-    unsigned char *qhi = lds, *qlo = lds + IMG, *ohi = lds + 2 * IMG, *olo = lds + 3 * IMG;
-    float* lse_s = reinterpret_cast<float*>(lds + 4 * IMG);
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG + 2 * TT * 4];
+    unsigned char *qimg = lds, *oimg = lds + NP * IMG;
+    float* lse_s = reinterpret_cast<float*>(lds + 2 * NP * IMG);
     float* dlt_s = lse_s + TT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
     const int h = blockIdx.y, b = blockIdx.z;
-    const int Nq = a.Nq, Nk = a.Nk;
+    const int Nq = a.Nq, Nk = a.Nk, hd = a.hd;
     const int key = blockIdx.x * RB + 32 * wave + r;
     const TrLane tl{(lane >> 4) & 1, (lane >> 2) & 3, lane & 3, hh};
 
@@ -364,15 +389,15 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
     const float* ob = a.dout + (long long)b * a.sdo.b + (long long)h * a.sdo.h;
     const float* lb = a.lse + ((long long)b * a.H + h) * Nq;
     const float* db_ = a.delta + ((long long)b * a.H + h) * Nq;
-    bf16x8 kh[4], kl[4], vh[4], vl[4];
-    load_fixed(a.k + (long long)b * a.sk.b + (long long)h * a.sk.h, a.sk.n, key, Nk, hh, kh, kl);
-    load_fixed(a.v + (long long)b * a.sv.b + (long long)h * a.sv.h, a.sv.n, key, Nk, hh, vh, vl);
+    Frag<NP> kf[4], vf[4];
+    load_fixed<NP>(a.k + (long long)b * a.sk.b + (long long)h * a.sk.h, a.sk.n, key, Nk, hd, hh, kf);
+    load_fixed<NP>(a.v + (long long)b * a.sv.b + (long long)h * a.sv.h, a.sv.n, key, Nk, hd, hh, vf);
 
     Stage sq, so;
     float lse_r = INFINITY, dlt_r = 0.f;
     auto load_rows = [&](int q0) {
-        stage_load(sq, qb, a.sq.n, q0, Nq, tid);
-        stage_load(so, ob, a.sdo.n, q0, Nq, tid);
+        stage_load(sq, qb, a.sq.n, q0, Nq, hd, tid);
+        stage_load(so, ob, a.sdo.n, q0, Nq, hd, tid);
         if (tid < TT) {
             const bool ok = q0 + tid < Nq;
             lse_r = ok ? lb[q0 + tid] : INFINITY;
@@ -384,8 +409,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
     const int T = (Nq + TT - 1) / TT;
     load_rows(0);
     for (int t = 0; t < T; ++t) {
-        stage_store(sq, qhi, qlo, tid);
-        stage_store(so, ohi, olo, tid);
+        stage_store<NP>(sq, qimg, tid);
+        stage_store<NP>(so, oimg, tid);
         if (tid < TT) {
             lse_s[tid] = lse_r;
             dlt_s[tid] = dlt_r;
@@ -397,8 +422,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
             f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
-                s = mfma3(rd_row(qhi, 32 * qbk + r, st, hh), rd_row(qlo, 32 * qbk + r, st, hh), kh[st], kl[st], s);
-                dp = mfma3(rd_row(ohi, 32 * qbk + r, st, hh), rd_row(olo, 32 * qbk + r, st, hh), vh[st], vl[st], dp);
+                s = mfmaN<NP>(rd_row<NP>(qimg, 32 * qbk + r, st, hh), kf[st], s);
+                dp = mfmaN<NP>(rd_row<NP>(oimg, 32 * qbk + r, st, hh), vf[st], dp);
             }
             // rows of this lane's accumulator entries: 32 qbk + 8 gi + 4 hh + (0..3)
 #pragma unroll
@@ -414,24 +439,21 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
                     dp[i] = p * (dp[i] - Ds[j]);
                 }
             }
-            bf16x8 ph[2], pl[2], dh[2], dl[2];
-            split_acc<0>(s, ph[0], pl[0]);
-            split_acc<1>(s, ph[1], pl[1]);
-            split_acc<0>(dp, dh[0], dl[0]);
-            split_acc<1>(dp, dh[1], dl[1]);
+            const Frag<NP> pf[2] = {split_acc<NP, 0>(s), split_acc<NP, 1>(s)};
+            const Frag<NP> df[2] = {split_acc<NP, 0>(dp), split_acc<NP, 1>(dp)};
 #pragma unroll
             for (int st = 0; st < 2; ++st)
 #pragma unroll
                 for (int d = 0; d < 2; ++d) {
-                    dv[d] = mfma3(rd_tr(ohi, tl, qbk, st, d), rd_tr(olo, tl, qbk, st, d), ph[st], pl[st], dv[d]);
-                    dk[d] = mfma3(rd_tr(qhi, tl, qbk, st, d), rd_tr(qlo, tl, qbk, st, d), dh[st], dl[st], dk[d]);
+                    dv[d] = mfmaN<NP>(rd_tr<NP>(oimg, tl, qbk, st, d), pf[st], dv[d]);
+                    dk[d] = mfmaN<NP>(rd_tr<NP>(qimg, tl, qbk, st, d), df[st], dk[d]);
                 }
         }
         __syncthreads();
     }
     if (key < Nk) {
-        store_tr(a.dk + (long long)b * a.sdk.b + (long long)key * a.sdk.n + (long long)h * a.sdk.h, dk, hh, a.scale);
-        store_tr(a.dv + (long long)b * a.sdv.b + (long long)key * a.sdv.n + (long long)h * a.sdv.h, dv, hh, 1.f);
+        store_tr(a.dk + (long long)b * a.sdk.b + (long long)key * a.sdk.n + (long long)h * a.sdk.h, dk, hh, a.scale, hd);
+        store_tr(a.dv + (long long)b * a.sdv.b + (long long)key * a.sdv.n + (long long)h * a.sdv.h, dv, hh, 1.f, hd);
     }
 }
 
@@ -444,8 +466,9 @@ bool strides_ok(const long long* s) {
 Strides mk(const long long* s) { return Strides{s[0], s[1], s[2]}; }
 bool aligned16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
-int check_shape(int B, int H, int Nq, int Nk, int head_dim) {
-    if (head_dim != HD) return VFM_NO_KERNEL;
+int check_shape(int B, int H, int Nq, int Nk, int head_dim, int precision) {
+    if (head_dim != HD && head_dim != 32) return VFM_NO_KERNEL;
+    if (precision != VFM_F32 && precision != VFM_F32X3) return VFM_ERR_ARGS;
     if (B <= 0 || H <= 0 || Nq <= 0 || Nk <= 0 || B > 65535 || H > 65535) return VFM_ERR_ARGS;
     return VFM_OK;
 }
@@ -454,8 +477,9 @@ int check_shape(int B, int H, int Nq, int Nk, int head_dim) {
 
 extern "C" int vfm_attention_f32_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int H,
                                      int Nq, int Nk, int head_dim, const long long* sq, const long long* sk,
-                                     const long long* sv, const long long* so, float scale, void* stream) {
-    int rc = check_shape(B, H, Nq, Nk, head_dim);
+                                     const long long* sv, const long long* so, float scale, int precision,
+                                     void* stream) {
+    int rc = check_shape(B, H, Nq, Nk, head_dim, precision);
     if (rc != VFM_OK) return rc;
     if (!q || !k || !v || !o || !lse) return VFM_ERR_ARGS;
     if (!strides_ok(sq) || !strides_ok(sk) || !strides_ok(sv) || !strides_ok(so)) return VFM_ERR_ARGS;
@@ -467,7 +491,10 @@ extern "C" int vfm_attention_f32_fwd(const void* q, const void* k, const void* v
     a.Nq = Nq; a.Nk = Nk; a.H = H;
     a.scale = scale;
     a.c = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn32_fwd, dim3((Nq + RB - 1) / RB, H, B), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    a.hd = head_dim;
+    const dim3 grid((Nq + RB - 1) / RB, H, B);
+    if (precision == VFM_F32) hipLaunchKernelGGL(attn32_fwd<3>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(attn32_fwd<2>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
     return launch_status();
 }
 
@@ -476,8 +503,8 @@ extern "C" int vfm_attention_f32_bwd(const void* q, const void* k, const void* v
                                      int Nk, int head_dim, const long long* sq, const long long* sk,
                                      const long long* sv, const long long* so, const long long* sdo,
                                      const long long* sdq, const long long* sdk, const long long* sdv, float scale,
-                                     void* stream) {
-    int rc = check_shape(B, H, Nq, Nk, head_dim);
+                                     int precision, void* stream) {
+    int rc = check_shape(B, H, Nq, Nk, head_dim, precision);
     if (rc != VFM_OK) return rc;
     if (!q || !k || !v || !o || !dout || !lse || !delta || !dq || !dk || !dv) return VFM_ERR_ARGS;
     const long long* ss[8] = {sq, sk, sv, so, sdo, sdq, sdk, sdv};
@@ -495,11 +522,18 @@ extern "C" int vfm_attention_f32_bwd(const void* q, const void* k, const void* v
     a.Nq = Nq; a.Nk = Nk; a.H = H;
     a.scale = scale;
     a.c = scale * 1.4426950408889634f;
+    a.hd = head_dim;
     hipStream_t st = (hipStream_t)stream;
     const long long rows = (long long)B * H * Nq;
     if (rows > (1ll << 31) / 16) return VFM_ERR_ARGS;
     hipLaunchKernelGGL(attn32_delta, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, st, a, (int)rows);
-    hipLaunchKernelGGL(attn32_dq, dim3((Nq + RB - 1) / RB, H, B), dim3(64 * WAVES), 0, st, a);
-    hipLaunchKernelGGL(attn32_dkdv, dim3((Nk + RB - 1) / RB, H, B), dim3(64 * WAVES), 0, st, a);
+    const dim3 gq((Nq + RB - 1) / RB, H, B), gk((Nk + RB - 1) / RB, H, B);
+    if (precision == VFM_F32) {
+        hipLaunchKernelGGL(attn32_dq<3>, gq, dim3(64 * WAVES), 0, st, a);
+        hipLaunchKernelGGL(attn32_dkdv<3>, gk, dim3(64 * WAVES), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(attn32_dq<2>, gq, dim3(64 * WAVES), 0, st, a);
+        hipLaunchKernelGGL(attn32_dkdv<2>, gk, dim3(64 * WAVES), 0, st, a);
+    }
     return launch_status();
 }

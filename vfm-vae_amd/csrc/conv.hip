@@ -1,19 +1,21 @@
-// 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA cores, fp32 through the
-// 3-term bf16 split (the LPIPS VGG16 stack: reference training/lpips.py:126-163, run in fp32 by
-// the reference; MIOpen's fp32 Winograd was the single largest kernel of the training step).
+// 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA cores, fp32 products as the
+// f32x6 bf16 split (fp32-equivalent; f32x3 opt-in) -- the LPIPS VGG16 stack: reference
+// training/lpips.py:126-163, run in fp32 by the reference; MIOpen's fp32 Winograd was the single
+// largest kernel of the training step.
 //
 //   out[p, n] = epi( sum_{tap, c} x[p + shift(tap), c] * w[n, tap, c] ),   p = (b, y, x) pixels,
 //   epi: + bias[n], ReLU, and/or x (mask[p, n] > 0) (the ReLU derivative of the layer below, for
 //   the data-gradient pass), fp32 out.
 //
 // Layout: activations NHWC fp32 ([B, H, W, C] contiguous: channels_last), weights [Cout][9][Cin]
-// (tap-major, channels contiguous) pre-split into bf16 hi / lo arrays with rows padded to ldw. Cin is a power of two >= 4 (the 3-channel image is
-// padded to 4), Cout a multiple of 64. The data gradient of the same conv is this kernel with the
-// flipped, transposed weights w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
+// (tap-major, channels contiguous) pre-split into NP bf16 piece arrays [NP][Cout][ldw] with rows
+// padded to ldw. Cin is a power of two >= 4 (the 3-channel image is padded to 4), Cout a multiple
+// of 64. The data gradient of the same conv is this kernel with the flipped, transposed weights
+// w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
 //
 // GEMM view: M = B*H*W pixels, N = Cout, K = 9*Cin (tap-major). Tile 128 pixels x BN (128 or 64)
-// couts x 64 k, 4 waves (2 x 2), 32x32x16 bf16 MFMA, fp32 operands split into hi/lo images on
-// the way into LDS (gemm.hip's f32x3; error per product <= ~2^-15.5 relative). The A loader is
+// couts x 64 k, 4 waves (2 x 2), 32x32x16 bf16 MFMA, fp32 activations split into NP piece images
+// on the way into LDS and the Terms<NP> piece products accumulated (gemm.hip's f32x6 / f32x3). The A loader is
 // implicit: each thread owns 8 pixel rows and one 4-channel column of the tile; a k-tile (64
 // channels of one tap, or for Cin < 64 several taps) becomes one 16-B load per row at
 // (p + dy*W + dx)*Cin + c, zero outside the image. The 9 shifted reads of a pixel hit L2.
@@ -31,9 +33,9 @@ constexpr int IMG_A = BM * BK * 2;   // bytes of one bf16 image of the A tile
 
 struct ConvArgs {
     const float* x;      // [B, H, W, Cin]
-    const __hip_bfloat16* wh;   // [Cout, ldw] hi = bf16(w), tap-major k, zero-padded to ldw
-    const __hip_bfloat16* wl;   // [Cout, ldw] lo = bf16(w - hi)
+    const __hip_bfloat16* w;    // [NP][Cout, ldw] pieces of w (hi[, mid], lo), tap-major k, zero-padded to ldw
     int ldw;
+    long long wps;              // elements between pieces (Cout * ldw)
     const float* bias;   // [Cout] or null
     const float* mask;   // [B, H, W, Cout] or null
     float* out;          // [B, H, W, Cout]
@@ -44,13 +46,14 @@ struct ConvArgs {
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
 
-// 4 fp32 (one uint4) -> hi/lo halves of a 16-B image chunk
-__device__ __forceinline__ void put4(unsigned char* hi, unsigned char* lo, int off, uint4 r) {
-    uint32_t h01, l01, h23, l23;
-    split2_bf16(__uint_as_float(r.x), __uint_as_float(r.y), h01, l01);
-    split2_bf16(__uint_as_float(r.z), __uint_as_float(r.w), h23, l23);
-    *reinterpret_cast<uint2*>(hi + off) = make_uint2(h01, h23);
-    *reinterpret_cast<uint2*>(lo + off) = make_uint2(l01, l23);
+// 4 fp32 (one uint4) -> the NP pieces' halves of a 16-B image chunk (piece p at img + p * pstride)
+template <int NP>
+__device__ __forceinline__ void put4(unsigned char* img, int pstride, int off, uint4 r) {
+    uint32_t p01[NP], p23[NP];
+    split_pieces<NP>(__uint_as_float(r.x), __uint_as_float(r.y), p01);
+    split_pieces<NP>(__uint_as_float(r.z), __uint_as_float(r.w), p23);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(img + p * pstride + off) = make_uint2(p01[p], p23[p]);
 }
 
 // thread -> (row = tid/16 + 16u, 4-element column tid%16) of a [rows][64] fp32 tile
@@ -114,35 +117,39 @@ struct StageA {
                        ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.x) + (unsigned)(off[u] + c) * 4u)
                        : make_uint4(0, 0, 0, 0);
     }
-    __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
+    template <int NP>
+    __device__ __forceinline__ void store(unsigned char* img, int tid) const {
         const int cc = tid & 15;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) put4(hi, lo, kc_off(tid / 16 + 16 * u, cc >> 1) + 8 * (cc & 1), r[u]);
+        for (int u = 0; u < 8; ++u) put4<NP>(img, IMG_A, kc_off(tid / 16 + 16 * u, cc >> 1) + 8 * (cc & 1), r[u]);
     }
 };
 
-// weights arrive pre-split (hi / lo bf16, split once per weight version on the host side):
-// thread -> 16-B chunks (8 k) c = tid + 256u of a [ROWS][64] tile, copied as-is into both images
-template <int ROWS>
+// weights arrive pre-split (NP bf16 pieces, split once per weight version on the host side):
+// thread -> 16-B chunks (8 k) c = tid + 256u of a [ROWS][64] tile, copied as-is into the piece images
+template <int ROWS, int NP>
 struct StageB {
     static constexpr int PER = ROWS * 8 / THREADS;
-    uint4 h[PER], l[PER];
+    static constexpr int IMG = ROWS * 64 * 2;
+    uint4 v[NP][PER];
     __device__ __forceinline__ void load(const ConvArgs& a, int n0, int k0, int tid) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int c = tid + THREADS * u, row = c >> 3, k = k0 + 8 * (c & 7), n = n0 + row;
             const bool ok = k < a.ldw && n < a.Cout;
-            const unsigned o = (unsigned)(n * a.ldw + k) * 2u;          // byte offset (host: Cout * ldw < 2^30)
-            h[u] = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.wh) + o) : make_uint4(0, 0, 0, 0);
-            l[u] = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.wl) + o) : make_uint4(0, 0, 0, 0);
+            const unsigned o = (unsigned)(n * a.ldw + k) * 2u;          // byte offset (host: NP * Cout * ldw < 2^30)
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                v[p][u] = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.w + p * a.wps) + o)
+                             : make_uint4(0, 0, 0, 0);
         }
     }
-    __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
+    __device__ __forceinline__ void store(unsigned char* img, int tid) const {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int c = tid + THREADS * u, off = kc_off(c >> 3, c & 7);
-            *reinterpret_cast<uint4*>(hi + off) = h[u];
-            *reinterpret_cast<uint4*>(lo + off) = l[u];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) *reinterpret_cast<uint4*>(img + p * IMG + off) = v[p][u];
         }
     }
 };
@@ -151,15 +158,13 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int s,
     return *reinterpret_cast<const bf16x8*>(img + kc_off(32 * blk + (lane & 31), 2 * s + (lane >> 5)));
 }
 
-template <int BN>
-__global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
+template <int BN, int NP>
+__global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3_kernel(ConvArgs a) {
     constexpr int NJ = BN / 64;                 // 32-col blocks per wave
     constexpr int IMG_B = BN * BK * 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    unsigned char* a_hi = lds;
-    unsigned char* a_lo = lds + IMG_A;
-    unsigned char* b_hi = lds + 2 * IMG_A;
-    unsigned char* b_lo = lds + 2 * IMG_A + IMG_B;
+    unsigned char* a_img = lds;                 // A piece p at a_img + p IMG_A
+    unsigned char* b_img = lds + NP * IMG_A;    // B piece p at b_img + p IMG_B
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
     const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
     StageA sa;
-    StageB<BN> sb;
+    StageB<BN, NP> sb;
     sa.init(a, m0, tid);
     sa.cur_tap = -1;
     const bool wide = a.lc >= 6;                        // Cin >= 64 (uniform)
@@ -186,8 +191,8 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
     else sa.load(a, 0, tid);
     sb.load(a, n0, 0, tid);
     for (int k0 = 0; k0 < a.K; k0 += BK) {
-        sa.store(a_hi, a_lo, tid);
-        sb.store(b_hi, b_lo, tid);
+        sa.store<NP>(a_img, tid);
+        sb.store(b_img, tid);
         __syncthreads();
         if (k0 + BK < a.K) {
             if (wide) sa.load_wide(a, k0 + BK, tid);
@@ -196,25 +201,22 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
         }
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
-            bf16x8 ah[2], al[2], bh[NJ], bl[NJ];
+            bf16x8 af[NP][2], bf[NP][NJ];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                ah[i] = frag(a_hi, 2 * wm + i, s, lane);
-                al[i] = frag(a_lo, 2 * wm + i, s, lane);
+            for (int p = 0; p < NP; ++p) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) af[p][i] = frag(a_img + p * IMG_A, 2 * wm + i, s, lane);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bf[p][j] = frag(b_img + p * IMG_B, NJ * wn + j, s, lane);
             }
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                bh[j] = frag(b_hi, NJ * wn + j, s, lane);
-                bl[j] = frag(b_lo, NJ * wn + j, s, lane);
-            }
+            for (int t = 0; t < Terms<NP>::N; ++t)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                }
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i], bf[Terms<NP>::b(t)][j],
+                                                                            acc[i][j], 0, 0, 0);
         }
         __syncthreads();
     }
@@ -240,29 +242,31 @@ __global__ __launch_bounds__(THREADS, 2) void conv3x3_kernel(ConvArgs a) {
     }
 }
 
-template <int BN>
+template <int BN, int NP>
 int launch(const ConvArgs& a, hipStream_t st) {
-    const size_t lds = 2 * IMG_A + 2 * BN * BK * 2;
+    const size_t lds = NP * (IMG_A + BN * BK * 2);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BN, NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
     const long long tiles = (long long)((a.M + BM - 1) / BM) * (a.Cout / BN);
     if (tiles > 0x7fffffff) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(conv3x3_kernel<BN>, dim3((unsigned)tiles), dim3(THREADS), lds, st, a);
+    hipLaunchKernelGGL((conv3x3_kernel<BN, NP>), dim3((unsigned)tiles), dim3(THREADS), lds, st, a);
     return launch_status();
 }
 
 }  // namespace
 
-extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void* w_lo, int ldw, const float* bias,
+extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int precision, int ldw, const float* bias,
                                     const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int relu,
                                     void* stream) {
-    if (!x || !w_hi || !w_lo || !out || B <= 0 || H <= 0 || W <= 0 || H > 32767 || W > 32767) return VFM_ERR_ARGS;
+    if (!x || !w_pieces || !out || B <= 0 || H <= 0 || W <= 0 || H > 32767 || W > 32767) return VFM_ERR_ARGS;
+    if (precision != VFM_F32 && precision != VFM_F32X3) return VFM_ERR_ARGS;
+    const int np = precision == VFM_F32 ? 3 : 2;
     if (Cin < 4 || (Cin & (Cin - 1)) || Cout <= 0 || Cout % 64) return VFM_NO_KERNEL;
     if (ldw < 9 * Cin || ldw % 64) return VFM_ERR_ARGS;
-    if (((uintptr_t)x | (uintptr_t)w_hi | (uintptr_t)w_lo) % 16) return VFM_ERR_ARGS;
+    if (((uintptr_t)x | (uintptr_t)w_pieces) % 16) return VFM_ERR_ARGS;
     const long long M = (long long)B * H * W;
     if (M * (long long)(Cin > Cout ? Cin : Cout) >= (1ll << 40) || M >= (1ll << 31) - 2 * (long long)W - 2)
         return VFM_ERR_ARGS;
@@ -270,7 +274,7 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void
     if (Cin >= 64 && (M + 2 * (long long)W + 2) * Cin >= (1ll << 30)) return VFM_ERR_ARGS;
     if (M * (long long)Cout >= (1ll << 30) || (long long)Cout * ldw >= (1ll << 30)) return VFM_ERR_ARGS;
     ConvArgs a;
-    a.x = x; a.wh = (const __hip_bfloat16*)w_hi; a.wl = (const __hip_bfloat16*)w_lo; a.ldw = ldw;
+    a.x = x; a.w = (const __hip_bfloat16*)w_pieces; a.ldw = ldw; a.wps = (long long)Cout * ldw;
     a.bias = bias; a.mask = mask; a.out = out;
     a.M = (int)M; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.K = 9 * Cin;
     a.lc = 0;
@@ -279,5 +283,6 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_hi, const void
     a.fH = make_fastdiv((uint32_t)H);
     a.relu = relu;
     hipStream_t st = (hipStream_t)stream;
-    return (Cout % 128 == 0) ? launch<128>(a, st) : launch<64>(a, st);
+    if (np == 3) return (Cout % 128 == 0) ? launch<128, 3>(a, st) : launch<64, 3>(a, st);
+    return (Cout % 128 == 0) ? launch<128, 2>(a, st) : launch<64, 2>(a, st);
 }

@@ -19,14 +19,15 @@
 // read as MFMA fragments with ds_read_b128; MN-contiguous ones as [64][128] (256-B rows,
 // the 4x4 XOR swizzle of pwgemm.hip), read with the transposing ds_read_b64_tr_b16.
 //
-// Precision modes:
-//   bf16 : bf16 inputs, v_mfma_f32_32x32x16_bf16.
-//   f32x3: fp32 inputs split on the way into LDS into hi = bf16(x), lo = bf16(x - hi);
-//          acc += lo_a.hi_b + hi_a.lo_b + hi_a.hi_b (3 bf16 MFMAs; products exact in fp32).
-//          |x - (hi + lo)| <= 2^-17 |x| and the dropped lo.lo term is <= 2^-16 |a b|, so each
-//          product carries <= ~2^-15.5 relative error (vs 2^-24 for an fp32 FMA), at 5.3x the
-//          fp32 MFMA rate. gfx950 has no TF32/xf32; this is the fp32 path of the decoder's
-//          fp32 blocks (TF32 is off in the reference, training_loop.py:504-505).
+// Precision modes (NP = bf16 pieces per operand element):
+//   bf16 (NP 1): bf16 inputs, v_mfma_f32_32x32x16_bf16.
+//   f32x6 (NP 3, VFM_F32, the default for fp32): fp32 inputs split on the way into LDS into
+//          hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (x = hi + mid + lo exactly);
+//          acc += the six piece products of order >= 2^-16 (vfm_common.h Terms<3>), each exact in
+//          fp32; the dropped ones total <= ~2^-23 |a b|, one fp32 rounding: fp32-equivalent
+//          products (gfx950 has no TF32/xf32; TF32 is off in the reference,
+//          training_loop.py:504-505) at 2.65x the fp32 MFMA rate.
+//   f32x3 (NP 2, VFM_F32X3, opt-in): hi / lo only, 3 products, <= ~2^-15.5 relative per product.
 //
 // Tile 128 x 128 x 64, 4 waves (2 x 2, each 64 x 64 = 2 x 2 blocks of 32 x 32), next K-tile
 // prefetched into registers while the current one is multiplied (written to LDS after the
@@ -81,9 +82,10 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // from registers into its LDS image(s).
 //   KCONT: global rows are outer (m or n), contiguous along k (lead = ld between rows)
 //   !KCONT: global rows are k, contiguous along the outer index
-// F32: fp32 input (split into hi/lo images), else bf16 input.
-template <bool KCONT, bool F32>
+// NP > 1: fp32 input split into NP bf16 images (hi, [mid,] lo), else bf16 input.
+template <bool KCONT, int NP>
 struct Stage {
+    static constexpr bool F32 = NP > 1;
     static constexpr int EPC = F32 ? 4 : 8;                  // elements per 16-B chunk
     static constexpr int CHUNKS = 128 * 64 / EPC;            // chunks per tile
     static constexpr int PER = CHUNKS / THREADS;             // chunks per thread
@@ -107,23 +109,24 @@ struct Stage {
         }
     }
 
-    __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
+    // piece p goes to img + p * IMG
+    __device__ __forceinline__ void store(unsigned char* img, int tid) const {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int c = tid + THREADS * u;
             const int row = c / ROWCH, cc = c % ROWCH;
             if (!F32) {
                 const int off = KCONT ? kc_off(row, cc) : mc_off(row, cc);
-                *reinterpret_cast<uint4*>(hi + off) = r[u];
+                *reinterpret_cast<uint4*>(img + off) = r[u];
             } else {
-                // 4 fp32 -> 4 bf16 hi + 4 bf16 lo (8 B each), half of a 16-B image chunk
+                // 4 fp32 -> 4 bf16 per piece (8 B each), half of a 16-B image chunk
                 const int ch = cc >> 1, half = cc & 1;
                 const int off = (KCONT ? kc_off(row, ch) : mc_off(row, ch)) + 8 * half;
-                uint32_t h01, l01, h23, l23;
-                split2_bf16(__uint_as_float(r[u].x), __uint_as_float(r[u].y), h01, l01);
-                split2_bf16(__uint_as_float(r[u].z), __uint_as_float(r[u].w), h23, l23);
-                *reinterpret_cast<uint2*>(hi + off) = make_uint2(h01, h23);
-                *reinterpret_cast<uint2*>(lo + off) = make_uint2(l01, l23);
+                uint32_t p01[NP], p23[NP];
+                split_pieces<NP>(__uint_as_float(r[u].x), __uint_as_float(r[u].y), p01);
+                split_pieces<NP>(__uint_as_float(r[u].z), __uint_as_float(r[u].w), p23);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(img + p * IMG + off) = make_uint2(p01[p], p23[p]);
             }
         }
     }
@@ -146,13 +149,12 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int s,
     }
 }
 
-template <bool AK, bool BKC, bool F32, bool OUTF32>
-__global__ __launch_bounds__(THREADS, 2) void gemm_kernel(GemmArgs a) {
+template <bool AK, bool BKC, int NP, bool OUTF32>
+__global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    unsigned char* a_hi = lds;
-    unsigned char* b_hi = lds + IMG;
-    unsigned char* a_lo = lds + 2 * IMG;      // f32x3 only
-    unsigned char* b_lo = lds + 3 * IMG;
+    constexpr bool F32 = NP > 1;
+    unsigned char* a_img = lds;               // A pieces at a_img + p IMG
+    unsigned char* b_img = lds + NP * IMG;    // B pieces at b_img + p IMG
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
@@ -167,8 +169,8 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_kernel(GemmArgs a) {
     const unsigned char* Ab = reinterpret_cast<const unsigned char*>(a.A) + (long long)z * a.sA * esz;
     const unsigned char* Bb = reinterpret_cast<const unsigned char*>(a.B) + (long long)z * a.sB * esz;
 
-    Stage<AK, F32> sa;
-    Stage<BKC, F32> sb;
+    Stage<AK, NP> sa;
+    Stage<BKC, NP> sb;
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -178,8 +180,8 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_kernel(GemmArgs a) {
     sa.load(Ab, a.lda, m0, kbeg, a.M, kend, tid);
     sb.load(Bb, a.ldb, n0, kbeg, a.N, kend, tid);
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        sa.store(a_hi, a_lo, tid);
-        sb.store(b_hi, b_lo, tid);
+        sa.store(a_img, tid);
+        sb.store(b_img, tid);
         __syncthreads();
         if (k0 + BK < kend) {
             sa.load(Ab, a.lda, m0, k0 + BK, a.M, kend, tid);
@@ -187,30 +189,23 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_kernel(GemmArgs a) {
         }
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
-            bf16x8 af[2], bfr[2];
+            bf16x8 af[NP][2], bfr[NP][2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = frag<AK>(a_hi, 2 * wm + i, s, lane);
+            for (int p = 0; p < NP; ++p) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bfr[j] = frag<BKC>(b_hi, 2 * wn + j, s, lane);
-            if (F32) {
-                bf16x8 al[2], bl[2];
+                for (int i = 0; i < 2; ++i) af[p][i] = frag<AK>(a_img + p * IMG, 2 * wm + i, s, lane);
 #pragma unroll
-                for (int i = 0; i < 2; ++i) al[i] = frag<AK>(a_lo, 2 * wm + i, s, lane);
+                for (int j = 0; j < 2; ++j) bfr[p][j] = frag<BKC>(b_img + p * IMG, 2 * wn + j, s, lane);
+            }
+            // the piece products, smallest first (Terms<NP>)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) bl[j] = frag<BKC>(b_lo, 2 * wn + j, s, lane);
+            for (int t = 0; t < Terms<NP>::N; ++t)
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bfr[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bl[j], acc[i][j], 0, 0, 0);
-                    }
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i],
+                                                                            bfr[Terms<NP>::b(t)][j], acc[i][j], 0, 0, 0);
         }
         __syncthreads();
     }
@@ -279,26 +274,26 @@ __global__ void gemm_reduce_kernel(GemmArgs a, int J, int zcount) {
     (void)zcount;
 }
 
-template <bool AK, bool BKC, bool F32, bool OUTF32>
+template <bool AK, bool BKC, int NP, bool OUTF32>
 int launch(const GemmArgs& a, int batch, hipStream_t st) {
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    const size_t lds = (F32 ? 4 : 2) * IMG;
+    const size_t lds = 2 * NP * IMG;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, F32, OUTF32>,
+        (void)hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, NP, OUTF32>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm_kernel<AK, BKC, F32, OUTF32>), dim3(tiles, batch * a.splits), dim3(THREADS), lds, st, a);
+    hipLaunchKernelGGL((gemm_kernel<AK, BKC, NP, OUTF32>), dim3(tiles, batch * a.splits), dim3(THREADS), lds, st, a);
     return launch_status();
 }
 
-template <bool F32, bool OUTF32>
+template <int NP, bool OUTF32>
 int launch_layout(const GemmArgs& a, int batch, int a_kcont, int b_kcont, hipStream_t st) {
-    if (a_kcont && b_kcont) return launch<true, true, F32, OUTF32>(a, batch, st);
-    if (a_kcont && !b_kcont) return launch<true, false, F32, OUTF32>(a, batch, st);
-    if (!a_kcont && b_kcont) return launch<false, true, F32, OUTF32>(a, batch, st);
-    return launch<false, false, F32, OUTF32>(a, batch, st);
+    if (a_kcont && b_kcont) return launch<true, true, NP, OUTF32>(a, batch, st);
+    if (a_kcont && !b_kcont) return launch<true, false, NP, OUTF32>(a, batch, st);
+    if (!a_kcont && b_kcont) return launch<false, true, NP, OUTF32>(a, batch, st);
+    return launch<false, false, NP, OUTF32>(a, batch, st);
 }
 
 }  // namespace
@@ -314,12 +309,12 @@ extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias
                         int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
                         int bias_mode, int act, int splits, int reduce_batch, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
-    if (in_dtype != VFM_BF16 && in_dtype != VFM_F32) return VFM_NO_KERNEL;
+    if (in_dtype != VFM_BF16 && in_dtype != VFM_F32 && in_dtype != VFM_F32X3) return VFM_NO_KERNEL;
     if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
     if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
     if (splits < 1) splits = 1;
     // 16-B chunks along every contiguous dimension; row starts 16-B aligned
-    const int epc = in_dtype == VFM_F32 ? 4 : 8;
+    const int epc = in_dtype == VFM_BF16 ? 8 : 4;
     const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
     if (a_c % epc || b_c % epc || lda % epc || ldb % epc || sA % epc || sB % epc) return VFM_NO_KERNEL;
     if (((uintptr_t)A | (uintptr_t)B) % 16) return VFM_NO_KERNEL;
@@ -336,12 +331,14 @@ extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias
     a.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
     a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
     hipStream_t st = (hipStream_t)stream;
-    const bool f32 = in_dtype == VFM_F32, of32 = out_dtype == VFM_F32;
+    const bool of32 = out_dtype == VFM_F32;
     int rc;
-    if (f32) rc = of32 ? launch_layout<true, true>(a, batch, a_kcont, b_kcont, st)
-                       : launch_layout<true, false>(a, batch, a_kcont, b_kcont, st);
-    else     rc = of32 ? launch_layout<false, true>(a, batch, a_kcont, b_kcont, st)
-                       : launch_layout<false, false>(a, batch, a_kcont, b_kcont, st);
+    if (in_dtype == VFM_F32) rc = of32 ? launch_layout<3, true>(a, batch, a_kcont, b_kcont, st)
+                                       : launch_layout<3, false>(a, batch, a_kcont, b_kcont, st);
+    else if (in_dtype == VFM_F32X3) rc = of32 ? launch_layout<2, true>(a, batch, a_kcont, b_kcont, st)
+                                              : launch_layout<2, false>(a, batch, a_kcont, b_kcont, st);
+    else     rc = of32 ? launch_layout<1, true>(a, batch, a_kcont, b_kcont, st)
+                       : launch_layout<1, false>(a, batch, a_kcont, b_kcont, st);
     if (rc != VFM_OK || !use_ws) return rc;
     const long long MN = (long long)M * N;
     const int J = reduce_batch ? batch * splits : splits;

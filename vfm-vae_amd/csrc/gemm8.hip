@@ -1,7 +1,12 @@
-// 256 x 256 bf16 GEMM with a 4-phase-per-K-tile LDS-DMA pipeline (the products of csrc/gemm_fast.hip
-// -- frozen-ViT projections, fusion-adapter linears, decoder 1x1 convolutions at batch 32, fp32
-// operands pre-split into a depth-3K bf16 GEMM -- on a deeper schedule):
-//   C[z] = epi(alpha A[z] B[z] + beta C[z]), same contract / epilogue as vfm_gemm_fast.
+// 256 x 256 bf16 GEMM with a 4-phase-per-K-tile LDS-DMA pipeline: the hot path's large products
+// (frozen-ViT projections, fusion-adapter linears, decoder 1x1 convolutions at batch 32):
+//   C[z] = epi(alpha A[z] B[z] + beta C[z]).
+//
+// fp32 operands arrive as bf16 PIECES along K (vfm_split_f32 below: [hi | mid | lo] for the
+// fp32-equivalent f32x6 products, [hi | lo] for the opt-in f32x3 ones), and the kernel walks
+// T x K/64 "virtual" K-tiles: term t multiplies piece Terms<NP>::a(t) of A by piece
+// Terms<NP>::b(t) of B (vfm_common.h), so the 6 (or 3) bf16 products accumulate in the same fp32
+// registers as one GEMM of depth T*K, without duplicated operand copies in HBM.
 //
 // Schedule (cdna_hip_programming.md §5 "The 256² 8-phase template", T2-T5; written from its rules):
 //   * 8 waves as 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 blocks of v_mfma_f32_16x16x32_bf16;
@@ -27,8 +32,8 @@
 //   * LDS images XOR-swizzled on the DMA source address (destination lane-linear): K-contiguous
 //     half-tiles [128 rows][64 k] (128-B rows, chunk ^= (row>>1)&7, ds_read_b128 fragments),
 //     MN-contiguous ones [64 k][128] (256-B rows, gemm.hip's 4x4 chunk swizzle, ds_read_b64_tr_b16);
-//   * XCD-aware bijective block -> tile remap; the epilogue is gemm_fast's (LDS-staged bf16 tile
-//     with 16-B stores when the tile is full).
+//   * XCD-aware bijective block -> tile remap, grouped tile order; bf16 and fp32 epilogues staged
+//     through LDS with 16-B row stores when the tile is full.
 #include "vfm_common.h"
 
 namespace {
@@ -59,6 +64,9 @@ struct G8Args {
     // partials to ws, gemm8_reduce applies the epilogue. ws == null: direct epilogue.
     float* ws;
     int kchunk, S, reduce, Z;
+    // fp32 emulation: T product terms over pieces of Kp columns (rows) each; term t reads piece
+    // (pa >> 2t) & 3 of A and (pb >> 2t) & 3 of B (T = 1, pa = pb = 0 for bf16 operands)
+    int T, Kp, pa, pb;
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -144,9 +152,10 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     const int rows_g = min(GROUP, tiles_m - grp * GROUP);
     const int tm = grp * GROUP + rem % rows_g, tn = rem / rows_g;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int KTz = a.K / BK;                          // K-tiles per batch
+    const int KTz = a.Kp / BK;                         // K-tiles per batch and piece
     const int zo = a.reduce ? 0 : (int)blockIdx.y / a.S, sp = (int)blockIdx.y - zo * a.S;
-    const int V = a.reduce ? a.Z * KTz : KTz;          // virtual K-tiles of this output
+    const int VT = a.reduce ? a.Z * KTz : KTz;         // virtual K-tiles of one product term
+    const int V = a.T * VT;                            // virtual K-tiles of this output
     const int v0 = sp * a.kchunk;
     const int KT = min(V, v0 + a.kchunk) - v0;         // >= 1 by construction of S on the host
     const int z = zo;                                  // output batch
@@ -157,22 +166,38 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
 
-    // half-tile h of local K-tile t into its buffer: h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi (issue order)
-    auto issue = [&](int t, int h) {
-        unsigned char* buf = lds + (t & 1) * BUF;
-        const int v = v0 + t;
-        const int zt = a.reduce ? v / KTz : zo, k0 = (a.reduce ? v - zt * KTz : v) * BK;
-        const __hip_bfloat16* Ab = a.A + (long long)zt * a.sA;
-        const __hip_bfloat16* Bb = a.B + (long long)zt * a.sB;
-        if (h == 0) dma_half<AK, true>(buf + OFF_ALO, Ab, a.lda, m0, a.M, k0, 0, tid);
-        else if (h == 1) dma_half<BKC, false>(buf + OFF_BLO, Bb, a.ldb, n0, a.N, k0, 0, tid);
-        else if (h == 2) dma_half<BKC, false>(buf + OFF_BHI, Bb, a.ldb, n0, a.N, k0, 1, tid);
-        else dma_half<AK, true>(buf + OFF_AHI, Ab, a.lda, m0, a.M, k0, 1, tid);
+    // source of local K-tile t: batch, term -> pieces, k offsets inside each operand (wave-uniform)
+    struct Src {
+        const __hip_bfloat16* Ab;
+        const __hip_bfloat16* Bb;
+        int ka, kb;
     };
-    issue(0, 0);
-    issue(0, 1);
-    issue(0, 2);
-    issue(0, 3);
+    auto src_of = [&](int t) {
+        const int v = v0 + t;
+        const int term = v / VT, rest = v - term * VT;
+        const int zt = a.reduce ? rest / KTz : zo, k0 = (a.reduce ? rest - zt * KTz : rest) * BK;
+        Src r;
+        r.Ab = a.A + (long long)zt * a.sA;
+        r.Bb = a.B + (long long)zt * a.sB;
+        r.ka = k0 + ((a.pa >> (2 * term)) & 3) * a.Kp;
+        r.kb = k0 + ((a.pb >> (2 * term)) & 3) * a.Kp;
+        return r;
+    };
+    // half-tile h of local K-tile t into its buffer: h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi (issue order)
+    auto issue = [&](const Src& sr, int t, int h) {
+        unsigned char* buf = lds + (t & 1) * BUF;
+        if (h == 0) dma_half<AK, true>(buf + OFF_ALO, sr.Ab, a.lda, m0, a.M, sr.ka, 0, tid);
+        else if (h == 1) dma_half<BKC, false>(buf + OFF_BLO, sr.Bb, a.ldb, n0, a.N, sr.kb, 0, tid);
+        else if (h == 2) dma_half<BKC, false>(buf + OFF_BHI, sr.Bb, a.ldb, n0, a.N, sr.kb, 1, tid);
+        else dma_half<AK, true>(buf + OFF_AHI, sr.Ab, a.lda, m0, a.M, sr.ka, 1, tid);
+    };
+    {
+        const Src s0 = src_of(0);
+        issue(s0, 0, 0);
+        issue(s0, 0, 1);
+        issue(s0, 0, 2);
+        issue(s0, 0, 3);
+    }
     VMCNT(4);                                   // A_lo, B_lo of tile 0
     __builtin_amdgcn_s_barrier();
     // ping-pong: the wm = 1 wave-row runs one barrier behind (2 barriers per phase), so one
@@ -183,11 +208,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     for (int t = 0; t < KT; ++t) {
         const unsigned char* buf = lds + (t & 1) * BUF;
         const bool nxt = t + 1 < KT;
+        const Src sn = src_of(nxt ? t + 1 : t);
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int qm = p >> 1;                          // 0 0 1 1
             const int qn = (p == 1 || p == 2) ? 1 : 0;      // 0 1 1 0
-            if (nxt) issue(t + 1, p);
+            if (nxt) issue(sn, t + 1, p);
             // this phase's fragments (A every second phase)
             if (p == 0 || p == 2) {
                 const unsigned char* ai = buf + (qm ? OFF_AHI : OFF_ALO);
@@ -388,28 +414,99 @@ int launch8(const G8Args& a, int batch, hipStream_t st) {
     return launch_status();
 }
 
+// fp32 -> NP bf16 pieces along the reduction dimension (NP = 3: [hi | mid | lo], NP = 2: [hi | lo]).
+//   kcont = 1: src [R][K] (row stride lds_) -> dst [R][NP K]; kcont = 0: src [K][R] -> dst [NP K][R].
+template <int NP>
+__global__ void split_f32_kernel(const float* __restrict__ src, __hip_bfloat16* __restrict__ dst, int R, int K,
+                                 long long lds_, long long sb, long long db, int kcont) {
+    const long long idx4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const long long total = (long long)R * K;
+    if (idx4 >= total) return;
+    const int z = blockIdx.y;
+    const float* s = src + (long long)z * sb;
+    __hip_bfloat16* d = dst + (long long)z * db;
+    // 4 consecutive elements along the contiguous dimension
+    long long r, c, inner;
+    if (kcont) { r = idx4 / K; c = idx4 % K; inner = K; }
+    else       { r = idx4 / R; c = idx4 % R; inner = R; }   // r = k row, c = column
+    const float4 v = *reinterpret_cast<const float4*>(s + r * lds_ + c);
+    uint32_t p01[NP], p23[NP];
+    split_pieces<NP>(v.x, v.y, p01);
+    split_pieces<NP>(v.z, v.w, p23);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        long long off;
+        if (kcont) off = r * ((long long)NP * K) + (long long)p * K + c;
+        else       off = ((long long)p * K + r) * inner + c;
+        *reinterpret_cast<uint2*>(d + off) = make_uint2(p01[p], p23[p]);
+    }
+}
+
 }  // namespace
 
-extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
-                         int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
-                         int kchunk, int reduce_batch, void* stream) {
+extern "C" int vfm_split_f32(const float* src, void* dst, int R, int K, long long ld, long long sb, long long db,
+                             int batch, int precision, int kcont, void* stream) {
+    if (!src || !dst || R <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
+    if (precision != VFM_F32 && precision != VFM_F32X3) return VFM_ERR_ARGS;
+    const int inner = kcont ? K : R;
+    if (inner % 4 || ld % 4 || sb % 4 || ((uintptr_t)src % 16) || ((uintptr_t)dst % 8)) return VFM_NO_KERNEL;
+    const long long total4 = ((long long)R * K) / 4;
+    dim3 grid((unsigned)((total4 + 255) / 256), batch);
+    if (precision == VFM_F32)
+        hipLaunchKernelGGL(split_f32_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, src, (__hip_bfloat16*)dst, R, K,
+                           ld, sb, db, kcont);
+    else
+        hipLaunchKernelGGL(split_f32_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, src, (__hip_bfloat16*)dst, R, K,
+                           ld, sb, db, kcont);
+    return launch_status();
+}
+
+// pieces per fp32 operand (1: bf16 operands) of a precision code, 0 = invalid
+static int pieces_of(int precision) {
+    return precision == VFM_F32 ? 3 : precision == VFM_F32X3 ? 2 : precision == VFM_BF16 ? 1 : 0;
+}
+
+// product terms over np pieces and their packed piece indices (G8Args::T / pa / pb)
+template <int NP>
+static void pack_terms(int& T, int& pa, int& pb) {
+    T = Terms<NP>::N;
+    pa = pb = 0;
+    for (int t = 0; t < T; ++t) {
+        pa |= Terms<NP>::a(t) << (2 * t);
+        pb |= Terms<NP>::b(t) << (2 * t);
+    }
+}
+static void terms_of(int np, int& T, int& pa, int& pb) {
+    if (np == 3) pack_terms<3>(T, pa, pb);
+    else if (np == 2) pack_terms<2>(T, pa, pb);
+    else pack_terms<1>(T, pa, pb);
+}
+
+extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype, int M,
+                         int N, int K, int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb,
+                         long long sB, long long ldc, long long sC, float alpha, float beta, int bias_mode, int act,
+                         float* workspace, int kchunk, int reduce_batch, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
     if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
+    const int np = pieces_of(precision);
+    if (!np) return VFM_ERR_ARGS;
     if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
     if (K % BK) return VFM_NO_KERNEL;
     const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
     if (a_c % 8 || b_c % 8 || lda % 8 || ldb % 8 || sA % 8 || sB % 8) return VFM_NO_KERNEL;
     if (((uintptr_t)A | (uintptr_t)B) % 16) return VFM_NO_KERNEL;
-    if (lda < (a_kcont ? K : M) || ldb < (b_kcont ? K : N) || ldc < N) return VFM_ERR_ARGS;
+    if (lda < (a_kcont ? (long long)np * K : M) || ldb < (b_kcont ? (long long)np * K : N) || ldc < N)
+        return VFM_ERR_ARGS;
     const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
     G8Args a;
+    a.Kp = K;
+    terms_of(np, a.T, a.pa, a.pb);
     a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
     // virtual K-tiles V per output; S = ceil(V / kchunk) splits (kchunk <= 0: one split)
-    const int V = (reduce_batch ? batch : 1) * (K / BK);
+    const int V = a.T * (reduce_batch ? batch : 1) * (K / BK);
     a.Z = batch;
     a.reduce = reduce_batch ? 1 : 0;
     a.kchunk = (kchunk <= 0 || kchunk > V) ? V : kchunk;
@@ -427,10 +524,13 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
 #undef VFM_G8
 }
 
-// fp32 workspace floats vfm_gemm8 needs for (M, N, K, batch, kchunk, reduce_batch); 0 = none
-extern "C" int vfm_gemm8_workspace_floats(int M, int N, int K, int batch, int kchunk, int reduce_batch) {
-    if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || K % BK) return -1;
-    const int V = (reduce_batch ? batch : 1) * (K / BK);
+// fp32 workspace floats vfm_gemm8 needs for (precision, M, N, K, batch, kchunk, reduce_batch); 0 = none
+extern "C" int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk, int reduce_batch) {
+    const int np = pieces_of(precision);
+    if (!np || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || K % BK) return -1;
+    int T, pa, pb;
+    terms_of(np, T, pa, pb);
+    const int V = T * (reduce_batch ? batch : 1) * (K / BK);
     const int kc = (kchunk <= 0 || kchunk > V) ? V : kchunk;
     const int S = (V + kc - 1) / kc;
     if (S <= 1 && !reduce_batch) return 0;

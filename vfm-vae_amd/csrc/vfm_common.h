@@ -40,6 +40,48 @@ __device__ __forceinline__ void split2_bf16(float x0, float x1, uint32_t& hi, ui
     lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(x - h, vfm_bf16x2));
 }
 
+// fp32 pair -> packed bf16 (hi, mid, lo) with x = hi + mid + lo EXACTLY (each remainder is exact in
+// fp32 and the last one has at most 8 significant bits): the operand split of the f32x6 products.
+// A product a.b then runs as the six bf16 products of order >= 2^-16 (hi.hi, hi.mid, mid.hi,
+// hi.lo, mid.mid, lo.hi), each exact in fp32 (|mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|); the three
+// dropped ones (mid.lo, lo.mid, lo.lo) total <= ~2^-23 |a b|, the size of one fp32 rounding.
+__device__ __forceinline__ void split3_bf16(float x0, float x1, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+    const vfm_f2 x = {x0, x1};
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, vfm_bf16x2));
+    const vfm_f2 h = {__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+    const vfm_f2 r1 = x - h;
+    mid = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, vfm_bf16x2));
+    const vfm_f2 m = {__uint_as_float(mid << 16), __uint_as_float(mid & 0xffff0000u)};
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1 - m, vfm_bf16x2));
+}
+
+// Split an fp32 pair into NP packed bf16 pieces (NP = 2: hi, lo; NP = 3: hi, mid, lo).
+template <int NP>
+__device__ __forceinline__ void split_pieces(float x0, float x1, uint32_t* p) {
+    if (NP == 3) split3_bf16(x0, x1, p[0], p[1], p[2]);
+    else split2_bf16(x0, x1, p[0], p[1]);
+}
+
+// Product terms of the fp32 emulation over NP pieces per operand, smallest first (fp32
+// accumulation): NP = 2 ("f32x3"): lo.hi, hi.lo, hi.hi; NP = 3 ("f32x6"): lo.hi, hi.lo, mid.mid,
+// mid.hi, hi.mid, hi.hi. Piece index of operand A / B for term t.
+template <int NP> struct Terms;
+template <> struct Terms<1> {
+    static constexpr int N = 1;
+    __device__ __host__ static constexpr int a(int) { return 0; }
+    __device__ __host__ static constexpr int b(int) { return 0; }
+};
+template <> struct Terms<2> {
+    static constexpr int N = 3;
+    __device__ __host__ static constexpr int a(int t) { return t == 0 ? 1 : 0; }
+    __device__ __host__ static constexpr int b(int t) { return t == 1 ? 1 : 0; }
+};
+template <> struct Terms<3> {
+    static constexpr int N = 6;
+    __device__ __host__ static constexpr int a(int t) { return t == 0 ? 2 : (t == 2 || t == 3) ? 1 : 0; }
+    __device__ __host__ static constexpr int b(int t) { return t == 1 ? 2 : (t == 2 || t == 4) ? 1 : 0; }
+};
+
 // floor(a / b) for b > 0 and any sign of a.
 __device__ __host__ __forceinline__ int floor_div(int a, int b) {
     int q = a / b;

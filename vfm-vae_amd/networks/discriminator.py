@@ -56,9 +56,9 @@ class SpectralConv1d(nn.Conv1d):
             cols = xp.unfold(2, k, 1)                                  # [B, C, L, k]
             L = cols.shape[2]
             x = cols.permute(0, 1, 3, 2).reshape(B, C * k, L)
-        # exact fp32 GEMM (hipBLASLt), not the 3-term bf16 split: the heads' BatchNormLocal over
-        # virtual batches of <= 8 samples amplifies 1e-5-level GEMM rounding into the input
-        # gradient (2.5 % at the 2-sample golden case); these GEMMs are a few GFLOP per step
+        # exact fp32 GEMM (hipBLASLt): the heads' BatchNormLocal over virtual batches of <= 8
+        # samples amplifies GEMM rounding into the input gradient, so these stay on the vendor's
+        # fp32 products; they are a few GFLOP per step
         y = torch.matmul(weight.reshape(O, -1), x)
         if bias is not None:
             y = y + bias.to(y.dtype)[None, :, None]

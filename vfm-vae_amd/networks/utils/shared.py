@@ -117,7 +117,7 @@ class DepthwiseConv2d(nn.Conv2d):
 
 
 class Conv1x1(nn.Conv2d):
-    """nn.Conv2d(I, O, 1) as the decoder's 1x1 GEMM (decoder_ops.pointwise: HIP f32x3 / bf16 MFMA GEMM
+    """nn.Conv2d(I, O, 1) as the decoder's 1x1 GEMM (decoder_ops.pointwise: HIP f32x6 / bf16 MFMA GEMM
     forward, data and weight gradient)."""
 
     def forward(self, x):

@@ -57,11 +57,9 @@ SIGNATURES = {
     "vfm_lpips_head_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_lpips_head_fwd_nhwc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_lpips_head_bwd_nhwc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
-    "vfm_gemm_fast": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
-                      c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
-    "vfm_gemm8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
-                      c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp, c_int, c_int, c_vp],
-    "vfm_gemm8_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "vfm_gemm8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
+                  c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    "vfm_gemm8_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_im2col_nhwc_f32": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_col2im_nhwc_f32": [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_int, c_vp],
@@ -83,22 +81,37 @@ SIGNATURES = {
     "vfm_torgb_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_torgb_bwd_splits": [c_int, c_int, c_int],
     "vfm_torgb_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
-    "vfm_split3": [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp],
+    "vfm_split_f32": [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp],
     "vfm_gemm_workspace_floats": [c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int,
                  c_ll, c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_int, c_int, c_vp],
     "vfm_attention_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp, c_llp, c_float,
                           c_vp],
-    "vfm_conv3x3_nhwc_f32": [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+    "vfm_conv3x3_nhwc_f32": [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_vp],
     "vfm_attention_f32_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp,
-                              c_llp, c_float, c_vp],
+                              c_llp, c_float, c_int, c_vp],
     "vfm_attention_f32_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
-                              c_int, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_float, c_vp],
+                              c_int, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_llp, c_float, c_int, c_vp],
 }
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}
 VFM_NO_KERNEL = -1
+VFM_F32, VFM_BF16, VFM_F32X3 = 0, 2, 4
+
+# Products of fp32 operands on the MFMA paths (GEMMs, the VGG conv, fp32 attention):
+#   "f32x6" (default): three exact bf16 pieces per operand, the six piece products of order
+#           >= 2^-16, fp32 accumulation -- fp32-equivalent (dropped terms <= ~2^-23 relative),
+#           the precision of the reference's fp32 legs (TF32 off, training_loop.py:504-505);
+#   "f32x3" (opt-in, VFM_F32_PRODUCTS=f32x3): hi / lo pieces, three products, ~2^-15.5 relative.
+F32_PRODUCTS = os.environ.get("VFM_F32_PRODUCTS", "f32x6")
+if F32_PRODUCTS not in ("f32x6", "f32x3"):
+    raise ValueError(f"VFM_F32_PRODUCTS must be f32x6 or f32x3, not {F32_PRODUCTS!r}")
+
+
+def f32_precision():
+    """(ABI precision code, piece count, region tag) of the fp32 product mode."""
+    return (VFM_F32, 3, "f32x6") if F32_PRODUCTS == "f32x6" else (VFM_F32X3, 2, "f32x3")
 
 
 class NativeError(RuntimeError):

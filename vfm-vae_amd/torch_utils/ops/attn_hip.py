@@ -56,8 +56,10 @@ def attention_packed(qkv, heads):
 
 # ------------------------------------------------------------------------------------------------
 # fp32 attention with gradients (csrc/attention_f32.hip): the generator's fusion-adapter
-# AttnProjection (reference networks/utils/ldm_utils.py:55-87) and decoder SelfAttention with
-# null key/value (reference networks/utils/gigagan_utils.py:53-91), both fp32 and trained.
+# AttnProjection (reference networks/utils/ldm_utils.py:55-93; encode heads of 64, the decode
+# post_quant's heads of 32) and decoder SelfAttention with null key/value (reference
+# networks/utils/gigagan_utils.py:53-91), both fp32 and trained, and the DINO discriminator
+# tower. fp32-equivalent products (f32x6; f32x3 opt-in, custom_ops.F32_PRODUCTS).
 
 def _s4(t):
     """(batch, token, head) strides of a [B, N, H, d] fp32 view the kernel can read in place."""
@@ -84,10 +86,11 @@ class _Attention32(torch.autograd.Function):
         o = torch.empty(B, Nq, H, d, dtype=torch.float32, device=q.device)
         lse = torch.empty(B, H, Nq, dtype=torch.float32, device=q.device)
         flops = 4 * B * H * Nq * Nk * d
-        with kernel_timer.region(f"attention_fwd<f32x3,{d}>", 4 * (2 * B * Nq * H * d + 2 * B * Nk * H * d), flops,
+        prec, _, tag = custom_ops.f32_precision()
+        with kernel_timer.region(f"attention_fwd<{tag},{d}>", 4 * (2 * B * Nq * H * d + 2 * B * Nk * H * d), flops,
                                  "mfma"):
             rc = _lib.vfm_attention_f32_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
-                                            B, H, Nq, Nk, d, sq, sk, sv, _s4(o), float(d) ** -0.5,
+                                            B, H, Nq, Nk, d, sq, sk, sv, _s4(o), float(d) ** -0.5, prec,
                                             custom_ops.stream_ptr(q.device))
         custom_ops.check(rc, "vfm_attention_f32_fwd")
         ctx.save_for_backward(q, k, v, o, lse)
@@ -104,12 +107,13 @@ class _Attention32(torch.autograd.Function):
         dv = torch.empty(B, Nk, H, d, dtype=torch.float32, device=q.device)
         delta = torch.empty(B, H, Nq, dtype=torch.float32, device=q.device)
         flops = 10 * B * H * Nq * Nk * d          # S and dP recomputed in both passes, dV, dK, dQ
-        with kernel_timer.region(f"attention_bwd<f32x3,{d}>", 4 * 4 * (B * Nq * H * d + B * Nk * H * d), flops,
+        prec, _, tag = custom_ops.f32_precision()
+        with kernel_timer.region(f"attention_bwd<{tag},{d}>", 4 * 4 * (B * Nq * H * d + B * Nk * H * d), flops,
                                  "mfma"):
             rc = _lib.vfm_attention_f32_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(),
                                             lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(),
                                             dv.data_ptr(), B, H, Nq, Nk, d, _s4(q), _s4(k), _s4(v), _s4(o), sdo,
-                                            _s4(dq), _s4(dk), _s4(dv), float(d) ** -0.5,
+                                            _s4(dq), _s4(dk), _s4(dv), float(d) ** -0.5, prec,
                                             custom_ops.stream_ptr(q.device))
         custom_ops.check(rc, "vfm_attention_f32_bwd")
         return dq, dk, dv
@@ -117,13 +121,13 @@ class _Attention32(torch.autograd.Function):
 
 def supported_f32(q, k, v):
     return (q.is_cuda and q.dtype == torch.float32 and k.dtype == torch.float32 and v.dtype == torch.float32
-            and q.shape[-1] == HEAD_DIM and k.shape == v.shape and q.shape[0] == k.shape[0]
+            and q.shape[-1] in (32, HEAD_DIM) and k.shape == v.shape and q.shape[0] == k.shape[0]
             and q.shape[1] == k.shape[1])
 
 
 def sdpa_f32(q, k, v):
-    """F.scaled_dot_product_attention(q, k, v) for fp32 [B, H, N, 64] operands (no mask, default
-    scale), forward and backward on the HIP kernels. Returns [B, H, Nq, 64] (a view of a
+    """F.scaled_dot_product_attention(q, k, v) for fp32 [B, H, N, 64 or 32] operands (no mask, default
+    scale), forward and backward on the HIP kernels. Returns [B, H, Nq, d] (a view of a
     token-major [B, Nq, H, 64] tensor)."""
     o = _Attention32.apply(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2))
     return o.transpose(1, 2)

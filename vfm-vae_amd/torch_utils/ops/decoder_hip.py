@@ -138,8 +138,8 @@ would be baked into the graph and go stale after the next optimizer step)."""
     return wc
 
 
-# Dense products of the decoder on the MFMA GEMM (csrc/gemm.hip: bf16, or fp32 operands as a
-# 3-term bf16 split); VFM_GEMM=torch keeps hipBLASLt (A/B switch). Shapes the kernel does not
+# Dense products of the decoder on the MFMA GEMM (csrc/gemm.hip: bf16, or fp32 operands with
+# fp32-equivalent f32x6 products); VFM_GEMM=torch keeps hipBLASLt (A/B switch). Shapes the kernel does not
 # cover fall back to torch.bmm explicitly.
 _USE_HIP_GEMM = os.environ.get("VFM_GEMM", "hip") != "torch"
 

@@ -3,9 +3,10 @@
 Replaces hipBLASLt (torch.addmm / torch.bmm) on the hot path's dense products: the frozen
 ViT projections (bf16, bias / bias+tanh-GELU epilogue; reference
 networks/utils/vfms/siglip2_utils.py:121), and the fp32 1x1 convolutions / linear layers of
-the decoder and fusion adapter (convnext_utils.py:36-142, gigagan_utils.py:53-185,
-ldm_utils.py:55-166), whose fp32 operands run as three bf16 MFMA products of a hi/lo split
-(`f32x3`, error per product <= ~2^-15.5 relative; csrc/gemm.hip header).
+the decoder, fusion adapter and discriminators (convnext_utils.py:36-142,
+gigagan_utils.py:53-185, ldm_utils.py:55-166), whose fp32 operands run as bf16 MFMA products
+of exact piece splits: `f32x6` (default, fp32-equivalent: six piece products, dropped terms
+<= ~2^-23 relative) or the opt-in `f32x3` (custom_ops.F32_PRODUCTS; csrc/gemm.hip header).
 
 `gemm(A, B, ...)` takes 2-D or batched 3-D views and the layout of each operand, so no
 transposes are materialised. A missing kernel library raises; shapes the kernel does not
@@ -38,48 +39,46 @@ def _layout(t, kdim_last):
     return None
 
 
-FAST = True                 # large-tile LDS-DMA kernel where it applies
-# the 4-phase pipelined form of the large-tile kernel (csrc/gemm8.hip); VFM_GEMM8=0 -> gemm_fast.hip
-GEMM8 = __import__("os").environ.get("VFM_GEMM8", "1") == "1"
+FAST = True                 # large-tile LDS-DMA kernel (csrc/gemm8.hip) where it applies
 SPLIT8 = __import__("os").environ.get("VFM_GEMM8_SPLIT", "0") == "1"
 FAST_MIN_MN = 1 << 18       # below ~256k outputs the 128-tile kernel fills the chip better
 
 
-def _split3(t3, R, K, kc, ld, sb, role, cache, stream):
-    """bf16 [hi|hi|lo] (role 0) / [hi;lo;hi] (role 1) copy of an fp32 operand view t3 [z, R, K]
-    (kc: K-contiguous) -> (tensor, kcont, ld, batch stride) in the split layout; cached on the
+def _split_f32(t3, R, K, kc, ld, sb, cache, stream):
+    """bf16 pieces ([hi | mid | lo] for f32x6, [hi | lo] for f32x3) of an fp32 operand view t3
+    [z, R, K] (kc: K-contiguous) stacked along K -> (tensor, kcont, ld, batch stride); cached on the
     tensor's storage owner until its version moves when `cache` (parameters)."""
+    prec, npc, _ = custom_ops.f32_precision()
     z = t3.shape[0] if sb else 1
     key = None
     if cache:
         base = t3._base if t3._base is not None else t3
-        key = (t3.data_ptr(), tuple(t3.shape), t3.stride(), base._version, role)
-        hit = getattr(base, "_vfm_split3", None)
+        key = (t3.data_ptr(), tuple(t3.shape), t3.stride(), base._version, prec)
+        hit = getattr(base, "_vfm_split_f32", None)
         if hit is not None and hit[0] == key and not torch.cuda.is_current_stream_capturing():
             return hit[1]
     if kc:
-        dst = torch.empty((z, R, 3 * K), dtype=torch.bfloat16, device=t3.device)
-        res = (dst, True, 3 * K, R * 3 * K if sb else 0)
+        dst = torch.empty((z, R, npc * K), dtype=torch.bfloat16, device=t3.device)
+        res = (dst, True, npc * K, R * npc * K if sb else 0)
     else:
-        dst = torch.empty((z, 3 * K, R), dtype=torch.bfloat16, device=t3.device)
-        res = (dst, False, R, 3 * K * R if sb else 0)
-    rc = _lib.vfm_split3(t3.data_ptr(), dst.data_ptr(), R, K, ld, sb, res[3], z, role, int(kc), stream)
+        dst = torch.empty((z, npc * K, R), dtype=torch.bfloat16, device=t3.device)
+        res = (dst, False, R, npc * K * R if sb else 0)
+    rc = _lib.vfm_split_f32(t3.data_ptr(), dst.data_ptr(), R, K, ld, sb, res[3], z, prec, int(kc), stream)
     if rc == custom_ops.VFM_NO_KERNEL:
         return None, None, None, None
-    custom_ops.check(rc, "vfm_split3")
+    custom_ops.check(rc, "vfm_split_f32")
     if key is not None and not torch.cuda.is_current_stream_capturing():
         try:
-            base._vfm_split3 = (key, res)
+            base._vfm_split_f32 = (key, res)
         except AttributeError:
             pass
     return res
 
 
 def preferred(A, M, N, reduce_batch=False):
-    """Where this kernel family beats hipBLASLt (tools_dev/gemmbench.py, MI355X): fp32 operands
-    (the 3-term split runs 1.5-1.9x hipBLASLt's fp32 MFMA GEMMs at >= 128-wide tiles, and the
-    batch-reduced weight gradients at any width). bf16 operands stay on hipBLASLt for now
-    (0.69-0.88 PF/s here vs 1.2-1.45 PF/s)."""
+    """Where this kernel family is routed (tools_dev/gemmbench.py, MI355X): fp32 operands (the
+    fp32-equivalent split at >= 128-wide tiles, and the batch-reduced weight gradients at any
+    width). bf16 operands stay on hipBLASLt (0.69-0.88 PF/s here vs 1.2-1.45 PF/s)."""
     if A.dtype != torch.float32:
         return False
     return reduce_batch or (M >= 128 and N >= 128)
@@ -143,75 +142,83 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     # decoder's batch-reduced weight gradients the 128-tile kernel, which splits fp32 operands in
     # registers, measured faster (0.35 vs 0.40 ms at 2048x512x32x1024: the depth-3K copies cost
     # ~1 GB of HBM traffic per product, tools_dev/gemmbench.py)
-    split8 = (FAST and GEMM8 and SPLIT8 and K % 64 == 0 and min(M, N) >= 256
+    split8 = (FAST and SPLIT8 and K % 64 == 0 and min(M, N) >= 256
               and (reduce_batch or splits > 1 or (auto and -(-M // 256) * -(-N // 256) * z < 256 and K >= 1024)))
     if split8 or (FAST and splits <= 1 and not reduce_batch and K % 64 == 0 and M * N >= FAST_MIN_MN):
-        # large tiles + LDS-DMA pipeline (csrc/gemm_fast.hip); fp32 operands as one bf16 GEMM of
-        # depth 3K over their [hi|hi|lo] x [hi;lo;hi] split
+        # large tiles + LDS-DMA pipeline (csrc/gemm8.hip); fp32 operands as their bf16 pieces
+        # along K, the kernel accumulating the piece products of every K-tile
         if A.dtype == torch.float32:
-            Ak, fa_kc, flda, fsA = _split3(a3, M, K, a_kc, lda, sA, 0, cache_a, stream)
-            Bk, fb_kc, fldb, fsB = _split3(b3, N, K, b_kc, ldb, sB, 1, cache_b, stream)
+            prec, npc, tag = custom_ops.f32_precision()
+            Ak, fa_kc, flda, fsA = _split_f32(a3, M, K, a_kc, lda, sA, cache_a, stream)
+            Bk, fb_kc, fldb, fsB = _split_f32(b3, N, K, b_kc, ldb, sB, cache_b, stream)
             if Ak is None or Bk is None:
                 Ak = None
-            Kf = 3 * K
+            nterm = 6 if npc == 3 else 3
         else:
-            Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB, Kf = a3, a_kc, lda, sA, b3, b_kc, ldb, sB, K
+            prec, tag, nterm = custom_ops.VFM_BF16, "bf16", 1
+            Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB = a3, a_kc, lda, sA, b3, b_kc, ldb, sB
         if Ak is not None:
-            tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
             tb = lambda v: "true" if v else "false"
-            args = (Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype], M, N, Kf,
-                    z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta), bias_mode,
-                    ACTS[act])
+            args = (Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), prec, _CODES[out_dtype], M,
+                    N, K, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta),
+                    bias_mode, ACTS[act])
             if split8:
                 zo = 1 if reduce_batch else z
-                V = (z if reduce_batch else 1) * (Kf // 64)
+                V = nterm * (z if reduce_batch else 1) * (K // 64)
                 S0 = max(1, -(-512 // (-(-M // 256) * -(-N // 256) * zo)))
                 kchunk = max(4, -(-V // S0))
-                n = _lib.vfm_gemm8_workspace_floats(M, N, Kf, z, kchunk, int(reduce_batch))
+                n = _lib.vfm_gemm8_workspace_floats(prec, M, N, K, z, kchunk, int(reduce_batch))
                 ws = torch.empty(max(n, 0), dtype=torch.float32, device=A.device) if n > 0 else None
                 region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
                 if kernel_timer.SHAPES:
                     region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}k{kchunk}]"
-                with kernel_timer.region(region, 0, flops, "mfma"):
+                with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch), flops, "mfma"):
                     rc = _lib.vfm_gemm8(*args, custom_ops.ptr(ws), kchunk, int(reduce_batch), stream)
                 if rc != custom_ops.VFM_NO_KERNEL:
                     custom_ops.check(rc, "vfm_gemm8")
                     return out
         if Ak is not None and not split8:
             # one timer region per kernel instantiation (rocprof: gemm8_kernel<AK, BK, OUTF32>)
-            kname = "gemm8" if GEMM8 else "gemm_fast"
-            region = f"{kname}<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
+            region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
             if kernel_timer.SHAPES:
                 region += f"[{M}x{N}x{K}x{z}]"
-            with kernel_timer.region(region, 0, flops, "mfma"):
-                if GEMM8:
-                    rc = _lib.vfm_gemm8(*args, None, 0, 0, stream)
-                else:
-                    rc = _lib.vfm_gemm_fast(*args, stream)
+            with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch), flops, "mfma"):
+                rc = _lib.vfm_gemm8(*args, None, 0, 0, stream)
             if rc != custom_ops.VFM_NO_KERNEL:
-                custom_ops.check(rc, "vfm_gemm_fast")
+                custom_ops.check(rc, "vfm_gemm8")
                 return out
     ws = None
     if splits > 1 or reduce_batch:
         n = _lib.vfm_gemm_workspace_floats(M, N, z, splits, int(reduce_batch))
         ws = torch.empty(n, dtype=torch.float32, device=A.device)
-    tag = "bf16" if A.dtype == torch.bfloat16 else "f32x3"
+    if A.dtype == torch.bfloat16:
+        in_code, tag = custom_ops.VFM_BF16, "bf16"
+    else:
+        in_code, _, tag = custom_ops.f32_precision()
     tb = lambda v: "true" if v else "false"
-    # one region per gemm_kernel<AK, BK, F32, OUTF32> instantiation; split-K / batch-reduced
+    # one region per gemm_kernel<AK, BK, NP, OUTF32> instantiation; split-K / batch-reduced
     # launches (kernel + gemm_reduce_kernel) are their own region
     kname = "gemm_ws" if ws is not None else "gemm"
     region = f"{kname}<{tag},{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
     if kernel_timer.SHAPES:
         region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
-    with kernel_timer.region(region, 0, flops, "mfma"):
+    with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch), flops, "mfma"):
         rc = _lib.vfm_gemm(A.data_ptr(), B.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(ws),
-                           _CODES[A.dtype], _CODES[out_dtype], M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB,
+                           in_code, _CODES[out_dtype], M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB,
                            ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], int(splits), int(reduce_batch),
                            custom_ops.stream_ptr(A.device))
     if rc == custom_ops.VFM_NO_KERNEL:
         return None
     custom_ops.check(rc, "vfm_gemm")
     return out
+
+
+def gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch=False):
+    """Algorithmic HBM bytes of one product: A, B and C once each at their own element size (a
+    batch-shared operand -- leading extent 1 -- counted once)."""
+    e = a3.element_size()
+    eo = 4 if out_dtype == torch.float32 else 2
+    return int((a3.shape[0] * M * K + b3.shape[0] * K * N) * e + (1 if reduce_batch else z) * M * N * eo)
 
 
 def gemm(A, B, **kw):

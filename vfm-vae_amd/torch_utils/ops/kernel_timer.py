@@ -121,8 +121,9 @@ _ROC = {
     "shuffle_blur_fwd": "blur_fwd<{T}, 2, {K}>", "shuffle_blur_bwd": "blur_bwd<{T}, 2, {K}>",
     "residual_layer_norm": "ln_rows<", "codebook_argmax": "codebook_argmax_kernel<",
     "convnext_mlp_fwd": "mlp_fwd<", "pw_gemm_gelu_bwd": "pw_gemm_gelu<1, ",
-    "conv3x3_nhwc": "conv3x3_kernel<{K}>", "attention_fwd": "attn_fwd_d64",
+    "attention_fwd": "attn_fwd_d64",
 }
+_NP = {"f32x6": 3, "f32x3": 2, "bf16": 1}
 _TNAME = {"f32": "float", "bf16": "__hip_bfloat16", "f16": "__half", "f64": "double"}
 
 
@@ -131,11 +132,15 @@ def rocprof_name(region):
     region = region.split("[", 1)[0]
     base, _, args = region.partition("<")
     args = args.rstrip(">").split(",") if args else []
-    if base in ("gemm8", "gemm_fast") and len(args) == 4:      # <tag, AK, BK, OUTF32>
-        return f"{base}_kernel<{args[1]}, {args[2]}, {args[3]}>"
-    if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, F32, OUTF32>
-        f32 = "true" if args[0] == "f32x3" else "false"
-        return f"gemm_kernel<{args[1]}, {args[2]}, {f32}, {args[3]}>"
+    if base == "gemm8" and len(args) == 4:                     # <tag, AK, BK, OUTF32>
+        return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}>"
+    if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32>
+        return f"gemm_kernel<{args[1]}, {args[2]}, {_NP.get(args[0], 1)}, {args[3]}>"
+    if base == "conv3x3_nhwc" and len(args) == 2:              # conv3x3_kernel<BN, NP>
+        return f"conv3x3_kernel<{args[1]}, {_NP.get(args[0], 3)}>"
+    if base in ("attention_fwd", "attention_bwd") and args and args[0] in ("f32x6", "f32x3"):
+        np_ = _NP[args[0]]
+        return f"attn32_fwd<{np_}>" if base == "attention_fwd" else f"attn32_dkdv<{np_}>"
     if base == "convnext_mlp_fwd" and len(args) == 3:          # mlp_fwd<C, SAVE>
         return f"mlp_fwd<{args[1]}, {args[2]}>"
     pat = _ROC.get(base)
@@ -156,11 +161,14 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None):
     if r["bound"] == "mfma":
         achieved = r["flops"] / t / 1e12
         peak, unit = mfma_peak_tflops, "TFLOP/s"
-        if "f32x3" in name:
-            # fp32 products as 3 bf16 MFMAs (hi.hi + hi.lo + lo.hi): the fp32 rate this path can
-            # reach is the dense bf16 peak / 3 (the fp32 MFMA peak is 157.3 TF/s)
+        if "f32x6" in name:
+            # fp32-equivalent products as 6 bf16 MFMAs over exact 3-piece splits: the fp32 rate this
+            # path can reach is the dense bf16 peak / 6 (the fp32 MFMA peak is 157.3 TF/s)
+            peak = round(mfma_peak_tflops / 6, 1)
+            note = "achieved = fp32 FLOPs of the op / time; peak = dense bf16 MFMA peak / 6 (f32x6 split)"
+        elif "f32x3" in name:
             peak = round(mfma_peak_tflops / 3, 1)
-            note = "achieved = fp32 FLOPs of the op / time; peak = dense bf16 MFMA peak / 3 (3-term split)"
+            note = "achieved = fp32 FLOPs of the op / time; peak = dense bf16 MFMA peak / 3 (opt-in f32x3 split)"
     else:
         achieved = r["bytes"] / t / 1e9
         peak, unit = hbm_peak_gbs, "GB/s"

@@ -5,7 +5,7 @@ PlainAttention.qkv / proj, AttnProjectionBlock.proj, GeGluMlp w0/w1/w2; fp32, ou
 autocast) and the frozen DINO ViT-S of the projected discriminator (discriminator.py:145-168,
 fp32, gradients w.r.t. its input only). `Linear` is a drop-in nn.Linear subclass (same
 parameters and state-dict keys); on ROCm tensors its forward and backward products run on
-the HIP GEMM (fp32 operands as the 3-term bf16 split, csrc/gemm.hip), elsewhere F.linear.
+the HIP GEMM (fp32 operands as the fp32-equivalent f32x6 split, csrc/gemm.hip), elsewhere F.linear.
 
   forward   y  = x W^T + b            (bias in the GEMM epilogue)
   backward  dx = dy W,  dW = dy^T x (fp32),  db = sum dy

@@ -2,7 +2,7 @@
 networks/discriminator.py:75-99 BatchNormLocal2d, :180-228 NLayerDiscriminator).
 
 Activations are NHWC fp32 (channels_last views of the reference's NCHW tensors). A k4 conv is
-im2col (csrc/patchgan.hip) + our MFMA GEMM (gemm_hip, fp32 through the 3-term bf16 split) with the
+im2col (csrc/patchgan.hip) + our MFMA GEMM (gemm_hip, fp32-equivalent f32x6 products) with the
 bias fused into the GEMM epilogue; its weight gradient is the same GEMM (split-K over the pixels) and
 its data gradient a GEMM followed by the col2im gather. The 1-channel logit layer uses a row dot /
 column dot instead of a 1-wide GEMM. BatchNormLocal2d + LeakyReLU(0.2) run as one fused forward and

@@ -2,8 +2,8 @@
 
 Replaces the torchvision `vgg16().features[:30]` forward/backward of the reference's LPIPS
 (training/lpips.py:126-163; MIOpen fp32 Winograd on ROCm) with 13 fused conv3x3 + bias + ReLU
-launches on NHWC fp32 activations (fp32 products through the 3-term bf16 split, error per
-product <= ~2^-15.5 relative), torch max-pool on the channels_last views, and a backward that
+launches on NHWC fp32 activations (fp32-equivalent products through the f32x6 bf16 split, the
+f32x3 split opt-in: custom_ops.F32_PRODUCTS), torch max-pool on the channels_last views, and a backward that
 runs the data gradients on the same kernel with flipped/transposed weights, the ReLU derivative
 of the layer below fused into the epilogue where no pool sits in between. VGG is frozen: no
 weight gradients.
@@ -40,33 +40,40 @@ def _plan():
 PLAN = _plan()
 
 
-def split_weight(w2d):
-    """fp32 [Cout, K] tap-major weights -> (hi, lo) bf16 [Cout, Kp] (Kp = K rounded up to 64, zero
-    padded): hi = bf16(w), lo = bf16(w - hi), round-to-nearest as the kernels' own split."""
+def split_weight(w2d, npieces=None):
+    """fp32 [Cout, K] tap-major weights -> bf16 pieces [np, Cout, Kp] (Kp = K rounded up to 64, zero
+    padded): np = 3: hi = bf16(w), mid = bf16(w - hi), lo = bf16(w - hi - mid) (w = hi + mid + lo
+    exactly); np = 2: hi, lo -- round-to-nearest, as the kernels' own split."""
+    npieces = npieces or custom_ops.f32_precision()[1]
     Cout, K = w2d.shape
     Kp = -(-K // 64) * 64
-    wp = torch.zeros(Cout, Kp, dtype=torch.float32, device=w2d.device)
-    wp[:, :K] = w2d
-    hi = wp.to(torch.bfloat16)
-    lo = (wp - hi.float()).to(torch.bfloat16)
-    return hi.contiguous(), lo.contiguous()
+    r = torch.zeros(Cout, Kp, dtype=torch.float32, device=w2d.device)
+    r[:, :K] = w2d
+    out = torch.empty(npieces, Cout, Kp, dtype=torch.bfloat16, device=w2d.device)
+    for p in range(npieces):
+        out[p] = r.to(torch.bfloat16)
+        r = r - out[p].float()
+    return out
 
 
 def conv3x3(x, w, bias=None, relu=False, mask=None):
-    """x: NHWC fp32 [B, H, W, Cin] contiguous; w: (hi, lo) from split_weight of the [Cout, 9*Cin]
-    tap-major weights -> [B, H, W, Cout] = relu?(conv(x) + bias) (x (mask > 0) when given)."""
+    """x: NHWC fp32 [B, H, W, Cin] contiguous; w: [np, Cout, Kp] pieces from split_weight of the
+    [Cout, 9*Cin] tap-major weights -> [B, H, W, Cout] = relu?(conv(x) + bias) (x (mask > 0) when
+    given)."""
     B, H, W, Cin = x.shape
-    wh, wl = w
-    Cout = wh.shape[0]
-    if not x.is_contiguous() or wh.shape[1] < 9 * Cin or (mask is not None and mask.shape != (B, H, W, Cout)):
-        raise RuntimeError("conv3x3: NHWC contiguous input, split [Cout, >= 9*Cin] weights, mask of the output shape")
+    npc, Cout, Kp = w.shape
+    prec, np_mode, tag = custom_ops.f32_precision()
+    if npc != np_mode:
+        raise RuntimeError(f"conv3x3: weights split into {npc} pieces, the {tag} mode needs {np_mode}")
+    if not x.is_contiguous() or Kp < 9 * Cin or (mask is not None and mask.shape != (B, H, W, Cout)):
+        raise RuntimeError("conv3x3: NHWC contiguous input, split [np, Cout, >= 9*Cin] weights, mask of the output shape")
     out = torch.empty(B, H, W, Cout, dtype=torch.float32, device=x.device)
     flops = 2 * B * H * W * Cout * 9 * Cin
     # one timer region per kernel instantiation (BN = 128 / 64 output channels per tile), as
-    # rocprofv3 names them: conv3x3_kernel<128> / <64>
-    with kernel_timer.region(f"conv3x3_nhwc<f32x3,{128 if Cout % 128 == 0 else 64}>",
+    # rocprofv3 names them: conv3x3_kernel<128, NP> / <64, NP>
+    with kernel_timer.region(f"conv3x3_nhwc<{tag},{128 if Cout % 128 == 0 else 64}>",
                              4 * (x.numel() + out.numel() + Cout * 9 * Cin), flops, "mfma"):
-        rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), wh.data_ptr(), wl.data_ptr(), wh.shape[1], custom_ops.ptr(bias),
+        rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), w.data_ptr(), prec, Kp, custom_ops.ptr(bias),
                                        custom_ops.ptr(mask), out.data_ptr(), B, H, W, Cin, Cout, int(relu),
                                        custom_ops.stream_ptr(x.device))
     custom_ops.check(rc, "vfm_conv3x3_nhwc_f32")
@@ -75,11 +82,11 @@ def conv3x3(x, w, bias=None, relu=False, mask=None):
 
 def prepare(convs):
     """Per nn.Conv2d: forward weights [Cout, 9*Cin'] (Cin' = Cin padded to 4 for the image layer),
-    data-gradient weights [Cin, 9*Cout] (flipped taps) -- both as split_weight (hi, lo) pairs --, bias
-    and the fp32 weight; cached on the module until the weight's version moves."""
+    data-gradient weights [Cin, 9*Cout] (flipped taps) -- both as split_weight pieces --, bias and
+    the fp32 weight; cached on the module until the weight's version (or the product mode) moves."""
     out = []
     for m in convs:
-        key = (m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version)
+        key = (m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version, custom_ops.F32_PRODUCTS)
         hit = getattr(m, "_vfm_vgg_prep", None)
         if hit is None or hit[0] != key:
             w = m.weight.detach().float()

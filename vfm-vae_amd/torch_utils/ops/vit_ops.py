@@ -5,11 +5,13 @@ Reference math: HF `SiglipEncoderLayer` / timm `Block` as used by
 under bf16 autocast: GEMMs in the compute dtype with fp32 accumulation,
 LayerNorm and residual stream in fp32.
 
-GEMMs are plain library GEMMs (hipBLASLt through torch.matmul, MFMA). On ROCm
-tensors outside autograd (the frozen towers), fc1's bias + tanh-GELU runs as the
-hipBLASLt GELU_BIAS epilogue (torch._addmm_activation, the tanh form SigLIP
-uses), and LayerNorm -> compute dtype (optionally fused with the residual add)
-is one HIP row kernel (`vit_hip`, csrc/vit.hip).
+bf16 GEMMs (the SigLIP2 tower under autocast) are library GEMMs (hipBLASLt through
+torch.matmul, MFMA); on ROCm tensors outside autograd fc1's bias + tanh-GELU runs as
+the hipBLASLt GELU_BIAS epilogue (torch._addmm_activation, the tanh form SigLIP uses).
+fp32 linears (the DINO ViT-S tower of the projected discriminator, whose input gradient
+the G phase takes) run on our GEMM with fp32-equivalent f32x6 products and autograd
+(torch_utils/ops/linear.py). LayerNorm -> compute dtype (optionally fused with the
+residual add) is one HIP row kernel (`vit_hip`, csrc/vit.hip).
 """
 import torch
 import torch.nn.functional as F
@@ -35,6 +37,9 @@ def patch_embed(pixels, weight, bias, patch, compute_dtype):
 
 def linear(x, w, b=None):
     """x @ w^T + b in x's dtype (bias added in fp32 then rounded)."""
+    if x.is_cuda and x.dtype == torch.float32:
+        from . import linear as linear_op
+        return linear_op.linear(x, w, b)
     if b is not None:
         return torch.addmm(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
     return torch.matmul(x, w.t())
