@@ -104,6 +104,16 @@ __device__ __forceinline__ f32x16 mfmaN(const Frag<NP>& a, const Frag<NP>& b, f3
     return c;
 }
 
+// the same with the smaller piece products into their own accumulator cs and hi.hi alone into c
+// (for the long reductions over keys / queries: full-magnitude roundings as in an fp32 GEMM of
+// exact products; cs is added once at the end)
+template <int NP>
+__device__ __forceinline__ void mfmaN2(const Frag<NP>& a, const Frag<NP>& b, f32x16& c, f32x16& cs) {
+#pragma unroll
+    for (int t = 0; t < Terms<NP>::N - 1; ++t) cs = mfma(a.p[Terms<NP>::a(t)], b.p[Terms<NP>::b(t)], cs);
+    c = mfma(a.p[0], b.p[0], c);
+}
+
 // A operand, rows of the tile images (piece p at img + p IMG): row `row`, k = d = 16s + 8hh .. +7
 template <int NP>
 __device__ __forceinline__ Frag<NP> rd_row(const unsigned char* img, int row, int s, int hh) {
@@ -218,7 +228,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
     load_fixed<NP>(a.q + (long long)b * a.sq.b + (long long)h * a.sq.h, a.sq.n, q_row, Nq, hd, hh, qf);
 
     Stage sk, sv;
-    f32x16 oacc[2] = {f32x16{}, f32x16{}};
+    f32x16 oacc[2] = {f32x16{}, f32x16{}}, oaccs[2] = {f32x16{}, f32x16{}};
     float m_run = -INFINITY, l_run = 0.f;
     const float c = a.c;
     const int T = (Nk + TT - 1) / TT;
@@ -270,6 +280,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
         for (int i = 0; i < 16; ++i) {
             oacc[0][i] *= alpha;
             oacc[1][i] *= alpha;
+            oaccs[0][i] *= alpha;
+            oaccs[1][i] *= alpha;
         }
 #pragma unroll
         for (int kbk = 0; kbk < 2; ++kbk) {
@@ -277,10 +289,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
 #pragma unroll
             for (int s = 0; s < 2; ++s)
 #pragma unroll
-                for (int db = 0; db < 2; ++db) oacc[db] = mfmaN<NP>(rd_tr<NP>(vimg, tl, kbk, s, db), pf[s], oacc[db]);
+                for (int db = 0; db < 2; ++db) mfmaN2<NP>(rd_tr<NP>(vimg, tl, kbk, s, db), pf[s], oacc[db], oaccs[db]);
         }
         __syncthreads();
     }
+    oacc[0] += oaccs[0];
+    oacc[1] += oaccs[1];
     const float l = l_run + xchg32(l_run);
     if (q_row < Nq) {
         store_tr(a.out + (long long)b * a.so.b + (long long)q_row * a.so.n + (long long)h * a.so.h, oacc, hh, 1.f / l,
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(64 * WAVES, NP == 3 ? 1 : 2) void attn32_dq(Args a)
     const float dlt = q_row < Nq ? a.delta[rix] : 0.f;
 
     Stage sk, sv;
-    f32x16 dq[2] = {f32x16{}, f32x16{}};
+    f32x16 dq[2] = {f32x16{}, f32x16{}}, dqs[2] = {f32x16{}, f32x16{}};
     const float c = a.c;
     const int T = (Nk + TT - 1) / TT;
     stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
@@ -362,10 +376,12 @@ __global__ __launch_bounds__(64 * WAVES, NP == 3 ? 1 : 2) void attn32_dq(Args a)
 #pragma unroll
             for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int db = 0; db < 2; ++db) dq[db] = mfmaN<NP>(rd_tr<NP>(kimg, tl, kbk, st, db), df[st], dq[db]);
+                for (int db = 0; db < 2; ++db) mfmaN2<NP>(rd_tr<NP>(kimg, tl, kbk, st, db), df[st], dq[db], dqs[db]);
         }
         __syncthreads();
     }
+    dq[0] += dqs[0];
+    dq[1] += dqs[1];
     if (q_row < Nq)
         store_tr(a.dq + (long long)b * a.sdq.b + (long long)q_row * a.sdq.n + (long long)h * a.sdq.h, dq, hh, a.scale,
                  hd);
@@ -405,6 +421,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
         }
     };
     f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+    f32x16 dks[2] = {f32x16{}, f32x16{}}, dvs[2] = {f32x16{}, f32x16{}};
     const float c = a.c;
     const int T = (Nq + TT - 1) / TT;
     load_rows(0);
@@ -445,11 +462,16 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
             for (int st = 0; st < 2; ++st)
 #pragma unroll
                 for (int d = 0; d < 2; ++d) {
-                    dv[d] = mfmaN<NP>(rd_tr<NP>(oimg, tl, qbk, st, d), pf[st], dv[d]);
-                    dk[d] = mfmaN<NP>(rd_tr<NP>(qimg, tl, qbk, st, d), df[st], dk[d]);
+                    mfmaN2<NP>(rd_tr<NP>(oimg, tl, qbk, st, d), pf[st], dv[d], dvs[d]);
+                    mfmaN2<NP>(rd_tr<NP>(qimg, tl, qbk, st, d), df[st], dk[d], dks[d]);
                 }
         }
         __syncthreads();
+    }
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        dk[d] += dks[d];
+        dv[d] += dvs[d];
     }
     if (key < Nk) {
         store_tr(a.dk + (long long)b * a.sdk.b + (long long)key * a.sdk.n + (long long)h * a.sdk.h, dk, hh, a.scale, hd);

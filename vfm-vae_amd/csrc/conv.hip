@@ -181,11 +181,11 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
     sa.init(a, m0, tid);
     sa.cur_tap = -1;
     const bool wide = a.lc >= 6;                        // Cin >= 64 (uniform)
-    f32x16 acc[2][NJ];
+    f32x16 acc[2][NJ], accs[2][NJ];             // hi.hi products / the smaller piece products
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = accs[i][j] = f32x16{};
 
     if (wide) sa.load_wide(a, 0, tid);
     else sa.load(a, 0, tid);
@@ -209,17 +209,26 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) bf[p][j] = frag(b_img + p * IMG_B, NJ * wn + j, s, lane);
             }
+            // small piece products into their own accumulator (rounded at their own ~2^-8 scale),
+            // hi.hi alone into acc: as many full-magnitude roundings as an fp32 GEMM of exact products
 #pragma unroll
             for (int t = 0; t < Terms<NP>::N; ++t)
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i], bf[Terms<NP>::b(t)][j],
-                                                                            acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < NJ; ++j) {
+                        f32x16& c = (t == Terms<NP>::N - 1) ? acc[i][j] : accs[i][j];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i], bf[Terms<NP>::b(t)][j], c,
+                                                                    0, 0, 0);
+                    }
         }
         __syncthreads();
     }
+
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] += accs[i][j];
 
     // acc[i][j][e] = out[m][n], m = m0 + 64wm + 32i + (e&3) + 8(e>>2) + 4hh, n = n0 + 32(NJ wn + j) + r
     const int r = lane & 31, hh = lane >> 5;

@@ -171,11 +171,11 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
 
     Stage<AK, NP> sa;
     Stage<BKC, NP> sb;
-    f32x16 acc[2][2];
+    f32x16 acc[2][2], accs[2][2];              // hi.hi products / the smaller piece products (NP > 1)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+        for (int j = 0; j < 2; ++j) acc[i][j] = accs[i][j] = f32x16{};
 
     sa.load(Ab, a.lda, m0, kbeg, a.M, kend, tid);
     sb.load(Bb, a.ldb, n0, kbeg, a.N, kend, tid);
@@ -197,17 +197,28 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
 #pragma unroll
                 for (int j = 0; j < 2; ++j) bfr[p][j] = frag<BKC>(b_img + p * IMG, 2 * wn + j, s, lane);
             }
-            // the piece products, smallest first (Terms<NP>)
+            // the piece products (Terms<NP>): the smaller ones into their own accumulator (rounded
+            // at their ~2^-8 scale), hi.hi alone into acc -- as many full-magnitude roundings as an
+            // fp32 GEMM of exact products
 #pragma unroll
             for (int t = 0; t < Terms<NP>::N; ++t)
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i],
-                                                                            bfr[Terms<NP>::b(t)][j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 2; ++j) {
+                        f32x16& c = (t == Terms<NP>::N - 1) ? acc[i][j] : accs[i][j];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i], bfr[Terms<NP>::b(t)][j], c,
+                                                                    0, 0, 0);
+                    }
         }
         __syncthreads();
+    }
+
+    if (F32) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] += accs[i][j];
     }
 
     // ---- epilogue: acc[i][j][e] = C[m][n], m = m0 + 64wm + 32i + (e&3) + 8(e>>2) + 4hh, n = n0 + 64wn + 32j + r
