@@ -60,6 +60,7 @@ for s in "$@"; do
     gc1)     REUSE=1 timeout -k 10 400 python tools_dev/graph_c1_debug.py > $out/gc1.log 2>&1; REUSE=0 timeout -k 10 400 python tools_dev/graph_c1_debug.py >> $out/gc1.log 2>&1 ;;
     gc2)     REUSE=0 timeout -k 10 400 python tools_dev/graph_c1_debug2.py > $out/gc2.log 2>&1; REUSE=1 timeout -k 10 400 python tools_dev/graph_c1_debug2.py >> $out/gc2.log 2>&1 ;;
     gemmbench) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;
+    gemm6bench) timeout -k 10 300 python tools_dev/gemm6bench.py > $out/gemm6bench.log 2>&1 ;;
     gc3)     timeout -k 10 400 python tools_dev/graph_c1_debug3.py > $out/gc3.log 2>&1 ;;
     gc4)     HOOKS=1 timeout -k 10 400 python tools_dev/graph_c1_debug4.py > $out/gc4.log 2>&1; HOOKS=0 timeout -k 10 400 python tools_dev/graph_c1_debug4.py >> $out/gc4.log 2>&1 ;;
     gc5)     for cfg in "PART=mapping" "PART=ldm_adapter" "PART=synthesis" "PART=synthesis NO_CUDNN=1" "PART=synthesis SDPA_MATH=1" "PART=synthesis NO_CUDNN=1 SDPA_MATH=1"; do

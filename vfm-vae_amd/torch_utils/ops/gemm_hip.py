@@ -84,12 +84,42 @@ def preferred(A, M, N, reduce_batch=False):
     return reduce_batch or (M >= 128 and N >= 128)
 
 
+def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
+    """Kernel and split of one product: ("g8", kchunk) -- the 256-tile kernel, kchunk virtual
+    K-tiles per split (0: no split) -- or ("g128", splits) -- the 128-tile kernel."""
+    if not FAST or K % 64:
+        return "g128", splits
+    nterm = 1 if dtype == torch.bfloat16 else (6 if custom_ops.f32_precision()[1] == 3 else 3)
+    zo = 1 if reduce_batch else z
+    V = nterm * (z if reduce_batch else 1) * (K // 64)            # virtual K-tiles per output
+    tiles = -(-M // 256) * -(-N // 256) * zo
+    if reduce_batch or splits > 1:
+        if not (SPLIT8 and min(M, N) >= 256):
+            return "g128", splits
+        S0 = max(1, -(-512 // tiles))
+        return "g8", max(4, -(-V // S0))
+    if M * N < FAST_MIN_MN:
+        return "g128", splits
+    if auto and tiles < SPLIT_TILES and V >= 2 * SPLIT_MIN_VT:
+        # few 256-tiles (token-major linears with a small output width, e.g. the DINO tower's
+        # 6304 x 384 products): split the virtual K-tiles so ~384 workgroups run
+        S = min(-(-384 // tiles), V // SPLIT_MIN_VT)
+        if S > 1:
+            return "g8", -(-V // S)
+    return "g8", 0
+
+
+SPLIT_TILES = 160           # fewer 256-tiles than this: split-K on the 256-tile kernel (auto routing)
+SPLIT_MIN_VT = 8            # at least this many virtual K-tiles per split
+
+
 def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=0.0, out_dtype=None,
-             splits=1, reduce_batch=False, cache_a=False, cache_b=False, auto=False):
+             splits=1, reduce_batch=False, cache_a=False, cache_b=False, auto=False, route=None):
     """C = epi(alpha * A @ B + beta * out). A: [M, K] or [z, M, K]; B: [K, N] or [z, K, N]
     (any strides with one unit-stride dim each). bias: fp32 [N] (bias_dim=1) or [M]
     (bias_dim=0). Returns C ([M, N] / [z, M, N], or [M, N] when reduce_batch sums over z),
-    or None when the kernel does not cover the shapes/strides."""
+    or None when the kernel does not cover the shapes/strides. `route` forces a plan
+    (("g8", kchunk) / ("g128", splits): microbenchmarks)."""
     if A.dtype != B.dtype or A.dtype not in _CODES or not A.is_cuda:
         return None
     a3 = A if A.dim() == 3 else A.unsqueeze(0)
@@ -105,9 +135,8 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         return None
     if auto and splits == 1:
         # few output tiles over a deep reduction (weight gradients of token-major linears):
-        # split K so the grid covers the 256 CUs several times
-        z0 = max(a3.shape[0], b3.shape[0]) if not reduce_batch else max(a3.shape[0], b3.shape[0])
-        tiles = -(-M // 128) * -(-N // 128) * z0
+        # split K so the grid covers the 256 CUs several times (128-tile kernel)
+        tiles = -(-M // 128) * -(-N // 128) * z
         if tiles < 512 and K >= 2048:
             splits = max(1, min(-(-1024 // tiles), K // 512, 64))
     la = _layout(a3, True)                       # A rows = m, cols = k
@@ -136,57 +165,43 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         bias = bias.detach().float().contiguous()
         bias_mode = 1 if bias_dim in (None, 1) else 2
     flops = 2.0 * z * M * N * K
+    nbytes = gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch)
     stream = custom_ops.stream_ptr(A.device)
-    # split-K / batch-reduced products on the large-tile kernel (weight gradients: few output
-    # tiles over a deep reduction): chunks of >= 4 K-tiles, ~512 workgroups. Opt-in: for the
-    # decoder's batch-reduced weight gradients the 128-tile kernel, which splits fp32 operands in
-    # registers, measured faster (0.35 vs 0.40 ms at 2048x512x32x1024: the depth-3K copies cost
-    # ~1 GB of HBM traffic per product, tools_dev/gemmbench.py)
-    split8 = (FAST and SPLIT8 and K % 64 == 0 and min(M, N) >= 256
-              and (reduce_batch or splits > 1 or (auto and -(-M // 256) * -(-N // 256) * z < 256 and K >= 1024)))
-    if split8 or (FAST and splits <= 1 and not reduce_batch and K % 64 == 0 and M * N >= FAST_MIN_MN):
-        # large tiles + LDS-DMA pipeline (csrc/gemm8.hip); fp32 operands as their bf16 pieces
-        # along K, the kernel accumulating the piece products of every K-tile
+    kern, arg = route or _plan(A.dtype, M, N, K, z, reduce_batch, splits, auto)
+    tb = lambda v: "true" if v else "false"
+    if kern == "g8":
+        # 256 tiles + LDS-DMA pipeline (csrc/gemm8.hip); fp32 operands as their bf16 pieces along
+        # K, the kernel accumulating the piece products of every K-tile
         if A.dtype == torch.float32:
-            prec, npc, tag = custom_ops.f32_precision()
+            prec, _, tag = custom_ops.f32_precision()
             Ak, fa_kc, flda, fsA = _split_f32(a3, M, K, a_kc, lda, sA, cache_a, stream)
             Bk, fb_kc, fldb, fsB = _split_f32(b3, N, K, b_kc, ldb, sB, cache_b, stream)
-            if Ak is None or Bk is None:
-                Ak = None
-            nterm = 6 if npc == 3 else 3
         else:
-            prec, tag, nterm = custom_ops.VFM_BF16, "bf16", 1
+            prec, tag = custom_ops.VFM_BF16, "bf16"
             Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB = a3, a_kc, lda, sA, b3, b_kc, ldb, sB
-        if Ak is not None:
-            tb = lambda v: "true" if v else "false"
-            args = (Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), prec, _CODES[out_dtype], M,
-                    N, K, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc, sC, float(alpha), float(beta),
-                    bias_mode, ACTS[act])
-            if split8:
-                zo = 1 if reduce_batch else z
-                V = nterm * (z if reduce_batch else 1) * (K // 64)
-                S0 = max(1, -(-512 // (-(-M // 256) * -(-N // 256) * zo)))
-                kchunk = max(4, -(-V // S0))
+        if Ak is not None and Bk is not None:
+            kchunk = int(arg)
+            ws = None
+            if kchunk > 0 or reduce_batch:
                 n = _lib.vfm_gemm8_workspace_floats(prec, M, N, K, z, kchunk, int(reduce_batch))
-                ws = torch.empty(max(n, 0), dtype=torch.float32, device=A.device) if n > 0 else None
-                region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
-                if kernel_timer.SHAPES:
-                    region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}k{kchunk}]"
-                with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch), flops, "mfma"):
-                    rc = _lib.vfm_gemm8(*args, custom_ops.ptr(ws), kchunk, int(reduce_batch), stream)
-                if rc != custom_ops.VFM_NO_KERNEL:
-                    custom_ops.check(rc, "vfm_gemm8")
-                    return out
-        if Ak is not None and not split8:
+                if n < 0:
+                    raise custom_ops.NativeError("vfm_gemm8: split-K workspace too large")
+                ws = torch.empty(max(n, 1), dtype=torch.float32, device=A.device) if n > 0 else None
             # one timer region per kernel instantiation (rocprof: gemm8_kernel<AK, BK, OUTF32>)
             region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
             if kernel_timer.SHAPES:
-                region += f"[{M}x{N}x{K}x{z}]"
-            with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch), flops, "mfma"):
-                rc = _lib.vfm_gemm8(*args, None, 0, 0, stream)
+                region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'k%d' % kchunk if kchunk else ''}]"
+            with kernel_timer.region(region, nbytes, flops, "mfma"):
+                rc = _lib.vfm_gemm8(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), prec,
+                                    _CODES[out_dtype], M, N, K, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc,
+                                    sC, float(alpha), float(beta), bias_mode, ACTS[act], custom_ops.ptr(ws), kchunk,
+                                    int(reduce_batch), stream)
             if rc != custom_ops.VFM_NO_KERNEL:
                 custom_ops.check(rc, "vfm_gemm8")
                 return out
+        splits = 1 if kern == "g8" else splits
+    else:
+        splits = int(arg)
     ws = None
     if splits > 1 or reduce_batch:
         n = _lib.vfm_gemm_workspace_floats(M, N, z, splits, int(reduce_batch))
@@ -195,14 +210,13 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         in_code, tag = custom_ops.VFM_BF16, "bf16"
     else:
         in_code, _, tag = custom_ops.f32_precision()
-    tb = lambda v: "true" if v else "false"
     # one region per gemm_kernel<AK, BK, NP, OUTF32> instantiation; split-K / batch-reduced
     # launches (kernel + gemm_reduce_kernel) are their own region
     kname = "gemm_ws" if ws is not None else "gemm"
     region = f"{kname}<{tag},{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
     if kernel_timer.SHAPES:
         region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
-    with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch), flops, "mfma"):
+    with kernel_timer.region(region, nbytes, flops, "mfma"):
         rc = _lib.vfm_gemm(A.data_ptr(), B.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(ws),
                            in_code, _CODES[out_dtype], M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB,
                            ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], int(splits), int(reduce_batch),
