@@ -32,6 +32,8 @@ CFG = os.path.join(PKG, "configs")
 
 
 def _build(name, batch, graphs=False, **loss_over):
+    if graphs:
+        os.environ["VFM_EXPERIMENTAL_GRAPHS"] = "1"   # the experimental path, asked for explicitly
     from train import resolve_config
     from training.training_loop import configure_backends, construct_networks, construct_iteration
     c = resolve_config(yaml.safe_load(open(os.path.join(CFG, name))))

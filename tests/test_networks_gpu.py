@@ -159,6 +159,7 @@ def test_total_loss_step_gpu(vfm_dir, graphed, gemm, monkeypatch):
     loss = TotalLoss(device=DEV, G=G2, D=D2, **net_cases.loss_kwargs(vfm_dir))
     det_init(loss.perceptual_module)
     if graphed:
+        monkeypatch.setenv("VFM_EXPERIMENTAL_GRAPHS", "1")      # experimental path
         loss.enable_graphed_nograd_forward()
     real = torch.from_numpy(_arr("T/real")).to(DEV)
     D2.requires_grad_(True)

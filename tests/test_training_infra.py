@@ -168,3 +168,16 @@ def test_ema_copies_buffers_only_when_changed():
     beta = 0.5 ** (4 / 10000.0)
     assert not torch.equal(G_ema.lin.weight, G.lin.weight)
     assert torch.isfinite(G_ema.lin.weight).all() and beta < 1
+
+
+def test_graphed_forward_refused_without_opt_in(monkeypatch):
+    """The HIP-graph replay of the D phase's generator forward is experimental (stale replays at the
+    full C1 size): enabling it without VFM_EXPERIMENTAL_GRAPHS=1 raises."""
+    import pytest
+    from training.loss import TotalLoss
+    monkeypatch.delenv("VFM_EXPERIMENTAL_GRAPHS", raising=False)
+    obj = TotalLoss.__new__(TotalLoss)
+    with pytest.raises(RuntimeError, match="experimental"):
+        obj.enable_graphed_nograd_forward()
+    obj.enable_graphed_nograd_forward(False)
+    assert obj.graphed_nograd is None

@@ -15,6 +15,7 @@ flag == MIN of the negated marks). Before the safe-loss check is active
 nothing in the step reads those values, so their copy is non-blocking and read
 lazily (`_HostValues`): the G backward is then issued without draining the GPU.
 """
+import os
 import math
 from collections import deque
 from typing import Optional, Tuple, Union
@@ -241,7 +242,14 @@ class TotalLoss:
 
     def enable_graphed_nograd_forward(self, flag=True):
         """Replay the D phase's no-grad generator forward from HIP graphs
-        (training/graphed_forward.py); numerics and RNG draws as the eager pass."""
+        (training/graphed_forward.py); numerics and RNG draws as the eager pass.
+        EXPERIMENTAL and refused unless VFM_EXPERIMENTAL_GRAPHS=1: at the full C1 configuration a
+        replay that follows an eager forward run after a decoder weight update has read stale
+        memory (unresolved), so enabling it could silently train D on wrong
+        generator outputs."""
+        if flag and os.environ.get("VFM_EXPERIMENTAL_GRAPHS", "0") != "1":
+            raise RuntimeError("graphed no-grad generator forward is experimental (stale replays at full size, "
+                               "DESIGN.md §5); set VFM_EXPERIMENTAL_GRAPHS=1 to use it anyway")
         from training.graphed_forward import GraphedNoGradForward
         self.graphed_nograd = GraphedNoGradForward(self.G) if flag else None
 
