@@ -368,6 +368,25 @@ def test_posterior_sample_kl(B, C, H):
     assert _rel(pg.grad, pr.grad) < 1e-5
 
 
+def test_posterior_nan_logvar_passes_through():
+    """torch.clamp passes NaN through: a NaN logvar gives a NaN sample and KL (as the reference's
+    DiagonalGaussianDistribution), not the clamped -30 that fminf / fmaxf would produce."""
+    from networks.utils import kl_utils
+    params = torch.randn(2, 8, 4, 4)
+    params[0, 4, 1, 2] = float("nan")
+    eps = torch.randn(2, 4, 4, 4)
+    kl_utils.set_noise_source(lambda shape: eps.clone())
+    try:
+        z, kl = kl_utils.sample_and_kl(params.to(DEV))
+        post = kl_utils.DiagonalGaussianDistribution(params.double())
+        zr, klr = post.sample(), post.kl()
+    finally:
+        kl_utils.set_noise_source(None)
+    assert torch.isnan(z[0, 0, 1, 2]) and torch.isnan(zr[0, 0, 1, 2])
+    assert torch.isnan(kl[0]) and torch.isnan(klr[0])
+    assert torch.isfinite(kl[1]) and torch.isfinite(z[1]).all()
+
+
 @pytest.mark.parametrize("C,res", [(128, 32), (64, 48)])
 def test_convnext_layer_residual_fusion(C, res, monkeypatch):
     """The residual-branch gradient handed to the dwconv data-gradient kernel (decoder_hip.ResidualSlot)

@@ -14,10 +14,13 @@
 // w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
 //
 // GEMM view: M = B*H*W pixels, N = Cout, K = 9*Cin (tap-major). Tile 128 pixels x BN (128 or 64)
-// couts x 64 k, 4 waves (2 x 2), 32x32x16 bf16 MFMA, fp32 activations split into NP piece images
-// on the way into LDS and the Terms<NP> piece products accumulated (gemm.hip's f32x6 / f32x3). The A loader is
-// implicit: each thread owns 8 pixel rows and one 4-channel column of the tile; a k-tile (64
-// channels of one tap, or for Cin < 64 several taps) becomes one 16-B load per row at
+// couts x 32 k, 4 waves (2 x 2), 32x32x16 bf16 MFMA; fp32 activations split into NP piece images on
+// the way into LDS, the Terms<NP> piece products accumulated (gemm.hip's f32x6 / f32x3: hi.hi in
+// its own accumulator). Two LDS stages (double buffer): the split + store of K-tile t+1 and the
+// global loads of K-tile t+2 are issued between the MFMA steps of K-tile t, one barrier per K-tile
+// (raw s_barrier after lgkmcnt(0): the in-flight global loads are not drained). The A loader is
+// implicit: each thread owns 4 pixel rows and one 4-channel column of the tile; a k-tile (32
+// channels of one tap, or for Cin < 32 several taps) becomes one 16-B load per row at
 // (p + dy*W + dx)*Cin + c, zero outside the image. The 9 shifted reads of a pixel hit L2.
 #include "vfm_common.h"
 
@@ -28,8 +31,9 @@ using namespace vfm;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BK = 64, THREADS = 256;
-constexpr int IMG_A = BM * BK * 2;   // bytes of one bf16 image of the A tile
+constexpr int BM = 128, BK = 32, THREADS = 256;
+constexpr int ROWB = BK * 2;          // bytes of one bf16 image row (4 16-B chunks)
+constexpr int IMG_A = BM * ROWB;      // bytes of one bf16 piece image of the A tile
 
 struct ConvArgs {
     const float* x;      // [B, H, W, Cin]
@@ -44,7 +48,11 @@ struct ConvArgs {
     int relu;
 };
 
-__device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
+// [rows][32 k] bf16 image, 64-B rows: 16-B chunk ch of row at chunk ch ^ ((row >> 2) & 3) -- the 16
+// rows of each ds_read_b128 lane group (same chunk) land on 16 distinct 16-B slots of the 256-B
+// bank row (MI355X_MICROARCH.md §LDS), and a ds_write_b64 / ds_write_b128 lane group covers two /
+// one whole 128-B row pairs
+__device__ __forceinline__ int k32_off(int row, int ch) { return row * ROWB + 16 * (ch ^ ((row >> 2) & 3)); }
 
 // 4 fp32 (one uint4) -> the NP pieces' halves of a 16-B image chunk (piece p at img + p * pstride)
 template <int NP>
@@ -56,15 +64,15 @@ __device__ __forceinline__ void put4(unsigned char* img, int pstride, int off, u
     for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(img + p * pstride + off) = make_uint2(p01[p], p23[p]);
 }
 
-// thread -> (row = tid/16 + 16u, 4-element column tid%16) of a [rows][64] fp32 tile
+// thread -> (row = tid/8 + 32u, 4-element column tid%8) of a [128][32] fp32 tile
 struct StageA {
-    uint4 r[8];
-    int pm[8];    // pixel index (or -1)
-    int pyx[8];   // y << 16 | x
+    uint4 r[4];
+    int pm[4];    // pixel index (or -1)
+    int pyx[4];   // y << 16 | x
     __device__ __forceinline__ void init(const ConvArgs& a, int m0, int tid) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int m = m0 + tid / 16 + 16 * u;
+        for (int u = 0; u < 4; ++u) {
+            const int m = m0 + tid / 8 + 32 * u;
             if (m < a.M) {
                 const uint32_t q = fdiv((uint32_t)m, a.fW);
                 const int xx = m - (int)q * a.W;
@@ -77,29 +85,30 @@ struct StageA {
             }
         }
     }
+    // Cin < 32 (the 4-channel image layer): the taps of a K-tile differ per column
     __device__ __forceinline__ void load(const ConvArgs& a, int k0, int tid) {
-        const int k = k0 + 4 * (tid & 15);
+        const int k = k0 + 4 * (tid & 7);
         const int tap = k >> a.lc, c = k & (a.Cin - 1);
         const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
         const bool tap_ok = tap < 9;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
             const int yy = (pyx[u] >> 16) + dy, xx = (pyx[u] & 0xffff) + dx;
             const bool ok = tap_ok && pm[u] >= 0 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
             r[u] = ok ? *reinterpret_cast<const uint4*>(a.x + (long long)(pm[u] + dy * a.W + dx) * a.Cin + c)
                       : make_uint4(0, 0, 0, 0);
         }
     }
-    // Cin >= 64: a K-tile is 64 channels of ONE tap, so the 8 rows' validity and 32-bit element offsets
+    // Cin >= 32: a K-tile is 32 channels of ONE tap, so the 4 rows' validity and 32-bit element offsets
     // (pixel + tap shift, times Cin) change only with the tap; per K-tile only the channel offset moves
-    int off[8];
+    int off[4];
     unsigned okm;
     int cur_tap;
     __device__ __forceinline__ void tap_setup(const ConvArgs& a, int tap) {
         const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
         okm = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
             const int yy = (pyx[u] >> 16) + dy, xx = (pyx[u] & 0xffff) + dx;
             const bool ok = pm[u] >= 0 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
             okm |= (unsigned)ok << u;
@@ -110,34 +119,34 @@ struct StageA {
     __device__ __forceinline__ void load_wide(const ConvArgs& a, int k0, int tid) {
         const int tap = k0 >> a.lc;                      // uniform
         if (tap != cur_tap) tap_setup(a, tap);
-        const int c = (k0 & (a.Cin - 1)) + 4 * (tid & 15);
+        const int c = (k0 & (a.Cin - 1)) + 4 * (tid & 7);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 4; ++u)
             r[u] = ((okm >> u) & 1)
                        ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.x) + (unsigned)(off[u] + c) * 4u)
                        : make_uint4(0, 0, 0, 0);
     }
     template <int NP>
     __device__ __forceinline__ void store(unsigned char* img, int tid) const {
-        const int cc = tid & 15;
+        const int cc = tid & 7;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) put4<NP>(img, IMG_A, kc_off(tid / 16 + 16 * u, cc >> 1) + 8 * (cc & 1), r[u]);
+        for (int u = 0; u < 4; ++u) put4<NP>(img, IMG_A, k32_off(tid / 8 + 32 * u, cc >> 1) + 8 * (cc & 1), r[u]);
     }
 };
 
 // weights arrive pre-split (NP bf16 pieces, split once per weight version on the host side):
-// thread -> 16-B chunks (8 k) c = tid + 256u of a [ROWS][64] tile, copied as-is into the piece images
+// thread -> 16-B chunks (8 k) c = tid + 256u of a [ROWS][32] tile, copied as-is into the piece images
 template <int ROWS, int NP>
 struct StageB {
-    static constexpr int PER = ROWS * 8 / THREADS;
-    static constexpr int IMG = ROWS * 64 * 2;
+    static constexpr int PER = ROWS * 4 / THREADS;
+    static constexpr int IMG = ROWS * ROWB;
     uint4 v[NP][PER];
     __device__ __forceinline__ void load(const ConvArgs& a, int n0, int k0, int tid) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int c = tid + THREADS * u, row = c >> 3, k = k0 + 8 * (c & 7), n = n0 + row;
+            const int c = tid + THREADS * u, row = c >> 2, k = k0 + 8 * (c & 3), n = n0 + row;
             const bool ok = k < a.ldw && n < a.Cout;
-            const unsigned o = (unsigned)(n * a.ldw + k) * 2u;          // byte offset (host: NP * Cout * ldw < 2^30)
+            const unsigned o = (unsigned)(n * a.ldw + k) * 2u;          // byte offset (host: Cout * ldw < 2^30)
 #pragma unroll
             for (int p = 0; p < NP; ++p)
                 v[p][u] = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.w + p * a.wps) + o)
@@ -147,24 +156,30 @@ struct StageB {
     __device__ __forceinline__ void store(unsigned char* img, int tid) const {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int c = tid + THREADS * u, off = kc_off(c >> 3, c & 7);
+            const int c = tid + THREADS * u, off = k32_off(c >> 2, c & 3);
 #pragma unroll
             for (int p = 0; p < NP; ++p) *reinterpret_cast<uint4*>(img + p * IMG + off) = v[p][u];
         }
     }
 };
 
+// MFMA operand fragment: 32-row block blk, k16 step s: lane (r, hh) holds row 32 blk + r, k = 16 s + 8 hh .. +7
 __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int s, int lane) {
-    return *reinterpret_cast<const bf16x8*>(img + kc_off(32 * blk + (lane & 31), 2 * s + (lane >> 5)));
+    return *reinterpret_cast<const bf16x8*>(img + k32_off(32 * blk + (lane & 31), 2 * s + (lane >> 5)));
+}
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
 
 template <int BN, int NP>
 __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3_kernel(ConvArgs a) {
     constexpr int NJ = BN / 64;                 // 32-col blocks per wave
-    constexpr int IMG_B = BN * BK * 2;
+    constexpr int IMG_B = BN * ROWB;
+    constexpr int STAGE = NP * (IMG_A + IMG_B); // A pieces, then B pieces
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    unsigned char* a_img = lds;                 // A piece p at a_img + p IMG_A
-    unsigned char* b_img = lds + NP * IMG_A;    // B piece p at b_img + p IMG_B
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
@@ -180,34 +195,40 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
     StageB<BN, NP> sb;
     sa.init(a, m0, tid);
     sa.cur_tap = -1;
-    const bool wide = a.lc >= 6;                        // Cin >= 64 (uniform)
+    const bool wide = a.lc >= 5;                        // Cin >= 32 (uniform)
     f32x16 acc[2][NJ], accs[2][NJ];             // hi.hi products / the smaller piece products
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = accs[i][j] = f32x16{};
 
-    if (wide) sa.load_wide(a, 0, tid);
-    else sa.load(a, 0, tid);
-    sb.load(a, n0, 0, tid);
-    for (int k0 = 0; k0 < a.K; k0 += BK) {
-        sa.store<NP>(a_img, tid);
-        sb.store(b_img, tid);
-        __syncthreads();
-        if (k0 + BK < a.K) {
-            if (wide) sa.load_wide(a, k0 + BK, tid);
-            else sa.load(a, k0 + BK, tid);
-            sb.load(a, n0, k0 + BK, tid);
-        }
+    const int KT = (a.K + BK - 1) / BK;
+    auto gload = [&](int kt) {
+        if (wide) sa.load_wide(a, kt * BK, tid);
+        else sa.load(a, kt * BK, tid);
+        sb.load(a, n0, kt * BK, tid);
+    };
+    auto lstore = [&](int buf) {
+        unsigned char* st = lds + buf * STAGE;
+        sa.store<NP>(st, tid);
+        sb.store(st + NP * IMG_A, tid);
+    };
+    gload(0);
+    lstore(0);
+    if (KT > 1) gload(1);
+    lds_barrier();
+    for (int kt = 0; kt < KT; ++kt) {
+        const unsigned char* ca = lds + (kt & 1) * STAGE;
+        const unsigned char* cb = ca + NP * IMG_A;
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
             bf16x8 af[NP][2], bf[NP][NJ];
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i) af[p][i] = frag(a_img + p * IMG_A, 2 * wm + i, s, lane);
+                for (int i = 0; i < 2; ++i) af[p][i] = frag(ca + p * IMG_A, 2 * wm + i, s, lane);
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) bf[p][j] = frag(b_img + p * IMG_B, NJ * wn + j, s, lane);
+                for (int j = 0; j < NJ; ++j) bf[p][j] = frag(cb + p * IMG_B, NJ * wn + j, s, lane);
             }
             // small piece products into their own accumulator (rounded at their own ~2^-8 scale),
             // hi.hi alone into acc: as many full-magnitude roundings as an fp32 GEMM of exact products
@@ -221,10 +242,15 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i], bf[Terms<NP>::b(t)][j], c,
                                                                     0, 0, 0);
                     }
+            // between the two MFMA steps: K-tile kt+1 from registers into the other stage, then the
+            // global loads of K-tile kt+2 (its stage was last read before the previous barrier)
+            if (s == 0 && kt + 1 < KT) {
+                lstore((kt + 1) & 1);
+                if (kt + 2 < KT) gload(kt + 2);
+            }
         }
-        __syncthreads();
+        lds_barrier();
     }
-
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -253,7 +279,7 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
 
 template <int BN, int NP>
 int launch(const ConvArgs& a, hipStream_t st) {
-    const size_t lds = NP * (IMG_A + BN * BK * 2);
+    const size_t lds = 2 * NP * (IMG_A + BN * ROWB);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BN, NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -16,7 +16,9 @@ namespace {
 
 using namespace vfm;
 
-__device__ __forceinline__ float clamp_lv(float v) { return fminf(fmaxf(v, -30.f), 20.f); }
+// torch.clamp semantics: NaN passes through (fminf / fmaxf alone would turn it into -30 and hide a
+// diverging encoder behind a finite z and KL)
+__device__ __forceinline__ float clamp_lv(float v) { return v != v ? v : fminf(fmaxf(v, -30.f), 20.f); }
 
 __global__ __launch_bounds__(256) void posterior_fwd(const float* __restrict__ params, const float* __restrict__ eps,
                                                      float* __restrict__ z, float* __restrict__ kl, int C, long long P) {

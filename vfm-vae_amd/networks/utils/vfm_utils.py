@@ -64,23 +64,31 @@ class VFMEncoder(nn.Module):
 
     def offer_features(self, img, transform, feats, pooled):
         """Register features of `img` under `transform` (held with a reference to img, so the
-        identity key cannot be recycled while the entry lives)."""
-        self._reuse_entry = (img, img._version, transform, feats, pooled)
+        identity key cannot be recycled while the entry lives). One entry per microbatch image:
+        with gradient accumulation every D-phase microbatch offers its own."""
+        reg = self.__dict__.setdefault('_reuse', {})
+        reg[id(img)] = (img, img._version, transform, feats, pooled)
 
     def clear_features(self):
-        self._reuse_entry = None
+        self.__dict__.setdefault('_reuse', {}).clear()
         self.last_features = None
 
     def _take(self, img, transform):
-        e = getattr(self, '_reuse_entry', None)
+        """The features offered for exactly this image tensor (same object, same version) under the
+        same input transform, consumed on a match; entries of other images are left alone."""
+        reg = self.__dict__.get('_reuse')
+        e = reg.get(id(img)) if reg else None
         if e is None:
             return None
-        self._reuse_entry = None
         src, ver, tr, feats, pooled = e
-        if src is img and ver == img._version and tr == transform:
-            self.reuse_hits = getattr(self, 'reuse_hits', 0) + 1
-            return feats, pooled
-        return None
+        if src is not img or ver != img._version:
+            del reg[id(img)]                     # stale (the tensor changed since it was offered)
+            return None
+        if tr != transform:
+            return None
+        del reg[id(img)]
+        self.reuse_hits = getattr(self, 'reuse_hits', 0) + 1
+        return feats, pooled
 
     def encode_image(self, img, eq_scale_factor: float = 1.0, is_eq_prior: bool = False):
         if not self.reuse_features:

@@ -446,7 +446,7 @@ class TotalLoss:
             enc = getattr(self.G, 'vfm_encoder', None)
             reuse = enc is not None and getattr(enc, 'reuse_features', False)
             if reuse:
-                enc.clear_features()
+                enc.last_features = None         # only this microbatch's tower pass is offered below
             with torch.no_grad():
                 out = self.run_G_nograd(real_img, real_c)
             if reuse and enc.last_features is not None:

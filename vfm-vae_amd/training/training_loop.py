@@ -276,10 +276,16 @@ class TrainingIteration:
     def run_phase(self, phase, real_imgs, real_cs, cur_nimg):
         self._apply_freeze(phase)
         phase.sync.prepare()
+        enc = getattr(self.G, 'vfm_encoder', None)
+        reuse = enc is not None and getattr(enc, 'reuse_features', False)
+        if reuse and phase.name == 'D':
+            enc.clear_features()                 # the D phase offers each microbatch's tower features
         n = len(real_imgs)
         for i, (img, c) in enumerate(zip(real_imgs, real_cs)):
             phase.sync.last_microbatch = (i == n - 1)
             self.loss.accumulate_gradients(phase=phase.name, real_img=img, real_c=c, cur_nimg=cur_nimg)
+        if reuse and phase.name == 'G':
+            enc.clear_features()                 # entries the G phase did not take (other draws) freed
         # requires_grad_(False) over the flag list of _apply_freeze (a module walk costs ms of host
         # time at the point where the GPU queue is shortest)
         flags = phase.active_flags
