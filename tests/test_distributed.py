@@ -240,3 +240,55 @@ def test_training_stats_reduce_over_ranks():
         assert abs(out["std"] - float(vals.std(unbiased=False))) < 1e-12
         assert out["r0"] == (1.0, 5.0)
 
+
+
+def _accum_worker(rank, world, bucket_mb):
+    """Two microbatches per phase (accumulate_gradients=2); m[0] is touched only in the first,
+    m.unused only in the second (the last), m[2] in both."""
+    from training.training_loop import FlatGradSync
+    m = _toy()
+    sync = FlatGradSync(m, bucket_mb=bucket_mb, collective=world > 1)
+    sync.prepare()
+    g = torch.Generator().manual_seed(200 + rank)
+    x = torch.randn(4, 6, generator=g)
+    h = torch.tanh(m[0](x)).detach()
+    sync.last_microbatch = False
+    (m[2](torch.tanh(m[0](x))).square().sum() * (rank + 1)).backward()          # microbatch 0: m[0], m[2]
+    sync.last_microbatch = True
+    ((m[2](h).sum() + m.unused.square().sum()) * (rank + 2)).backward()          # microbatch 1: m[2], unused
+    sync.finish(gain=2.0)
+    return {n: (None if p.grad is None else p.grad.clone()) for n, p in m.named_parameters()}
+
+
+def _accum_expect(world):
+    """sum over ranks and microbatches of the plain-autograd gradients / world * gain."""
+    tot = {}
+    for r in range(world):
+        m = _toy()
+        g = torch.Generator().manual_seed(200 + r)
+        x = torch.randn(4, 6, generator=g)
+        h = torch.tanh(m[0](x)).detach()
+        (m[2](torch.tanh(m[0](x))).square().sum() * (r + 1)).backward()
+        ((m[2](h).sum() + m.unused.square().sum()) * (r + 2)).backward()
+        for n, p in m.named_parameters():
+            tot[n] = tot.get(n, 0) + p.grad
+    return {n: v / world * 2.0 for n, v in tot.items()}
+
+
+@pytest.mark.parametrize("bucket_mb", [64.0, 1e-4])
+def test_flat_grad_sync_two_microbatches(bucket_mb):
+    """FlatGradSync over two microbatches with parameters touched in only one of them, on the
+    collective path (gloo, 2 ranks: buckets launched from the last microbatch's hooks, the rest in
+    finish()) and on the world-size-1 path (stolen gradients gathered in chunks): both equal
+    sum / world * gain."""
+    res = _spawn("_accum_worker", 2, bucket_mb)
+    expect = _accum_expect(2)
+    for r in (0, 1):
+        for n, v in expect.items():
+            assert res[r][n] is not None, n
+            assert torch.allclose(torch.from_numpy(res[r][n]), v, rtol=1e-5, atol=1e-6), (r, n)
+    from training.training_loop import FlatGradSync  # noqa: F401  (world size 1, in this process)
+    out = _accum_worker(0, 1, bucket_mb)
+    expect1 = _accum_expect(1)
+    for n, v in expect1.items():
+        assert torch.allclose(out[n], v, rtol=1e-5, atol=1e-6), n

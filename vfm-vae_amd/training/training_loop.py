@@ -43,7 +43,14 @@ from torch_utils.ops import conv2d_gradfix
 
 
 class FlatGradSync:
-    """Owns the .grad storage of the trainable parameters of one phase."""
+    """Owns the .grad storage of the trainable parameters of one phase.
+
+    Gradient accumulation: non-last microbatches leave each parameter's (stolen) gradient in place;
+    the last microbatch's hooks launch the bucket all-reduces, finish() launches the buckets whose
+    parameters the last microbatch did not touch (tests/test_distributed.py covers two microbatches
+    with parameters seen in only one of them). The rank-agreement check on the parameter set runs
+    without a host sync and therefore raises one step late, at the next prepare(): by then Adam has
+    applied one step of the divergent gradients."""
 
     def __init__(self, module: nn.Module, bucket_mb: float = 64.0, collective: Optional[bool] = None):
         self.module = module
