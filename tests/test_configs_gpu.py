@@ -15,7 +15,7 @@ size-independent properties of one iteration:
     iteration when both phases draw the same input transform).
 
 Configs: C1 = stage-0 SigLIP2-L at B=32 (the benchmark workload), C2 = stage-3 PatchGAN
-fine-tune (B=8 per GPU here), C3 = DINOv2-L on the 256/384/512 stream (B=4 per size),
+fine-tune (B=32 per GPU), C3 = DINOv2-L on the 256/384/512 stream (B=4 per size),
 C4 = VQ latent with fp16 decoder blocks (B=8).
 """
 import os
@@ -94,26 +94,43 @@ def test_c1_stage0_full_size_iteration():
     eqt.forced = forced
     eqt.outcomes = lambda: [forced]                     # capture only the outcome this test draws
     img, labels = _images(32, 256), ['a photo'] * 32
+    taken = []
+    take = G.vfm_encoder._take
+
+    def spy(im, tr):
+        hit = take(im, tr)
+        if hit is not None:
+            taken.append([f.clone() for f in hit[0]])
+        return hit
+
+    G.vfm_encoder._take = spy
     for phase in step.phases:
         _run_phase_checked(step, phase, img, labels)
+    G.vfm_encoder._take = take
     assert getattr(step.loss, "graphed_nograd", None) is None       # the measured path: eager D phase
-    assert G.vfm_encoder.reuse_hits == 1                              # G phase reused the D phase's tower pass
+    assert G.vfm_encoder.reuse_hits == 1 and len(taken) == 1        # G phase reused the D phase's tower pass
     vals = _losses_finite(step.loss)
     assert vals["l1_pixel_loss"] > 0 and vals["perceptual_loss"] > 0
     step.update_ema(32)
-    # the G phase's reused tower features equal a fresh tower pass on the same image
+    # the G phase's reused tower features equal a fresh tower pass on the same image, bit for bit
+    # (frozen tower, deterministic kernels: reuse is exact)
     with torch.no_grad():
         fresh, _ = G.vfm_encoder.encoder.encode_image(img, 1.0, False)
         G.vfm_encoder.clear_features()
-    assert all(torch.isfinite(f).all() for f in fresh)
+    assert len(fresh) == len(taken[0])
+    for f, t in zip(fresh, taken[0]):
+        assert torch.isfinite(f).all()
+        assert torch.equal(f, t)
 
 
 def test_c2_stage3_patchgan_iteration():
-    c, step = _build("vfm_vae_f16d32_siglip2_stage_3_patchgan_fine_tuning.yaml", batch=8)
+    """Stage-3 PatchGAN fine-tune at its stated 32 images per GPU: 4 BatchNormLocal virtual batches
+    of 8 per scale (reference networks/discriminator.py:76,89)."""
+    c, step = _build("vfm_vae_f16d32_siglip2_stage_3_patchgan_fine_tuning.yaml", batch=32)
     G = step.G
     assert G.train_mode == "train_the_second_half_decoder"
     res = G.synthesis.block_resolutions
-    img, labels = _images(8, 256, seed=1), ['a photo'] * 8
+    img, labels = _images(32, 256, seed=1), ['a photo'] * 32
     d_train, d_grads = _run_phase_checked(step, step.phases[0], img, labels)
     assert any(n.startswith("patchgan") or "patch" in n for n in d_grads), sorted(d_grads)[:5]
     assert not any(n.startswith("dino.") for n in d_train)
@@ -149,3 +166,44 @@ def test_c4_vq_fp16_iteration():
     _losses_finite(step.loss)
     usage = step.G.ldm_adapter.quantizer.codebooks[0].vocab_usage
     assert torch.isfinite(usage).all() and float(usage.sum()) > 0
+
+
+@pytest.mark.xfail(reason="known open bug (DESIGN.md §5): at the full C1 size a graph replay that follows an "
+                          "eager forward run after a decoder weight update has returned stale outputs; the "
+                          "path is refused without VFM_EXPERIMENTAL_GRAPHS=1", strict=False)
+def test_graph_replay_after_weight_update_c1():
+    """Regression test for the experimental HIP-graph replay of the D phase's generator forward at
+    the full C1 size (replaces the round-2 bisection scripts): replay == eager after an in-place
+    decoder weight update, both right after the update and after an intervening eager forward."""
+    B = 4
+    c, step = _build("vfm_vae_f16d32_siglip2_stage_0_synthetic.yaml", batch=B, graphs=True)
+    G = step.G
+    G.vfm_encoder.reuse_features = False
+    forced = (1.0, 0, False)
+    G.equivariance_transform.forced = forced
+    G.equivariance_transform.outcomes = lambda: [forced]
+    img, labels = _images(B, 256), ['a photo'] * B
+    gr = step.loss.graphed_nograd
+
+    def rep():
+        with torch.no_grad():
+            torch.manual_seed(7)
+            return gr(img, labels).gen_img.float().clone()
+
+    def eag():
+        with torch.no_grad():
+            torch.manual_seed(7)
+            return G(img, labels).gen_img.float().clone()
+
+    rep()
+    eag()
+    with torch.no_grad():
+        for p in G.synthesis.parameters():
+            p.add_(1e-3 * torch.randn_like(p))
+    o1 = rep()
+    e2 = eag()
+    o2 = rep()
+    assert gr.disabled is None and gr.replays >= 3
+    tol = 1e-4 * float(e2.abs().max())
+    assert float((o1 - e2).abs().max()) <= tol
+    assert float((o2 - e2).abs().max()) <= tol

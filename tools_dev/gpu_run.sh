@@ -57,19 +57,8 @@ for s in "$@"; do
     gemmbench8) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;
     ptest)   timeout -k 10 ${PT_TIMEOUT:-900} python -u -m pytest $PT -m gpu -v --timeout ${PT_CASE:-240} --timeout-method thread > $out/ptest.log 2>&1 ;;
     attnbench) timeout -k 10 300 python tools_dev/attnbench.py > $out/attnbench.log 2>&1 ;;
-    gc1)     REUSE=1 timeout -k 10 400 python tools_dev/graph_c1_debug.py > $out/gc1.log 2>&1; REUSE=0 timeout -k 10 400 python tools_dev/graph_c1_debug.py >> $out/gc1.log 2>&1 ;;
-    gc2)     REUSE=0 timeout -k 10 400 python tools_dev/graph_c1_debug2.py > $out/gc2.log 2>&1; REUSE=1 timeout -k 10 400 python tools_dev/graph_c1_debug2.py >> $out/gc2.log 2>&1 ;;
     gemmbench) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;
     gemm6bench) timeout -k 10 300 python tools_dev/gemm6bench.py > $out/gemm6bench.log 2>&1 ;;
-    gc3)     timeout -k 10 400 python tools_dev/graph_c1_debug3.py > $out/gc3.log 2>&1 ;;
-    gc4)     HOOKS=1 timeout -k 10 400 python tools_dev/graph_c1_debug4.py > $out/gc4.log 2>&1; HOOKS=0 timeout -k 10 400 python tools_dev/graph_c1_debug4.py >> $out/gc4.log 2>&1 ;;
-    gc5)     for cfg in "PART=mapping" "PART=ldm_adapter" "PART=synthesis" "PART=synthesis NO_CUDNN=1" "PART=synthesis SDPA_MATH=1" "PART=synthesis NO_CUDNN=1 SDPA_MATH=1"; do
-               env $cfg timeout -k 10 300 python tools_dev/graph_c1_debug5.py 2>&1 | grep flags >> $out/gc5.log || break; done ;;
-    gc6)     for cfg in "PART=synthesis VFM_NO_CAST_CACHE=1" "PART=synthesis VFM_NO_CAST_CACHE=0"; do
-               env $cfg timeout -k 10 300 python tools_dev/graph_c1_debug5.py 2>&1 | grep flags >> $out/gc6.log || break; done ;;
-    gc7)     for cfg in "PART=synthesis HIPBLASLT_WORKSPACE_SIZE=0" "PART=synthesis TORCH_BLAS_PREFER_HIPBLASLT=0" "PART=synthesis VFM_GEMM=torch"; do
-               env $cfg timeout -k 10 300 python tools_dev/graph_c1_debug5.py 2>&1 | grep flags | sed "s/^/$cfg: /" >> $out/gc7.log || break; done ;;
-    dhead)   timeout -k 10 300 python tools_dev/dhead_debug.py > $out/dhead.log 2>&1 && SPY_MODE=torch_out timeout -k 10 300 python tools_dev/dhead_debug.py > $out/dhead2.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
