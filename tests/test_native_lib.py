@@ -71,3 +71,24 @@ def test_dwconv_partial_tiles_host_query():
     assert lib.vfm_dwconv2d_bwd_weight_tiles(3, 2, 5, 130, 3, 1) == 9       # 3 column tiles x 3 samples
     assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 5, 130, 3, 1) == 3
     assert lib.vfm_dwconv2d_bwd_weight_tiles(1, 1, 2, 2, 7, 0) == -2      # empty output -> VFM_ERR_ARGS
+
+
+def test_torch_library_schemas():
+    """TORCH_LIBRARY(vfmvae) registers the reference plugins' ops with their schemas
+    (reference upfirdn2d.cpp:16, bias_act.cpp:32, filtered_lrelu.cpp:16,213), backed by the
+    extern "C" launchers; argument checks run before any device work."""
+    import pytest
+    import torch
+    import torch_utils.custom_ops as co
+    ops = co.get_torch_ops()
+    sch = {n: str(getattr(ops, n).default._schema) for n in ("upfirdn2d", "bias_act", "filtered_lrelu",
+                                                                "filtered_lrelu_act_")}
+    assert sch["upfirdn2d"] == ("vfmvae::upfirdn2d(Tensor x, Tensor f, int upx, int upy, int downx, int downy, "
+                                "int padx0, int padx1, int pady0, int pady1, bool flip, float gain) -> Tensor")
+    assert sch["bias_act"] == ("vfmvae::bias_act(Tensor x, Tensor b, Tensor xref, Tensor yref, Tensor dy, int grad, "
+                               "int dim, int act, float alpha, float gain, float clamp) -> Tensor")
+    assert sch["filtered_lrelu"].endswith("bool flip_filters, bool writeSigns) -> (Tensor, Tensor, int)")
+    assert sch["filtered_lrelu_act_"].startswith("vfmvae::filtered_lrelu_act_(Tensor(a!) x, Tensor si")
+    # CPU tensors: the ops are registered for the CUDA (ROCm) dispatch key only
+    with pytest.raises(NotImplementedError):
+        ops.upfirdn2d(torch.zeros(1, 1, 4, 4), torch.ones(1, 1), 1, 1, 1, 1, 0, 0, 0, 0, False, 1.0)

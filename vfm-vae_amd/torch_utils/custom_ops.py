@@ -14,6 +14,9 @@ import threading
 import torch
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libvfmvae_hip.so")
+# TORCH_LIBRARY(vfmvae) registration of the reference's plugin ops (csrc/torch_ops.cpp)
+_TORCH_LIB_PATH = os.path.join(os.path.dirname(_LIB_PATH), "libvfmvae_torch.so")
+_torch_ops = None
 _lock = threading.Lock()
 _lib = None
 
@@ -142,6 +145,25 @@ def get_native():
             lib.vfm_bnl_workspace_floats.restype = c_ll
             _lib = lib
     return _lib
+
+
+def get_torch_ops():
+    """Load (once) the TORCH_LIBRARY(vfmvae) library and return `torch.ops.vfmvae`: upfirdn2d,
+    bias_act, filtered_lrelu, filtered_lrelu_act_ with the reference plugins' schemas
+    (upfirdn2d.cpp:102-105, bias_act.cpp:94-97, filtered_lrelu.cpp:295-299 of the reference).
+    A missing library is a hard error."""
+    global _torch_ops
+    if _torch_ops is not None:
+        return _torch_ops
+    with _lock:
+        if _torch_ops is None:
+            get_native()
+            if not os.path.exists(_TORCH_LIB_PATH):
+                raise NativeError(f"torch op library not found at {_TORCH_LIB_PATH}; run the build "
+                                  "(`make -C vfm-vae_amd/csrc`)")
+            torch.ops.load_library(_TORCH_LIB_PATH)
+            _torch_ops = torch.ops.vfmvae
+    return _torch_ops
 
 
 def get_plugin(module_name=None, sources=None, headers=None, source_dir=None, **_build_kwargs):

@@ -75,28 +75,12 @@ def _memfmt(x):
 
 
 def _run(x, b, xref, yref, dy, grad, dim, spec, alpha, gain, clamp):
-    """One `vfm_bias_act` launch; all tensors dense with x's element order."""
-    lib = custom_ops.get_native()
-    y = torch.empty_like(x)
-    if x.numel() == 0:
-        return y
-    if b is not None:
-        if b.ndim != 1 or not (0 <= dim < x.ndim) or b.shape[0] != x.shape[dim]:
-            raise RuntimeError("b must be a vector matching x along dim")
-        if b.dtype != x.dtype or b.device != x.device:
-            raise RuntimeError("b must have the same dtype and device as x")
-        step_b = x.stride(dim)
-    else:
-        step_b = 1
-    for t in (xref, yref, dy):
-        if t is not None and (t.shape != x.shape or t.dtype != x.dtype or t.stride() != x.stride()):
-            raise RuntimeError("xref/yref/dy must match x in shape, dtype and layout")
-    rc = lib.vfm_bias_act(x.data_ptr(), custom_ops.ptr(b), custom_ops.ptr(xref), custom_ops.ptr(yref),
-                          custom_ops.ptr(dy), y.data_ptr(), custom_ops.dtype_code(x), x.numel(), grad,
-                          spec.cuda_idx, alpha, gain, clamp, step_b, b.numel() if b is not None else 0,
-                          custom_ops.stream_ptr(x.device))
-    custom_ops.check(rc, "vfm_bias_act")
-    return y
+    """One launch through the registered op torch.ops.vfmvae.bias_act (csrc/torch_ops.cpp over
+    vfm_bias_act; the reference plugin's schema, empty tensors for absent inputs, bias_act.cpp:32-90)."""
+    e = x.new_empty([0])
+    return custom_ops.get_torch_ops().bias_act(x, e if b is None else b.contiguous(), e if xref is None else xref,
+                                               e if yref is None else yref, e if dy is None else dy, int(grad),
+                                               int(dim), int(spec.cuda_idx), float(alpha), float(gain), float(clamp))
 
 
 class _BiasActHip(torch.autograd.Function):

@@ -100,70 +100,30 @@ def _as_2d(f):
 
 
 def _filtered_lrelu_native(x, fu, fd, b, si, sx, sy, cfg, write_signs):
-    """Fused kernel launch. Returns (y, signs_out) or None when no kernel exists."""
+    """Fused kernel launch through torch.ops.vfmvae.filtered_lrelu (csrc/torch_ops.cpp over
+    vfm_filtered_lrelu, the reference plugin's schema, filtered_lrelu.cpp:16-204). Returns
+    (y, signs_out or None) or None when no kernel exists (the op's return code -1)."""
     up, down, px0, px1, py0, py1, gain, slope, clamp, flip = cfg
     if x.dtype not in (torch.float16, torch.float32, torch.bfloat16):
         return None
-    lib = custom_ops.get_native()
-    fu2, fd2 = _as_2d(fu), _as_2d(fd)
-    n, c, xh, xw = x.shape
-    fuh, fuw = fu2.shape
-    fdh, fdw = fd2.shape
-    cw = xw * up + (px0 + px1) - (fuw - 1)
-    ch = xh * up + (py0 + py1) - (fuh - 1)
-    if not (cw > fdw - 1 and ch > fdh - 1):
-        raise RuntimeError("upsampled buffer must be at least the size of downsampling filter")
-    yw = (cw - (fdw - 1) + (down - 1)) // down
-    yh = (ch - (fdh - 1) + (down - 1)) // down
-    if yw <= 0 or yh <= 0:
-        raise RuntimeError("output must be at least 1x1")
-    y = torch.empty([n, c, yh, yw], dtype=x.dtype, device=x.device,
-                    memory_format=upfirdn2d._memory_format(x))
-    so = None
-    if write_signs:
-        sw_active = yw * down - (down - 1) + (fdw - 1)
-        sh = yh * down - (down - 1) + (fdh - 1)
-        sw = (sw_active + 15) & ~15
-        so = torch.empty([n, c, sh, sw >> 2], dtype=torch.uint8, device=x.device)
-        s, mode = so, 1
-    elif si is not None and si.numel():
-        if not si.is_contiguous() or si.dtype != torch.uint8 or si.ndim != 4 or si.shape[:2] != x.shape[:2]:
-            raise RuntimeError("signs must be a contiguous uint8 [N, C, sh, sw/4] tensor")
-        s, mode = si, 2
-    else:
-        s, mode = None, 0
-    sh_, swb = (s.shape[2], s.shape[3]) if s is not None else (0, 0)
-    bb = b.contiguous() if b is not None else None
-    rc = lib.vfm_filtered_lrelu(x.data_ptr(), fu2.data_ptr(), fd2.data_ptr(), custom_ops.ptr(bb),
-                                custom_ops.ptr(s), y.data_ptr(), custom_ops.dtype_code(x),
-                                n, c, xh, xw, custom_ops.strides(x), yh, yw, custom_ops.strides(y),
-                                fuh, fuw, fdh, fdw, up, down, px0, py0, sh_, swb, sx, sy, mode,
-                                gain, slope, clamp, int(flip), custom_ops.stream_ptr(x.device))
-    if custom_ops.check(rc, "vfm_filtered_lrelu", allow_no_kernel=True) == custom_ops.VFM_NO_KERNEL:
+    e8 = torch.empty([0], dtype=torch.uint8, device=x.device)
+    bb = b if b is not None else torch.zeros([x.shape[1]], dtype=x.dtype, device=x.device)
+    y, so, rc = custom_ops.get_torch_ops().filtered_lrelu(
+        x, fu, fd, bb, si if (si is not None and si.numel()) else e8, int(up), int(down), int(px0), int(px1),
+        int(py0), int(py1), int(sx), int(sy), float(gain), float(slope), float(clamp), bool(flip), bool(write_signs))
+    if rc == custom_ops.VFM_NO_KERNEL:
         return None
-    return y, so
+    return y, (so if write_signs else None)
 
 
 def filtered_lrelu_act_(x, si, sx, sy, gain, slope, clamp, write_signs):
     """In-place gain/lrelu/clamp with sign write or read (reference plugin
-    `filtered_lrelu_act_`, filtered_lrelu.cpp:213-290). Returns the new sign
-    tensor [N, C, H, round16(W)/4] when writing, else an empty tensor."""
-    lib = custom_ops.get_native()
-    n, c, h, w = x.shape
-    so = torch.empty([0], dtype=torch.uint8, device=x.device)
-    if write_signs:
-        so = torch.empty([n, c, h, ((w + 15) & ~15) >> 2], dtype=torch.uint8, device=x.device)
-        s, mode = so, 1
-    elif si is not None and si.numel():
-        s, mode = si, 2
-    else:
-        s, mode = None, 0
-    sh_, swb = (s.shape[2], s.shape[3]) if s is not None else (0, 0)
-    rc = lib.vfm_filtered_lrelu_act(x.data_ptr(), custom_ops.ptr(s), custom_ops.dtype_code(x), n, c, h, w,
-                                    custom_ops.strides(x), sh_, swb, sx, sy, mode, float(gain), float(slope),
-                                    float(clamp), custom_ops.stream_ptr(x.device))
-    custom_ops.check(rc, "vfm_filtered_lrelu_act")
-    return so
+    `filtered_lrelu_act_`, filtered_lrelu.cpp:213-290) through torch.ops.vfmvae.filtered_lrelu_act_.
+    Returns the new sign tensor [N, C, H, round16(W)/4] when writing, else an empty tensor."""
+    e8 = torch.empty([0], dtype=torch.uint8, device=x.device)
+    return custom_ops.get_torch_ops().filtered_lrelu_act_(x, si if (si is not None and si.numel()) else e8, int(sx),
+                                                          int(sy), float(gain), float(slope), float(clamp),
+                                                          bool(write_signs))
 
 
 class _FilteredLReluHip(torch.autograd.Function):

@@ -147,28 +147,14 @@ def _out_size(size, up, pad0, pad1, taps, down):
 
 
 def _launch(x, f2, up, down, pads, flip, gain):
-    """One kernel launch with a 2-D filter f2 (already shaped [fh, fw])."""
-    lib = custom_ops.get_native()
+    """One kernel launch with a 2-D filter f2 (already shaped [fh, fw]) through the registered op
+    torch.ops.vfmvae.upfirdn2d (csrc/torch_ops.cpp over vfm_upfirdn2d; the reference plugin's
+    schema and checks, upfirdn2d.cpp:16-98)."""
     upx, upy = up
     downx, downy = down
     px0, px1, py0, py1 = pads
-    n, c, h, w = x.shape
-    fh, fw = f2.shape
-    oh = _out_size(h, upy, py0, py1, fh, downy)
-    ow = _out_size(w, upx, px0, px1, fw, downx)
-    if oh < 1 or ow < 1:
-        raise RuntimeError("output must be at least 1x1")
-    if x.numel() == 0:
-        raise RuntimeError("x has zero size")
-    if f2.dtype != torch.float32 or f2.device != x.device:
-        raise RuntimeError("f must be float32 and on the same device as x")
-    y = torch.empty([n, c, oh, ow], dtype=x.dtype, device=x.device, memory_format=_memory_format(x))
-    rc = lib.vfm_upfirdn2d(x.data_ptr(), y.data_ptr(), f2.data_ptr(), custom_ops.dtype_code(x),
-                           n, c, h, w, custom_ops.strides(x), oh, ow, custom_ops.strides(y),
-                           fh, fw, f2.stride(0), f2.stride(1), upx, upy, downx, downy, px0, py0,
-                           int(flip), float(gain), custom_ops.stream_ptr(x.device))
-    custom_ops.check(rc, "vfm_upfirdn2d")
-    return y
+    return custom_ops.get_torch_ops().upfirdn2d(x, f2, upx, upy, downx, downy, px0, px1, py0, py1, bool(flip),
+                                                float(gain))
 
 
 def _memory_format(x):
