@@ -112,6 +112,12 @@ def build(cfg_path, batch_gpu, device, world, graphs=True):
     return c, step
 
 
+def _fp32_mode():
+    from torch_utils import custom_ops
+    return {"f32x6": "f32x6 (three exact bf16 pieces per operand, six products, fp32 accumulation)",
+            "f32x3": "f32x3 OPT-IN (hi/lo, three products, ~2^-15.5 per product: below fp32)"}[custom_ops.F32_PRODUCTS]
+
+
 def _log(rank, msg):
     """Progress on stderr (the JSON line is the only stdout output)."""
     if rank == 0:
@@ -291,6 +297,9 @@ def main(argv=None):
                        "resolution": 256, "parallelism": f"dp{world}",
                        "decoder_ops": "torch" if args.force_ref_ops else "hip",
                        "d_phase_g_forward": "hip_graph" if args.graphs else "eager",
+                       "precision": ("bf16 where the reference autocasts (SigLIP2 tower, decoder blocks 3-5); the "
+                                     "reference's fp32 legs (decoder blocks 0-2, adapter, fp32 attention, LPIPS VGG16, "
+                                     "DINO D) with fp32-equivalent products: " + _fp32_mode()),
                        "gemm_table": tunable["table"] if tunable and tunable["mode"] == "use" else None},
             "roofline": roof,
             "step_mfma": step_mfma,

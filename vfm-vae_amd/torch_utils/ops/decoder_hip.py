@@ -151,13 +151,19 @@ def _gemm(A, B, **kw):
     return gemm_hip.try_gemm(A, B, auto=True, **kw)
 
 
+def _tn(t):
+    return {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16"}.get(t.dtype, str(t.dtype))
+
+
 def weight_grad_1x1(dy, x, wdt):
     """sum_b dy[b] @ x[b]^T in fp32 -> wdt ([O, P] x [I, P] per sample)."""
     dw = _gemm(dy, x.transpose(1, 2), out_dtype=torch.float32, reduce_batch=True,
                splits=_splits(dy.shape[1], x.shape[1], dy.shape[2], dy.shape[0]))
     if dw is None:
-        dw = torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32) if dy.dtype != torch.float32 else \
-            torch.bmm(dy, x.transpose(1, 2))
+        B, O, P = dy.shape
+        with kernel_timer.vendor_gemm(f"{_tn(dy)},1x1_dw", O, x.shape[1], P, B, dy.element_size()):
+            dw = torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32) if dy.dtype != torch.float32 else \
+                torch.bmm(dy, x.transpose(1, 2))
         dw = dw.sum(0)
     return dw.to(wdt)
 
@@ -180,7 +186,10 @@ class _Pointwise(torch.autograd.Function):
         ctx.save_for_backward(wc, x)
         ctx.wdt = w.dtype
         y = _gemm(wc, x, cache_a=True)
-        return y if y is not None else torch.bmm(wc.expand(B, O, I), x)
+        if y is None:
+            with kernel_timer.vendor_gemm(f"{_tn(x)},1x1", O, P, I, B, x.element_size()):
+                y = torch.bmm(wc.expand(B, O, I), x)
+        return y
 
     @staticmethod
     @torch.autograd.function.once_differentiable
@@ -196,7 +205,8 @@ class _Pointwise(torch.autograd.Function):
         if _wanted(ctx, 1):
             dx = _gemm(wc.t(), dy, cache_a=True)
             if dx is None:
-                dx = torch.bmm(wc.t().expand(B, I, O), dy)
+                with kernel_timer.vendor_gemm(f"{_tn(dy)},1x1_dx", I, P, O, B, dy.element_size()):
+                    dx = torch.bmm(wc.t().expand(B, I, O), dy)
         return dw, dx
 
 
@@ -576,7 +586,8 @@ class _ConvNeXtMLP(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dm = _gemm(w1c.t(), dh)
             if dm is None:
-                dm = torch.bmm(w1c.t().expand(B, C, O), dh)
+                with kernel_timer.vendor_gemm(f"{_tn(dh)},1x1_dx", C, dh.shape[2], O, B, dh.element_size()):
+                    dm = torch.bmm(w1c.t().expand(B, C, O), dh)
         dx = dout if ctx.needs_input_grad[7] and not _stash_residual(ctx.slot, dout) else None
         return dm, dw1, ds, db1, dw2, db2, dgm, dx, None
 

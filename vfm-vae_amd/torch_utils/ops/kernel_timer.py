@@ -94,6 +94,15 @@ def region(name, nbytes=0, flops=0, bound="hbm"):
     return _timed(name, nbytes, flops, bound)
 
 
+def vendor_gemm(tag, M, N, K, z=1, esize=2):
+    """Region around a library GEMM (hipBLASLt through torch.matmul / bmm / addmm) with its
+    algorithmic FLOPs and bytes (A, B, C once each), so the bench can rank the vendor kernels next
+    to ours; names start with `vendor_gemm<`."""
+    if not _enabled:
+        return _NULL
+    return region(f"vendor_gemm<{tag}>", esize * z * (M * K + K * N + M * N), 2.0 * z * M * N * K, "mfma")
+
+
 def summary():
     torch.cuda.synchronize()
     out = {}
@@ -151,11 +160,7 @@ def rocprof_name(region):
     return pat.format(T=T, K=K)
 
 
-def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None):
-    s = summary()
-    if not s:
-        return None
-    name, r = max(s.items(), key=lambda kv: kv[1]["total_ms"])
+def _roof(name, r, hbm_peak_gbs, mfma_peak_tflops):
     t = r["total_ms"] / 1e3
     note = None
     if r["bound"] == "mfma":
@@ -169,9 +174,26 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None):
         elif "f32x3" in name:
             peak = round(mfma_peak_tflops / 3, 1)
             note = "achieved = fp32 FLOPs of the op / time; peak = dense bf16 MFMA peak / 3 (opt-in f32x3 split)"
+        elif "<f32" in name:
+            peak = 157.3
+            note = "exact fp32 MFMA peak"
     else:
         achieved = r["bytes"] / t / 1e9
         peak, unit = hbm_peak_gbs, "GB/s"
+    return achieved, peak, unit, note
+
+
+def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None, steps=None):
+    """The roofline object of the bench line: our kernel (timer region) with the largest total
+    time, plus `vendor_top`, the library GEMM region with the largest total time (ranked the same
+    way; hipBLASLt kernels are not ours, so they never become the roofline kernel itself)."""
+    s = summary()
+    if not s:
+        return None
+    own = {k: v for k, v in s.items() if not k.startswith("vendor_gemm<")}
+    vend = {k: v for k, v in s.items() if k.startswith("vendor_gemm<")}
+    name, r = max(own.items(), key=lambda kv: kv[1]["total_ms"])
+    achieved, peak, unit, note = _roof(name, r, hbm_peak_gbs, mfma_peak_tflops)
     roc = rocprof_name(name)
     traffic = None
     if traffic_table and roc:
@@ -180,12 +202,24 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None):
         n = sum(h[0] for h in hits)
         if n:
             traffic = int(sum(c * t for c, t in hits) / n)
-    return {"bound": r["bound"], "achieved": round(achieved, 1), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": name, "rocprof_kernel": roc,
-            "peak_note": note,
-            "launches": r["launches"], "timed_launches": r["timed_launches"],
-            "avg_us": round(r["total_ms"] * 1e3 / r["launches"], 2),
-            "bytes_per_launch": int(r["bytes"] / r["launches"]),
-            "all_kernels": {k: {"ms": round(v["total_ms"], 3), "launches": v["launches"],
-                                "GBps": round(v["bytes"] / max(v["total_ms"], 1e-9) / 1e6, 1)}
-                            for k, v in sorted(s.items(), key=lambda kv: -kv[1]["total_ms"])}}
+    bpl = int(r["bytes"] / r["launches"])
+    out = {"bound": r["bound"], "achieved": round(achieved, 1), "peak": peak, "unit": unit,
+           "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": name, "rocprof_kernel": roc,
+           "peak_note": note,
+           "launches": r["launches"], "timed_launches": r["timed_launches"],
+           "avg_us": round(r["total_ms"] * 1e3 / r["launches"], 2),
+           "bytes_per_launch": bpl,
+           "flops_per_launch": int(r["flops"] / r["launches"]),
+           "traffic_over_algorithmic": round(traffic / bpl, 3) if traffic and bpl else None}
+    if vend:
+        vn, vr = max(vend.items(), key=lambda kv: kv[1]["total_ms"])
+        va, vp, vu, vnote = _roof(vn, vr, hbm_peak_gbs, mfma_peak_tflops)
+        out["vendor_top"] = {"kernel": vn, "achieved": round(va, 1), "peak": vp, "unit": vu, "frac": round(va / vp, 4),
+                             "ms_total": round(vr["total_ms"], 3), "launches": vr["launches"],
+                             "avg_us": round(vr["total_ms"] * 1e3 / vr["launches"], 2)}
+        out["vendor_gemm_ms_total"] = round(sum(v["total_ms"] for v in vend.values()), 3)
+    out["all_kernels"] = {k: {"ms": round(v["total_ms"], 3), "launches": v["launches"],
+                              "GBps": round(v["bytes"] / max(v["total_ms"], 1e-9) / 1e6, 1),
+                              "TFps": round(v["flops"] / max(v["total_ms"], 1e-9) / 1e9, 1)}
+                          for k, v in sorted(s.items(), key=lambda kv: -kv[1]["total_ms"])}
+    return out

@@ -16,6 +16,17 @@ residual add) is one HIP row kernel (`vit_hip`, csrc/vit.hip).
 import torch
 import torch.nn.functional as F
 
+from . import kernel_timer
+
+
+def _vg(x, w, tag):
+    """Timer region of a library GEMM x [.., K] @ w^T [K, N] (kernel_timer.vendor_gemm)."""
+    if not kernel_timer.is_enabled() or not x.is_cuda:
+        return kernel_timer._NULL
+    M = x.numel() // x.shape[-1]
+    return kernel_timer.vendor_gemm(f"{'bf16' if x.dtype == torch.bfloat16 else 'f32'},{tag}", M, w.shape[0],
+                                    x.shape[-1], 1, x.element_size())
+
 
 def _frozen(*ts):
     """ROCm tensors that need no autograd graph."""
@@ -29,7 +40,8 @@ def patch_embed(pixels, weight, bias, patch, compute_dtype):
     x = pixels[:, :, :gh * patch, :gw * patch].to(compute_dtype)
     x = x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * patch * patch)
     w = weight.reshape(weight.shape[0], -1).to(compute_dtype)
-    y = torch.matmul(x, w.t())
+    with _vg(x, w, "vit_patch"):
+        y = torch.matmul(x, w.t())
     if bias is not None:
         y = y + bias.to(compute_dtype)
     return y
@@ -40,15 +52,17 @@ def linear(x, w, b=None):
     if x.is_cuda and x.dtype == torch.float32:
         from . import linear as linear_op
         return linear_op.linear(x, w, b)
-    if b is not None:
-        return torch.addmm(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
-    return torch.matmul(x, w.t())
+    with _vg(x, w, "vit_linear"):
+        if b is not None:
+            return torch.addmm(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
+        return torch.matmul(x, w.t())
 
 
 def linear_gelu_tanh(x, w, b=None):
     """gelu_tanh(x @ w^T + b): GEMM with the GELU_BIAS epilogue on ROCm (frozen towers)."""
     if b is not None and x.dtype != torch.float32 and _frozen(x, w, b):
-        y = torch._addmm_activation(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
+        with _vg(x, w, "vit_fc1_gelu"):
+            y = torch._addmm_activation(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
         return y.reshape(*x.shape[:-1], w.shape[0])
     return F.gelu(linear(x, w, b), approximate="tanh")
 
