@@ -17,8 +17,10 @@
 // -> RuntimeError naming the launcher. Kernels are enqueued on the current HIP stream, no host sync.
 #include <torch/library.h>
 #include <ATen/ATen.h>
-#include <ATen/hip/HIPContext.h>
-#include <c10/hip/HIPGuard.h>
+// ROCm builds of PyTorch present HIP devices as DeviceType::CUDA: the guard and stream types are the
+// "masquerading" ones (c10::hip::HIPGuardImpl would reject a cuda device)
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <climits>
 #include <tuple>
@@ -39,7 +41,7 @@ int dtype_code(const at::Tensor& t) {
 }
 
 void* stream_of(const at::Tensor& t) {
-    return (void*)at::hip::getCurrentHIPStream(t.device().index()).stream();
+    return (void*)c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 void check_rc(int rc, const char* name) { TORCH_CHECK(rc == VFM_OK, name, " failed with code ", rc); }
@@ -77,7 +79,7 @@ at::Tensor upfirdn2d(const at::Tensor& x, const at::Tensor& f, int64_t upx, int6
     TORCH_CHECK(f.size(0) >= 1 && f.size(1) >= 1, "f must be at least 1x1");
     TORCH_CHECK(upx >= 1 && upy >= 1, "upsampling factor must be at least 1");
     TORCH_CHECK(downx >= 1 && downy >= 1, "downsampling factor must be at least 1");
-    const c10::hip::OptionalHIPGuard guard(x.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
     const int outW = ((int)x.size(3) * (int)upx + (int)padx0 + (int)padx1 - (int)f.size(1) + (int)downx) / (int)downx;
     const int outH = ((int)x.size(2) * (int)upy + (int)pady0 + (int)pady1 - (int)f.size(0) + (int)downy) / (int)downy;
     TORCH_CHECK(outW >= 1 && outH >= 1, "output must be at least 1x1");
@@ -116,7 +118,7 @@ at::Tensor bias_act(const at::Tensor& x, const at::Tensor& b, const at::Tensor& 
     TORCH_CHECK(xref.numel() == 0 || has_same_layout(xref, x), "xref must have the same layout as x");
     TORCH_CHECK(yref.numel() == 0 || has_same_layout(yref, x), "yref must have the same layout as x");
     TORCH_CHECK(dy.numel() == 0 || has_same_layout(dy, x), "dy must have the same layout as x");
-    const c10::hip::OptionalHIPGuard guard(x.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
     at::Tensor y = at::empty_like(x);
     TORCH_CHECK(has_same_layout(y, x), "y must have the same layout as x");
     if (x.numel() == 0) return y;
@@ -137,7 +139,7 @@ std::tuple<at::Tensor, at::Tensor, int64_t> filtered_lrelu(const at::Tensor& x, 
                                                            int64_t sy, double gain, double slope, double clamp,
                                                            bool flip_filters, bool writeSigns) {
     TORCH_CHECK(x.is_cuda(), "x must reside on CUDA device");
-    const c10::hip::OptionalHIPGuard guard(x.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
     TORCH_CHECK(fu.device() == x.device() && fd.device() == x.device() && b.device() == x.device(),
                 "all input tensors must reside on the same device");
     TORCH_CHECK(fu.dtype() == at::kFloat && fd.dtype() == at::kFloat, "fu and fd must be float32");
@@ -190,7 +192,7 @@ std::tuple<at::Tensor, at::Tensor, int64_t> filtered_lrelu(const at::Tensor& x, 
 at::Tensor filtered_lrelu_act(const at::Tensor& x, const at::Tensor& si, int64_t sx, int64_t sy, double gain,
                               double slope, double clamp, bool writeSigns) {
     TORCH_CHECK(x.is_cuda(), "x must reside on CUDA device");
-    const c10::hip::OptionalHIPGuard guard(x.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
     TORCH_CHECK(x.dim() == 4, "x must be rank 4");
     TORCH_CHECK(x.size(0) * x.size(1) <= INT_MAX && x.size(2) <= INT_MAX && x.size(3) <= INT_MAX, "x is too large");
     TORCH_CHECK(x.numel() > 0, "x is empty");
