@@ -86,31 +86,39 @@ def preferred(A, M, N, reduce_batch=False):
 
 def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
     """Kernel and split of one product: ("g8", kchunk) -- the 256-tile kernel, kchunk virtual
-    K-tiles per split (0: no split) -- or ("g128", splits) -- the 128-tile kernel."""
+    K-tiles per split (0: no split) -- or ("g128", splits) -- the 128-tile kernel. The rules follow
+    tools_dev/gemm6bench.py on MI355X (profiles/r3_f_gemm6bench.txt, f32x6):
+      * batch-reduced weight gradients: 256-tile split-K over the batch-concatenated K, 16 splits
+        (b2 dW 2048x512x1024x32: 560 vs 583 us on the 128-tile kernel; b0: 66 vs 89 us);
+      * fewer than SPLIT_TILES 256-tiles (token-major linears with a small output width, the DINO
+        tower's 6304 x 384 / x 1152 products): the 128-tile kernel, which splits fp32 operands in
+        registers and fills the chip with 4x the tiles (6304x384x1536: 95 us vs 101 us for the best
+        256-tile split-K);
+      * otherwise the 256-tile kernel."""
     if not FAST or K % 64:
         return "g128", splits
     nterm = 1 if dtype == torch.bfloat16 else (6 if custom_ops.f32_precision()[1] == 3 else 3)
     zo = 1 if reduce_batch else z
     V = nterm * (z if reduce_batch else 1) * (K // 64)            # virtual K-tiles per output
     tiles = -(-M // 256) * -(-N // 256) * zo
-    if reduce_batch or splits > 1:
+    if reduce_batch:
+        if min(M, N) >= 256 and (SPLIT8 or auto):
+            return "g8", max(4, -(-V // REDUCE_SPLITS))
+        return "g128", splits
+    if splits > 1:
         if not (SPLIT8 and min(M, N) >= 256):
             return "g128", splits
         S0 = max(1, -(-512 // tiles))
         return "g8", max(4, -(-V // S0))
     if M * N < FAST_MIN_MN:
         return "g128", splits
-    if auto and tiles < SPLIT_TILES and V >= 2 * SPLIT_MIN_VT:
-        # few 256-tiles (token-major linears with a small output width, e.g. the DINO tower's
-        # 6304 x 384 products): split the virtual K-tiles so ~384 workgroups run
-        S = min(-(-384 // tiles), V // SPLIT_MIN_VT)
-        if S > 1:
-            return "g8", -(-V // S)
+    if auto and tiles < SPLIT_TILES:
+        return "g128", splits
     return "g8", 0
 
 
-SPLIT_TILES = 160           # fewer 256-tiles than this: split-K on the 256-tile kernel (auto routing)
-SPLIT_MIN_VT = 8            # at least this many virtual K-tiles per split
+SPLIT_TILES = 128           # fewer 256-tiles than this: the 128-tile kernel (auto routing)
+REDUCE_SPLITS = 16          # splits of a batch-reduced weight gradient on the 256-tile kernel
 
 
 def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=0.0, out_dtype=None,
