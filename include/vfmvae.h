@@ -283,6 +283,9 @@ int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int prec
               int kchunk, int reduce_batch, void* stream);
 int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
                                int reduce_batch);  /* -1: too large */
+/* K-tile staging schedule of vfm_gemm8 (process-wide A/B switch for microbenchmarks): 1 = half-tiles
+ * restaged two K-tiles ahead (default), 0 = one K-tile ahead. Returns the previous setting. */
+int vfm_gemm8_set_schedule(int deep);
 /* fp32 -> bf16 pieces of one GEMM operand along its reduction dimension K (precision VFM_F32: 3
  * pieces hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid), x = hi + mid + lo exactly;
  * VFM_F32X3: 2 pieces hi, lo). kcont = 1: src [R][K] (row stride ld) -> dst [R][np K];

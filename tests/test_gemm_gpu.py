@@ -165,12 +165,24 @@ def test_gemm_unsupported_shape_returns_none():
     assert gemm_hip.try_gemm(A, B) is None
 
 
+@pytest.fixture(params=[0, 1], ids=["sched1", "sched2"])
+def g8_schedule(request):
+    """Both K-tile staging schedules of gemm8 (one / two K-tiles ahead)."""
+    from torch_utils import custom_ops
+    lib = custom_ops.get_native()
+    prev = lib.vfm_gemm8_set_schedule(request.param)
+    yield request.param
+    lib.vfm_gemm8_set_schedule(prev)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
-@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128), (256, 256, 64), (1000, 264, 704)])
-def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, monkeypatch):
-    """The 256-tile LDS-DMA kernel (csrc/gemm8.hip, 4-phase pipeline) and, for fp32, the piece split
-    walked as 6 product terms; K = 64 is the single-K-tile-per-term path of gemm8's schedule."""
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128), (256, 256, 64), (1000, 264, 704),
+                                   (512, 512, 128)])
+def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, monkeypatch, g8_schedule):
+    """The 256-tile LDS-DMA kernel (csrc/gemm8.hip, 4-phase pipeline, both staging schedules) and, for
+    fp32, the piece split walked as 6 product terms; bf16 K = 64 / 128 are the one- and two-K-tile
+    paths of the schedules' prologue and tail."""
     from torch_utils.ops import gemm_hip, kernel_timer
     kernel = "gemm8"
     monkeypatch.setattr(gemm_hip, "FAST_MIN_MN", 0)
@@ -211,7 +223,7 @@ def test_gemm_fast_epilogue_batched(dtype):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("act", [None, "gelu_tanh"])
 @pytest.mark.parametrize("bias_dim", [None, 1, 0])
-def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch):
+def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch, g8_schedule):
     """gemm8's fp32-output epilogue: full 256 x 256 tiles go through the LDS-staged 16-B store form
     (alpha, row / column bias, GELU), the ragged last tiles through the per-element form."""
     from torch_utils.ops import gemm_hip
@@ -239,7 +251,7 @@ def test_gemm_generic_path_when_fast_off(monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("O,I,P,Bn", [(512, 256, 1024, 6), (304, 264, 320, 3)])
-def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, monkeypatch):
+def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, monkeypatch, g8_schedule):
     """sum_b dy[b] . x[b]^T on gemm8's split-K over the batch-concatenated K (opt-in path,
     VFM_GEMM8_SPLIT=1): fp32 partials + fixed-order reduce; every operand layout; ragged M/N."""
     from torch_utils.ops import gemm_hip, kernel_timer
@@ -260,7 +272,7 @@ def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, mon
 
 
 @pytest.mark.parametrize("M,N,K", [(768, 512, 8192), (256, 300, 2048)])
-def test_gemm8_split_k(M, N, K, monkeypatch):
+def test_gemm8_split_k(M, N, K, monkeypatch, g8_schedule):
     """Few output tiles over a deep K (the adapter's weight gradients): split-K on gemm8 with a bias
     epilogue in the reduce pass."""
     from torch_utils.ops import gemm_hip

@@ -59,6 +59,7 @@ for s in "$@"; do
     attnbench) timeout -k 10 300 python tools_dev/attnbench.py > $out/attnbench.log 2>&1 ;;
     gemmbench) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;
     gemm6bench) timeout -k 10 300 python tools_dev/gemm6bench.py > $out/gemm6bench.log 2>&1 ;;
+    g8sched) timeout -k 10 300 python tools_dev/g8sched.py > $out/g8sched.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

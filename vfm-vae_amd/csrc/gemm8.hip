@@ -136,7 +136,18 @@ __device__ __forceinline__ bf16x8 frag16(const unsigned char* img, int blk, int 
 
 #define VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-template <bool AK, bool BKC, bool OUTF32>
+// wait until at most n half-tiles (2 DMA each) of this wave are in flight (n wave-uniform)
+__device__ __forceinline__ void vm_halves(int n) {
+    switch (n) {
+    case 4: VMCNT(8); break;
+    case 3: VMCNT(6); break;
+    case 2: VMCNT(4); break;
+    case 1: VMCNT(2); break;
+    default: VMCNT(0); break;
+    }
+}
+
+template <bool AK, bool BKC, bool OUTF32, bool DEEP>
 __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -191,6 +202,92 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
         else if (h == 2) dma_half<BKC, false>(buf + OFF_BHI, sr.Bb, a.ldb, n0, a.N, sr.kb, 1, tid);
         else dma_half<AK, true>(buf + OFF_AHI, sr.Ab, a.lda, m0, a.M, sr.ka, 1, tid);
     };
+    bf16x8 af[4][2], bl[2][2], bh[2][2];        // A quadrant rows; B_lo / B_hi columns (both kept)
+    // half-tile h, phase p: which fragments phase p reads (A_lo + B_lo at p0, B_hi at p1, A_hi at p2;
+    // A every second phase) and multiplies (quadrant (qm, qn))
+    auto phase_math = [&](const unsigned char* buf, int p) {
+        const int qm = p >> 1;                          // 0 0 1 1
+        const int qn = (p == 1 || p == 2) ? 1 : 0;      // 0 1 1 0
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        af[i][s], qn ? bh[j][s] : bl[j][s], acc[4 * qm + i][2 * qn + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+        (void)buf;
+    };
+    auto phase_reads = [&](const unsigned char* buf, int p) {
+        if (p == 0 || p == 2) {
+            const unsigned char* ai = buf + (p ? OFF_AHI : OFF_ALO);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) af[i][s] = frag16<AK>(ai, 4 * wm + i, s, lane);
+        }
+        if (p == 0 || p == 1) {                         // B_lo read once (p0, reused p3), B_hi once (p1, reused p2)
+            const unsigned char* bi = buf + (p ? OFF_BHI : OFF_BLO);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if (p == 0) bl[j][s] = frag16<BKC>(bi, 2 * wn + j, s, lane);
+                    else bh[j][s] = frag16<BKC>(bi, 2 * wn + j, s, lane);
+                }
+        }
+    };
+    if (DEEP) {
+        // Two K-tiles ahead: the fragments of a half-tile live in VGPRs after their phase, so its LDS
+        // slot is restaged for K-tile t+2 two phases later (WAR >= 2 phases with the rows one barrier
+        // apart). Phase p of tile t issues p0: B_hi(t+1), p1: A_hi(t+1) (buffer (t+1)&1), p2:
+        // A_lo(t+2), p3: B_lo(t+2) (buffer t&1); the counted waits leave 4 half-tiles (8 DMA) in
+        // flight: each half-tile is issued 5-6 phases before its read instead of 2-4.
+        {
+            const Src s0 = src_of(0);
+            issue(s0, 0, 0);
+            issue(s0, 0, 1);
+            issue(s0, 0, 2);
+            issue(s0, 0, 3);
+        }
+        Src s1 = src_of(KT > 1 ? 1 : 0);
+        if (KT > 1) {
+            issue(s1, 1, 0);
+            issue(s1, 1, 1);
+        }
+        vm_halves(2 + (KT > 1 ? 2 : 0));            // A_lo(0), B_lo(0)
+        __builtin_amdgcn_s_barrier();
+        if (wm == 1) __builtin_amdgcn_s_barrier();
+        for (int t = 0; t < KT; ++t) {
+            const unsigned char* buf = lds + (t & 1) * BUF;
+            const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
+            const Src s2 = src_of(n2 ? t + 2 : t);
+            // p0: issue B_hi(t+1); read A_lo(t), B_lo(t); wait for B_hi(t)
+            if (n1) issue(s1, t + 1, 2);
+            phase_reads(buf, 0);
+            vm_halves(1 + (n1 ? 3 : 0));
+            phase_math(buf, 0);
+            // p1: issue A_hi(t+1); read B_hi(t); wait for A_hi(t)
+            if (n1) issue(s1, t + 1, 3);
+            phase_reads(buf, 1);
+            vm_halves(n1 ? 4 : 0);
+            phase_math(buf, 1);
+            // p2: issue A_lo(t+2); read A_hi(t)
+            if (n2) issue(s2, t + 2, 0);
+            phase_reads(buf, 2);
+            phase_math(buf, 2);
+            // p3: issue B_lo(t+2); wait for A_lo(t+1), B_lo(t+1)
+            if (n2) issue(s2, t + 2, 1);
+            if (n1) vm_halves(2 + (n2 ? 2 : 0));
+            phase_math(buf, 3);
+            s1 = s2;
+        }
+    } else {
     {
         const Src s0 = src_of(0);
         issue(s0, 0, 0);
@@ -204,34 +301,14 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     // wave-row's 16 MFMAs overlap the other's DMA issue + fragment reads (see the header)
     if (wm == 1) __builtin_amdgcn_s_barrier();
 
-    bf16x8 af[4][2], bl[2][2], bh[2][2];        // A quadrant rows; B_lo / B_hi columns (both kept)
     for (int t = 0; t < KT; ++t) {
         const unsigned char* buf = lds + (t & 1) * BUF;
         const bool nxt = t + 1 < KT;
         const Src sn = src_of(nxt ? t + 1 : t);
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const int qm = p >> 1;                          // 0 0 1 1
-            const int qn = (p == 1 || p == 2) ? 1 : 0;      // 0 1 1 0
             if (nxt) issue(sn, t + 1, p);
-            // this phase's fragments (A every second phase)
-            if (p == 0 || p == 2) {
-                const unsigned char* ai = buf + (qm ? OFF_AHI : OFF_ALO);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) af[i][s] = frag16<AK>(ai, 4 * wm + i, s, lane);
-            }
-            if (p == 0 || p == 1) {                         // B_lo read once (p0, reused p3), B_hi once (p1, reused p2)
-                const unsigned char* bi = buf + (p ? OFF_BHI : OFF_BLO);
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        if (p == 0) bl[j][s] = frag16<BKC>(bi, 2 * wn + j, s, lane);
-                        else bh[j][s] = frag16<BKC>(bi, 2 * wn + j, s, lane);
-                    }
-            }
+            phase_reads(buf, p);
             // wait for the NEXT phase's half-tile (see the header), then the phase barrier
             if (nxt) {
                 if (p == 0 || p == 1 || p == 3) VMCNT(4);
@@ -239,21 +316,9 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
                 if (p == 0) VMCNT(2);
                 else if (p == 1) VMCNT(0);
             }
-            __builtin_amdgcn_s_barrier();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-                        acc[4 * qm + i][2 * qn + j] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], qn ? bh[j][s] : bl[j][s],
-                                                                    acc[4 * qm + i][2 * qn + j], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_s_barrier();
+            phase_math(buf, p);
         }
+    }
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();
     VMCNT(0);
@@ -396,17 +461,25 @@ __global__ __launch_bounds__(256) void gemm8_reduce(G8Args a) {
     st(cp, v);
 }
 
-template <bool AK, bool BKC, bool OUTF32>
-int launch8(const G8Args& a, int batch, hipStream_t st) {
-    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+int g_sched = 0;   // 1: two-K-tiles-ahead staging (DEEP), 0: one tile ahead (vfm_gemm8_set_schedule)
+
+template <bool AK, bool BKC, bool OUTF32, bool DEEP>
+void launch8k(const G8Args& a, int nwg, int zo, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32>,
+        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32, DEEP>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
         attr = true;
     }
+    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32, DEEP>), dim3(nwg, zo * a.S), dim3(THREADS), 2 * BUF, st, a);
+}
+
+template <bool AK, bool BKC, bool OUTF32>
+int launch8(const G8Args& a, int batch, hipStream_t st) {
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const int zo = a.reduce ? 1 : batch;
-    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32>), dim3(nwg, zo * a.S), dim3(THREADS), 2 * BUF, st, a);
+    if (g_sched) launch8k<AK, BKC, OUTF32, true>(a, nwg, zo, st);
+    else launch8k<AK, BKC, OUTF32, false>(a, nwg, zo, st);
     if (a.ws) {
         const long long MN = (long long)a.M * a.N;
         hipLaunchKernelGGL(gemm8_reduce<OUTF32>, dim3((unsigned)((MN + 255) / 256), zo), dim3(256), 0, st, a);
@@ -522,6 +595,14 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
     if (!a_kcont && b_kcont) VFM_G8(false, true);
     VFM_G8(false, false);
 #undef VFM_G8
+}
+
+// K-tile staging schedule of vfm_gemm8 (A/B switch for microbenchmarks): 1 = two K-tiles ahead
+// (default), 0 = one K-tile ahead. Returns the previous value.
+extern "C" int vfm_gemm8_set_schedule(int deep) {
+    const int prev = g_sched;
+    g_sched = deep ? 1 : 0;
+    return prev;
 }
 
 // fp32 workspace floats vfm_gemm8 needs for (precision, M, N, K, batch, kchunk, reduce_batch); 0 = none
