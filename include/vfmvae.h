@@ -223,6 +223,13 @@ int vfm_attention_fwd(const void* q, const void* k, const void* v, void* o, int 
  * when mask is given (bias / mask may be null). */
 int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int precision, int ldw, const float* bias,
                          const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int relu, void* stream);
+/* Input gradient of a 3x3 / pad 1 conv with few input channels (the VGG16 image layer, C = 3), exact fp32
+ * FMAs on the VALU (replaces torch.nn.grad.conv2d_input = MIOpen fp32 Winograd there):
+ *   dx[b, c, y, x] = sum_{o, ky, kx} w[o, c, ky, kx] dz[b, y + 1 - ky, x + 1 - kx, o].
+ * dz NHWC fp32 [B, H, W, K] (K % 4 == 0, K <= 128, 16-B aligned), w fp32 [K][C][3][3] (torch layout of
+ * the forward weight), dx NCHW fp32 [B, C, H, W], C <= 4 (else VFM_NO_KERNEL). Deterministic. */
+int vfm_conv3x3_dgrad_small_f32(const float* dz, const float* w, float* dx, int B, int H, int W, int C, int K,
+                                void* stream);
 
 /* fp32 attention with gradients (replaces F.scaled_dot_product_attention on the fp32 paths of the
  * generator: fusion-adapter AttnProjection, reference networks/utils/ldm_utils.py:55-93 (encode,

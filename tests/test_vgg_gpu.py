@@ -90,3 +90,21 @@ def test_vgg16_taps_forward_backward(res):
     assert _rel(x.grad, gx) < 1e-4
     l2 = float((x.grad.double() - xr.grad).norm() / xr.grad.norm())
     assert l2 < 2e-2, l2
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 37, 70), (1, 64, 64), (3, 5, 130)])
+def test_image_layer_input_gradient(B, H, W):
+    """The VGG16 image layer's input gradient (3 <- 64 channels) on the VALU kernel
+    vfm_conv3x3_dgrad_small_f32 vs the fp64 torch conv2d_input: fp32 FMAs over 576 terms, 2e-6 of
+    max |ref|, and within 2x of the exact-fp32 torch conv's own error (+1e-7)."""
+    from torch_utils.ops import vgg_hip
+    g = torch.Generator(device=DEV).manual_seed(B * H + W)
+    w = torch.randn(64, 3, 3, 3, generator=g, device=DEV) * 0.1
+    dz = torch.randn(B, H, W, 64, generator=g, device=DEV)
+    out = vgg_hip.image_grad(dz, w, (B, 3, H, W))
+    ref = torch.nn.grad.conv2d_input((B, 3, H, W), w.double(), dz.permute(0, 3, 1, 2).double(), padding=1)
+    with torch.backends.cudnn.flags(enabled=False):
+        t32 = torch.nn.grad.conv2d_input((B, 3, H, W), w, dz.permute(0, 3, 1, 2).contiguous(), padding=1)
+    e = _rel(out, ref)
+    assert e < 2e-6, e
+    assert e <= 2 * _rel(t32, ref) + 1e-7, (e, _rel(t32, ref))

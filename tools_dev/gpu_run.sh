@@ -55,6 +55,7 @@ for s in "$@"; do
     cparents) timeout -k 10 600 python tools_dev/copy_parents.py > $out/cparents.log 2>&1 ;;
     tprof)   timeout -k 10 600 python tools_dev/torchprof.py --out $out/tp > $out/tprof.log 2>&1 ;;
     gemmbench8) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;
+    ptests)  timeout -k 10 ${PT_TIMEOUT:-900} python -u -m pytest $PT -m gpu -v -s --timeout ${PT_CASE:-240} --timeout-method thread > $out/ptests.log 2>&1 ;;
     ptest)   timeout -k 10 ${PT_TIMEOUT:-900} python -u -m pytest $PT -m gpu -v --timeout ${PT_CASE:-240} --timeout-method thread > $out/ptest.log 2>&1 ;;
     attnbench) timeout -k 10 300 python tools_dev/attnbench.py > $out/attnbench.log 2>&1 ;;
     gemmbench) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;

@@ -321,3 +321,108 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int pr
     if (np == 3) return (Cout % 128 == 0) ? launch<128, 3>(a, st) : launch<64, 3>(a, st);
     return (Cout % 128 == 0) ? launch<128, 2>(a, st) : launch<64, 2>(a, st);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Input gradient of the image layer (3 -> 64 channels) of the VGG16 stack: few output channels, so
+// neither the implicit GEMM above (Cout % 64) nor MFMA fits; exact fp32 FMAs on the VALU
+// (replaces the MIOpen fp32 Winograd that torch.nn.grad.conv2d_input ran here).
+//   dx[b, c, y, x] = sum_{o, ky, kx} w[o, c, ky, kx] dz[b, y + 1 - ky, x + 1 - kx, o]   (zero outside)
+// dz NHWC fp32 [B, H, W, K] (K % 4 == 0, K <= 128), w fp32 [K][C][3][3] (the forward weight, torch
+// layout), dx NCHW fp32 [B, C, H, W], C <= 4. A workgroup = 64 pixels of one image row x 4 channel
+// groups: the 3 input rows x 66 pixels it touches are staged in LDS once (coalesced 16-B loads, pixel
+// stride K + 4 floats so the 16 lanes of a ds_read_b128 group hit 16 different bank slots), each
+// thread sums K / 4 channels of its pixel for all C outputs, and the 4 partial sums per pixel are
+// combined with two xor-shuffles in a fixed order (deterministic).
+namespace {
+
+constexpr int DG_PX = 64;
+
+template <int C>
+__global__ __launch_bounds__(256) void conv3x3_dgrad_small(const float* __restrict__ dz, const float* __restrict__ w,
+                                                           float* __restrict__ dx, int H, int W, int K) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int KP = K + 4;                                   // padded pixel stride (floats)
+    float* tile = sm;                                       // [3][DG_PX + 2][KP]
+    float* ws = sm + 3 * (DG_PX + 2) * KP;                  // [9][C][K]: ws[(tap * C + c) * K + o]
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * DG_PX, y = blockIdx.y, b = blockIdx.z;
+    for (int i = tid; i < 9 * C * K; i += 256) {
+        const int o = i % K, c = (i / K) % C, tap = i / (K * C);
+        ws[i] = w[((long long)o * C + c) * 9 + tap];
+    }
+    const int K4 = K >> 2;
+    for (int i = tid; i < 3 * (DG_PX + 2) * K4; i += 256) {
+        const int q = i % K4, px = (i / K4) % (DG_PX + 2), r = i / (K4 * (DG_PX + 2));
+        const int yy = y + 1 - r, xx = x0 - 1 + px;        // row r holds dz row y + 1 - r (ky = r)
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+            v = *reinterpret_cast<const float4*>(dz + (((long long)b * H + yy) * W + xx) * K + 4 * q);
+        *reinterpret_cast<float4*>(tile + (r * (DG_PX + 2) + px) * KP + 4 * q) = v;
+    }
+    __syncthreads();
+    const int px = tid & (DG_PX - 1), cg = tid >> 6;        // pixel, channel group (K / 4 channels each)
+    const int kq = K >> 2, kb = cg * kq;
+    float acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            // x' + 1 - kx = x0 + px + 1 - kx  ->  staged column px + 2 - kx
+            const float* src = tile + (ky * (DG_PX + 2) + px + 2 - kx) * KP + kb;
+            const float* wt = ws + (ky * 3 + kx) * C * K + kb;
+            for (int o = 0; o < kq; o += 4) {
+                const float4 d = *reinterpret_cast<const float4*>(src + o);
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const float4 wv = *reinterpret_cast<const float4*>(wt + c * K + o);
+                    acc[c] = fmaf(d.x, wv.x, acc[c]);
+                    acc[c] = fmaf(d.y, wv.y, acc[c]);
+                    acc[c] = fmaf(d.z, wv.z, acc[c]);
+                    acc[c] = fmaf(d.w, wv.w, acc[c]);
+                }
+            }
+        }
+    // combine the 4 channel groups (lanes px, px+64, ... live in different waves): through LDS
+    __syncthreads();
+    float* red = sm;                                        // [4][C][DG_PX]
+#pragma unroll
+    for (int c = 0; c < C; ++c) red[(cg * C + c) * DG_PX + px] = acc[c];
+    __syncthreads();
+    if (tid < DG_PX * C) {
+        const int p = tid % DG_PX, c = tid / DG_PX, xx = x0 + p;
+        const float v = ((red[(0 * C + c) * DG_PX + p] + red[(1 * C + c) * DG_PX + p]) + red[(2 * C + c) * DG_PX + p]) +
+                        red[(3 * C + c) * DG_PX + p];
+        if (xx < W) dx[(((long long)b * C + c) * H + y) * W + xx] = v;
+    }
+}
+
+template <int C>
+int launch_dgrad(const float* dz, const float* w, float* dx, int B, int H, int W, int K, hipStream_t st) {
+    const size_t lds = (3 * (DG_PX + 2) * (size_t)(K + 4) + 9 * (size_t)C * K) * 4;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)conv3x3_dgrad_small<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (3 * (DG_PX + 2) * (128 + 4) + 9 * 4 * 128) * 4);
+        attr = true;
+    }
+    hipLaunchKernelGGL((conv3x3_dgrad_small<C>), dim3((W + DG_PX - 1) / DG_PX, H, B), dim3(256), lds, st, dz, w, dx, H, W,
+                       K);
+    return launch_status();
+}
+
+}  // namespace
+
+extern "C" int vfm_conv3x3_dgrad_small_f32(const float* dz, const float* w, float* dx, int B, int H, int W, int C,
+                                           int K, void* stream) {
+    if (!dz || !w || !dx || B <= 0 || H <= 0 || W <= 0 || B > 65535 || H > 65535) return VFM_ERR_ARGS;
+    if (C < 1 || C > 4 || K % 4 || K <= 0 || K > 128 || ((uintptr_t)dz % 16)) return VFM_NO_KERNEL;
+    hipStream_t st = (hipStream_t)stream;
+    switch (C) {
+    case 1: return launch_dgrad<1>(dz, w, dx, B, H, W, K, st);
+    case 2: return launch_dgrad<2>(dz, w, dx, B, H, W, K, st);
+    case 3: return launch_dgrad<3>(dz, w, dx, B, H, W, K, st);
+    default: return launch_dgrad<4>(dz, w, dx, B, H, W, K, st);
+    }
+}

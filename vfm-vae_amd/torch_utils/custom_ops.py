@@ -91,6 +91,7 @@ SIGNATURES = {
                  c_ll, c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_int, c_int, c_vp],
     "vfm_attention_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp, c_llp, c_float,
                           c_vp],
+    "vfm_conv3x3_dgrad_small_f32": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_conv3x3_nhwc_f32": [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_vp],
     "vfm_attention_f32_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp,

@@ -173,12 +173,30 @@ def backward_chain(ys, pools, prep, in_shape, gtaps, conv=None):
                 g = g * (ys[ci] > 0)
             _, wb, _, w = prep[ci]
             if ci == 0:
+                if conv is conv3x3 and g.dtype == torch.float32:
+                    return image_grad(g, w, in_shape)
                 return torch.nn.grad.conv2d_input(in_shape, w.to(g.dtype), _nchw(g), padding=1)
             # the op before is conv ci-1 (taps are always followed by a pool): fuse its ReLU derivative
             fuse = PLAN[at - 1][0] == 'conv'
             g = conv(g, wb, None, relu=False, mask=ys[ci - 1] if fuse else None)
             masked = fuse
     return None
+
+
+def image_grad(g, w, in_shape):
+    """Input gradient of the image layer (3 -> 64 channels): g NHWC fp32 [B, H, W, 64], w the fp32
+    torch weight [64, 3, 3, 3] -> NCHW [B, 3, H, W] on the VALU kernel vfm_conv3x3_dgrad_small_f32
+    (exact fp32 FMAs; replaces MIOpen's fp32 Winograd of torch.nn.grad.conv2d_input)."""
+    B, C, H, W = in_shape
+    g = g.contiguous()
+    K = g.shape[-1]
+    out = torch.empty(B, C, H, W, dtype=torch.float32, device=g.device)
+    with kernel_timer.region("conv3x3_dgrad_small<f32>", 4 * (g.numel() + out.numel()), 2 * B * H * W * C * 9 * K,
+                             "hbm"):
+        rc = _lib.vfm_conv3x3_dgrad_small_f32(g.data_ptr(), w.detach().float().contiguous().data_ptr(),
+                                              out.data_ptr(), B, H, W, C, K, custom_ops.stream_ptr(g.device))
+    custom_ops.check(rc, "vfm_conv3x3_dgrad_small_f32")
+    return out
 
 
 def _pool_input(ys, pool_index):
