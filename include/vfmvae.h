@@ -290,9 +290,22 @@ int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int prec
               int kchunk, int reduce_batch, void* stream);
 int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
                                int reduce_batch);  /* -1: too large */
-/* K-tile staging schedule of vfm_gemm8 (process-wide A/B switch for microbenchmarks): 1 = half-tiles
- * restaged two K-tiles ahead (default), 0 = one K-tile ahead. Returns the previous setting. */
-int vfm_gemm8_set_schedule(int deep);
+/* The ConvNeXt MLP's bf16 1x1 GEMMs with their GELU fused into the epilogue (replaces the
+ * pwconv1 -> nn.GELU and the GELU backward of reference networks/utils/convnext_utils.py:135-142
+ * around torch's batched matmul): C[z] = W X[z], W [M, K] K-contiguous (row stride lda), X[z]
+ * [K, N] N-contiguous (row stride ldb, batch stride sB); C, C2, H: [batch][M][N] (ldc, sC).
+ *   mode 1: C = h = bf16(W X) (C may be null), C2 = g = bf16(GELU(h * rscale[z][m] + bias[m]));
+ *   mode 2: acc = dg: dz = bf16(dg) * GELU'(H * s + b), C = dh = bf16(dz * s); per-row partial
+ *           sums of dz * H (rsum0, may be null) and dz (rsum1) at [z][p][m], p < vfm_gemm8_gelu_parts(N).
+ * GELU is the exact-erf form. K % 64, N % 8 and the strides % 8 == 0, else VFM_NO_KERNEL. */
+int vfm_gemm8_gelu(const void* W, const void* X, void* C, void* C2, const void* H, const float* rscale,
+                   const float* bias, float* rsum0, float* rsum1, int mode, int M, int N, int K, int batch,
+                   long long lda, long long ldb, long long sB, long long ldc, long long sC, void* stream);
+int vfm_gemm8_gelu_parts(int N);
+/* Microbenchmarks only: a device buffer of 16 int64 per launched block that the following gemm8
+ * launches fill with s_memrealtime (100 MHz) stamps (entry, first K-tile landed, then per tile: main loop done,
+ * epilogue done); NULL (the default) turns them off. */
+int vfm_gemm8_set_stamps(long long* buf);
 /* fp32 -> bf16 pieces of one GEMM operand along its reduction dimension K (precision VFM_F32: 3
  * pieces hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid), x = hi + mid + lo exactly;
  * VFM_F32X3: 2 pieces hi, lo). kcont = 1: src [R][K] (row stride ld) -> dst [R][np K];

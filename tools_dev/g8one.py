@@ -1,0 +1,26 @@
+"""One gemm8 bf16 TN shape (env G8_M/G8_N/G8_K, default 8192 x 8192 x 4096), 10 timed calls: the
+target of the rocprofv3 --pmc passes of tools_dev/gpu_run.sh g8pmc1."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "vfm-vae_amd"), ROOT]
+import torch
+
+from torch_utils.ops import gemm_hip
+
+M, N, K = (int(os.environ.get(k, d)) for k, d in (("G8_M", 8192), ("G8_N", 8192), ("G8_K", 4096)))
+A = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+W = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+fn = lambda: gemm_hip.try_gemm(A, W.t(), route=("g8", 0))
+for _ in range(3):
+    fn()
+torch.cuda.synchronize()
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record()
+for _ in range(10):
+    fn()
+e.record()
+torch.cuda.synchronize()
+ms = s.elapsed_time(e) / 10
+print(f"gemm8 bf16 {M}x{N}x{K}: {ms * 1e3:.1f} us, {2.0 * M * N * K / ms / 1e9:.1f} TF/s", flush=True)

@@ -1,5 +1,4 @@
-"""Microbench: gemm8's two K-tile staging schedules (one / two K-tiles ahead,
-vfm_gemm8_set_schedule) against hipBLASLt on the bf16 square and SigLIP2 shapes and the f32x6
+"""Microbench: gemm8 against hipBLASLt on the bf16 square and SigLIP2 shapes and the f32x6
 decoder / adapter shapes (times include the activation split for fp32; weights cached)."""
 import os
 import sys
@@ -32,14 +31,10 @@ def rnd(*shape, dt=torch.bfloat16):
 
 
 def row(name, fl, ours, blas):
-    res = []
-    for sched in (0, 1):
-        lib.vfm_gemm8_set_schedule(sched)
-        res.append(bench(ours))
+    t8 = bench(ours)
     tb = bench(blas)
-    lib.vfm_gemm8_set_schedule(0)
-    print(f"{name:34s} sched1 {res[0] * 1e3:8.1f}us {fl / res[0] / 1e9:7.1f} | sched2 {res[1] * 1e3:8.1f}us "
-          f"{fl / res[1] / 1e9:7.1f} | blas {tb * 1e3:8.1f}us {fl / tb / 1e9:7.1f}  TF/s", flush=True)
+    print(f"{name:34s} gemm8 {t8 * 1e3:8.1f}us {fl / t8 / 1e9:7.1f} | blas {tb * 1e3:8.1f}us {fl / tb / 1e9:7.1f}  TF/s",
+          flush=True)
 
 
 torch.backends.cuda.matmul.allow_tf32 = False

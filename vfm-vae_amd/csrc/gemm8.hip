@@ -15,7 +15,7 @@
 //     K-tile (A_lo p0, B_lo p0, B_hi p1, A_hi p2; 24 ds_read_b128 per wave) and kept in VGPRs;
 //   * each operand tile is staged as two half-tiles: A_lo = the first 64 rows of both wave-rows'
 //     128-row bands, A_hi the second 64; B_lo / B_hi the first / second 32 columns of each
-//     wave-column's 64. A half-tile is 16 KB = 2 LDS-DMA (global_load_lds_dwordx4) per thread;
+//     wave-column's 64. A half-tile is 16 KB = 2 LDS-DMA (buffer_load_dwordx4 ... lds) per thread;
 //   * phase p of K-tile t issues ONE half-tile of K-tile t+1 into the other LDS buffer (order
 //     A_lo, B_lo, B_hi, A_hi), reads its own fragments (made visible by the previous phase's
 //     counted wait + barrier), waits with a COUNTED s_waitcnt vmcnt for the next phase's
@@ -33,7 +33,9 @@
 //     half-tiles [128 rows][64 k] (128-B rows, chunk ^= (row>>1)&7, ds_read_b128 fragments),
 //     MN-contiguous ones [64 k][128] (256-B rows, gemm.hip's 4x4 chunk swizzle, ds_read_b64_tr_b16);
 //   * XCD-aware bijective block -> tile remap, grouped tile order; bf16 and fp32 epilogues staged
-//     through LDS with 16-B row stores when the tile is full.
+//     through LDS (8 KB per wave of the consumed buffer) with 16-B row stores;
+//   * operands read through buffer descriptors: the 8 per-lane DMA offsets of a tile are computed
+//     once, the K-tile advance is a scalar offset (no per-lane address arithmetic in the K-loop).
 #include "vfm_common.h"
 
 namespace {
@@ -67,6 +69,19 @@ struct G8Args {
     // fp32 emulation: T product terms over pieces of Kp columns (rows) each; term t reads piece
     // (pa >> 2t) & 3 of A and (pb >> 2t) & 3 of B (T = 1, pa = pb = 0 for bf16 operands)
     int T, Kp, pa, pb;
+    // microbenchmark stamps (null in production): per block, s_memrealtime (100 MHz) at entry, after the first
+    // K-tile's wait, then per item: main loop done, epilogue stores issued, stores drained
+    long long* stamps;
+    // operand spans in bytes from A / B (buffer-descriptor ranges; < 2^31, checked on the host)
+    unsigned spanA, spanB;
+    // ConvNeXt-MLP GELU epilogues (EPI = 1 / 2, bf16 C; see gelu_epilogue): second output C2 (g),
+    // aux input H (h, C's layout), per-(batch, row) scale [Z][M], bias per row, and per-row partial
+    // sums [Z][4 tiles_n][M] of the backward
+    void* C2;
+    const __hip_bfloat16* H;
+    const float* rscale;
+    float* rs0;
+    float* rs1;
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -86,36 +101,35 @@ __device__ __forceinline__ int b_outer(int r, int q) { return 64 * (r >> 5) + 32
 // LDS offsets of the half-tiles inside one buffer
 constexpr int OFF_ALO = 0, OFF_AHI = HALF, OFF_BLO = 2 * HALF, OFF_BHI = 3 * HALF;
 
-// One LDS-DMA instruction (global_load_lds_dwordx4: lane l's 16 B land at lds_dst + 16 l). Issued
-// from inline asm so that hipcc's waitcnt pass does not see an LDS write in flight and drain it
-// with vmcnt(0) before every ds_read (which serialised the pipeline of the builtin form: see
-// gemm_fast.hip); the counted waits below are the only ones. m0 is set in the same statement.
-__device__ __forceinline__ void glds16(const void* g, const unsigned char* lds_dst) {
-    const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void*)lds_dst);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
+// One LDS-DMA instruction through a buffer descriptor (buffer_load_dwordx4 ... offen lds: lane l's
+// 16 B from rsrc + voff + soff land at M0 + 16 l). The per-lane byte offsets of a tile's 8 DMA slots
+// are computed once per tile (dma_voff) and the K-tile advance is the scalar soff, so the K-loop
+// issues its loads with no per-lane address arithmetic and no generic->LDS pointer conversion.
+// Issued from inline asm so that hipcc's waitcnt pass does not see an LDS write in flight and drain
+// it with vmcnt(0) before every ds_read; the counted waits below are the only ones. M0 is written in
+// the same statement (and the s_nop covers the M0 -> LDS-DMA hazard).
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned m0) {
+    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
+                 "s"(soff), "s"(m0)
+                 : "memory");
 }
 
-// Issue the DMA of one half-tile (2 x 16 B per thread).
+// Per-lane byte offset (relative to the operand's K-tile origin) of DMA slot u of the half-tile
+// (q, ISA) of a tile starting at outer0: K-contiguous images [128 rows][64 k] (chunk ^= (row>>1)&7),
+// MN-contiguous ones [64 k][128] (gemm.hip's 4x4 chunk swizzle); rows beyond outer_n are clamped /
+// redirected to a valid chunk whose result is unused.
 template <bool KCONT, bool ISA>
-__device__ __forceinline__ void dma_half(unsigned char* img, const __hip_bfloat16* base, long long ld, int outer0,
-                                         int outer_n, int k0, int q, int tid) {
-    const int wave = tid >> 6, lane = tid & 63;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int cbase = wave * 64 + 512 * u;
-        const int ci = cbase + lane;
-        const __hip_bfloat16* src;
-        if (KCONT) {
-            const int row = ci >> 3, chs = (ci & 7) ^ ((row >> 1) & 7);
-            const int o = min(outer0 + (ISA ? a_outer(row, q) : b_outer(row, q)), outer_n - 1);
-            src = base + (long long)o * ld + k0 + 8 * chs;
-        } else {
-            const int row = ci >> 4, chs = (ci & 15) ^ mc_swz(row);
-            int o = outer0 + (ISA ? a_outer(8 * chs, q) : b_outer(8 * chs, q));
-            if (o >= outer_n) o = 0;                       // (outer_n % 8 == 0): a valid chunk, result unused
-            src = base + (long long)(k0 + row) * ld + o;
-        }
-        glds16(src, img + cbase * 16);
+__device__ __forceinline__ unsigned dma_voff(long long ld, int outer0, int outer_n, int q, int u, int tid) {
+    const int ci = tid + 512 * u;
+    if (KCONT) {
+        const int row = ci >> 3, chs = (ci & 7) ^ ((row >> 1) & 7);
+        const int o = min(outer0 + (ISA ? a_outer(row, q) : b_outer(row, q)), outer_n - 1);
+        return (unsigned)(((long long)o * ld + 8 * chs) * 2);
+    } else {
+        const int row = ci >> 4, chs = (ci & 15) ^ mc_swz(row);
+        int o = outer0 + (ISA ? a_outer(8 * chs, q) : b_outer(8 * chs, q));
+        if (o >= outer_n) o = 0;                       // (outer_n % 8 == 0): a valid chunk, result unused
+        return (unsigned)(((long long)row * ld + o) * 2);
     }
 }
 
@@ -136,76 +150,297 @@ __device__ __forceinline__ bf16x8 frag16(const unsigned char* img, int blk, int 
 
 #define VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-// wait until at most n half-tiles (2 DMA each) of this wave are in flight (n wave-uniform)
-__device__ __forceinline__ void vm_halves(int n) {
-    switch (n) {
-    case 4: VMCNT(8); break;
-    case 3: VMCNT(6); break;
-    case 2: VMCNT(4); break;
-    case 1: VMCNT(2); break;
-    default: VMCNT(0); break;
+__device__ __forceinline__ unsigned short bf16_bits(float v) {
+    return __builtin_bit_cast(unsigned short, __float2bfloat16(v));
+}
+__device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((uint32_t)b << 16); }
+
+// Work item of the grid: one 256 x 256 output tile of one output batch and K split (y = batch * S +
+// split): block (blockIdx.x, blockIdx.y).
+struct Item {
+    int m0, n0, tn, z, v0, KT, y;
+};
+
+// acc rows of quarter hf (rows 32 hf .. 32 hf + 31 of the wave block): a select on the wave-uniform
+// quarter index, so the quarter loops of the epilogues stay rolled (one copy of their code: the
+// unrolled forms were ~7k instructions per kernel and the epilogue ran out of instruction cache,
+// ~13 us per tile).
+__device__ __forceinline__ float acc_q(const f32x4 (&acc)[8][4], int hf, int ii, int j, int r) {
+    const float v0 = acc[ii][j][r], v1 = acc[2 + ii][j][r], v2 = acc[4 + ii][j][r], v3 = acc[6 + ii][j][r];
+    return hf == 0 ? v0 : hf == 1 ? v1 : hf == 2 ? v2 : v3;
+}
+
+// Stage quarter hf of the wave's 128 x 64 fp32 block into its 8 KB of LDS: 16-B chunk c (4 columns)
+// of row ml at chunk c ^ (ml & 15) (conflict-free writes in the accumulator layout and row reads).
+__device__ __forceinline__ void stage_quarter(float* wl, const f32x4 (&acc)[8][4], int hf, int lane) {
+    const int cl = lane & 15, rq = 4 * (lane >> 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ml = 16 * ii + rq + r, nl = 16 * j + cl;
+                wl[ml * 64 + (((nl >> 2) ^ (ml & 15)) << 2) + (nl & 3)] = acc_q(acc, hf, ii, j, r);
+            }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// GELU epilogues of the ConvNeXt MLP's 1x1 GEMMs (reference networks/utils/convnext_utils.py:
+// 135-142: pwconv1 -> GELU -> pwconv2, with the modulation scale s[b, o] and bias b1[o] of the
+// channel o = GEMM row; the same roundings as the separate scale_bias_gelu kernels, csrc/decoder.hip
+// gelu_fwd / gelu_bwd):
+//   EPI 1 (forward):  h = bf16(acc) -> C (if non-null); g = bf16(GELU(h s + b1)) -> C2;
+//   EPI 2 (backward): dg = bf16(acc); dz = dg GELU'(h s + b1) with h from H; dh = bf16(dz s) -> C;
+//                     per-row sums of dz h and dz over this wave's 64 columns -> rs0 / rs1 at
+//                     [z][4 tn + wn][m] (the host sums the 4 tiles_n partials: fixed order).
+// The wave's 128 x 64 fp32 block goes through its 8 KB of LDS in four 32-row quarters; each lane then
+// walks 8-column row chunks in a rolled loop (16-B global loads / stores of h, g, dh; the row scale
+// and bias loaded once per chunk), which keeps the epilogue's registers out of the accumulator's way
+// (the element-wise form of this epilogue spilled ~300 VGPRs).
+template <int EPI>
+__device__ __forceinline__ void gelu_epilogue(const G8Args& a, f32x4 (&acc)[8][4], float* wl, int lane, int wm,
+                                              int wn, int m0, int n0, int z, int tn) {
+    const int mw = m0 + 128 * wm, nw = n0 + 64 * wn;           // this wave's 128 x 64 block
+    const long long zo = (long long)z * a.sC;
+    __hip_bfloat16* Cb = reinterpret_cast<__hip_bfloat16*>(a.C);
+    __hip_bfloat16* C2b = reinterpret_cast<__hip_bfloat16*>(a.C2);
+    const float* sc_row = a.rscale ? a.rscale + (long long)z * a.M : nullptr;
+    const bool vec = (a.ldc % 8) == 0 && (a.sC % 8) == 0 &&
+                     ((reinterpret_cast<uintptr_t>(a.C) | reinterpret_cast<uintptr_t>(a.C2) |
+                       reinterpret_cast<uintptr_t>(a.H)) % 16) == 0;
+    const long long pbase = ((long long)z * (4LL * ((a.N + BN - 1) / BN)) + 4 * tn + wn) * a.M;
+#pragma unroll 1
+    for (int hf = 0; hf < 4; ++hf) {
+        stage_quarter(wl, acc, hf, lane);
+        // item c: row ml = c >> 3 of the quarter, columns 8 (c & 7) .. + 7; 8 lanes share a row
+#pragma unroll 1
+        for (int c = lane; c < 32 * 8; c += 64) {
+            const int ml = c >> 3, q = c & 7;
+            const int m = mw + 32 * hf + ml, n = nw + 8 * q;
+            const float4 v0 = *reinterpret_cast<const float4*>(wl + ml * 64 + (((2 * q) ^ (ml & 15)) << 2));
+            const float4 v1 = *reinterpret_cast<const float4*>(wl + ml * 64 + (((2 * q + 1) ^ (ml & 15)) << 2));
+            float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            const bool mok = m < a.M;
+            const int mr = mok ? m : a.M - 1;
+            const float sc = sc_row ? sc_row[mr] : 1.f;
+            const float bi = a.bias ? a.bias[mr] : 0.f;
+            const long long off = zo + (long long)mr * a.ldc + n;
+            const bool full = mok && vec && n + 8 <= a.N;
+            float s0 = 0.f, s1 = 0.f;
+            if (EPI == 1) {
+                unsigned short hb[8], gb[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    hb[k] = bf16_bits(v[k]);
+                    const float zz = fmaf(bf16_val(hb[k]), sc, bi);
+                    gb[k] = bf16_bits(zz * gelu_parts(zz).cdf);
+                }
+                if (full) {
+                    if (Cb) *reinterpret_cast<uint4*>(Cb + off) = *reinterpret_cast<const uint4*>(hb);
+                    *reinterpret_cast<uint4*>(C2b + off) = *reinterpret_cast<const uint4*>(gb);
+                } else if (mok) {
+                    for (int k = 0; k < 8 && n + k < a.N; ++k) {
+                        if (Cb) Cb[off + k] = __builtin_bit_cast(__hip_bfloat16, hb[k]);
+                        C2b[off + k] = __builtin_bit_cast(__hip_bfloat16, gb[k]);
+                    }
+                }
+            } else {
+                unsigned short hb[8], db[8];
+                if (full) {
+                    *reinterpret_cast<uint4*>(hb) = *reinterpret_cast<const uint4*>(a.H + off);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        hb[k] = (mok && n + k < a.N) ? __builtin_bit_cast(unsigned short, a.H[off + k]) : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float hv = bf16_val(hb[k]);
+                    const GeluParts gp = gelu_parts(fmaf(hv, sc, bi));
+                    float dz = bf16_val(bf16_bits(v[k])) * (gp.cdf + gp.zpdf);
+                    if (!full && (!mok || n + k >= a.N)) dz = 0.f;
+                    s0 = fmaf(dz, hv, s0);
+                    s1 += dz;
+                    db[k] = bf16_bits(dz * sc);
+                }
+                if (full) {
+                    *reinterpret_cast<uint4*>(Cb + off) = *reinterpret_cast<const uint4*>(db);
+                } else if (mok) {
+                    for (int k = 0; k < 8 && n + k < a.N; ++k) Cb[off + k] = __builtin_bit_cast(__hip_bfloat16, db[k]);
+                }
+                // the 8 lanes of this row: xor 1, 2, 4 (fixed order, identical on every lane)
+                s0 += __shfl_xor(s0, 1);
+                s1 += __shfl_xor(s1, 1);
+                s0 += __shfl_xor(s0, 2);
+                s1 += __shfl_xor(s1, 2);
+                s0 += __shfl_xor(s0, 4);
+                s1 += __shfl_xor(s1, 4);
+                if (q == 0 && mok) {
+                    if (a.rs0) a.rs0[pbase + m] = s0;
+                    a.rs1[pbase + m] = s1;
+                }
+            }
+        }
     }
 }
 
-template <bool AK, bool BKC, bool OUTF32, bool DEEP>
+// Epilogue of one item (everything but the GELU forms): acc -> C = act(alpha acc + beta C + bias), or
+// the raw split-K partial. The wave's 128 x 64 fp32 block goes through its 8 KB of the consumed LDS
+// buffer in four 32-row quarters; each lane then walks 8-column row chunks (16-B / 32-B stores where
+// the chunk is whole and aligned, guarded element stores at the edges). Both loops are rolled.
+template <bool OUTF32>
+__device__ __forceinline__ void store_tile(const G8Args& a, f32x4 (&acc)[8][4], float* wl, int lane, int wm, int wn,
+                                           const Item& it) {
+    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
+    const int mw = it.m0 + 128 * wm, nw = it.n0 + 64 * wn;
+    const bool part = a.ws != nullptr;
+    float* wsb = part ? a.ws + (long long)it.y * a.M * a.N : nullptr;
+    TC* Cb = reinterpret_cast<TC*>(a.C) + (long long)it.z * a.sC;
+    const bool cvec = OUTF32 ? ((a.ldc % 4) == 0 && (a.sC % 4) == 0 && (reinterpret_cast<uintptr_t>(a.C) % 16) == 0)
+                             : ((a.ldc % 8) == 0 && (a.sC % 8) == 0 && (reinterpret_cast<uintptr_t>(a.C) % 16) == 0);
+    const bool wvec = (a.N % 4) == 0;
+    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
+#pragma unroll 1
+    for (int hf = 0; hf < 4; ++hf) {
+        stage_quarter(wl, acc, hf, lane);
+#pragma unroll 1
+        for (int c = lane; c < 32 * 8; c += 64) {
+            const int ml = c >> 3, q = c & 7;
+            const int m = mw + 32 * hf + ml, n = nw + 8 * q;
+            if (m >= a.M || n >= a.N) continue;
+            const float4 v0 = *reinterpret_cast<const float4*>(wl + ml * 64 + (((2 * q) ^ (ml & 15)) << 2));
+            const float4 v1 = *reinterpret_cast<const float4*>(wl + ml * 64 + (((2 * q + 1) ^ (ml & 15)) << 2));
+            float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            const bool whole = n + 8 <= a.N;
+            if (part) {
+                float* d = wsb + (long long)m * a.N + n;
+                if (whole && wvec) {
+                    *reinterpret_cast<float4*>(d) = v0;
+                    *reinterpret_cast<float4*>(d + 4) = v1;
+                } else {
+                    for (int k = 0; k < 8 && n + k < a.N; ++k) d[k] = v[k];
+                }
+                continue;
+            }
+            TC* d = Cb + (long long)m * a.ldc + n;
+            if (!plain) {
+                const float brow = (a.bias_mode == 2) ? a.bias[m] : 0.f;
+#pragma unroll 1
+                for (int k = 0; k < 8; ++k) {
+                    const bool in = whole || n + k < a.N;
+                    float x = a.alpha * v[k];
+                    if (a.beta != 0.f && in) x = fmaf(a.beta, ld(d + k), x);
+                    x += (a.bias_mode == 1) ? (in ? a.bias[n + k] : 0.f) : brow;
+                    if (a.act == 1) x = gelu_tanh(x);
+                    else if (a.act == 2) x = x * gelu_parts(x).cdf;
+                    v[k] = x;
+                }
+            }
+            if (whole && cvec) {
+                if (OUTF32) {
+                    float* df = reinterpret_cast<float*>(d);
+                    *reinterpret_cast<float4*>(df) = make_float4(v[0], v[1], v[2], v[3]);
+                    *reinterpret_cast<float4*>(df + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                } else {
+                    unsigned short b[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) b[k] = bf16_bits(v[k]);
+                    *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(b);
+                }
+            } else {
+                for (int k = 0; k < 8 && n + k < a.N; ++k) st(d + k, v[k]);
+            }
+        }
+    }
+}
+
+template <bool AK, bool BKC, bool OUTF32, int EPI = 0>
 __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 2, wn = wave & 3;
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
     const int nwg = tiles_m * tiles_n;
-    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    // grouped order: consecutive tiles (the ~32 an XCD runs at once) cover GROUP tile-rows x 32/GROUP
-    // tile-columns, so the XCD's L2 holds GROUP A panels + 32/GROUP B panels instead of 1 + 32
-    constexpr int GROUP = 4;
-    const int gsz = GROUP * tiles_n, grp = tile / gsz, rem = tile - grp * gsz;
-    const int rows_g = min(GROUP, tiles_m - grp * GROUP);
-    const int tm = grp * GROUP + rem % rows_g, tn = rem / rows_g;
-    const int m0 = tm * BM, n0 = tn * BN;
     const int KTz = a.Kp / BK;                         // K-tiles per batch and piece
-    const int zo = a.reduce ? 0 : (int)blockIdx.y / a.S, sp = (int)blockIdx.y - zo * a.S;
     const int VT = a.reduce ? a.Z * KTz : KTz;         // virtual K-tiles of one product term
-    const int V = a.T * VT;                            // virtual K-tiles of this output
-    const int v0 = sp * a.kchunk;
-    const int KT = min(V, v0 + a.kchunk) - v0;         // >= 1 by construction of S on the host
-    const int z = zo;                                  // output batch
+    const int V = a.T * VT;                            // virtual K-tiles of one output
 
+    Item it;
+    {
+        const int y = blockIdx.y, bid = blockIdx.x;
+        // XCD-aware bijective remap, then grouped order: consecutive tiles (the ~32 an XCD runs at
+        // once) cover GROUP tile-rows x 32/GROUP tile-columns, so the XCD's L2 holds GROUP A panels +
+        // 32/GROUP B panels instead of 1 + 32
+        const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+        const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        constexpr int GROUP = 4;
+        const int gsz = GROUP * tiles_n, grp = tile / gsz, rem = tile - grp * gsz;
+        const int rows_g = min(GROUP, tiles_m - grp * GROUP);
+        const int tm = grp * GROUP + rem % rows_g;
+        it.tn = rem / rows_g;
+        it.m0 = tm * BM;
+        it.n0 = it.tn * BN;
+        it.z = a.reduce ? 0 : y / a.S;
+        it.v0 = (y - it.z * a.S) * a.kchunk;
+        it.KT = min(V, it.v0 + a.kchunk) - it.v0;      // >= 1 by construction of S on the host
+        it.y = y;
+    }
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.spanA, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.spanB, 0x00020000);
+    // per-lane byte offsets of the 8 DMA slots (half-tile h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi; slot u)
+    unsigned vo[8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        vo[0 + u] = dma_voff<AK, true>(a.lda, it.m0, a.M, 0, u, tid);
+        vo[2 + u] = dma_voff<BKC, false>(a.ldb, it.n0, a.N, 0, u, tid);
+        vo[4 + u] = dma_voff<BKC, false>(a.ldb, it.n0, a.N, 1, u, tid);
+        vo[6 + u] = dma_voff<AK, true>(a.lda, it.m0, a.M, 1, u, tid);
+    }
+    const unsigned lds0 =
+        __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void*)lds + (unsigned)wave * 64 * 16);
+    // virtual K-tile iterator: term (piece pair), batch zt (batch-reduced products), K-tile kk of the batch
+    int term, zt, kk;
+    {
+        const int v = it.v0;
+        term = v / VT;
+        const int rest = v - term * VT;
+        zt = a.reduce ? rest / KTz : it.z;
+        kk = a.reduce ? rest - (rest / KTz) * KTz : rest;
+    }
+    // scalar byte offsets of the current K-tile inside A / B
+    auto soffs = [&](unsigned& sa, unsigned& sb) {
+        const long long ka = (long long)kk * BK + ((a.pa >> (2 * term)) & 3) * (long long)a.Kp;
+        const long long kb = (long long)kk * BK + ((a.pb >> (2 * term)) & 3) * (long long)a.Kp;
+        sa = (unsigned)((zt * a.sA + (AK ? ka : ka * a.lda)) * 2);
+        sb = (unsigned)((zt * a.sB + (BKC ? kb : kb * a.ldb)) * 2);
+    };
+    auto advance = [&]() {
+        if (++kk == KTz) {
+            kk = 0;
+            if (a.reduce && ++zt < a.Z) return;
+            zt = a.reduce ? 0 : zt;
+            ++term;
+        }
+    };
+    auto issue = [&](unsigned sa, unsigned sb, int bsel, int h) {
+        const unsigned m0 = lds0 + bsel * BUF + (h == 0 ? OFF_ALO : h == 1 ? OFF_BLO : h == 2 ? OFF_BHI : OFF_AHI);
+        const bool isa = (h == 0 || h == 3);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) bdma16(isa ? rA : rB, vo[2 * h + u], isa ? sa : sb, m0 + u * 512 * 16);
+    };
     f32x4 acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
-
-    // source of local K-tile t: batch, term -> pieces, k offsets inside each operand (wave-uniform)
-    struct Src {
-        const __hip_bfloat16* Ab;
-        const __hip_bfloat16* Bb;
-        int ka, kb;
-    };
-    auto src_of = [&](int t) {
-        const int v = v0 + t;
-        const int term = v / VT, rest = v - term * VT;
-        const int zt = a.reduce ? rest / KTz : zo, k0 = (a.reduce ? rest - zt * KTz : rest) * BK;
-        Src r;
-        r.Ab = a.A + (long long)zt * a.sA;
-        r.Bb = a.B + (long long)zt * a.sB;
-        r.ka = k0 + ((a.pa >> (2 * term)) & 3) * a.Kp;
-        r.kb = k0 + ((a.pb >> (2 * term)) & 3) * a.Kp;
-        return r;
-    };
-    // half-tile h of local K-tile t into its buffer: h = 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi (issue order)
-    auto issue = [&](const Src& sr, int t, int h) {
-        unsigned char* buf = lds + (t & 1) * BUF;
-        if (h == 0) dma_half<AK, true>(buf + OFF_ALO, sr.Ab, a.lda, m0, a.M, sr.ka, 0, tid);
-        else if (h == 1) dma_half<BKC, false>(buf + OFF_BLO, sr.Bb, a.ldb, n0, a.N, sr.kb, 0, tid);
-        else if (h == 2) dma_half<BKC, false>(buf + OFF_BHI, sr.Bb, a.ldb, n0, a.N, sr.kb, 1, tid);
-        else dma_half<AK, true>(buf + OFF_AHI, sr.Ab, a.lda, m0, a.M, sr.ka, 1, tid);
-    };
     bf16x8 af[4][2], bl[2][2], bh[2][2];        // A quadrant rows; B_lo / B_hi columns (both kept)
-    // half-tile h, phase p: which fragments phase p reads (A_lo + B_lo at p0, B_hi at p1, A_hi at p2;
-    // A every second phase) and multiplies (quadrant (qm, qn))
-    auto phase_math = [&](const unsigned char* buf, int p) {
+    // phase p multiplies quadrant (qm, qn) with the fragments read in this or an earlier phase
+    // (A_lo + B_lo at p0, B_hi at p1, A_hi at p2)
+    auto phase_math = [&](int p) {
         const int qm = p >> 1;                          // 0 0 1 1
         const int qn = (p == 1 || p == 2) ? 1 : 0;      // 0 1 1 0
         __builtin_amdgcn_s_barrier();
@@ -221,7 +456,6 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
                         af[i][s], qn ? bh[j][s] : bl[j][s], acc[4 * qm + i][2 * qn + j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
-        (void)buf;
     };
     auto phase_reads = [&](const unsigned char* buf, int p) {
         if (p == 0 || p == 2) {
@@ -242,72 +476,38 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
                 }
         }
     };
-    if (DEEP) {
-        // Two K-tiles ahead: the fragments of a half-tile live in VGPRs after their phase, so its LDS
-        // slot is restaged for K-tile t+2 two phases later (WAR >= 2 phases with the rows one barrier
-        // apart). Phase p of tile t issues p0: B_hi(t+1), p1: A_hi(t+1) (buffer (t+1)&1), p2:
-        // A_lo(t+2), p3: B_lo(t+2) (buffer t&1); the counted waits leave 4 half-tiles (8 DMA) in
-        // flight: each half-tile is issued 5-6 phases before its read instead of 2-4.
-        {
-            const Src s0 = src_of(0);
-            issue(s0, 0, 0);
-            issue(s0, 0, 1);
-            issue(s0, 0, 2);
-            issue(s0, 0, 3);
-        }
-        Src s1 = src_of(KT > 1 ? 1 : 0);
-        if (KT > 1) {
-            issue(s1, 1, 0);
-            issue(s1, 1, 1);
-        }
-        vm_halves(2 + (KT > 1 ? 2 : 0));            // A_lo(0), B_lo(0)
-        __builtin_amdgcn_s_barrier();
-        if (wm == 1) __builtin_amdgcn_s_barrier();
-        for (int t = 0; t < KT; ++t) {
-            const unsigned char* buf = lds + (t & 1) * BUF;
-            const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
-            const Src s2 = src_of(n2 ? t + 2 : t);
-            // p0: issue B_hi(t+1); read A_lo(t), B_lo(t); wait for B_hi(t)
-            if (n1) issue(s1, t + 1, 2);
-            phase_reads(buf, 0);
-            vm_halves(1 + (n1 ? 3 : 0));
-            phase_math(buf, 0);
-            // p1: issue A_hi(t+1); read B_hi(t); wait for A_hi(t)
-            if (n1) issue(s1, t + 1, 3);
-            phase_reads(buf, 1);
-            vm_halves(n1 ? 4 : 0);
-            phase_math(buf, 1);
-            // p2: issue A_lo(t+2); read A_hi(t)
-            if (n2) issue(s2, t + 2, 0);
-            phase_reads(buf, 2);
-            phase_math(buf, 2);
-            // p3: issue B_lo(t+2); wait for A_lo(t+1), B_lo(t+1)
-            if (n2) issue(s2, t + 2, 1);
-            if (n1) vm_halves(2 + (n2 ? 2 : 0));
-            phase_math(buf, 3);
-            s1 = s2;
-        }
-    } else {
+
+    const long long t_entry = a.stamps ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     {
-        const Src s0 = src_of(0);
-        issue(s0, 0, 0);
-        issue(s0, 0, 1);
-        issue(s0, 0, 2);
-        issue(s0, 0, 3);
+        unsigned sa, sb;
+        soffs(sa, sb);
+        issue(sa, sb, 0, 0);
+        issue(sa, sb, 0, 1);
+        issue(sa, sb, 0, 2);
+        issue(sa, sb, 0, 3);
     }
-    VMCNT(4);                                   // A_lo, B_lo of tile 0
+    VMCNT(4);                                   // A_lo, B_lo of the first K-tile
     __builtin_amdgcn_s_barrier();
+    long long* stamp = (a.stamps && tid == 0) ? a.stamps + (long long)(blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
+    if (stamp) {
+        stamp[0] = t_entry;
+        stamp[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
     // ping-pong: the wm = 1 wave-row runs one barrier behind (2 barriers per phase), so one
     // wave-row's 16 MFMAs overlap the other's DMA issue + fragment reads (see the header)
     if (wm == 1) __builtin_amdgcn_s_barrier();
-
-    for (int t = 0; t < KT; ++t) {
+    for (int t = 0; t < it.KT; ++t) {
         const unsigned char* buf = lds + (t & 1) * BUF;
-        const bool nxt = t + 1 < KT;
-        const Src sn = src_of(nxt ? t + 1 : t);
+        const bool nxt = t + 1 < it.KT;
+        unsigned sa = 0, sb = 0;
+        if (nxt) {
+            advance();
+            soffs(sa, sb);
+        }
+        const int nb = (t + 1) & 1;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            if (nxt) issue(sn, t + 1, p);
+            if (nxt) issue(sa, sb, nb, p);
             phase_reads(buf, p);
             // wait for the NEXT phase's half-tile (see the header), then the phase barrier
             if (nxt) {
@@ -316,127 +516,22 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
                 if (p == 0) VMCNT(2);
                 else if (p == 1) VMCNT(0);
             }
-            phase_math(buf, p);
+            phase_math(p);
         }
-    }
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();
-    VMCNT(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-
-    // epilogue: acc[i][j][r] = C[m0 + 128wm + 16i + 4(l>>4) + r][n0 + 64wn + 16j + (l&15)]
-    const int cl = lane & 15, rq = 4 * (lane >> 4);
-    if (a.ws) {                                        // split-K partial, raw fp32
-        float* w = a.ws + (long long)blockIdx.y * a.M * a.N;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + 64 * wn + 16 * j + cl;
-            if (n >= a.N) continue;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = m0 + 128 * wm + 16 * i + rq + r;
-                    if (m < a.M) w[(long long)m * a.N + n] = acc[i][j][r];
-                }
-        }
-        return;
-    }
-    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
-    TC* Cb = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
-    if (!OUTF32 && a.beta == 0.f && m0 + BM <= a.M && n0 + BN <= a.N && (a.ldc % 8) == 0 &&
-        (reinterpret_cast<uintptr_t>(a.C) % 16) == 0 && (a.sC % 8) == 0) {
-        unsigned short* wl = reinterpret_cast<unsigned short*>(lds + wave * 128 * 128);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int nl = 16 * j + cl;
-            const int n = n0 + 64 * wn + nl;
-            const float bcol = (a.bias_mode == 1) ? a.bias[n] : 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int ml = 16 * i + rq + r;
-                    float v = a.alpha * acc[i][j][r];
-                    v += (a.bias_mode == 2) ? a.bias[m0 + 128 * wm + ml] : bcol;
-                    if (a.act == 1) v = gelu_tanh(v);
-                    else if (a.act == 2) v = v * gelu_parts(v).cdf;
-                    const int ch = (nl >> 3) ^ (ml & 7);
-                    wl[ml * 64 + ch * 8 + (nl & 7)] = __builtin_bit_cast(unsigned short, __float2bfloat16(v));
-                }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        __hip_bfloat16* crow = reinterpret_cast<__hip_bfloat16*>(a.C) + (long long)z * a.sC +
-                               (long long)(m0 + 128 * wm) * a.ldc + n0 + 64 * wn;
-#pragma unroll 4
-        for (int c = lane; c < 128 * 8; c += 64) {
-            const int ml = c >> 3, chl = c & 7;
-            const uint4 v = *reinterpret_cast<const uint4*>(wl + ml * 64 + 8 * (chl ^ (ml & 7)));
-            *reinterpret_cast<uint4*>(crow + (long long)ml * a.ldc + 8 * chl) = v;
-        }
-        return;
-    }
-    if (OUTF32 && a.beta == 0.f && m0 + BM <= a.M && n0 + BN <= a.N && (a.ldc % 4) == 0 &&
-        (reinterpret_cast<uintptr_t>(a.C) % 16) == 0 && (a.sC % 4) == 0) {
-        // fp32 tile through LDS in two 64-row halves per wave (16 KB each, the wave's share of the
-        // operand buffers): 16-B stores of whole 256-B row segments instead of 4-B stores with
-        // per-element address arithmetic. 16-B chunk c of row ml sits at chunk c ^ (ml & 15), so
-        // both the row-group writes of the accumulator layout and the row reads are conflict-free.
-        float* wl = reinterpret_cast<float*>(lds + wave * 128 * 128);
-        float* crow0 = reinterpret_cast<float*>(a.C) + (long long)z * a.sC + (long long)(m0 + 128 * wm) * a.ldc +
-                       n0 + 64 * wn;
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            if (hf) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int nl = 16 * j + cl;
-                const float bcol = (a.bias_mode == 1) ? a.bias[n0 + 64 * wn + nl] : 0.f;
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int ml = 16 * ii + rq + r;
-                        float v = a.alpha * acc[4 * hf + ii][j][r];
-                        v += (a.bias_mode == 2) ? a.bias[m0 + 128 * wm + 64 * hf + ml] : bcol;
-                        if (a.act == 1) v = gelu_tanh(v);
-                        else if (a.act == 2) v = v * gelu_parts(v).cdf;
-                        wl[ml * 64 + (((nl >> 2) ^ (ml & 15)) << 2) + (nl & 3)] = v;
-                    }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            float* crow = crow0 + (long long)(64 * hf) * a.ldc;
-#pragma unroll 4
-            for (int c = lane; c < 64 * 16; c += 64) {
-                const int ml = c >> 4, ch = c & 15;
-                const float4 v = *reinterpret_cast<const float4*>(wl + ml * 64 + ((ch ^ (ml & 15)) << 2));
-                *reinterpret_cast<float4*>(crow + (long long)ml * a.ldc + 4 * ch) = v;
-            }
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = n0 + 64 * wn + 16 * j + cl;
-        if (n >= a.N) continue;
-        const float bcol = (a.bias_mode == 1) ? a.bias[n] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + 128 * wm + 16 * i + rq + r;
-                if (m >= a.M) continue;
-                TC* cp = Cb + (long long)m * a.ldc + n;
-                float v = a.alpha * acc[i][j][r];
-                if (a.beta != 0.f) v = fmaf(a.beta, ld(cp), v);
-                v += (a.bias_mode == 2) ? a.bias[m] : bcol;
-                if (a.act == 1) v = gelu_tanh(v);
-                else if (a.act == 2) v = v * gelu_parts(v).cdf;
-                st(cp, v);
-            }
+    if (stamp) stamp[2] = (long long)__builtin_amdgcn_s_memrealtime();
+    // epilogue through this wave's 8 KB of the buffer the last K-tile was read from;
+    // acc[i][j][r] = C[m0 + 128wm + 16i + 4(l>>4) + r][n0 + 64wn + 16j + (l&15)]
+    unsigned char* wl = lds + ((it.KT - 1) & 1) * BUF + wave * (BUF / 8);
+    if (EPI) gelu_epilogue<EPI>(a, acc, reinterpret_cast<float*>(wl), lane, wm, wn, it.m0, it.n0, it.z, it.tn);
+    else store_tile<OUTF32>(a, acc, reinterpret_cast<float*>(wl), lane, wm, wn, it);
+    if (stamp) {
+        stamp[3] = (long long)__builtin_amdgcn_s_memrealtime();     // stores issued
+        VMCNT(0);
+        stamp[4] = (long long)__builtin_amdgcn_s_memrealtime();     // stores drained
     }
 }
 
@@ -461,30 +556,39 @@ __global__ __launch_bounds__(256) void gemm8_reduce(G8Args a) {
     st(cp, v);
 }
 
-int g_sched = 0;   // 1: two-K-tiles-ahead staging (DEEP), 0: one tile ahead (vfm_gemm8_set_schedule)
+long long* g_stamps = nullptr;   // microbenchmark stamp buffer (vfm_gemm8_set_stamps)
 
-template <bool AK, bool BKC, bool OUTF32, bool DEEP>
-void launch8k(const G8Args& a, int nwg, int zo, hipStream_t st) {
+template <bool AK, bool BKC, bool OUTF32, int EPI = 0>
+void launch8k(const G8Args& a, int nwg, int ny, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32, DEEP>,
+        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32, EPI>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32, DEEP>), dim3(nwg, zo * a.S), dim3(THREADS), 2 * BUF, st, a);
+    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32, EPI>), dim3(nwg, ny), dim3(THREADS), 2 * BUF, st, a);
 }
 
 template <bool AK, bool BKC, bool OUTF32>
 int launch8(const G8Args& a, int batch, hipStream_t st) {
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const int zo = a.reduce ? 1 : batch;
-    if (g_sched) launch8k<AK, BKC, OUTF32, true>(a, nwg, zo, st);
-    else launch8k<AK, BKC, OUTF32, false>(a, nwg, zo, st);
+    launch8k<AK, BKC, OUTF32>(a, nwg, zo * a.S, st);
     if (a.ws) {
         const long long MN = (long long)a.M * a.N;
         hipLaunchKernelGGL(gemm8_reduce<OUTF32>, dim3((unsigned)((MN + 255) / 256), zo), dim3(256), 0, st, a);
     }
     return launch_status();
+}
+
+// Bytes an operand spans from its base: rows x ld (+ batch stride), as the buffer descriptor range;
+// -1 when it does not fit the 32-bit offsets of the DMA (2 GiB).
+static long long span_bytes(int kcont, long long outer, long long kdim, long long ld, long long sb, int batch) {
+    const long long rows = kcont ? outer : kdim;
+    const long long cols = kcont ? kdim : outer;
+    const long long e = (rows - 1) * ld + cols + (long long)(batch - 1) * sb;
+    const long long bytes = e * 2;
+    return bytes >= (1LL << 31) ? -1 : bytes;
 }
 
 // fp32 -> NP bf16 pieces along the reduction dimension (NP = 3: [hi | mid | lo], NP = 2: [hi | lo]).
@@ -572,7 +676,13 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
         return VFM_ERR_ARGS;
     const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
-    G8Args a;
+    const long long spA = span_bytes(a_kcont, M, (long long)np * K, lda, sA, batch);
+    const long long spB = span_bytes(b_kcont, N, (long long)np * K, ldb, sB, batch);
+    if (spA < 0 || spB < 0) return VFM_NO_KERNEL;
+    G8Args a{};
+    a.stamps = g_stamps;
+    a.spanA = (unsigned)spA;
+    a.spanB = (unsigned)spB;
     a.Kp = K;
     terms_of(np, a.T, a.pa, a.pb);
     a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
@@ -597,13 +707,48 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
 #undef VFM_G8
 }
 
-// K-tile staging schedule of vfm_gemm8 (A/B switch for microbenchmarks): 1 = two K-tiles ahead
-// (default), 0 = one K-tile ahead. Returns the previous value.
-extern "C" int vfm_gemm8_set_schedule(int deep) {
-    const int prev = g_sched;
-    g_sched = deep ? 1 : 0;
-    return prev;
+// ConvNeXt-MLP 1x1 GEMMs with the GELU epilogues (gelu_epilogue above), bf16 operands and outputs:
+//   C[z] = W[M, K] X[z][K, N] with W K-contiguous (lda), X N-contiguous (ldb, batch stride sB);
+//   mode 1: C = h (may be null), C2 = g = GELU(h s + b1); mode 2: C = dh from acc = dg and H = h,
+//   rsum0 (may be null) / rsum1 = [batch][vfm_gemm8_gelu_parts(N)][M] partial sums.
+// rscale [batch][M] (null: 1), bias [M] (null: 0). C, C2, H share (ldc, sC).
+extern "C" int vfm_gemm8_gelu(const void* W, const void* X, void* C, void* C2, const void* H, const float* rscale,
+                              const float* bias, float* rsum0, float* rsum1, int mode, int M, int N, int K, int batch,
+                              long long lda, long long ldb, long long sB, long long ldc, long long sC, void* stream) {
+    if (!W || !X || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
+    if (mode == 1 ? !C2 : (mode == 2 ? (!C || !H || !rsum1) : true)) return VFM_ERR_ARGS;
+    if (K % BK || K % 8 || N % 8 || lda % 8 || ldb % 8 || sB % 8 || ldc % 8 || sC % 8) return VFM_NO_KERNEL;
+    if (((uintptr_t)W | (uintptr_t)X) % 16) return VFM_NO_KERNEL;
+    if (lda < K || ldb < N || ldc < N) return VFM_ERR_ARGS;
+    const long long spA = span_bytes(1, M, K, lda, 0, 1), spB = span_bytes(0, N, K, ldb, sB, batch);
+    if (spA < 0 || spB < 0) return VFM_NO_KERNEL;
+    G8Args a{};
+    a.spanA = (unsigned)spA;
+    a.spanB = (unsigned)spB;
+    a.A = (const __hip_bfloat16*)W; a.B = (const __hip_bfloat16*)X; a.C = C; a.C2 = C2;
+    a.H = (const __hip_bfloat16*)H; a.rscale = rscale; a.bias = bias; a.rs0 = rsum0; a.rs1 = rsum1;
+    a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = 0; a.sB = sB; a.sC = sC;
+    a.M = M; a.N = N; a.K = K; a.alpha = 1.f; a.beta = 0.f; a.bias_mode = 0; a.act = 0;
+    a.Kp = K; a.T = 1; a.pa = a.pb = 0;
+    a.Z = batch; a.reduce = 0; a.kchunk = K / BK; a.S = 1; a.ws = nullptr;
+    a.stamps = g_stamps;
+    const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    if (mode == 1) launch8k<true, false, false, 1>(a, (int)nwg, batch, st);
+    else launch8k<true, false, false, 2>(a, (int)nwg, batch, st);
+    return launch_status();
 }
+
+// Microbenchmarks only: device buffer of 16 int64 per block (s_memrealtime stamps, see G8Args::stamps)
+// for the following vfm_gemm8 / vfm_gemm8_gelu launches; null turns the stamps off.
+extern "C" int vfm_gemm8_set_stamps(long long* buf) {
+    g_stamps = buf;
+    return VFM_OK;
+}
+
+// Partial-sum slots per (batch, row) of vfm_gemm8_gelu mode 2 for N columns.
+extern "C" int vfm_gemm8_gelu_parts(int N) { return N <= 0 ? -1 : 4 * ((N + BN - 1) / BN); }
 
 // fp32 workspace floats vfm_gemm8 needs for (precision, M, N, K, batch, kchunk, reduce_batch); 0 = none
 extern "C" int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk, int reduce_batch) {

@@ -507,10 +507,140 @@ def layer_scale_residual(y, bias, gamma, x_in, slot=None):
 
 # measured faster than the unfused chain only at C = 128 (b5 256^2); VFM_NO_FUSED_MLP=1 for A/B
 MLP_CHANNELS = () if os.environ.get("VFM_NO_FUSED_MLP") else (128,)
+# wider layers (b3: C = 512 at 64^2, b4: C = 256 at 128^2): the two 1x1s on the 256-tile GEMM with
+# the GELU fused into pwconv1's epilogue (forward) and into the 4C-wide data gradient's (backward)
+# (csrc/gemm8.hip vfm_gemm8_gelu) with VFM_GEMM_MLP=1; off by default while the layer measures 1.09-1.12x
+# the unfused chain on hipBLASLt (profiles/r3_j_mlpbench.txt)
+GEMM_MLP_CHANNELS = (256, 512) if os.environ.get("VFM_GEMM_MLP") == "1" else ()
+GEMM_MLP_TESTED = (256, 512)
 
 
 def convnext_mlp_supported(m, C, P):
-    return m.is_cuda and m.dtype == torch.bfloat16 and C in MLP_CHANNELS and P % 128 == 0
+    if not (m.is_cuda and m.dtype == torch.bfloat16):
+        return False
+    if C in MLP_CHANNELS:
+        return P % 128 == 0
+    return C in GEMM_MLP_CHANNELS and P % 8 == 0
+
+
+def _g8(A, B, **kw):
+    """bf16 product on the 256-tile kernel (gemm_hip route ("g8", 0)); raises if not covered."""
+    from . import gemm_hip
+    out = gemm_hip.try_gemm(A, B, route=("g8", 0), **kw)
+    if out is None:
+        raise custom_ops.NativeError(f"vfm_gemm8 does not cover {tuple(A.shape)} x {tuple(B.shape)}")
+    return out
+
+
+def gemm_gelu_fwd(w1c, m, s, b1, want_h=True):
+    """(h, g): h = W1 m[b] (bf16 [B, O, P], None unless want_h) and g = GELU(h s[b] + b1) in one
+    GEMM (vfm_gemm8_gelu mode 1). w1c bf16 [O, I] contiguous, m bf16 [B, I, P], s fp32 [B, O] or
+    None, b1 fp32 [O] or None."""
+    B, I, P = m.shape
+    O = w1c.shape[0]
+    g = torch.empty([B, O, P], dtype=torch.bfloat16, device=m.device)
+    h = torch.empty_like(g) if want_h else None
+    with kernel_timer.region('gemm8_gelu<1>', _nb(m, g, h) + w1c.numel() * 2, flops=2.0 * B * O * I * P, bound="mfma"):
+        _check(_lib.vfm_gemm8_gelu(w1c.data_ptr(), m.data_ptr(), _p(h), g.data_ptr(), None, _p(s), _p(b1), None, None,
+                                   1, O, P, I, B, w1c.stride(0), m.stride(1), m.stride(0), P, O * P, _stream()),
+               'vfm_gemm8_gelu')
+    return h, g
+
+
+def gemm_gelu_bwd(w2t, dy, h, s, b1):
+    """dh = (W2^T dy[b]) GELU'(h s + b1) s with the per-(b, o) sums for d_s ([B, O], None when s is
+    None) and d_b1 ([O]) (vfm_gemm8_gelu mode 2). w2t bf16 [O, C] contiguous, dy bf16 [B, C, P]."""
+    B, C, P = dy.shape
+    O = w2t.shape[0]
+    parts = _lib.vfm_gemm8_gelu_parts(P)
+    dh = torch.empty_like(h)
+    p1 = torch.empty([B, parts, O], dtype=torch.float32, device=dy.device)
+    p0 = torch.empty_like(p1) if s is not None else None
+    with kernel_timer.region('gemm8_gelu<2>', _nb(dy, h, dh) + w2t.numel() * 2, flops=2.0 * B * O * C * P,
+                             bound="mfma"):
+        _check(_lib.vfm_gemm8_gelu(w2t.data_ptr(), dy.data_ptr(), dh.data_ptr(), None, h.data_ptr(), _p(s), _p(b1),
+                                   _p(p0), p1.data_ptr(), 2, O, P, C, B, w2t.stride(0), dy.stride(1), dy.stride(0), P,
+                                   O * P, _stream()), 'vfm_gemm8_gelu')
+    return dh, (p0.sum(1) if p0 is not None else None), p1.sum((0, 1))
+
+
+class _ConvNeXtMLPGemm(torch.autograd.Function):
+    """The ConvNeXt MLP of the wide bf16 blocks (reference convnext_utils.py:135-142) on the 256-tile
+    GEMM: forward pwconv1 + scale/bias/GELU in one kernel (h and g written for the backward), pwconv2,
+    the layer-scale residual kernel; backward: the residual kernel's dy, dW2 (batch-reduced fp32
+    GEMM), the 4C-wide data gradient with GELU' and the d_s / d_b1 row sums in its epilogue, dW1 and
+    dm. Same arithmetic and bf16 roundings as the unfused Functions above."""
+
+    @staticmethod
+    def forward(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in, slot=None):
+        _edges(ctx, m, w1, dcoef, b1, w2, b2, gamma, x_in, slot)
+        ctx.slot = slot
+        m, x_in = _c(m), _c(x_in)
+        B, C, P = m.shape
+        w1c = _cast_cached(w1, torch.bfloat16).contiguous()
+        w2c = _cast_cached(w2, torch.bfloat16).contiguous()
+        s = None if dcoef is None else dcoef.detach().float().contiguous()
+        fb1, fb2, fg = _f32(b1), _f32(b2), _f32(gamma)
+        h, g = gemm_gelu_fwd(w1c, m, s, fb1, want_h=True)
+        y = _g8(w2c, g)
+        out = torch.empty_like(x_in)
+        with kernel_timer.region(_rn('layer_scale_residual_fwd', y), _nb(y, x_in, out)):
+            _check(_lib.vfm_layer_scale_residual_fwd(y.data_ptr(), _p(fb2), _p(fg), x_in.data_ptr(), out.data_ptr(),
+                                                     _code(y), _code(x_in), B, C, P, _stream()),
+                   'vfm_layer_scale_residual_fwd')
+        ctx.save_for_backward(m, h, g, y, w1c, w2c, s, fb1, fb2, fg)
+        ctx.meta = (w1.dtype, w2.dtype, None if dcoef is None else dcoef.dtype, None if b1 is None else b1.dtype,
+                    None if b2 is None else b2.dtype, None if gamma is None else gamma.dtype)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout):
+        m, h, g, y, w1c, w2c, s, fb1, fb2, fg = ctx.saved_tensors
+        w1dt, w2dt, sdt, b1dt, b2dt, gdt = ctx.meta
+        B, C, P = m.shape
+        dout = _c(dout.to(torch.bfloat16))
+        dy = torch.empty_like(y)
+        r0 = torch.empty([B * C], dtype=torch.float32, device=m.device)
+        r1 = torch.empty_like(r0)
+        with kernel_timer.region(_rn('layer_scale_residual_bwd', y), _nb(y, dout, dy)):
+            _check(_lib.vfm_layer_scale_residual_bwd(y.data_ptr(), _p(fb2), _p(fg), dout.data_ptr(), dy.data_ptr(),
+                                                     r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout), B, C, P,
+                                                     _stream()), 'vfm_layer_scale_residual_bwd')
+        dw1 = db1 = ds = dw2 = db2 = dgm = dm = None
+        if fb2 is not None and _wanted(ctx, 5):
+            s1 = r1.view(B, C).sum(0)
+            db2 = (s1 * fg if fg is not None else s1).to(b2dt)
+        if fg is not None and _wanted(ctx, 6):
+            dgm = r0.view(B, C).sum(0).to(gdt)
+        if _wanted(ctx, 4):
+            dw2 = weight_grad_1x1(dy, g, w2dt)
+        dh, sum_s, sum_b = gemm_gelu_bwd(w2c.t().contiguous(), dy, h, s, fb1)
+        if s is not None and _wanted(ctx, 2):
+            ds = sum_s.to(sdt)
+        if fb1 is not None and _wanted(ctx, 3):
+            db1 = sum_b.to(b1dt)
+        if _wanted(ctx, 1):
+            dw1 = weight_grad_1x1(dh, m, w1dt)
+        if ctx.needs_input_grad[0]:
+            dm = _g8(w1c.t(), dh)
+        dx = dout if ctx.needs_input_grad[7] and not _stash_residual(ctx.slot, dout) else None
+        return dm, dw1, ds, db1, dw2, db2, dgm, dx, None
+
+
+def _mlp_gemm_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
+    B, C, P = m.shape
+    w1c = _cast_cached(w1, torch.bfloat16).contiguous()
+    w2c = _cast_cached(w2, torch.bfloat16).contiguous()
+    s = None if dcoef is None else dcoef.detach().float().contiguous()
+    _, g = gemm_gelu_fwd(w1c, m, s, _f32(b1), want_h=False)
+    y = _g8(w2c, g)
+    out = torch.empty_like(x_in)
+    with kernel_timer.region(_rn('layer_scale_residual_fwd', y), _nb(y, x_in, out)):
+        _check(_lib.vfm_layer_scale_residual_fwd(y.data_ptr(), _p(_f32(b2)), _p(_f32(gamma)), x_in.data_ptr(),
+                                                 out.data_ptr(), _code(y), _code(x_in), B, C, P, _stream()),
+               'vfm_layer_scale_residual_fwd')
+    return out
 
 
 class _ConvNeXtMLP(torch.autograd.Function):
@@ -593,7 +723,10 @@ class _ConvNeXtMLP(torch.autograd.Function):
 
 
 def convnext_mlp(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot=None):
-    """Autograd form of the fused MLP (same arguments as convnext_mlp_nograd)."""
+    """Autograd form of the fused MLP (same arguments as convnext_mlp_nograd): the whole-MLP kernel
+    at C in MLP_CHANNELS, else the GELU-epilogue GEMM form."""
+    if m.shape[1] not in MLP_CHANNELS:
+        return _ConvNeXtMLPGemm.apply(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot)
     return _ConvNeXtMLP.apply(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot)
 
 
@@ -602,6 +735,8 @@ def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
     dcoef [B, 4C] fp32 or None; b1 [4C], b2, gamma [C] or None. Returns bf16 [B, C, P]."""
     m, x_in = _c(m), _c(x_in)
     B, C, P = m.shape
+    if C not in MLP_CHANNELS:
+        return _mlp_gemm_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in)
     w1c = _cast_cached(w1, torch.bfloat16).contiguous()
     w2c = _cast_cached(w2, torch.bfloat16).contiguous()
     s = None if dcoef is None else dcoef.detach().float().contiguous()

@@ -5,18 +5,45 @@ Reference math: HF `SiglipEncoderLayer` / timm `Block` as used by
 under bf16 autocast: GEMMs in the compute dtype with fp32 accumulation,
 LayerNorm and residual stream in fp32.
 
-bf16 GEMMs (the SigLIP2 tower under autocast) are library GEMMs (hipBLASLt through
-torch.matmul, MFMA); on ROCm tensors outside autograd fc1's bias + tanh-GELU runs as
-the hipBLASLt GELU_BIAS epilogue (torch._addmm_activation, the tanh form SigLIP uses).
+bf16 GEMMs (the SigLIP2 tower under autocast) run on our 256-tile MFMA GEMM on ROCm tensors outside
+autograd (csrc/gemm8.hip), with the bias and fc1's tanh-GELU (the form SigLIP uses) in the epilogue;
+elsewhere (and with VFM_VIT_GEMM=torch) they are hipBLASLt GEMMs through torch.matmul / addmm.
 fp32 linears (the DINO ViT-S tower of the projected discriminator, whose input gradient
 the G phase takes) run on our GEMM with fp32-equivalent f32x6 products and autograd
 (torch_utils/ops/linear.py). LayerNorm -> compute dtype (optionally fused with the
 residual add) is one HIP row kernel (`vit_hip`, csrc/vit.hip).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import kernel_timer
+
+# bf16 linears of the frozen towers on our 256-tile GEMM (csrc/gemm8.hip, bias / bias + tanh-GELU in
+# the epilogue) with VFM_VIT_GEMM=hip; off by default while gemm8 measures 0.72-0.82x hipBLASLt on the
+# SigLIP2 shapes (profiles/r3_j_gemm8_shapes.txt)
+OWN_GEMM = os.environ.get("VFM_VIT_GEMM", "torch") == "hip"
+
+
+def frozen_weight(w, dtype):
+    """w cast to dtype, cached on the parameter until its version moves (the frozen towers' weights are
+    cast once instead of at every forward; not cached while a HIP graph is being captured)."""
+    from .decoder_hip import _cast_cached
+    return _cast_cached(w, dtype)
+
+
+def _own_linear(x, w, b, act=None):
+    """x @ w^T (+ b, + act) on gemm8 for ROCm bf16 tensors outside autograd, else None. The bias is
+    rounded to x's dtype first and added to the fp32 accumulator (hipBLASLt's bias epilogue)."""
+    if not (OWN_GEMM and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and _frozen(x, w, b)):
+        return None
+    from . import gemm_hip
+    from .decoder_hip import _cast_cached
+    bias = None if b is None else _cast_cached(_cast_cached(b, x.dtype), torch.float32)
+    x2 = x.reshape(-1, x.shape[-1])
+    y = gemm_hip.try_gemm(x2, w.t(), bias=bias, bias_dim=1, act=act, route=("g8", 0))
+    return None if y is None else y.reshape(*x.shape[:-1], w.shape[0])
 
 
 def _vg(x, w, tag):
@@ -52,6 +79,10 @@ def linear(x, w, b=None):
     if x.is_cuda and x.dtype == torch.float32:
         from . import linear as linear_op
         return linear_op.linear(x, w, b)
+    if x.is_cuda:
+        y = _own_linear(x, w, b)
+        if y is not None:
+            return y
     with _vg(x, w, "vit_linear"):
         if b is not None:
             return torch.addmm(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
@@ -61,6 +92,9 @@ def linear(x, w, b=None):
 def linear_gelu_tanh(x, w, b=None):
     """gelu_tanh(x @ w^T + b): GEMM with the GELU_BIAS epilogue on ROCm (frozen towers)."""
     if b is not None and x.dtype != torch.float32 and _frozen(x, w, b):
+        y = _own_linear(x, w, b, act="gelu_tanh")
+        if y is not None:
+            return y
         with _vg(x, w, "vit_fc1_gelu"):
             y = torch._addmm_activation(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
         return y.reshape(*x.shape[:-1], w.shape[0])
