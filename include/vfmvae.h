@@ -290,6 +290,10 @@ int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int prec
               int kchunk, int reduce_batch, void* stream);
 int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
                                int reduce_batch);  /* -1: too large */
+/* K-tile staging schedule of vfm_gemm8 / vfm_gemm8_gelu (process-wide A/B switch for microbenchmarks):
+ * 1 = half-tile slots restaged two K-tiles ahead, 0 = one K-tile ahead (default). Returns the previous
+ * setting. */
+int vfm_gemm8_set_schedule(int deep);
 /* The ConvNeXt MLP's bf16 1x1 GEMMs with their GELU fused into the epilogue (replaces the
  * pwconv1 -> nn.GELU and the GELU backward of reference networks/utils/convnext_utils.py:135-142
  * around torch's batched matmul): C[z] = W X[z], W [M, K] K-contiguous (row stride lda), X[z]

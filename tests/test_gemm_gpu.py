@@ -165,11 +165,21 @@ def test_gemm_unsupported_shape_returns_none():
     assert gemm_hip.try_gemm(A, B) is None
 
 
+@pytest.fixture(params=[1, 0], ids=["deep", "one_ahead"])
+def g8_schedule(request):
+    """Both K-tile staging schedules of gemm8 (two / one K-tiles ahead)."""
+    from torch_utils import custom_ops
+    lib = custom_ops.get_native()
+    prev = lib.vfm_gemm8_set_schedule(request.param)
+    yield request.param
+    lib.vfm_gemm8_set_schedule(prev)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 256), (520, 776, 128), (256, 256, 64), (1000, 264, 704),
                                    (512, 512, 128)])
-def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, monkeypatch):
+def test_gemm_fast_path_layouts(dtype, a_t, b_t, M, N, K, monkeypatch, g8_schedule):
     """The 256-tile LDS-DMA kernel (csrc/gemm8.hip, 4-phase pipeline) and, for fp32, the piece split
     walked as 6 product terms; bf16 K = 64 / 128 are the one- and two-K-tile paths of the prologue and
     tail."""
@@ -213,7 +223,7 @@ def test_gemm_fast_epilogue_batched(dtype):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("act", [None, "gelu_tanh"])
 @pytest.mark.parametrize("bias_dim", [None, 1, 0])
-def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch):
+def test_gemm8_fp32_output_epilogue(dtype, act, bias_dim, monkeypatch, g8_schedule):
     """gemm8's fp32-output epilogue: full 256 x 256 tiles go through the LDS-staged 16-B store form
     (alpha, row / column bias, GELU), the ragged last tiles through the per-element form."""
     from torch_utils.ops import gemm_hip
@@ -241,7 +251,7 @@ def test_gemm_generic_path_when_fast_off(monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("O,I,P,Bn", [(512, 256, 1024, 6), (304, 264, 320, 3)])
-def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, monkeypatch):
+def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, monkeypatch, g8_schedule):
     """sum_b dy[b] . x[b]^T on gemm8's split-K over the batch-concatenated K (opt-in path,
     VFM_GEMM8_SPLIT=1): fp32 partials + fixed-order reduce; every operand layout; ragged M/N."""
     from torch_utils.ops import gemm_hip, kernel_timer
@@ -262,7 +272,7 @@ def test_gemm8_batch_reduced_weight_gradient(dtype, a_kc, b_kc, O, I, P, Bn, mon
 
 
 @pytest.mark.parametrize("M,N,K", [(768, 512, 8192), (256, 300, 2048)])
-def test_gemm8_split_k(M, N, K, monkeypatch):
+def test_gemm8_split_k(M, N, K, monkeypatch, g8_schedule):
     """Few output tiles over a deep K (the adapter's weight gradients): split-K on gemm8 with a bias
     epilogue in the reduce pass."""
     from torch_utils.ops import gemm_hip
@@ -280,7 +290,7 @@ def test_gemm8_split_k(M, N, K, monkeypatch):
 @pytest.mark.parametrize("a_t,b_t", [(False, True), (True, False)])
 @pytest.mark.parametrize("M,N,K,Z", [(4352, 4608, 192, 1), (520, 1000, 128, 40), (4400, 2056, 64, 1)])
 @pytest.mark.parametrize("out_bf16", [False, True])
-def test_gemm8_many_tiles(dtype, a_t, b_t, M, N, K, Z, out_bf16):
+def test_gemm8_many_tiles(dtype, a_t, b_t, M, N, K, Z, out_bf16, g8_schedule):
     """More tiles than CUs (289-480 blocks), batched operands and ragged edges through the buffer-
     descriptor DMA offsets."""
     from torch_utils.ops import gemm_hip
@@ -297,7 +307,7 @@ def test_gemm8_many_tiles(dtype, a_t, b_t, M, N, K, Z, out_bf16):
     assert _rel(out.float(), ref) < tol
 
 
-def test_gemm8_split_k_ragged_chunks():
+def test_gemm8_split_k_ragged_chunks(g8_schedule):
     """Split-K over several chunks per tile, the last one shorter."""
     from torch_utils.ops import gemm_hip
     g = torch.Generator().manual_seed(11)

@@ -30,6 +30,7 @@ def rnd(*shape):
     return (torch.rand(*shape, device="cuda") * 2 - 1).to(torch.bfloat16)
 
 
+lib.vfm_gemm8_set_schedule(int(os.environ.get("G8_DEEP", "1")))
 for M, N in [(32768, 1024), (32768, 3072), (8192, 8192)]:
     tiles = (M // 256) * (N // 256)
     for K in (64, 128, 256, 512, 1024, 2048, 4096):

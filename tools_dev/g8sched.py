@@ -1,4 +1,4 @@
-"""Microbench: gemm8 against hipBLASLt on the bf16 square and SigLIP2 shapes and the f32x6
+"""Microbench: gemm8 (both K-tile staging schedules, vfm_gemm8_set_schedule) against hipBLASLt on the bf16 square and SigLIP2 shapes and the f32x6
 decoder / adapter shapes (times include the activation split for fp32; weights cached)."""
 import os
 import sys
@@ -31,10 +31,14 @@ def rnd(*shape, dt=torch.bfloat16):
 
 
 def row(name, fl, ours, blas):
-    t8 = bench(ours)
+    res = []
+    for sched in (1, 0):
+        lib.vfm_gemm8_set_schedule(sched)
+        res.append(bench(ours))
+    lib.vfm_gemm8_set_schedule(1)
     tb = bench(blas)
-    print(f"{name:34s} gemm8 {t8 * 1e3:8.1f}us {fl / t8 / 1e9:7.1f} | blas {tb * 1e3:8.1f}us {fl / tb / 1e9:7.1f}  TF/s",
-          flush=True)
+    print(f"{name:34s} deep {res[0] * 1e3:8.1f}us {fl / res[0] / 1e9:7.1f} | one-ahead {res[1] * 1e3:8.1f}us "
+          f"{fl / res[1] / 1e9:7.1f} | blas {tb * 1e3:8.1f}us {fl / tb / 1e9:7.1f}  TF/s", flush=True)
 
 
 torch.backends.cuda.matmul.allow_tf32 = False

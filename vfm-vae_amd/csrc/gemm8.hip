@@ -107,9 +107,9 @@ constexpr int OFF_ALO = 0, OFF_AHI = HALF, OFF_BLO = 2 * HALF, OFF_BHI = 3 * HAL
 // issues its loads with no per-lane address arithmetic and no generic->LDS pointer conversion.
 // Issued from inline asm so that hipcc's waitcnt pass does not see an LDS write in flight and drain
 // it with vmcnt(0) before every ds_read; the counted waits below are the only ones. M0 is written in
-// the same statement (and the s_nop covers the M0 -> LDS-DMA hazard).
+// the same statement; the s_nops cover the readfirstlane -> soffset and M0 -> LDS-DMA hazards.
 __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned m0) {
-    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
                  "s"(soff), "s"(m0)
                  : "memory");
 }
@@ -358,7 +358,7 @@ __device__ __forceinline__ void store_tile(const G8Args& a, f32x4 (&acc)[8][4], 
     }
 }
 
-template <bool AK, bool BKC, bool OUTF32, int EPI = 0>
+template <bool AK, bool BKC, bool OUTF32, bool DEEP, int EPI = 0>
 __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -415,16 +415,16 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     auto soffs = [&](unsigned& sa, unsigned& sb) {
         const long long ka = (long long)kk * BK + ((a.pa >> (2 * term)) & 3) * (long long)a.Kp;
         const long long kb = (long long)kk * BK + ((a.pb >> (2 * term)) & 3) * (long long)a.Kp;
-        sa = (unsigned)((zt * a.sA + (AK ? ka : ka * a.lda)) * 2);
-        sb = (unsigned)((zt * a.sB + (BKC ? kb : kb * a.ldb)) * 2);
+        sa = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sA + (AK ? ka : ka * a.lda)) * 2));
+        sb = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sB + (BKC ? kb : kb * a.ldb)) * 2));
     };
-    auto advance = [&]() {
-        if (++kk == KTz) {
-            kk = 0;
-            if (a.reduce && ++zt < a.Z) return;
-            zt = a.reduce ? 0 : zt;
-            ++term;
-        }
+    auto advance = [&]() {                               // branch-free: selects on wave-uniform values
+        const bool w1 = ++kk == KTz;
+        kk = w1 ? 0 : kk;
+        const int zn = zt + (a.reduce && w1 ? 1 : 0);
+        const bool w2 = a.reduce ? zn == a.Z : w1;
+        zt = (a.reduce && w2) ? 0 : zn;
+        term += w2 ? 1 : 0;
     };
     auto issue = [&](unsigned sa, unsigned sb, int bsel, int h) {
         const unsigned m0 = lds0 + bsel * BUF + (h == 0 ? OFF_ALO : h == 1 ? OFF_BLO : h == 2 ? OFF_BHI : OFF_AHI);
@@ -478,6 +478,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     };
 
     const long long t_entry = a.stamps ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    const int KT = it.KT;
+    unsigned sa1 = 0, sb1 = 0;                  // offsets of K-tile t + 1
     {
         unsigned sa, sb;
         soffs(sa, sb);
@@ -485,8 +487,15 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
         issue(sa, sb, 0, 1);
         issue(sa, sb, 0, 2);
         issue(sa, sb, 0, 3);
+        if (DEEP && KT > 1) {
+            advance();
+            soffs(sa1, sb1);
+            issue(sa1, sb1, 1, 0);
+            issue(sa1, sb1, 1, 1);
+        }
     }
-    VMCNT(4);                                   // A_lo, B_lo of the first K-tile
+    if (DEEP && KT > 1) VMCNT(8);               // A_lo(0), B_lo(0) landed; B_hi(0), A_hi(0), A_lo(1), B_lo(1) in flight
+    else VMCNT(4);                              // A_lo, B_lo of the first K-tile
     __builtin_amdgcn_s_barrier();
     long long* stamp = (a.stamps && tid == 0) ? a.stamps + (long long)(blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
     if (stamp) {
@@ -496,27 +505,69 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     // ping-pong: the wm = 1 wave-row runs one barrier behind (2 barriers per phase), so one
     // wave-row's 16 MFMAs overlap the other's DMA issue + fragment reads (see the header)
     if (wm == 1) __builtin_amdgcn_s_barrier();
-    for (int t = 0; t < it.KT; ++t) {
-        const unsigned char* buf = lds + (t & 1) * BUF;
-        const bool nxt = t + 1 < it.KT;
-        unsigned sa = 0, sb = 0;
-        if (nxt) {
-            advance();
-            soffs(sa, sb);
-        }
-        const int nb = (t + 1) & 1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            if (nxt) issue(sa, sb, nb, p);
-            phase_reads(buf, p);
-            // wait for the NEXT phase's half-tile (see the header), then the phase barrier
-            if (nxt) {
-                if (p == 0 || p == 1 || p == 3) VMCNT(4);
-            } else {
-                if (p == 0) VMCNT(2);
-                else if (p == 1) VMCNT(0);
+    if (DEEP) {
+        // Two K-tiles ahead: the fragments of a half-tile live in VGPRs after their phase, so its LDS
+        // slot is restaged for K-tile t+2 two or more phases later (WAR with the rows one barrier
+        // apart). Phase p of K-tile t issues p0: B_hi(t+1), p1: A_hi(t+1) (buffer (t+1)&1), p2:
+        // A_lo(t+2), p3: B_lo(t+2) (buffer t&1); the counted waits leave 4 half-tiles (8 DMA) in
+        // flight, so each half-tile is issued 5-6 phases before its read (2-4 in the other schedule).
+        for (int t = 0; t < KT; ++t) {
+            const unsigned char* buf = lds + (t & 1) * BUF;
+            const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
+            unsigned sa2 = 0, sb2 = 0;
+            if (n2) {
+                advance();
+                soffs(sa2, sb2);
             }
-            phase_math(p);
+            // p0: issue B_hi(t+1); read A_lo(t), B_lo(t); wait for B_hi(t)
+            if (n1) issue(sa1, sb1, (t + 1) & 1, 2);
+            phase_reads(buf, 0);
+            if (n1) VMCNT(8);
+            else VMCNT(2);
+            phase_math(0);
+            // p1: issue A_hi(t+1); read B_hi(t); wait for A_hi(t)
+            if (n1) issue(sa1, sb1, (t + 1) & 1, 3);
+            phase_reads(buf, 1);
+            if (n1) VMCNT(8);
+            else VMCNT(0);
+            phase_math(1);
+            // p2: issue A_lo(t+2); read A_hi(t)
+            if (n2) issue(sa2, sb2, t & 1, 0);
+            phase_reads(buf, 2);
+            phase_math(2);
+            // p3: issue B_lo(t+2); wait for A_lo(t+1), B_lo(t+1)
+            if (n2) issue(sa2, sb2, t & 1, 1);
+            if (n1) {
+                if (n2) VMCNT(8);
+                else VMCNT(4);
+            }
+            phase_math(3);
+            sa1 = sa2;
+            sb1 = sb2;
+        }
+    } else {
+        for (int t = 0; t < KT; ++t) {
+            const unsigned char* buf = lds + (t & 1) * BUF;
+            const bool nxt = t + 1 < KT;
+            unsigned sa = 0, sb = 0;
+            if (nxt) {
+                advance();
+                soffs(sa, sb);
+            }
+            const int nb = (t + 1) & 1;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                if (nxt) issue(sa, sb, nb, p);
+                phase_reads(buf, p);
+                // wait for the NEXT phase's half-tile (see the header), then the phase barrier
+                if (nxt) {
+                    if (p == 0 || p == 1 || p == 3) VMCNT(4);
+                } else {
+                    if (p == 0) VMCNT(2);
+                    else if (p == 1) VMCNT(0);
+                }
+                phase_math(p);
+            }
         }
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();
@@ -557,16 +608,23 @@ __global__ __launch_bounds__(256) void gemm8_reduce(G8Args a) {
 }
 
 long long* g_stamps = nullptr;   // microbenchmark stamp buffer (vfm_gemm8_set_stamps)
+int g_deep = 0;                  // K-tile staging: 1 = two K-tiles ahead, 0 = one (vfm_gemm8_set_schedule)
 
-template <bool AK, bool BKC, bool OUTF32, int EPI = 0>
-void launch8k(const G8Args& a, int nwg, int ny, hipStream_t st) {
+template <bool AK, bool BKC, bool OUTF32, bool DEEP, int EPI>
+void launch8d(const G8Args& a, int nwg, int ny, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32, EPI>,
+        (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32, DEEP, EPI>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32, EPI>), dim3(nwg, ny), dim3(THREADS), 2 * BUF, st, a);
+    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32, DEEP, EPI>), dim3(nwg, ny), dim3(THREADS), 2 * BUF, st, a);
+}
+
+template <bool AK, bool BKC, bool OUTF32, int EPI = 0>
+void launch8k(const G8Args& a, int nwg, int ny, hipStream_t st) {
+    if (g_deep) launch8d<AK, BKC, OUTF32, true, EPI>(a, nwg, ny, st);
+    else launch8d<AK, BKC, OUTF32, false, EPI>(a, nwg, ny, st);
 }
 
 template <bool AK, bool BKC, bool OUTF32>
@@ -745,6 +803,15 @@ extern "C" int vfm_gemm8_gelu(const void* W, const void* X, void* C, void* C2, c
 extern "C" int vfm_gemm8_set_stamps(long long* buf) {
     g_stamps = buf;
     return VFM_OK;
+}
+
+// K-tile staging schedule of vfm_gemm8 / vfm_gemm8_gelu (A/B switch for microbenchmarks): 1 = half-tile
+// slots restaged two K-tiles ahead, 0 = one K-tile ahead (default: 8192^3 1284 vs 1120 TF/s, SigLIP2
+// qkv 879 vs 805, profiles/r3_k_gemm8_shapes.txt). Returns the previous value.
+extern "C" int vfm_gemm8_set_schedule(int deep) {
+    const int prev = g_deep;
+    g_deep = deep ? 1 : 0;
+    return prev;
 }
 
 // Partial-sum slots per (batch, row) of vfm_gemm8_gelu mode 2 for N columns.
