@@ -118,6 +118,13 @@ int vfm_filtered_lrelu_act(void* x, unsigned char* s, int dtype,
                            int sh, int sw_bytes, int sx, int sy, int sign_mode,
                            float gain, float slope, float clamp, void* stream);
 
+/* DiffAugment random translation (replaces the padded gather of reference training/diffaug.py
+ * rand_translation and its indexing backward): y[b, c, i, j] = x[b, c, i + sign tx[b], j + sign ty[b]]
+ * inside the image, else 0; x, y contiguous NCHW (VFM_F32 / VFM_BF16); tx, ty int64 [B] on the device.
+ * The backward is the same call with sign = -1. */
+int vfm_shift2d(const void* x, void* y, const long long* tx, const long long* ty, int dtype, int B, int C, int H,
+                int W, int sign, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Decoder ops (ConvNeXt synthesis layer, separable upsampler). The reference runs
  * these as stock torch modules; the entry points below replace the calls at

@@ -68,6 +68,7 @@ SIGNATURES = {
                        c_ll, c_ll, c_ll, c_ll, c_ll, c_vp],
     "vfm_gemm8_gelu_parts": [c_int],
     "vfm_gemm8_set_stamps": [c_vp],
+    "vfm_shift2d": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_im2col_nhwc_f32": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_col2im_nhwc_f32": [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_int, c_vp],

@@ -40,11 +40,51 @@ def rand_contrast(x):
     return (x - m) * (_u(x) + 0.5) + m
 
 
+class _Shift2d(torch.autograd.Function):
+    """Per-sample integer shift with zero fill on the HIP kernel (csrc/diffaug.hip vfm_shift2d): the
+    reference's padded gather, whose backward is the shift by -t (a bijection between in-range pixels)."""
+
+    @staticmethod
+    def forward(ctx, x, tx, ty):
+        from torch_utils import custom_ops
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        B, C, H, W = x.shape
+        lib = custom_ops.get_native()
+        custom_ops.check(lib.vfm_shift2d(x.data_ptr(), y.data_ptr(), tx.data_ptr(), ty.data_ptr(),
+                                         custom_ops.dtype_code(x), B, C, H, W, 1, custom_ops.stream_ptr(x.device)),
+                         "vfm_shift2d")
+        ctx.save_for_backward(tx, ty)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        from torch_utils import custom_ops
+        tx, ty = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        B, C, H, W = dy.shape
+        lib = custom_ops.get_native()
+        custom_ops.check(lib.vfm_shift2d(dy.data_ptr(), dx.data_ptr(), tx.data_ptr(), ty.data_ptr(),
+                                         custom_ops.dtype_code(dy), B, C, H, W, -1, custom_ops.stream_ptr(dy.device)),
+                         "vfm_shift2d")
+        return dx, None, None
+
+
 def rand_translation(x, ratio=0.125):
     B, C, H, W = x.shape
     sx, sy = int(H * ratio + 0.5), int(W * ratio + 0.5)
     tx = torch.randint(-sx, sx + 1, size=[B, 1, 1], device=x.device)
     ty = torch.randint(-sy, sy + 1, size=[B, 1, 1], device=x.device)
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and C * H <= 65535 and B <= 65535:
+        return _Shift2d.apply(x, tx.reshape(B).contiguous(), ty.reshape(B).contiguous())
+    return translate_gather(x, tx, ty)
+
+
+def translate_gather(x, tx, ty):
+    """The reference formulation: one-pixel zero pad, gather at the clamped shifted grid."""
+    B, C, H, W = x.shape
     gb, gx, gy = torch.meshgrid(torch.arange(B, device=x.device), torch.arange(H, device=x.device),
                                 torch.arange(W, device=x.device), indexing='ij')
     gx = torch.clamp(gx + tx + 1, 0, H + 1)
