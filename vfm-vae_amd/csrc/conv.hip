@@ -13,8 +13,11 @@
 // of 64. The data gradient of the same conv is this kernel with the flipped, transposed weights
 // w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
 //
-// GEMM view: M = B*H*W pixels, N = Cout, K = 9*Cin (tap-major). Tile 128 pixels x BN (128 or 64)
-// couts x 32 k, 4 waves (2 x 2), 32x32x16 bf16 MFMA; fp32 activations split into NP piece images on
+// GEMM view: M = B*H*W pixels, N = Cout, K = 9*Cin (tap-major). Tile BM pixels x BN couts x 32 k with
+// 2 BM threads as (BM/64) x 2 waves of 64 x BN/2, 32x32x16 bf16 MFMA: 256 x 128 with 8 waves (two per
+// SIMD: one wave's MFMAs overlap the other's loads, split and LDS writes) for the f32x6 products at
+// Cout % 128 == 0 (vggbench: 146 -> 196 TF/s; 256 x 64 measured no faster than 128 x 64 for the
+// Cout = 64 layers), 128 x BN with 4 waves otherwise; fp32 activations split into NP piece images on
 // the way into LDS, the Terms<NP> piece products accumulated (gemm.hip's f32x6 / f32x3: hi.hi in
 // its own accumulator). Two LDS stages (double buffer): the split + store of K-tile t+1 and the
 // global loads of K-tile t+2 are issued between the MFMA steps of K-tile t, one barrier per K-tile
@@ -31,9 +34,8 @@ using namespace vfm;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BK = 32, THREADS = 256;
+constexpr int BK = 32;
 constexpr int ROWB = BK * 2;          // bytes of one bf16 image row (4 16-B chunks)
-constexpr int IMG_A = BM * ROWB;      // bytes of one bf16 piece image of the A tile
 
 struct ConvArgs {
     const float* x;      // [B, H, W, Cin]
@@ -64,15 +66,17 @@ __device__ __forceinline__ void put4(unsigned char* img, int pstride, int off, u
     for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(img + p * pstride + off) = make_uint2(p01[p], p23[p]);
 }
 
-// thread -> (row = tid/8 + 32u, 4-element column tid%8) of a [128][32] fp32 tile
+// thread -> (row = tid/8 + (THREADS/8) u, 4-element column tid%8) of a [4 THREADS/8][32] fp32 tile
+template <int THREADS>
 struct StageA {
+    static constexpr int IMG = 4 * (THREADS / 8) * ROWB;   // bytes of one bf16 piece image of the A tile
     uint4 r[4];
     int pm[4];    // pixel index (or -1)
     int pyx[4];   // y << 16 | x
     __device__ __forceinline__ void init(const ConvArgs& a, int m0, int tid) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int m = m0 + tid / 8 + 32 * u;
+            const int m = m0 + tid / 8 + (THREADS / 8) * u;
             if (m < a.M) {
                 const uint32_t q = fdiv((uint32_t)m, a.fW);
                 const int xx = m - (int)q * a.W;
@@ -130,22 +134,24 @@ struct StageA {
     __device__ __forceinline__ void store(unsigned char* img, int tid) const {
         const int cc = tid & 7;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) put4<NP>(img, IMG_A, k32_off(tid / 8 + 32 * u, cc >> 1) + 8 * (cc & 1), r[u]);
+        for (int u = 0; u < 4; ++u) put4<NP>(img, IMG, k32_off(tid / 8 + (THREADS / 8) * u, cc >> 1) + 8 * (cc & 1), r[u]);
     }
 };
 
 // weights arrive pre-split (NP bf16 pieces, split once per weight version on the host side):
-// thread -> 16-B chunks (8 k) c = tid + 256u of a [ROWS][32] tile, copied as-is into the piece images
-template <int ROWS, int NP>
+// thread -> 16-B chunks (8 k) c = tid + THREADS u of a [ROWS][32] tile, copied as-is into the piece
+// images (with more threads than chunks, the threads past ROWS * 4 load nothing)
+template <int ROWS, int NP, int THREADS>
 struct StageB {
-    static constexpr int PER = ROWS * 4 / THREADS;
+    static constexpr int CHUNKS = ROWS * 4;
+    static constexpr int PER = CHUNKS >= THREADS ? CHUNKS / THREADS : 1;
     static constexpr int IMG = ROWS * ROWB;
     uint4 v[NP][PER];
     __device__ __forceinline__ void load(const ConvArgs& a, int n0, int k0, int tid) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int c = tid + THREADS * u, row = c >> 2, k = k0 + 8 * (c & 3), n = n0 + row;
-            const bool ok = k < a.ldw && n < a.Cout;
+            const bool ok = k < a.ldw && n < a.Cout && c < CHUNKS;
             const unsigned o = (unsigned)(n * a.ldw + k) * 2u;          // byte offset (host: Cout * ldw < 2^30)
 #pragma unroll
             for (int p = 0; p < NP; ++p)
@@ -157,6 +163,7 @@ struct StageB {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int c = tid + THREADS * u, off = k32_off(c >> 2, c & 3);
+            if (CHUNKS < THREADS && c >= CHUNKS) continue;
 #pragma unroll
             for (int p = 0; p < NP; ++p) *reinterpret_cast<uint4*>(img + p * IMG + off) = v[p][u];
         }
@@ -174,15 +181,19 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <int BN, int NP>
-__global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3_kernel(ConvArgs a) {
+// BM x BN tile, THREADS = 2 BM: waves as (BM / 64) (M) x 2 (N), each 64 rows x BN / 2 columns.
+template <int BM, int BN, int NP>
+__global__ __launch_bounds__(2 * BM, (BM == 256 || (NP == 3 && BN == 128)) ? 1 : 2) void conv3x3_kernel(ConvArgs a) {
+    constexpr int THREADS = 2 * BM;
+    constexpr int WM = BM / 64;                 // waves along M
     constexpr int NJ = BN / 64;                 // 32-col blocks per wave
+    constexpr int IMG_A = StageA<THREADS>::IMG;
     constexpr int IMG_B = BN * ROWB;
     constexpr int STAGE = NP * (IMG_A + IMG_B); // A pieces, then B pieces
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
+    const int wm = wave % WM, wn = wave / WM;
     const int tiles_n = a.Cout / BN;
     // XCD-aware bijective remap: the blocks b, b+8, b+16, ... (one XCD, one L2) take consecutive
     // tiles, i.e. all Cout tiles of neighbouring pixel rows, which share the same input rows
@@ -191,8 +202,8 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
-    StageA sa;
-    StageB<BN, NP> sb;
+    StageA<THREADS> sa;
+    StageB<BN, NP, THREADS> sb;
     sa.init(a, m0, tid);
     sa.cur_tap = -1;
     const bool wide = a.lc >= 5;                        // Cin >= 32 (uniform)
@@ -210,7 +221,7 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
     };
     auto lstore = [&](int buf) {
         unsigned char* st = lds + buf * STAGE;
-        sa.store<NP>(st, tid);
+        sa.template store<NP>(st, tid);
         sb.store(st + NP * IMG_A, tid);
     };
     gload(0);
@@ -277,17 +288,18 @@ __global__ __launch_bounds__(THREADS, NP == 3 && BN == 128 ? 1 : 2) void conv3x3
     }
 }
 
-template <int BN, int NP>
+template <int BM, int BN, int NP>
 int launch(const ConvArgs& a, hipStream_t st) {
-    const size_t lds = 2 * NP * (IMG_A + BN * ROWB);
+    const size_t lds = 2 * NP * (BM + BN) * ROWB;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BN, NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BM, BN, NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
         attr = true;
     }
     const long long tiles = (long long)((a.M + BM - 1) / BM) * (a.Cout / BN);
     if (tiles > 0x7fffffff) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL((conv3x3_kernel<BN, NP>), dim3((unsigned)tiles), dim3(THREADS), lds, st, a);
+    hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NP>), dim3((unsigned)tiles), dim3(2 * BM), lds, st, a);
     return launch_status();
 }
 
@@ -318,8 +330,8 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int pr
     a.fH = make_fastdiv((uint32_t)H);
     a.relu = relu;
     hipStream_t st = (hipStream_t)stream;
-    if (np == 3) return (Cout % 128 == 0) ? launch<128, 3>(a, st) : launch<64, 3>(a, st);
-    return (Cout % 128 == 0) ? launch<128, 2>(a, st) : launch<64, 2>(a, st);
+    if (np == 3) return (Cout % 128 == 0) ? launch<256, 128, 3>(a, st) : launch<128, 64, 3>(a, st);
+    return (Cout % 128 == 0) ? launch<128, 128, 2>(a, st) : launch<128, 64, 2>(a, st);
 }
 
 // ---------------------------------------------------------------------------------------------

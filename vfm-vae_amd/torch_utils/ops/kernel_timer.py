@@ -141,12 +141,16 @@ def rocprof_name(region):
     region = region.split("[", 1)[0]
     base, _, args = region.partition("<")
     args = args.rstrip(">").split(",") if args else []
-    if base == "gemm8" and len(args) == 4:                     # <tag, AK, BK, OUTF32>
-        return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}>"
+    if base == "gemm8" and len(args) == 4:                     # <tag, AK, BK, OUTF32> (default schedule, EPI 0)
+        return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}, false, 0>"
+    if base == "gemm8_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2)
+        return f"gemm8_kernel<true, false, false, false, {args[0]}>"
     if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32>
         return f"gemm_kernel<{args[1]}, {args[2]}, {_NP.get(args[0], 1)}, {args[3]}>"
-    if base == "conv3x3_nhwc" and len(args) == 2:              # conv3x3_kernel<BN, NP>
-        return f"conv3x3_kernel<{args[1]}, {_NP.get(args[0], 3)}>"
+    if base == "conv3x3_nhwc" and len(args) == 2:              # conv3x3_kernel<BM, BN, NP>
+        np_ = _NP.get(args[0], 3)
+        bm = 256 if (np_ == 3 and args[1] == "128") else 128
+        return f"conv3x3_kernel<{bm}, {args[1]}, {np_}>"
     if base in ("attention_fwd", "attention_bwd") and args and args[0] in ("f32x6", "f32x3"):
         np_ = _NP[args[0]]
         return f"attn32_fwd<{np_}>" if base == "attention_fwd" else f"attn32_dkdv<{np_}>"

@@ -70,7 +70,7 @@ def conv3x3(x, w, bias=None, relu=False, mask=None):
     out = torch.empty(B, H, W, Cout, dtype=torch.float32, device=x.device)
     flops = 2 * B * H * W * Cout * 9 * Cin
     # one timer region per kernel instantiation (BN = 128 / 64 output channels per tile), as
-    # rocprofv3 names them: conv3x3_kernel<128, NP> / <64, NP>
+    # rocprofv3 names them: conv3x3_kernel<BM, 128, NP> / <128, 64, NP> (kernel_timer.rocprof_name)
     with kernel_timer.region(f"conv3x3_nhwc<{tag},{128 if Cout % 128 == 0 else 64}>",
                              4 * (x.numel() + out.numel() + Cout * 9 * Cin), flops, "mfma"):
         rc = _lib.vfm_conv3x3_nhwc_f32(x.data_ptr(), w.data_ptr(), prec, Kp, custom_ops.ptr(bias),
