@@ -94,7 +94,7 @@ def setup_tunableop(mode, out_path):
     return {"mode": "tune", "out": out_path}
 
 
-def build(cfg_path, batch_gpu, device, world, graphs=True):
+def build(cfg_path, batch_gpu, device, world, graphs=False):
     """G, G_ema, D, loss, optimisers and the TrainingIteration, through the SAME helpers
     training_loop() uses (training/training_loop.py construct_networks / construct_iteration /
     configure_backends), so the measured iteration is the one train.py runs."""

@@ -152,3 +152,21 @@ def test_train_main_snapshot_and_auto_resume(tmp_path, monkeypatch):
     for name in ("G", "D"):
         for n, t in ck[name].items():
             assert torch.equal(seen[name][n], t), (name, n)
+
+
+def test_wds_process_workers_batches(tmp_path):
+    """Decode in spawned worker processes (the GPU-host default): whole batches per worker, the same
+    decoded images as the thread workers (one-epoch pass, so the sample set is fixed)."""
+    from training.data_wds import WdsWrapper
+    _write_shards(str(tmp_path / "wds"), n_shards=4, per_shard=4)
+    c2t = tmp_path / "c2t.json"
+    c2t.write_text(json.dumps({"0": "zero", "1": "one", "2": "two"}))
+    kw = dict(label_type="cls2text", cls_to_text_path=str(c2t), workers=2, one_epoch=True, sample_shuffle_size=2)
+    got = {}
+    for procs in (False, True):
+        ds = WdsWrapper(str(tmp_path / "wds"), 64, processes=procs, **kw)
+        batches = list(ds.iterate(batch_size=4, seed=3))
+        assert all(b[0].shape == (4, 3, 64, 64) and b[0].dtype == torch.uint8 for b in batches)
+        assert all(len(b[1]) == 4 and all(lab in ("zero", "one", "two") for lab in b[1]) for b in batches)
+        got[procs] = sorted(bytes(x.numpy().tobytes()[:64]) for b in batches for x in b[0])
+    assert len(got[True]) == 16 and got[True] == got[False]

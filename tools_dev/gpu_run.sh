@@ -52,6 +52,8 @@ for s in "$@"; do
     btrace)  timeout -k 10 900 python bench.py --steps 3 --warmup 2 --trace --no-cpu-baseline > $out/btrace.log 2>&1 ;;
     bsteps)  timeout -k 10 900 python bench.py --steps 6 --warmup 2 --trace --no-cpu-baseline > $out/bsteps.log 2>&1 ;;
     bstepsng) timeout -k 10 900 python bench.py --steps 6 --warmup 2 --trace --no-cpu-baseline --no-gc-freeze > $out/bstepsng.log 2>&1 ;;
+    wdsbench) timeout -k 10 600 python tools_dev/wdsbench.py > $out/wdsbench.log 2>&1 ;;
+    torchops) timeout -k 10 600 python tools_dev/torchops.py > $out/torchops.log 2>&1 ;;
     cparents) timeout -k 10 600 python tools_dev/copy_parents.py > $out/cparents.log 2>&1 ;;
     tprof)   timeout -k 10 600 python tools_dev/torchprof.py --out $out/tp > $out/tprof.log 2>&1 ;;
     gemmbench8) timeout -k 10 300 python tools_dev/gemmbench.py > $out/gemmbench.log 2>&1 ;;

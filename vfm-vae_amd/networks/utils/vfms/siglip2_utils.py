@@ -126,7 +126,7 @@ class SiglipAttention(nn.Module):
         w, b = self.fused_qkv(x.dtype)
         qkv = vit_ops.linear(x, w, b)                                         # [B, N, 3D]
         o = vit_ops.attention_packed(qkv, self.num_heads)                     # [B, N, D]
-        return vit_ops.linear(o, self.out_proj.weight.to(x.dtype), self.out_proj.bias)
+        return vit_ops.linear(o, vit_ops.frozen_weight(self.out_proj.weight, x.dtype), self.out_proj.bias)
 
 
 class SiglipMLP(nn.Module):
@@ -136,8 +136,8 @@ class SiglipMLP(nn.Module):
         self.fc2 = nn.Linear(cfg["intermediate_size"], cfg["hidden_size"])
 
     def forward(self, x):
-        h = vit_ops.linear_gelu_tanh(x, self.fc1.weight.to(x.dtype), self.fc1.bias)
-        return vit_ops.linear(h, self.fc2.weight.to(x.dtype), self.fc2.bias)
+        h = vit_ops.linear_gelu_tanh(x, vit_ops.frozen_weight(self.fc1.weight, x.dtype), self.fc1.bias)
+        return vit_ops.linear(h, vit_ops.frozen_weight(self.fc2.weight, x.dtype), self.fc2.bias)
 
 
 class SiglipEncoderLayer(nn.Module):

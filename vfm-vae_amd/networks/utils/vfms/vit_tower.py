@@ -64,7 +64,7 @@ def mha(x, wq, bq, wk, bk, wv, bv, wo, bo, heads):
     b = torch.cat([bq, bk, bv], 0) if bq is not None else None
     qkv = vit_ops.linear(x, w, b)
     o = vit_ops.attention_packed(qkv, heads)
-    return vit_ops.linear(o, wo.to(x.dtype), bo)
+    return vit_ops.linear(o, vit_ops.frozen_weight(wo, x.dtype), bo)
 
 
 def ln(h, norm, dtype):
@@ -75,7 +75,7 @@ class Linear(nn.Linear):
     """nn.Linear whose forward runs in the input's (compute) dtype."""
 
     def forward(self, x):
-        return vit_ops.linear(x, self.weight.to(x.dtype), self.bias)
+        return vit_ops.linear(x, vit_ops.frozen_weight(self.weight, x.dtype), self.bias)
 
 
 def seeded_init(module, seed, std=0.02):

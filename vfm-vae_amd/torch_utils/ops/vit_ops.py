@@ -27,8 +27,13 @@ OWN_GEMM = os.environ.get("VFM_VIT_GEMM", "torch") == "hip"
 
 
 def frozen_weight(w, dtype):
-    """w cast to dtype, cached on the parameter until its version moves (the frozen towers' weights are
-    cast once instead of at every forward; not cached while a HIP graph is being captured)."""
+    """w cast to dtype; for a tensor that needs no gradient (the frozen towers' weights and biases)
+    cached on it until its version moves, so the cast runs once instead of at every forward (not
+    cached while a HIP graph is being captured: decoder_hip._cast_cached)."""
+    if w is None or w.dtype == dtype:
+        return w
+    if not w.is_cuda or (w.requires_grad and torch.is_grad_enabled()):
+        return w.to(dtype)
     from .decoder_hip import _cast_cached
     return _cast_cached(w, dtype)
 
@@ -66,11 +71,11 @@ def patch_embed(pixels, weight, bias, patch, compute_dtype):
     gh, gw = H // patch, W // patch
     x = pixels[:, :, :gh * patch, :gw * patch].to(compute_dtype)
     x = x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * patch * patch)
-    w = weight.reshape(weight.shape[0], -1).to(compute_dtype)
+    w = frozen_weight(weight, compute_dtype).reshape(weight.shape[0], -1)
     with _vg(x, w, "vit_patch"):
         y = torch.matmul(x, w.t())
     if bias is not None:
-        y = y + bias.to(compute_dtype)
+        y = y + frozen_weight(bias, compute_dtype)
     return y
 
 
@@ -85,7 +90,8 @@ def linear(x, w, b=None):
             return y
     with _vg(x, w, "vit_linear"):
         if b is not None:
-            return torch.addmm(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
+            return torch.addmm(frozen_weight(b, x.dtype), x.reshape(-1, x.shape[-1]), w.t()).reshape(
+                *x.shape[:-1], w.shape[0])
         return torch.matmul(x, w.t())
 
 
@@ -96,7 +102,7 @@ def linear_gelu_tanh(x, w, b=None):
         if y is not None:
             return y
         with _vg(x, w, "vit_fc1_gelu"):
-            y = torch._addmm_activation(b.to(x.dtype), x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
+            y = torch._addmm_activation(frozen_weight(b, x.dtype), x.reshape(-1, x.shape[-1]), w.t(), use_gelu=True)
         return y.reshape(*x.shape[:-1], w.shape[0])
     return F.gelu(linear(x, w, b), approximate="tanh")
 

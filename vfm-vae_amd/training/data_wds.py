@@ -20,10 +20,14 @@ stage YAML names (`training_set_kwargs.class_name: training.data_wds.WdsWrapper`
   labels    cls2text: class index -> text (`cls_to_text_path` JSON); cls2id: one-hot over
             the classes; text: the stripped caption.
 
-MI355X-side design: decode and augmentation run on `workers` host threads (PIL releases the
-GIL while decoding and resampling), each owning its shard stream, and whole batches are
-assembled into pinned uint8 [B, 3, R, R] tensors, so the training loop's host->device copy
-is asynchronous (`training_loop.fetch_data`, `non_blocking=True`) and overlaps the previous
+MI355X-side design: decode and augmentation run in `workers` host processes (`processes=True`,
+the default on a GPU host: the training loop's own Python thread issues ~10k kernel launches per
+iteration and held the GIL long enough that decode threads fell behind -- 53 ms of every
+~420 ms step waiting for a batch in `tools_dev/wdsbench.py` with 12 threads that decode 440 img/s
+on an idle host), each owning its shard stream and emitting whole batches, like the reference's
+WebLoader workers; or on threads (`processes=False`: the one-epoch shard log and CPU runs). Batches
+land in pinned uint8 [B, 3, R, R] tensors, so the training loop's host->device copy is
+asynchronous (`training_loop.fetch_data`, `non_blocking=True`) and overlaps the previous
 iteration. The key filter file (reference: a pickled key set) is read with a loader that
 accepts only plain containers and strings (nothing in the file is executed); JSON or text
 (one key per line) files work too.
@@ -173,11 +177,32 @@ class _WorkerError:
         self.exc = exc
 
 
+def _batch_worker(ds, rank, world, seed, w, batch_size, out_q, stop):
+    """Process entry of WdsWrapper._iterate_processes: worker w's shard stream -> whole batches
+    (uint8 [B, 3, R, R] numpy, labels); the same per-worker seeds as the thread workers."""
+    try:
+        shards, _ = ds._shard_plan(rank, world, seed)
+        keep = load_key_filter(ds.filter_keys_path) if ds.label_type != "text" else None
+        rng = random.Random((seed + rank * 1000 + w) * 7919 + 1)
+        R = ds.resolution
+        arr, labels = np.empty([batch_size, 3, R, R], dtype=np.uint8), []
+        for img, lab in ds._samples(shards[w], None, rng, keep, stop):
+            arr[len(labels)] = img
+            labels.append(lab)
+            if len(labels) == batch_size:
+                out_q.put((arr, labels))
+                arr, labels = np.empty([batch_size, 3, R, R], dtype=np.uint8), []
+    except Exception as e:                            # surfaced in iterate(), not swallowed
+        out_q.put(_WorkerError(e))
+    finally:
+        out_q.put(None)
+
+
 class WdsWrapper:
     def __init__(self, path, resolution, label_type="text", filter_keys_path=None, cls_to_text_path=None,
                  data_augmentation=False, one_epoch=False, processed_tar_read_dir=None,
                  processed_tar_write_dir=None, workers=3, shard_shuffle_size=50_000, sample_shuffle_size=50_000,
-                 **_unused):
+                 processes=None, **_unused):
         self._root = Path(path)
         self.resolution = int(resolution)
         self.label_type = label_type
@@ -196,6 +221,9 @@ class WdsWrapper:
             if cls_to_text_path and os.path.isfile(cls_to_text_path) else None
         self.num_classes = len(self._cls2text) if self._cls2text else 0
         self.urls = self._get_urls(str(path))
+        # decode in processes on a GPU host (see the module docstring); threads for the one-epoch
+        # shard log (a per-rank file the workers append to) and by request
+        self.processes = bool(torch.cuda.is_available() if processes is None else processes)
 
     def _get_urls(self, path):
         if self.label_type in ("cls2text", "cls2id"):
@@ -291,39 +319,84 @@ class WdsWrapper:
         return [iter(mine[w::self.workers]) for w in range(self.workers)], tracker
 
     def _worker(self, shards, tracker, rng, keep, out_q, stop):
-        buf = []
         try:
-            for url in shards:
-                if stop.is_set():
-                    return
-                for sample in iter_tar_samples(url):
-                    if tracker is not None:
-                        tracker(sample["__url__"])
-                    if keep is not None and os.path.basename(sample["__key__"]) not in keep \
-                            and sample["__key__"] not in keep:
-                        continue
-                    buf.append(sample)
-                    if len(buf) >= self.sample_shuffle_size:
-                        s = buf.pop(rng.randrange(len(buf)))
-                        item = self._decode(s, rng)
-                        if item is not None:
-                            out_q.put(item)
-                    if stop.is_set():
-                        return
-            rng.shuffle(buf)
-            for s in buf:
-                item = self._decode(s, rng)
-                if item is not None:
-                    out_q.put(item)
+            for item in self._samples(shards, tracker, rng, keep, stop):
+                out_q.put(item)
         except Exception as e:                        # surfaced in iterate(), not swallowed
             out_q.put(_WorkerError(e))
         finally:
             out_q.put(None)                           # this worker is exhausted
 
+    def _samples(self, shards, tracker, rng, keep, stop):
+        """Decoded (image, label) items of one worker's shard stream through its shuffle buffer."""
+        buf = []
+        for url in shards:
+            if stop.is_set():
+                return
+            for sample in iter_tar_samples(url):
+                if tracker is not None:
+                    tracker(sample["__url__"])
+                if keep is not None and os.path.basename(sample["__key__"]) not in keep \
+                        and sample["__key__"] not in keep:
+                    continue
+                buf.append(sample)
+                if len(buf) >= self.sample_shuffle_size:
+                    item = self._decode(buf.pop(rng.randrange(len(buf))), rng)
+                    if item is not None:
+                        yield item
+                if stop.is_set():
+                    return
+        rng.shuffle(buf)
+        for smp in buf:
+            item = self._decode(smp, rng)
+            if item is not None:
+                yield item
+
+    def _iterate_processes(self, batch_size, rank, world, seed):
+        """Worker processes (spawned: no CUDA state is inherited) each decode their shard stream into
+        whole batches; the parent copies each into a pinned tensor."""
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        out_q = ctx.Queue(maxsize=2 * self.workers)
+        stop = ctx.Event()
+        procs = [ctx.Process(target=_batch_worker, daemon=True, args=(self, rank, world, seed, w, batch_size, out_q,
+                                                                           stop))
+                 for w in range(self.workers)]
+        for p in procs:
+            p.start()
+        live = len(procs)
+        pin = torch.cuda.is_available()
+        try:
+            while True:
+                item = out_q.get()
+                if isinstance(item, _WorkerError):
+                    raise RuntimeError("WebDataset worker failed") from item.exc
+                if item is None:
+                    live -= 1
+                    if live == 0:
+                        return
+                    continue
+                arr, labels = item
+                imgs = torch.from_numpy(arr)
+                if pin:
+                    imgs = imgs.pin_memory()
+                if self.label_type == "cls2id":
+                    labels = torch.from_numpy(np.stack(labels))
+                yield imgs, labels
+        finally:
+            stop.set()
+            for p in procs:
+                p.join(timeout=0.5)
+                if p.is_alive():
+                    p.terminate()
+
     def iterate(self, batch_size, rank=0, world=1, seed=DEFAULT_SEED):
         """Batches (pinned uint8 [batch_size, 3, R, R], labels) for this rank: endless, or one
         pass over this rank's shards in one-epoch mode (the last partial batch is dropped, as
         `wds.batched` + the loop's full-batch split)."""
+        if self.processes and not (self.one_epoch and (self.processed_tar_write_dir or self.processed_tar_read_dir)):
+            yield from self._iterate_processes(batch_size, rank, world, seed)
+            return
         shards, tracker = self._shard_plan(rank, world, seed)
         keep = load_key_filter(self.filter_keys_path) if self.label_type != "text" else None
         out_q = queue.Queue(maxsize=4 * batch_size)
