@@ -118,6 +118,30 @@ int vfm_filtered_lrelu_act(void* x, unsigned char* s, int dtype,
                            int sh, int sw_bytes, int sx, int sy, int sign_mode,
                            float gain, float slope, float clamp, void* stream);
 
+/* Channel RMS norm of the decoder attention blocks (replaces F.normalize(x, dim=1) * scale * gamma of
+ * reference networks/utils/gigagan_utils.py:31-39 ChannelRMSNorm): fp32 contiguous [B, C, P];
+ * rinv [B, P] = 1 / max(||x||, 1e-12) saved for the backward (may be null in the forward). The
+ * backward writes dx, and dgamma [C] through the workspace gpart [vfm_channel_rms_norm_rows, C]
+ * (both null: no gamma gradient). */
+long long vfm_channel_rms_norm_rows(int B, int C, int P);
+int vfm_channel_rms_norm_fwd(const float* x, const float* gamma, float* y, float* rinv, int B, int C, int P,
+                             float scale, void* stream);
+int vfm_channel_rms_norm_bwd(const float* x, const float* gamma, const float* rinv, const float* dy, float* dx,
+                             float* gpart, float* dgamma, int B, int C, int P, float scale, void* stream);
+
+/* Style affine + demodulation coefficients of a ConvNeXt synthesis layer (replaces StyleSplit /
+ * FullyConnectedLayer of reference networks/utils/shared.py and the demodulation of
+ * networks/utils/convnext_utils.py:60-66): m = wg w A^T + bg ab [B, 3C], s = m1 m2 + m3 [B, C],
+ * d = rsqrt(s^2 (W1^2)^T + eps) [B, O] (W1 null: no d). fp32; w rows ldw apart. The backward takes
+ * dL/ds (ds_in) and dL/dd (dd) and writes any of dw [B, WD], dA [3C, WD], dab [3C], dW1 [O, C]
+ * (null: skipped); ds_ws [B, C] is its workspace. */
+int vfm_style_demod_fwd(const float* w, long long ldw, const float* A, const float* ab, const float* W1, float wg,
+                        float bg, float eps, int B, int C, int WD, int O, float* m, float* s, float* d, void* stream);
+int vfm_style_demod_bwd(const float* w, long long ldw, const float* A, const float* W1, const float* m,
+                        const float* s, const float* d, const float* ds_in, const float* dd, float wg, float bg,
+                        int B, int C, int WD, int O, float* ds_ws, float* dW1, float* dA, float* dab, float* dw,
+                        void* stream);
+
 /* DiffAugment random translation (replaces the padded gather of reference training/diffaug.py
  * rand_translation and its indexing backward): y[b, c, i, j] = x[b, c, i + sign tx[b], j + sign ty[b]]
  * inside the image, else 0; x, y contiguous NCHW (VFM_F32 / VFM_BF16); tx, ty int64 [B] on the device.
@@ -395,6 +419,15 @@ int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const float* w, co
  * 16-B aligned x / y / noise / res; VFM_NO_KERNEL otherwise. */
 int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise, const void* res,
                           void* y, int B, int C, int H, int W, int K, int pad, void* stream);
+/* The same convs with the taps read rotated by 180 degrees when flip != 0: the data gradient
+ * (dx = dwconv(dy, rot180(w)), pad' = K - 1 - pad) without a flipped copy of the weights. */
+int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* bias, const float* noise, void* y, int dtype,
+                        int B, int C, int H, int W, int K, int pad, int flip, void* stream);
+int vfm_dwconv2d_fwd_mfma_ex(const void* x, const float* w, const float* bias, const float* noise, const void* res,
+                             void* y, int B, int C, int H, int W, int K, int pad, int flip, void* stream);
+/* dw[c, t] = sum_r partial[r, c, t] (t < KK), db[c] = sum_r partial[r, c, KK] over the [rows, C, KK + 1]
+ * partials of the depthwise weight-gradient kernels (either output may be null). */
+int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float* db, int rows, int C, int KK, void* stream);
 /* Weight (and bias) gradient of the same conv on MFMA: partial[t, c, 0 .. K*K-1] = per-wave sums of
  * dW[c][ky][kx] = sum dy[b,c,y,x] x[b,c,y+ky-pad,x+kx-pad], partial[t, c, K*K] = sum dy; t < tiles
  * = vfm_dwconv2d_bwd_weight_mfma_tiles(...) (same partial layout as vfm_dwconv2d_bwd_weight; the

@@ -168,13 +168,12 @@ def test_c4_vq_fp16_iteration():
     assert torch.isfinite(usage).all() and float(usage.sum()) > 0
 
 
-@pytest.mark.xfail(reason="known open bug (DESIGN.md §5): at the full C1 size a graph replay that follows an "
-                          "eager forward run after a decoder weight update has returned stale outputs; the "
-                          "path is refused without VFM_EXPERIMENTAL_GRAPHS=1", strict=False)
 def test_graph_replay_after_weight_update_c1():
-    """Regression test for the experimental HIP-graph replay of the D phase's generator forward at
-    the full C1 size (replaces the round-2 bisection scripts): replay == eager after an in-place
-    decoder weight update, both right after the update and after an intervening eager forward."""
+    """Regression test for the HIP-graph replay of the D phase's generator forward at the full C1
+    size: replay == eager after an in-place decoder weight update, both right after the update and
+    after an intervening eager forward. It failed while the attention blocks' channel norm ran on
+    torch's reduction kernel (tools_dev/graph_c1.py bisection: exact with the norm on a GEMM or under
+    AMD_SERIALIZE_KERNEL=3, wrong otherwise); the norm is now one HIP kernel (csrc/rmsnorm.hip)."""
     B = 4
     c, step = _build("vfm_vae_f16d32_siglip2_stage_0_synthetic.yaml", batch=B, graphs=True)
     G = step.G

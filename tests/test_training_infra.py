@@ -173,9 +173,34 @@ def test_ema_copies_buffers_only_when_changed():
     assert torch.isfinite(G_ema.lin.weight).all() and beta < 1
 
 
+def test_ema_averages_frozen_tensor_that_comes_to_differ():
+    """A frozen tensor equal in G and G_ema is left out of the lerp; once either side is written (a
+    checkpoint loaded into G_ema) it is averaged again (version counters checked every step)."""
+    import copy
+    from training.training_loop import TrainingIteration
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(4, 4)
+            self.frozen = torch.nn.Linear(4, 4)
+            self.trainable_layers = ['lin']
+
+    G = Net()
+    G_ema = copy.deepcopy(G)
+    it = TrainingIteration.__new__(TrainingIteration)
+    it.G, it.G_ema, it.batch_size, it.ema_kimg, it.ema_rampup, it._ema_pairs = G, G_ema, 4, 0.001, None, None
+    it.update_ema(1000)
+    assert torch.equal(G_ema.frozen.weight, G.frozen.weight)
+    with torch.no_grad():
+        G_ema.frozen.weight.zero_()                   # e.g. a checkpoint loaded into G_ema only
+    it.update_ema(1000)                               # lerp weight 1 - beta = 1 - 0.5 ** (4 / 1)
+    assert torch.allclose(G_ema.frozen.weight, (1 - 0.5 ** 4) * G.frozen.weight)
+
+
 def test_graphed_forward_refused_without_opt_in(monkeypatch):
-    """The HIP-graph replay of the D phase's generator forward is experimental (stale replays at the
-    full C1 size): enabling it without VFM_EXPERIMENTAL_GRAPHS=1 raises."""
+    """The HIP-graph replay of the D phase's generator forward is opt-in (torch reductions replay
+    wrongly from HIP graphs): enabling it without VFM_EXPERIMENTAL_GRAPHS=1 raises."""
     import pytest
     from training.loss import TotalLoss
     monkeypatch.delenv("VFM_EXPERIMENTAL_GRAPHS", raising=False)

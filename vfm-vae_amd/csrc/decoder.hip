@@ -34,6 +34,7 @@ struct DwArgs {
     const float* noise;   // [Ho, Wo] or null
     void* y;
     int B, C, H, W, Ho, Wo, pad;
+    int flip;             // taps read rotated by 180 degrees (the data gradient)
     int TW, TH;           // tile width (pow2, <= 64), tile height (multiple of RPT)
     int ppw;              // planes side by side in one wave row (64 / TW)
     int spp;              // row strips per plane tile (TH / RPT)
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(NT) void dw_fwd(DwArgs a) {
 
     float wk[K * K];
 #pragma unroll
-    for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + i];
+    for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + (a.flip ? K * K - 1 - i : i)];
     float acc[RPT];
     const float b = a.bias ? a.bias[c] : 0.f;
 #pragma unroll
@@ -280,6 +281,7 @@ struct DwRowArgs {
     const void* dy;       // weight-gradient mode
     float* partial;       // [wpc, C, K*K+1]
     int B, C, H, W;
+    int flip;             // taps read rotated by 180 degrees (the data gradient)
     int L, R;             // lanes per row, row groups per wave
     int BH;               // band height
     int nb;               // bands per plane
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
     const bool live = ln.live;
     float wk[K * K];
 #pragma unroll
-    for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + i];
+    for (int i = 0; i < K * K; ++i) wk[i] = a.w[c * K * K + (a.flip ? K * K - 1 - i : i)];
     const float bias = a.bias ? a.bias[c] : 0.f;
     const T* xp = reinterpret_cast<const T*>(a.x) + ln.poff;
     T* yp = reinterpret_cast<T*>(a.y) + ln.poff;
@@ -1329,21 +1331,46 @@ int blur_launch(BlurArgs& a, int mode, const void* dout, void* dx, long long gri
     return VFM_ERR_ARGS;
 }
 
+// dw[c, t] = sum_r partial[r, c, t] (t < KK), db[c] = sum_r partial[r, c, KK]; rows in order
+__global__ __launch_bounds__(256) void dw_wgrad_reduce(const float* __restrict__ partial, float* __restrict__ dw,
+                                                       float* __restrict__ db, int rows, int C, int KK) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long long)C * (KK + 1)) return;
+    const int c = (int)(e / (KK + 1)), t = (int)(e - (long long)c * (KK + 1));
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += partial[((long long)r * C + c) * (KK + 1) + t];
+    if (t < KK) {
+        if (dw) dw[(long long)c * KK + t] = s;
+    } else if (db) {
+        db[c] = s;
+    }
+}
+
 }  // namespace
 
 // ============================== C ABI ==========================================================
 
-extern "C" int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,
-                                int dtype, int B, int C, int H, int W, int K, int pad, void* stream) {
+extern "C" int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float* db, int rows, int C, int KK,
+                                         void* stream) {
+    if (!partial || rows <= 0 || C <= 0 || KK <= 0 || (!dw && !db)) return VFM_ERR_ARGS;
+    const long long n = (long long)C * (KK + 1);
+    hipLaunchKernelGGL(dw_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), partial, dw, db, rows, C, KK);
+    return launch_status();
+}
+
+extern "C" int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                                   int dtype, int B, int C, int H, int W, int K, int pad, int flip, void* stream) {
     if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0 || pad < 0) return VFM_ERR_ARGS;
     DwArgs a{};
     a.x = x; a.w = w; a.bias = bias; a.noise = noise; a.y = y;
-    a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad; a.flip = flip != 0;
     a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     DwRowArgs r{};
     r.x = x; r.w = w; r.bias = bias; r.noise = noise; r.y = y; r.B = B; r.C = C; r.H = H; r.W = W;
+    r.flip = flip != 0;
     if (dwr_plan(r, K, pad)) {
         switch (dtype) {
         case VFM_F32: return dwr_launch<float>(r, K, 0, st);
@@ -1359,6 +1386,11 @@ extern "C" int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias
     case VFM_BF16: return dw_dispatch<__hip_bfloat16>(a, K, 0, nullptr, nullptr, st);
     }
     return VFM_ERR_ARGS;
+}
+
+extern "C" int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                                int dtype, int B, int C, int H, int W, int K, int pad, void* stream) {
+    return vfm_dwconv2d_fwd_ex(x, w, bias, noise, y, dtype, B, C, H, W, K, pad, 0, stream);
 }
 
 extern "C" int vfm_dwconv2d_bwd_weight_tiles(int B, int C, int H, int W, int K, int pad) {

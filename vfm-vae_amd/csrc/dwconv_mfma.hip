@@ -41,6 +41,7 @@ struct DwmArgs {
     const __hip_bfloat16* res;            // [B, C, H, W] bf16 added before the output rounding, or null
     __hip_bfloat16* y;
     int B, C, H, W, XW, nyb, nxs, rb;     // rb: 16-row blocks per wave
+    int flip;                             // taps read rotated by 180 degrees (the data gradient)
     long long units;
 };
 
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     fetch(16 * yb0);
 
     // the channel's taps, one per lane, through LDS (one global load per lane instead of 8 K)
-    if (lane < K * K) taps[wave][lane] = a.w[(long long)c * K * K + lane];
+    if (lane < K * K) taps[wave][lane] = a.w[(long long)c * K * K + (a.flip ? K * K - 1 - lane : lane)];
     __builtin_amdgcn_wave_barrier();
     // A fragments: lane l holds A_ky[i = l & 15][j = 8 (l >> 4) + e], e < 8
     const int i = lane & 15, g = lane >> 4;
@@ -337,16 +338,16 @@ bool dwm_bw_plan(DwmBwArgs& a, int B, int C, int H, int W, int& XW) {
 // y = dwconv(x, w) + bias on bf16 NCHW planes via MFMA (see the header). VFM_NO_KERNEL for shapes it
 // does not cover (W % 16, pad != (K - 1) / 2, K not in {3, 5, 7}, misaligned pointers): the caller
 // then uses vfm_dwconv2d_fwd.
-extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise,
-                                     const void* res, void* y, int B, int C, int H, int W, int K, int pad,
-                                     void* stream) {
+extern "C" int vfm_dwconv2d_fwd_mfma_ex(const void* x, const float* w, const float* bias, const float* noise,
+                                        const void* res, void* y, int B, int C, int H, int W, int K, int pad, int flip,
+                                        void* stream) {
     if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
     if ((K != 3 && K != 5 && K != 7) || pad != (K - 1) / 2 || W % 16) return VFM_NO_KERNEL;
     if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)noise | (uintptr_t)res) % 16) return VFM_NO_KERNEL;
     DwmArgs a;
     a.x = (const __hip_bfloat16*)x; a.w = w; a.bias = bias; a.noise = noise; a.y = (__hip_bfloat16*)y;
     a.res = (const __hip_bfloat16*)res;
-    a.B = B; a.C = C; a.H = H; a.W = W;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.flip = flip != 0;
     a.XW = W % 64 == 0 ? 64 : 16;
     const int rows16 = (H + 15) / 16;
     a.rb = rows16 < 4 ? rows16 : 4;                        // up to 64 output rows per wave
@@ -359,6 +360,12 @@ extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float*
     case 5: return dwm_launch<5>(a, st);
     default: return dwm_launch<7>(a, st);
     }
+}
+
+extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise,
+                                     const void* res, void* y, int B, int C, int H, int W, int K, int pad,
+                                     void* stream) {
+    return vfm_dwconv2d_fwd_mfma_ex(x, w, bias, noise, res, y, B, C, H, W, K, pad, 0, stream);
 }
 
 // tiles (rows of the partial buffer) of vfm_dwconv2d_bwd_weight_mfma; VFM_NO_KERNEL if not covered

@@ -1,0 +1,145 @@
+// Channel RMS norm of the decoder's attention blocks (reference networks/utils/gigagan_utils.py:31-39,
+// ChannelRMSNorm: F.normalize(x, dim=1) * sqrt(C) * gamma) on fp32 NCHW planes, forward and backward,
+// one launch each (+ one for the gamma-gradient partial sums). torch's formulation is a norm reduction
+// over the strided channel dim, a clamp, a division and two scalings (five kernels; its backward about
+// ten), and its global-reduce path zeroes semaphores with a memset per call.
+//
+//   n[b, p]    = max(sqrt(sum_c x[b, c, p]^2), 1e-12)          (p < P = H W)
+//   y[b, c, p] = x[b, c, p] / n[b, p] * k[c],   k = scale * gamma
+//   dx         = k dy / n - x (sum_c k dy x) / n^3   where the norm is not clamped,   k dy / n  where it is
+//   dgamma[c]  = scale * sum_{b, p} dy x / n
+//
+// Block = 16 columns (consecutive p) x 16 channel groups; a thread sums every 16th channel of its
+// column, the 16 partial sums meet in LDS, then the same threads write their channels. The gamma
+// gradient: each block reduces dy x / n over its 16 columns per channel into one partial row,
+// and a second kernel sums the rows of every channel in a fixed order (deterministic).
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+constexpr int COLS = 16, GROUPS = 16, THREADS = COLS * GROUPS;
+constexpr float NORM_EPS = 1e-12f;
+
+__global__ __launch_bounds__(THREADS) void crms_fwd(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                    float* __restrict__ y, float* __restrict__ rinv, int C, int P,
+                                                    int tiles, float scale) {
+    __shared__ float red[GROUPS][COLS + 1];
+    const int b = blockIdx.x / tiles, p0 = (blockIdx.x - b * tiles) * COLS;
+    const int col = threadIdx.x % COLS, g = threadIdx.x / COLS;
+    const int p = p0 + col;
+    const bool ok = p < P;
+    const float* xb = x + (long long)b * C * P + p;
+    float ss = 0.f;
+    if (ok)
+        for (int c = g; c < C; c += GROUPS) {
+            const float v = xb[(long long)c * P];
+            ss = fmaf(v, v, ss);
+        }
+    red[g][col] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < GROUPS; ++i) tot += red[i][col];
+    const float r = 1.f / fmaxf(sqrtf(tot), NORM_EPS);
+    if (!ok) return;
+    if (g == 0 && rinv) rinv[(long long)b * P + p] = r;
+    float* yb = y + (long long)b * C * P + p;
+    for (int c = g; c < C; c += GROUPS) yb[(long long)c * P] = xb[(long long)c * P] * r * (scale * gamma[c]);
+}
+
+__global__ __launch_bounds__(THREADS) void crms_bwd(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                    const float* __restrict__ rinv, const float* __restrict__ dy,
+                                                    float* __restrict__ dx, float* __restrict__ gpart, int C, int P,
+                                                    int tiles, float scale) {
+    __shared__ float red[GROUPS][COLS + 1];
+    const int b = blockIdx.x / tiles, p0 = (blockIdx.x - b * tiles) * COLS;
+    const int col = threadIdx.x % COLS, g = threadIdx.x / COLS;
+    const int p = p0 + col;
+    const bool ok = p < P;
+    const long long base = (long long)b * C * P + p;
+    float dot = 0.f;
+    if (ok)
+        for (int c = g; c < C; c += GROUPS) {
+            const long long o = base + (long long)c * P;
+            dot = fmaf(scale * gamma[c] * dy[o], x[o], dot);
+        }
+    red[g][col] = dot;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < GROUPS; ++i) tot += red[i][col];
+    const float r = ok ? rinv[(long long)b * P + p] : 0.f;
+    // r == 1 / 1e-12 exactly when the norm was clamped: no gradient through the norm then
+    const float corr = (r < 1.f / NORM_EPS) ? tot * r * r * r : 0.f;
+    for (int c = g; c < C; c += GROUPS) {
+        float gx = 0.f;
+        if (ok) {
+            const long long o = base + (long long)c * P;
+            const float d = dy[o], xv = x[o];
+            dx[o] = scale * gamma[c] * d * r - xv * corr;
+            gx = d * xv * r;
+        }
+        if (gpart) {
+            // sum over the block's 16 columns: lanes col = 0..15 of one channel group are 16 consecutive lanes
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) gx += __shfl_xor(gx, o, 16);
+            if (col == 0) gpart[(long long)blockIdx.x * C + c] = gx;
+        }
+    }
+}
+
+// dgamma[c] = scale * sum_rows gpart[row, c], rows in order
+__global__ __launch_bounds__(256) void crms_gamma(const float* __restrict__ gpart, float* __restrict__ dgamma, int C,
+                                                  int rows, float scale) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += gpart[(long long)r * C + c];
+    dgamma[c] = scale * s;
+}
+
+bool crms_grid(int B, int C, int P, int& tiles, long long& blocks) {
+    tiles = (P + COLS - 1) / COLS;
+    blocks = (long long)B * tiles;
+    return B > 0 && C > 0 && P > 0 && blocks <= 0x7fffffffLL;
+}
+
+}  // namespace
+
+// rows of the gamma-gradient partial buffer vfm_channel_rms_norm_bwd needs ([rows, C] fp32)
+extern "C" long long vfm_channel_rms_norm_rows(int B, int C, int P) {
+    int tiles;
+    long long blocks;
+    if (!crms_grid(B, C, P, tiles, blocks)) return VFM_ERR_ARGS;
+    return blocks;
+}
+
+// y = x / max(||x||_channels, 1e-12) * scale * gamma on fp32 [B, C, P]; rinv [B, P] (optional) keeps
+// 1 / max(norm, 1e-12) for the backward.
+extern "C" int vfm_channel_rms_norm_fwd(const float* x, const float* gamma, float* y, float* rinv, int B, int C, int P,
+                                        float scale, void* stream) {
+    int tiles;
+    long long blocks;
+    if (!x || !gamma || !y || !crms_grid(B, C, P, tiles, blocks)) return VFM_ERR_ARGS;
+    hipLaunchKernelGGL(crms_fwd, dim3((unsigned)blocks), dim3(THREADS), 0, (hipStream_t)stream, x, gamma, y, rinv, C,
+                       P, tiles, scale);
+    return vfm::launch_status();
+}
+
+// dx (required) and dgamma (optional: then gpart [vfm_channel_rms_norm_rows, C] is its workspace)
+extern "C" int vfm_channel_rms_norm_bwd(const float* x, const float* gamma, const float* rinv, const float* dy,
+                                        float* dx, float* gpart, float* dgamma, int B, int C, int P, float scale,
+                                        void* stream) {
+    int tiles;
+    long long blocks;
+    if (!x || !gamma || !rinv || !dy || !dx || !crms_grid(B, C, P, tiles, blocks)) return VFM_ERR_ARGS;
+    if ((gpart == nullptr) != (dgamma == nullptr)) return VFM_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(crms_bwd, dim3((unsigned)blocks), dim3(THREADS), 0, st, x, gamma, rinv, dy, dx, gpart, C, P,
+                       tiles, scale);
+    if (dgamma)
+        hipLaunchKernelGGL(crms_gamma, dim3((C + 255) / 256), dim3(256), 0, st, gpart, dgamma, C, (int)blocks, scale);
+    return vfm::launch_status();
+}

@@ -1,0 +1,322 @@
+// Style affine + demodulation coefficients of a ConvNeXt synthesis layer, forward (two launches)
+// and backward (two launches), fp32. Reference: networks/utils/convnext_utils.py ConvNeXtBlock
+// (affine_pw1 = StyleSplit(FullyConnectedLayer(w_dim, 3C)), networks/utils/shared.py StyleSplit /
+// FullyConnectedLayer, and the demodulation of ModulatedPointwiseConv2DLayer, convnext_utils.py:60-66):
+//
+//   m[b, j] = wg sum_k w[b, k] A[j, k] + bg ab[j]                     j < 3C   (FullyConnectedLayer)
+//   s[b, c] = m[b, c] m[b, C + c] + m[b, 2C + c]                               (StyleSplit)
+//   d[b, o] = rsqrt(sum_i W1[o, i]^2 s[b, i]^2 + eps)                 o < O    (demodulation)
+//
+// torch runs this as ~9 kernels per layer forward (gain scalings, addmm, split products, squares, the
+// mm, eps, rsqrt) and ~25 in its backward. Backward, with q = -dd d^3 / 2:
+//   launch 1:  ds[b, i]  = ds_in[b, i] + 2 s[b, i] sum_o q[b, o] W1[o, i]^2
+//              dW1[o, i] = 2 W1[o, i] sum_b q[b, o] s[b, i]^2
+//   launch 2:  dm = (ds m2, ds m1, ds)  (per split part),
+//              dA[j, k] = wg sum_b dm[b, j] w[b, k],   dab[j] = bg sum_b dm[b, j],
+//              dw[b, k] = wg sum_j dm[b, j] A[j, k]
+// The products are skinny (one side is the batch, <= a few dozen rows), so there are two job shapes:
+//  * long reductions (over WD, C, O or 3C): one wave per 4-row x CB-column output block, the 64 lanes
+//    striding over k (coalesced along k), each lane keeping 4 x CB partial sums that are then reduced
+//    across the wave with xor shuffles;
+//  * reductions over the batch (dW1, dA, dab): one thread per 8-wide output strip of a row (the row's
+//    batch factor computed once per sample), a loop over the batch.
+// All sums are plain fp32 FMAs (the reference runs them in fp32 with TF32 off).
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+constexpr int THREADS = 256, WAVES = THREADS / 64, RB = 4;
+
+struct StyleArgs {
+    const float* w;
+    long long ldw;                        // row stride of w [B, WD] (a column slice of ws)
+    const float* A;                       // [3C, WD]
+    const float* ab;                      // [3C]
+    const float* W1;                      // [O, C] or null (no demodulation)
+    float wg, bg, eps;
+    int B, C, WD, O;
+    float* m;                             // [B, 3C]
+    float* s;                             // [B, C]
+    float* d;                             // [B, O]
+    const float* dsin;                    // [B, C] or null
+    const float* dd;                      // [B, O]
+    const float* dsv;                     // ds for launch 2 (the workspace of launch 1, or dsin)
+    float* ds;                            // [B, C] workspace written by launch 1
+    float* dW1;                           // [O, C] or null
+    float* dA;                            // [3C, WD] or null
+    float* dab;                           // [3C] or null
+    float* dw;                            // [B, WD] or null
+    long long units0;                     // work units (waves or threads) of the launch's first job
+    int blocks0;                          // blocks of the first job
+};
+
+// acc[r][c] = sum_k X(r, k) Y(c, k) over k < K for one wave: ldx(k, x[RB]) / ldy(k, y[CB]) load the
+// operand values of one k (zero outside the operand); the result is complete in every lane.
+template <int CB, class LX, class LY>
+__device__ __forceinline__ void wave_mm(int K, int lane, LX ldx, LY ldy, float (&acc)[RB][CB]) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) acc[r][c] = 0.f;
+#pragma unroll 2
+    for (int k = lane; k < K; k += 64) {
+        float x[RB], y[CB];
+        ldx(k, x);
+        ldy(k, y);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[r][c] = fmaf(x[r], y[c], acc[r][c]);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[r][c] += __shfl_xor(acc[r][c], o, 64);
+}
+
+__device__ __forceinline__ float dm_at(const StyleArgs& a, int b, int j) {
+    const int part = j / a.C, c = j - part * a.C;
+    const float g = a.dsv[(long long)b * a.C + c];
+    const float* mb = a.m + (long long)b * 3 * a.C;
+    return part == 0 ? g * mb[a.C + c] : (part == 1 ? g * mb[c] : g);
+}
+
+__device__ __forceinline__ float q_at(const StyleArgs& a, int b, int o) {
+    const long long i = (long long)b * a.O + o;
+    const float dv = a.d[i];
+    return -0.5f * a.dd[i] * dv * dv * dv;
+}
+
+// LAUNCH 0 (waves): m, s         — 4 samples x 4 channels (x 3 split parts) per wave, k < WD
+// LAUNCH 1 (waves): d            — 4 samples x 8 outputs per wave, k < C
+// LAUNCH 2: ds (waves: 4 samples x 8 channels, k < O) | dW1 (threads: 8-channel strips, b < B)
+// LAUNCH 3: dA + dab (threads: 8-column strips, b < B) | dw (waves: 4 samples x 8 columns, k < 3C)
+template <int LAUNCH>
+__global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool second = (int)blockIdx.x >= a.blocks0;
+    const int blk = second ? blockIdx.x - a.blocks0 : blockIdx.x;
+    const long long wunit = (long long)blk * WAVES + wave;            // wave jobs
+    const long long tunit = (long long)blk * THREADS + threadIdx.x;   // thread jobs
+    const int C = a.C, C3 = 3 * a.C, WD = a.WD, O = a.O, B = a.B;
+    const int nbg = (B + RB - 1) / RB;                                 // 4-sample groups
+
+    if (LAUNCH == 0) {
+        constexpr int CC = 4;
+        if (wunit >= (long long)nbg * ((C + CC - 1) / CC)) return;
+        const int b0 = (int)(wunit % nbg) * RB, c0 = (int)(wunit / nbg) * CC;
+        float acc[RB][3 * CC];
+        wave_mm<3 * CC>(WD, lane,
+            [&](int k, float (&x)[RB]) {
+#pragma unroll
+                for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? a.w[(long long)(b0 + r) * a.ldw + k] : 0.f;
+            },
+            [&](int k, float (&y)[3 * CC]) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+#pragma unroll
+                    for (int c = 0; c < CC; ++c)
+                        y[p * CC + c] = c0 + c < C ? a.A[(long long)(p * C + c0 + c) * WD + k] : 0.f;
+            }, acc);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CC; ++c) {
+                const int b = b0 + r, cc = c0 + c;
+                if (lane != r * CC + c || b >= B || cc >= C) continue;
+                const float m1 = fmaf(a.wg, acc[r][c], a.bg * a.ab[cc]);
+                const float m2 = fmaf(a.wg, acc[r][CC + c], a.bg * a.ab[C + cc]);
+                const float m3 = fmaf(a.wg, acc[r][2 * CC + c], a.bg * a.ab[2 * C + cc]);
+                float* mb = a.m + (long long)b * C3;
+                mb[cc] = m1; mb[C + cc] = m2; mb[2 * C + cc] = m3;
+                a.s[(long long)b * C + cc] = fmaf(m1, m2, m3);
+            }
+    } else if (LAUNCH == 1) {
+        constexpr int CB = 8;
+        if (wunit >= (long long)nbg * ((O + CB - 1) / CB)) return;
+        const int b0 = (int)(wunit % nbg) * RB, o0 = (int)(wunit / nbg) * CB;
+        float acc[RB][CB];
+        wave_mm<CB>(C, lane,
+            [&](int k, float (&x)[RB]) {
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const float v = b0 + r < B ? a.s[(long long)(b0 + r) * C + k] : 0.f;
+                    x[r] = v * v;
+                }
+            },
+            [&](int k, float (&y)[CB]) {
+#pragma unroll
+                for (int c = 0; c < CB; ++c) {
+                    const float v = o0 + c < O ? a.W1[(long long)(o0 + c) * C + k] : 0.f;
+                    y[c] = v * v;
+                }
+            }, acc);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                if (lane == r * CB + c && b0 + r < B && o0 + c < O)
+                    a.d[(long long)(b0 + r) * O + o0 + c] = rsqrtf(acc[r][c] + a.eps);
+    } else if (LAUNCH == 2) {
+        if (!second) {            // ds [B, C]: waves, k < O
+            constexpr int CB = 8;
+            if (wunit >= (long long)nbg * ((C + CB - 1) / CB)) return;
+            const int b0 = (int)(wunit % nbg) * RB, i0 = (int)(wunit / nbg) * CB;
+            float acc[RB][CB];
+            wave_mm<CB>(O, lane,
+                [&](int k, float (&x)[RB]) {
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? q_at(a, b0 + r, k) : 0.f;
+                },
+                [&](int k, float (&y)[CB]) {
+                    const float* row = a.W1 + (long long)k * C + i0;
+#pragma unroll
+                    for (int c = 0; c < CB; ++c) {
+                        const float v = i0 + c < C ? row[c] : 0.f;
+                        y[c] = v * v;
+                    }
+                }, acc);
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int c = 0; c < CB; ++c) {
+                    const int b = b0 + r, i = i0 + c;
+                    if (lane != r * CB + c || b >= B || i >= C) continue;
+                    const long long o = (long long)b * C + i;
+                    a.ds[o] = (a.dsin ? a.dsin[o] : 0.f) + 2.f * a.s[o] * acc[r][c];
+                }
+        } else {                  // dW1 [O, C]: one thread per 8-channel strip of a row, b < B
+            const int strips = (C + 7) / 8;
+            if (tunit >= (long long)O * strips) return;
+            const int o = (int)(tunit / strips), i0 = (int)(tunit - (long long)o * strips) * 8;
+            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int b = 0; b < B; ++b) {
+                const float q = q_at(a, b, o);
+                const float* sr = a.s + (long long)b * C + i0;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float v = i0 + e < C ? sr[e] : 0.f;
+                    acc[e] = fmaf(q, v * v, acc[e]);
+                }
+            }
+            const long long row = (long long)o * C;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (i0 + e < C) a.dW1[row + i0 + e] = 2.f * a.W1[row + i0 + e] * acc[e];
+        }
+    } else {
+        if (!second) {            // dA [3C, WD] and dab [3C]: one thread per 8-column strip of a row, b < B
+            const int strips = (WD + 7) / 8;
+            if (tunit >= (long long)C3 * strips) return;
+            const int j = (int)(tunit / strips), k0 = (int)(tunit - (long long)j * strips) * 8;
+            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            float sb = 0.f;
+            for (int b = 0; b < B; ++b) {
+                const float g = dm_at(a, b, j);
+                const float* wr = a.w + (long long)b * a.ldw + k0;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] = fmaf(g, k0 + e < WD ? wr[e] : 0.f, acc[e]);
+                sb += g;
+            }
+            if (a.dA) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (k0 + e < WD) a.dA[(long long)j * WD + k0 + e] = a.wg * acc[e];
+            }
+            if (a.dab && k0 == 0) a.dab[j] = a.bg * sb;
+        } else {                  // dw [B, WD]: waves, k < 3C
+            constexpr int CB = 8;
+            if (wunit >= (long long)nbg * ((WD + CB - 1) / CB)) return;
+            const int b0 = (int)(wunit % nbg) * RB, n0 = (int)(wunit / nbg) * CB;
+            float acc[RB][CB];
+            wave_mm<CB>(C3, lane,
+                [&](int k, float (&x)[RB]) {
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? dm_at(a, b0 + r, k) : 0.f;
+                },
+                [&](int k, float (&y)[CB]) {
+                    const float* row = a.A + (long long)k * WD + n0;
+#pragma unroll
+                    for (int c = 0; c < CB; ++c) y[c] = n0 + c < WD ? row[c] : 0.f;
+                }, acc);
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int c = 0; c < CB; ++c)
+                    if (lane == r * CB + c && b0 + r < B && n0 + c < WD)
+                        a.dw[(long long)(b0 + r) * WD + n0 + c] = a.wg * acc[r][c];
+        }
+    }
+}
+
+inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+
+template <int L>
+int launch(StyleArgs& a, long long blocks, hipStream_t st) {
+    if (blocks <= 0) return 0;
+    if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
+    hipLaunchKernelGGL(style_kernel<L>, dim3((unsigned)blocks), dim3(THREADS), 0, st, a);
+    return launch_status();
+}
+
+bool sizes_ok(int B, int C, int WD, int O) {
+    return B > 0 && C > 0 && WD > 0 && O >= 0 && (long long)B * 3 * C < (1LL << 31) &&
+           (long long)O * C < (1LL << 31) && (long long)3 * C * WD < (1LL << 31);
+}
+
+}  // namespace
+
+// m [B, 3C], s [B, C] and (W1 given) d [B, O] of the layer's style path (see the header).
+extern "C" int vfm_style_demod_fwd(const float* w, long long ldw, const float* A, const float* ab, const float* W1,
+                                   float wg, float bg, float eps, int B, int C, int WD, int O, float* m, float* s,
+                                   float* d, void* stream) {
+    if (!w || !A || !ab || !m || !s || !sizes_ok(B, C, WD, O) || ldw < WD) return VFM_ERR_ARGS;
+    if (W1 && (!d || O <= 0)) return VFM_ERR_ARGS;
+    StyleArgs a{};
+    a.w = w; a.ldw = ldw; a.A = A; a.ab = ab; a.W1 = W1; a.wg = wg; a.bg = bg; a.eps = eps;
+    a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = m; a.s = s; a.d = d;
+    hipStream_t st = (hipStream_t)stream;
+    const long long nbg = cdiv(B, RB);
+    a.blocks0 = (int)cdiv(nbg * cdiv(C, 4), WAVES);
+    int rc = launch<0>(a, a.blocks0, st);
+    if (rc || !W1) return rc;
+    a.blocks0 = (int)cdiv(nbg * cdiv(O, 8), WAVES);
+    return launch<1>(a, a.blocks0, st);
+}
+
+// Gradients of the style path from ds_in = dL/ds (or null) and dd = dL/dd (null without demodulation):
+// dw [B, WD], dA [3C, WD], dab [3C], dW1 [O, C], each optional (null: not computed). ds_ws [B, C] is a
+// workspace (required when dd is given).
+extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A, const float* W1, const float* m,
+                                   const float* s, const float* d, const float* ds_in, const float* dd, float wg,
+                                   float bg, int B, int C, int WD, int O, float* ds_ws, float* dW1, float* dA,
+                                   float* dab, float* dw, void* stream) {
+    if (!w || !A || !m || !s || !sizes_ok(B, C, WD, O) || ldw < WD) return VFM_ERR_ARGS;
+    const bool demod = dd != nullptr;
+    if (demod && (!W1 || !d || !ds_ws || O <= 0)) return VFM_ERR_ARGS;
+    if (!demod && (dW1 || !ds_in)) return VFM_ERR_ARGS;
+    StyleArgs a{};
+    a.w = w; a.ldw = ldw; a.A = A; a.W1 = W1; a.wg = wg; a.bg = bg;
+    a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = const_cast<float*>(m); a.s = const_cast<float*>(s);
+    a.d = const_cast<float*>(d); a.dsin = ds_in; a.dd = dd; a.ds = ds_ws; a.dW1 = dW1; a.dA = dA; a.dab = dab;
+    a.dw = dw;
+    hipStream_t st = (hipStream_t)stream;
+    const long long nbg = cdiv(B, RB);
+    if (demod) {
+        a.blocks0 = (int)cdiv(nbg * cdiv(C, 8), WAVES);
+        const long long b1 = dW1 ? cdiv((long long)O * cdiv(C, 8), THREADS) : 0;
+        const int rc = launch<2>(a, a.blocks0 + b1, st);
+        if (rc) return rc;
+        a.dsv = ds_ws;
+    } else {
+        a.dsv = ds_in;
+    }
+    if (!dA && !dab && !dw) return 0;
+    a.blocks0 = (dA || dab) ? (int)cdiv(3LL * C * cdiv(WD, 8), THREADS) : 0;
+    const long long b1 = dw ? cdiv(nbg * cdiv(WD, 8), WAVES) : 0;
+    return launch<3>(a, a.blocks0 + b1, st);
+}

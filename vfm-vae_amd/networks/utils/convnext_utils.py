@@ -92,7 +92,9 @@ class ConvNeXtSynthesisLayer(nn.Module):
         cdt = compute_dtype or x.dtype
         x_in = x
         B, C, H, W = x.shape
-        style = self.affine_pw1(w).float()                                     # [B, C]
+        w1 = self.pwconv1.weight.reshape(4 * C, C)
+        # style [B, C] = affine_pw1(w), dcoef [B, 4C] = demodulation of pwconv1 (csrc/style.hip on ROCm)
+        style, dcoef = decoder_ops.style_and_demod(self.affine_pw1, w, w1 if self.pwconv1.demodulate else None)
         # x feeds the dwconv and the residual: on the HIP path the residual's gradient is added in the
         # dwconv data-gradient kernel instead of by autograd (decoder_hip.ResidualSlot)
         slot = None
@@ -103,8 +105,6 @@ class ConvNeXtSynthesisLayer(nn.Module):
                                  noise=self._noise(H, W), slot=slot)
         m = decoder_ops.group_norm(d, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps,
                                    out_dtype=cdt, style=style)                 # GN(d) * s_b
-        w1 = self.pwconv1.weight.reshape(4 * C, C)
-        dcoef = decoder_ops.demod_coefficients(w1, style) if self.pwconv1.demodulate else None
         gamma = self.gamma.reshape(-1) if self.gamma is not None else None
         if decoder_ops.convnext_mlp_fusable(m, C, H * W, x_in):
             # the whole MLP forward in one kernel (hidden 4C tensor on chip without autograd)

@@ -31,6 +31,12 @@ class ChannelRMSNorm(nn.Module):
         self.gamma = nn.Parameter(torch.ones(dim, 1, 1))
 
     def forward(self, x):
+        if x.is_cuda:
+            from torch_utils.ops import decoder_hip
+            if decoder_hip.channel_rms_norm_supported(x):
+                # one HIP launch (csrc/rmsnorm.hip); torch's channel-norm reduction also replays wrongly
+                # from a HIP graph
+                return decoder_hip.channel_rms_norm(x, self.gamma, self.scale)
         return F.normalize(x, dim=1) * self.scale * self.gamma
 
 

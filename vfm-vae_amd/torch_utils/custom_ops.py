@@ -68,6 +68,18 @@ SIGNATURES = {
                        c_ll, c_ll, c_ll, c_ll, c_ll, c_vp],
     "vfm_gemm8_gelu_parts": [c_int],
     "vfm_gemm8_set_stamps": [c_vp],
+    "vfm_channel_rms_norm_rows": [c_int, c_int, c_int],
+    "vfm_channel_rms_norm_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp],
+    "vfm_channel_rms_norm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp],
+    "vfm_style_demod_fwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_float, c_float, c_float, c_int, c_int, c_int, c_int,
+                            c_vp, c_vp, c_vp, c_vp],
+    "vfm_style_demod_bwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_int, c_int,
+                            c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "vfm_dwconv2d_fwd_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                            c_vp],
+    "vfm_dwconv2d_fwd_mfma_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_vp],
+    "vfm_dwconv2d_wgrad_reduce": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
     "vfm_shift2d": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_im2col_nhwc_f32": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_col2im_nhwc_f32": [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -150,6 +162,7 @@ def get_native():
                 fn.restype = c_int
             lib.vfm_version.restype = ctypes.c_char_p
             lib.vfm_bnl_workspace_floats.restype = c_ll
+            lib.vfm_channel_rms_norm_rows.restype = c_ll
             _lib = lib
     return _lib
 

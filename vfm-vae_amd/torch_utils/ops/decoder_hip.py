@@ -221,9 +221,10 @@ def pointwise(w, x):
 DW_MFMA = os.environ.get("VFM_DW_MFMA", "1") == "1"      # A/B switch for the banded-MFMA dwconv
 
 
-def _dw_fwd(x, w3, bias, noise, pad, name, res=None):
+def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False):
     """y = dwconv(x) (+ bias, + noise plane) (+ res, a tensor of y's shape: the residual-branch
-    gradient added in the MFMA kernel's epilogue, else by a torch add)."""
+    gradient added in the MFMA kernel's epilogue, else by a torch add); flip: taps rotated by 180
+    degrees in the kernel (the data gradient)."""
     B, C, H, W = x.shape
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -235,14 +236,14 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None):
         # the reference's autocast conv does
         r = None if res is None else _c(res.to(torch.bfloat16))
         with kernel_timer.region(_rn(name.replace('dwconv2d', 'dwconv2d_mfma'), x, K), _nb(x, y, r)):
-            rc = _lib.vfm_dwconv2d_fwd_mfma(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), _p(r), y.data_ptr(), B,
-                                            C, H, W, K, pad, _stream())
+            rc = _lib.vfm_dwconv2d_fwd_mfma_ex(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), _p(r), y.data_ptr(),
+                                               B, C, H, W, K, pad, int(flip), _stream())
         if rc != custom_ops.VFM_NO_KERNEL:
             _check(rc, name)
             return y
     with kernel_timer.region(_rn(name, x, K), _nb(x, y)):
-        _check(_lib.vfm_dwconv2d_fwd(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
-                                     B, C, H, W, K, pad, _stream()), name)
+        _check(_lib.vfm_dwconv2d_fwd_ex(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
+                                        B, C, H, W, K, pad, int(flip), _stream()), name)
     return y if res is None else y.add_(res.to(y.dtype))
 
 
@@ -273,6 +274,15 @@ def _stash_residual(slot, dout):
         return False
     slot.grad = dout
     return True
+
+
+def _dw_wgrad(part, want_w, want_b, C, K, wshape, wdt, bdt):
+    """(dw, db) from the weight-gradient partials [rows, C, K K + 1] in one reduce launch."""
+    dw = torch.empty(wshape, dtype=torch.float32, device=part.device) if want_w else None
+    db = torch.empty([C], dtype=torch.float32, device=part.device) if want_b else None
+    _check(_lib.vfm_dwconv2d_wgrad_reduce(part.data_ptr(), _p(dw), _p(db), part.shape[0], C, K * K, _stream()),
+           'vfm_dwconv2d_wgrad_reduce')
+    return (None if dw is None else dw.to(wdt)), (None if db is None else db.to(bdt))
 
 
 class _DwConv2d(torch.autograd.Function):
@@ -307,7 +317,7 @@ class _DwConv2d(torch.autograd.Function):
         if ctx.slot is not None and ctx.slot.grad is not None:
             res, ctx.slot.grad = ctx.slot.grad, None
         if _wanted(ctx, 0):
-            dx = _dw_fwd(dy, torch.flip(w3, [1, 2]).contiguous(), None, None, K - 1 - pad, 'dwconv2d_bwd_data', res)
+            dx = _dw_fwd(dy, w3, None, None, K - 1 - pad, 'dwconv2d_bwd_data', res, flip=True)
         # (res unused when dx is not wanted: then nothing consumes x's gradient in this pass)
         if (want_w or want_b) and DW_MFMA and x.dtype == torch.bfloat16 and \
                 _lib.vfm_dwconv2d_bwd_weight_mfma_tiles(B, C, H, W, K, pad) > 0:
@@ -317,11 +327,7 @@ class _DwConv2d(torch.autograd.Function):
             with kernel_timer.region(_rn('dwconv2d_mfma_bwd_weight', x, K), _nb(x, dy)):
                 _check(_lib.vfm_dwconv2d_bwd_weight_mfma(x.data_ptr(), dy.data_ptr(), part.data_ptr(), B, C, H, W, K,
                                                          pad, _stream()), 'vfm_dwconv2d_bwd_weight_mfma')
-            s = part.sum(0)
-            if want_w:
-                dw = s[:, :K * K].reshape(wshape).to(wdt)
-            if want_b:
-                db = s[:, K * K].to(bdt)
+            dw, db = _dw_wgrad(part, want_w, want_b, C, K, wshape, wdt, bdt)
         elif want_w or want_b:
             tiles = _lib.vfm_dwconv2d_bwd_weight_tiles(B, C, H, W, K, pad)
             if tiles <= 0:
@@ -330,11 +336,7 @@ class _DwConv2d(torch.autograd.Function):
             with kernel_timer.region(_rn('dwconv2d_bwd_weight', x, K), _nb(x, dy)):
                 _check(_lib.vfm_dwconv2d_bwd_weight(x.data_ptr(), dy.data_ptr(), part.data_ptr(), _code(x),
                                                     B, C, H, W, K, pad, _stream()), 'vfm_dwconv2d_bwd_weight')
-            s = part.sum(0)
-            if want_w:
-                dw = s[:, :K * K].reshape(wshape).to(wdt)
-            if want_b:
-                db = s[:, K * K].to(bdt)
+            dw, db = _dw_wgrad(part, want_w, want_b, C, K, wshape, wdt, bdt)
         if _wanted(ctx, 3):
             dn = dy.sum(dim=(0, 1), dtype=torch.float32).to(ndt)       # fp32 accumulation, no fp32 copy of dy
         return dx, dw, db, dn, None, None
@@ -854,3 +856,123 @@ def torgb_supported(x, O):
 def torgb(x, w2, style, bias):
     """y = (w2 @ (style * x)) + bias in fp32: x [B, C, H, W], w2 [O, C], style [B, C], bias [1, O, 1, 1]."""
     return _ToRGB.apply(x, w2, style, bias)
+
+
+# ---------------------------------------------------------------------------
+# Channel RMS norm of the decoder attention blocks (csrc/rmsnorm.hip; reference
+# networks/utils/gigagan_utils.py:31-39): one launch forward, one (+ the gamma row sum) backward.
+
+
+class _ChannelRMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, scale):
+        _edges(ctx, x, gamma, scale)
+        x = _c(x)
+        B, C = x.shape[:2]
+        P = x[0, 0].numel()
+        g = _f32(gamma)
+        y = torch.empty_like(x)
+        rinv = torch.empty([B, P], dtype=torch.float32, device=x.device)
+        with kernel_timer.region(_rn('channel_rms_norm_fwd', x), _nb(x, y)):
+            _check(_lib.vfm_channel_rms_norm_fwd(x.data_ptr(), g.data_ptr(), y.data_ptr(), rinv.data_ptr(), B, C, P,
+                                                 float(scale), _stream()), 'vfm_channel_rms_norm_fwd')
+        ctx.save_for_backward(x, g, rinv)
+        ctx.scale, ctx.gmeta = float(scale), (gamma.dtype, gamma.shape)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x, g, rinv = ctx.saved_tensors
+        B, C = x.shape[:2]
+        P = x[0, 0].numel()
+        dy = _c(dy.float())
+        dx = torch.empty_like(x)
+        want_g = _wanted(ctx, 1)
+        gpart = dg = None
+        if want_g:
+            gpart = torch.empty([_lib.vfm_channel_rms_norm_rows(B, C, P), C], dtype=torch.float32, device=x.device)
+            dg = torch.empty([C], dtype=torch.float32, device=x.device)
+        with kernel_timer.region(_rn('channel_rms_norm_bwd', x), _nb(x, dy, dx)):
+            _check(_lib.vfm_channel_rms_norm_bwd(x.data_ptr(), g.data_ptr(), rinv.data_ptr(), dy.data_ptr(),
+                                                 dx.data_ptr(), _p(gpart), _p(dg), B, C, P, ctx.scale, _stream()),
+                   'vfm_channel_rms_norm_bwd')
+        gdt, gshape = ctx.gmeta
+        return (dx if ctx.needs_input_grad[0] else None), (dg.reshape(gshape).to(gdt) if want_g else None), None
+
+
+def channel_rms_norm_supported(x):
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() >= 3 and x.numel() > 0
+
+
+def channel_rms_norm(x, gamma, scale):
+    """F.normalize(x, dim=1) * scale * gamma for fp32 [B, C, ...] (gamma [C] / [C, 1, 1])."""
+    return _ChannelRMSNorm.apply(x, gamma, scale)
+
+
+# ---------------------------------------------------------------------------
+# Style affine + demodulation of a ConvNeXt synthesis layer (csrc/style.hip; reference
+# networks/utils/shared.py StyleSplit / FullyConnectedLayer, convnext_utils.py:60-66):
+# two launches forward, two backward, instead of ~9 / ~25 torch kernels per layer.
+
+
+class _StyleDemod(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, w, A, ab, W1, wg, bg, eps):
+        _edges(ctx, w, A, ab, W1, wg, bg, eps)
+        wv = w.detach()
+        if wv.dtype != torch.float32 or wv.stride(1) != 1 or wv.data_ptr() % 16:
+            wv = wv.float().contiguous()
+        B, WD = wv.shape
+        C = A.shape[0] // 3
+        A32, ab32 = _f32(A).reshape(3 * C, WD), _f32(ab)
+        W132 = None if W1 is None else _f32(W1).reshape(W1.shape[0], C)
+        O = 0 if W1 is None else W132.shape[0]
+        dev = w.device
+        m = torch.empty([B, 3 * C], dtype=torch.float32, device=dev)
+        s = torch.empty([B, C], dtype=torch.float32, device=dev)
+        d = torch.empty([B, O], dtype=torch.float32, device=dev) if W1 is not None else None
+        with kernel_timer.region('style_demod_fwd<f32>', _nb(wv, A32, W132, m, s, d)):
+            _check(_lib.vfm_style_demod_fwd(wv.data_ptr(), wv.stride(0), A32.data_ptr(), ab32.data_ptr(), _p(W132),
+                                            float(wg), float(bg), float(eps), B, C, WD, O, m.data_ptr(), s.data_ptr(),
+                                            _p(d), _stream()), 'vfm_style_demod_fwd')
+        ctx.save_for_backward(wv, A32, W132, m, s, d)
+        ctx.meta = (float(wg), float(bg), w.dtype, A.dtype, ab.dtype, None if W1 is None else W1.dtype)
+        if d is None:
+            return s
+        return s, d
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, ds_in, dd=None):
+        wv, A32, W132, m, s, d = ctx.saved_tensors
+        wg, bg, wdt, adt, abdt, w1dt = ctx.meta
+        B, WD = wv.shape
+        C = s.shape[1]
+        O = 0 if d is None else d.shape[1]
+        dev = wv.device
+        want_w, want_A, want_ab = _wanted(ctx, 0), _wanted(ctx, 1), _wanted(ctx, 2)
+        want_W1 = d is not None and _wanted(ctx, 3)
+        f32 = dict(dtype=torch.float32, device=dev)
+        ds_in = _c(ds_in.float()) if ds_in is not None else torch.zeros([B, C], **f32)
+        if d is not None:
+            dd = _c(dd.float()) if dd is not None else torch.zeros([B, O], **f32)
+        ds_ws = torch.empty([B, C], **f32) if d is not None else None
+        dW1 = torch.empty([O, C], **f32) if want_W1 else None
+        dA = torch.empty([3 * C, WD], **f32) if want_A else None
+        dab = torch.empty([3 * C], **f32) if want_ab else None
+        dw = torch.empty([B, WD], **f32) if want_w else None
+        with kernel_timer.region('style_demod_bwd<f32>', _nb(wv, A32, W132, m, s, d, dW1, dA, dw)):
+            _check(_lib.vfm_style_demod_bwd(wv.data_ptr(), wv.stride(0), A32.data_ptr(), _p(W132), m.data_ptr(),
+                                            s.data_ptr(), _p(d), ds_in.data_ptr(), _p(dd if d is not None else None),
+                                            wg, bg, B, C, WD, O, _p(ds_ws), _p(dW1), _p(dA), _p(dab), _p(dw),
+                                            _stream()), 'vfm_style_demod_bwd')
+        return (None if dw is None else dw.to(wdt), None if dA is None else dA.to(adt),
+                None if dab is None else dab.to(abdt), None if dW1 is None else dW1.to(w1dt), None, None, None)
+
+
+def style_demod(w, A, ab, W1, wg, bg, eps):
+    """(s [B, C], d [B, O] or None): s = StyleSplit(FullyConnectedLayer(A, ab, gains wg / bg))(w),
+    d = rsqrt(s^2 @ (W1^2)^T + eps) when W1 [O, C] is given. fp32."""
+    out = _StyleDemod.apply(w, A, ab, W1, wg, bg, eps)
+    return (out, None) if W1 is None else out

@@ -187,6 +187,24 @@ def convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in, slot=None):
     return decoder_hip.convnext_mlp_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in)
 
 
+STYLE_HIP = __import__("os").environ.get("VFM_STYLE_HIP", "1") == "1"     # A/B switch
+
+
+def style_and_demod(affine, w, w1=None, eps=1e-8):
+    """(style [B, C] fp32, dcoef [B, O] or None) of a ConvNeXt synthesis layer: style =
+    affine(w) (a StyleSplit over a linear FullyConnectedLayer, reference networks/utils/shared.py),
+    dcoef = demod_coefficients(w1, style) when w1 is given. ROCm fp32: csrc/style.hip (two launches
+    each way); elsewhere the torch formulation."""
+    fc = affine.proj
+    if (STYLE_HIP and w.is_cuda and not _FORCE_REF and w.dtype == torch.float32 and w.dim() == 2 and fc.activation == 'linear'
+            and fc.bias is not None and fc.weight.dtype == torch.float32
+            and (w1 is None or w1.dtype == torch.float32)):
+        from . import decoder_hip
+        return decoder_hip.style_demod(w, fc.weight, fc.bias, w1, fc.weight_gain, fc.bias_gain, eps)
+    style = affine(w).float()
+    return style, (demod_coefficients(w1, style, eps) if w1 is not None else None)
+
+
 def demod_coefficients(weight2d, style, eps=1e-8):
     """dcoef[b, o] = rsqrt(sum_i (W[o, i] * s[b, i])^2 + eps), computed as a tiny GEMM."""
     return torch.rsqrt(style.float().square() @ weight2d.float().square().t() + eps)

@@ -310,19 +310,25 @@ class TrainingIteration:
         if self.ema_rampup is not None:
             ema_nimg = min(ema_nimg, cur_nimg * self.ema_rampup)
         beta = 0.5 ** (self.batch_size / max(ema_nimg, 1e-8))
-        if self._ema_pairs is None or self._ema_pairs[0] != tuple(self.G.trainable_layers):
+        # frozen tensors equal in G and G_ema are left out of the lerp; the pair list is rebuilt when the
+        # trainable set changes or any left-out tensor was written since (a checkpoint loaded into one
+        # side bumps its version counter), so a frozen tensor that comes to differ is averaged again
+        pairs = self._ema_pairs
+        if pairs is not None and (pairs[0] != tuple(self.G.trainable_layers)
+                                  or any(pe._version != ve or p._version != vp for pe, p, ve, vp in pairs[3])):
+            pairs = None
+        if pairs is None:
             names = self.G.trainable_layers
-            dst, src = [], []
+            dst, src, same = [], [], []
             for (n, pe), (_, p) in zip(self.G_ema.named_parameters(), self.G.named_parameters()):
                 mod = n.rsplit('.', 1)[0]
-                if any(t in mod for t in names):
+                if any(t in mod for t in names) or not torch.equal(pe, p):
                     dst.append(pe)
                     src.append(p)
-                elif not torch.equal(pe, p):   # a frozen tensor that differs: keep it in the update
-                    dst.append(pe)
-                    src.append(p)
-            self._ema_pairs = (tuple(names), dst, src)
-        _, dst, src = self._ema_pairs
+                else:
+                    same.append((pe, p, pe._version, p._version))
+            pairs = self._ema_pairs = (tuple(names), dst, src, same)
+        _, dst, src, _ = pairs
         if dst:
             # p_ema <- p.lerp(p_ema, beta) == p_ema + (1 - beta) * (p - p_ema)
             torch._foreach_lerp_(dst, src, 1.0 - beta)
