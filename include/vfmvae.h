@@ -142,6 +142,24 @@ int vfm_style_demod_bwd(const float* w, long long ldw, const float* A, const flo
                         int B, int C, int WD, int O, float* ds_ws, float* dW1, float* dA, float* dab, float* dw,
                         void* stream);
 
+/* Spectral normalisation in training mode (torch.nn.utils.spectral_norm, one power iteration, dim 0: the
+ * projected discriminator heads' SpectralConv1d, reference networks/discriminator.py): for fp32 W [O, I],
+ * v <- normalize(W^T u), u <- normalize(W v) in place (copies to u_copy / v_copy when given), sigma [1] =
+ * u . (W v), Wsn = W / sigma. The backward: dW = g / sigma - (sum g W) / sigma^2 u v^T. ws: workspace of
+ * vfm_specnorm_workspace_floats floats. */
+long long vfm_specnorm_workspace_floats(int O, int I);
+int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_copy, float* v_copy, float* sigma, float* Wsn,
+                     float* ws, int O, int I, float eps, void* stream);
+int vfm_specnorm_bwd(const float* g, const float* W, const float* u, const float* v, const float* sigma, float* dW,
+                     float* ws, int O, int I, void* stream);
+
+/* im2col of a 1-D conv with zero / circular padding and its adjoint, fp32 (the D heads' k = 9
+ * SpectralConv1d, padding_mode='circular', reference networks/discriminator.py make_block):
+ * cols [B, C k, Lo] (Lo = L + 2 p - k + 1; circular needs Lo == L) from x [B, C, L]; VFM_NO_KERNEL
+ * for shapes not covered. */
+int vfm_im2col1d_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular, void* stream);
+int vfm_col2im1d_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular, void* stream);
+
 /* DiffAugment random translation (replaces the padded gather of reference training/diffaug.py
  * rand_translation and its indexing backward): y[b, c, i, j] = x[b, c, i + sign tx[b], j + sign ty[b]]
  * inside the image, else 0; x, y contiguous NCHW (VFM_F32 / VFM_BF16); tx, ty int64 [B] on the device.

@@ -71,6 +71,8 @@ for s in "$@"; do
     opsites) timeout -k 10 600 python tools_dev/opsites.py > $out/opsites.log 2>&1 ;;
     benchg) VFM_EXPERIMENTAL_GRAPHS=1 timeout -k 10 600 python bench.py --graphs --no-cpu-baseline > $out/benchg.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_e.log 2>&1 ;;
     benchst) VFM_STYLE_HIP=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_st1.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_st0.log 2>&1 ;;
+    stylebench) timeout -k 10 300 python tools_dev/stylebench.py > $out/stylebench.log 2>&1 ;;
+    decgn) timeout -k 10 300 python tools_dev/decbench.py --only gn,dw > $out/decgn.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

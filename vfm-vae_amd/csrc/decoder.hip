@@ -652,6 +652,8 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
     const float shift = ld(xp);
     float s1 = 0.f, s2 = 0.f;
     const long long nv = vec ? n / 8 : 0;
+    // unrolled so that several 16-B loads per thread are in flight (the loop is latency-bound otherwise)
+#pragma unroll 4
     for (long long i = threadIdx.x; i < nv; i += NT) {
         float v[8];
         load8(xp + i * 8, v);
@@ -697,6 +699,7 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
         }
         __syncthreads();
         const int lg = __builtin_ctz(cpc);
+#pragma unroll 4
         for (long long i = threadIdx.x; i < nv; i += NT) {
             const int cl = (int)(i >> lg);
             const float sc = s_sc[cl], sh = s_sh[cl];
@@ -768,17 +771,30 @@ __device__ __forceinline__ void gn_bwd_flat(const GnBwdArgs& a, int bg, int bidx
     __syncthreads();
     const int seg = cpc < 64 ? cpc : 64;
     float sa = 0.f, sb = 0.f;
+    // one chunk of lookahead: the next chunk's two 16-B loads are issued before this one is used
+    float xv[8], gv[8];
+    if (threadIdx.x < nch) {
+        load8(xp + threadIdx.x * 8, xv);
+        load8(gp + threadIdx.x * 8, gv);
+    }
     for (long long base = 0; base < nch; base += NT) {
         const long long i = base + threadIdx.x;
+        float xn[8], gn[8];
+        if (i + NT < nch) {
+            load8(xp + (i + NT) * 8, xn);
+            load8(gp + (i + NT) * 8, gn);
+        }
         if (i < nch) {
-            float xv[8], gv[8];
-            load8(xp + i * 8, xv);
-            load8(gp + i * 8, gv);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 sa = fmaf(gv[k], (xv[k] - mean) * rstd, sa);
                 sb += gv[k];
             }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            xv[k] = xn[k];
+            gv[k] = gn[k];
         }
         const long long w0 = base + 64 * wave;        // this wave's first chunk
         const bool flush = cpc < 64 || w0 + NT >= nch || ((w0 + NT) >> lg) != (w0 >> lg);
@@ -813,6 +829,7 @@ __device__ __forceinline__ void gn_bwd_flat(const GnBwdArgs& a, int bg, int bidx
     const float n = (float)nch * 8.f;
     const float m1 = block_sum(cx, scratch) / n, m2 = block_sum(cxx, scratch + 4) / n;
     TX* dxp = reinterpret_cast<TX*>(a.dx) + (long long)bg * nch * 8;
+#pragma unroll 4
     for (long long i = threadIdx.x; i < nch; i += NT) {
         const float k = s_k[(int)(i >> lg)];
         float xv[8], gv[8], o[8];

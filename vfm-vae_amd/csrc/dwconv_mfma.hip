@@ -14,8 +14,8 @@
 // ~20x the needed rate, the kernel is left HBM-bound). The band origin x0 - 8 keeps every B fragment
 // (8 consecutive input columns of one row) a 16-B aligned read. One wave owns a 16-row x XW-column
 // output block of one plane: it stages the 16 + K - 1 input rows x (XW + 16) columns in LDS once
-// (16-B loads, zero halo, row stride an odd multiple of 16 B so the 16 row-lanes of a fragment read
-// hit distinct bank groups), builds its K A-fragments from the channel's taps (staged through LDS),
+// (16-B loads, zero halo, row stride chosen so each ds_read_b128 lane group of a fragment read hits
+// 16 distinct 16-B bank slots), builds its K A-fragments from the channel's taps (staged through LDS),
 // and runs XW / 16 tiles x K MFMAs; a wave walks up to 4 such row blocks down the plane with the next
 // block's loads in flight during the current block's MFMAs. Output: lane l holds
 // out[y0 + (l & 15)][x0 + 16 s + 4 (l >> 4) + r], r < 4 -> one 8-B store per tile (+ the fp32 noise
@@ -55,7 +55,12 @@ template <int K, int XW>
 __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     constexpr int P = (K - 1) / 2;
     constexpr int NQ = XW / 8 + 2;                          // 16-B chunks per staged row
-    constexpr int RS = ((NQ * 16 / 16) | 1) * 16;           // row stride (bytes): odd multiple of 16
+    // row stride: R 16-B slots with R = 2 (mod 4), R >= NQ. The B-fragment ds_read_b128 of lane
+    // (n = l & 15, g = l >> 4) starts at slot R n + 2 s + g; with R = 2 (mod 4) the 16 lanes of each
+    // of its four lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) land on 16 distinct slots of
+    // the 256-B bank row (conflict-free; the odd strides used before were 2-way), and the staging
+    // stores stay contiguous when R = NQ.
+    constexpr int RS = (NQ + (6 - NQ % 4) % 4) * 16;
     constexpr int NR = 16 + K - 1;
     constexpr int NL = (NR * NQ + 63) / 64;                 // staging loads per lane per row block
     __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES][ROWS * RS];

@@ -1,0 +1,80 @@
+// im2col of a 1-D convolution with zero or circular padding, and its adjoint, fp32 (the projected
+// discriminator heads' k = 9 SpectralConv1d with padding_mode='circular', reference
+// networks/discriminator.py DiscHead / make_block: F.pad(circular) + unfold + permute + reshape in the
+// GEMM formulation, ~4 kernels forward and ~6 backward (CopySlices, slice / unfold backward)).
+//   cols[b, c k + j, l] = x[b, c, s],  s = l + j - p  (circular: mod L; zeros: 0 outside [0, L))
+//   dx[b, c, t]        = sum_j dcols[b, c k + j, l_j(t)]   over the l that read t
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+__global__ __launch_bounds__(256) void im2col1d(const float* __restrict__ x, float* __restrict__ cols, int C, int L,
+                                                int k, int p, int Lo, int circ, long long n) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int l = (int)(e % Lo);
+        const long long r = e / Lo;                  // (b C + c) k + j
+        const int j = (int)(r % k);
+        const long long bc = r / k;
+        int s = l + j - p;
+        float v = 0.f;
+        if (circ) {
+            s %= L;
+            if (s < 0) s += L;
+            v = x[bc * L + s];
+        } else if (s >= 0 && s < L) {
+            v = x[bc * L + s];
+        }
+        cols[e] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols, float* __restrict__ dx, int C, int L,
+                                                int k, int p, int Lo, int circ, long long n) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int t = (int)(e % L);
+        const long long bc = e / L;
+        const float* dr = dcols + bc * k * Lo;
+        float acc = 0.f;
+        for (int j = 0; j < k; ++j) {
+            int l = t - j + p;
+            if (circ) {                              // Lo == L: exactly one l per (t, j)
+                l %= L;
+                if (l < 0) l += L;
+            } else if (l < 0 || l >= Lo) {
+                continue;
+            }
+            acc += dr[(long long)j * Lo + l];
+        }
+        dx[e] = acc;
+    }
+}
+
+int grid_of(long long n) { return (int)std::min<long long>((n + 255) / 256, 16384); }
+
+}  // namespace
+
+// cols [B, C k, Lo] from x [B, C, L], Lo = L + 2 p - k + 1; circular padding needs Lo == L.
+extern "C" int vfm_im2col1d_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular,
+                                void* stream) {
+    if (!x || !cols || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
+    const int Lo = L + 2 * p - k + 1;
+    if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
+    const long long n = (long long)B * C * k * Lo;
+    hipLaunchKernelGGL(im2col1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, C, L, k, p, Lo,
+                       circular ? 1 : 0, n);
+    return launch_status();
+}
+
+// dx [B, C, L] = the adjoint of vfm_im2col1d_f32 applied to dcols [B, C k, Lo].
+extern "C" int vfm_col2im1d_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular,
+                                void* stream) {
+    if (!dcols || !dx || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
+    const int Lo = L + 2 * p - k + 1;
+    if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
+    const long long n = (long long)B * C * L;
+    hipLaunchKernelGGL(col2im1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, C, L, k, p, Lo,
+                       circular ? 1 : 0, n);
+    return launch_status();
+}

@@ -1,0 +1,172 @@
+// Spectral normalisation of a weight in training mode (torch.nn.utils.spectral_norm with one power
+// iteration, dim 0, as the projected discriminator's heads use it: reference networks/discriminator.py
+// SpectralConv1d, `SpectralNorm.apply(self, name='weight', n_power_iterations=1, dim=0, eps=1e-12)`),
+// forward in three launches and backward in two (torch: ~13 and ~6 small kernels per call).
+//
+// W [O, I] (the weight reshaped to a matrix), u [O] and v [I] the persistent power-iteration vectors:
+//   v <- normalize(W^T u),  u <- normalize(W v)          (normalize(x) = x / max(||x||, eps)), in place
+//   sigma = u . (W v) = ||W v||^2 / max(||W v||, eps),  W_sn = W / sigma
+// backward (u, v constants, as torch detaches them):
+//   dW = g / sigma - (sum_ij g_ij W_ij) / sigma^2 * u v^T
+// Launches (fwd): K1 t = W^T u (64 columns x 4 row groups per block) + per-block ||t||^2 partials;
+// K2 r = W v (one row per wave, v = t / max(||t||, eps) formed from the K1 partials on the fly; block 0
+// stores v) + per-block ||r||^2 partials; K3 W_sn = W / sigma (grid-stride; block 0 stores u and sigma).
+// (bwd): K4 per-block partials of sum g W; K5 dW. Partial sums are added in a fixed order.
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+constexpr int THREADS = 256;
+
+__device__ __forceinline__ float block_reduce(float v, float* sh) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    return (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+// sum of n partials in a fixed order (every thread gets the same value)
+__device__ __forceinline__ float sum_parts(const float* p, int n, float* sh) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += THREADS) s += p[i];
+    return block_reduce(s, sh);
+}
+
+__global__ __launch_bounds__(THREADS) void sn_wtu(const float* __restrict__ W, const float* __restrict__ u,
+                                                  float* __restrict__ t, float* __restrict__ part, int O, int I) {
+    __shared__ float red[4][65];
+    __shared__ float sh[4];
+    const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + col;
+    float s = 0.f;
+    if (i < I)
+#pragma unroll 4
+        for (int o = rg; o < O; o += 4) s = fmaf(W[(long long)o * I + i], u[o], s);
+    red[rg][col] = s;
+    __syncthreads();
+    float tv = 0.f;
+    if (rg == 0) {
+        tv = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+        if (i < I) t[i] = tv;
+    }
+    const float ss = block_reduce(rg == 0 && i < I ? tv * tv : 0.f, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = ss;
+}
+
+__global__ __launch_bounds__(THREADS) void sn_wv(const float* __restrict__ W, const float* __restrict__ t,
+                                                 const float* __restrict__ tpart, int ntp, float* __restrict__ v,
+                                                 float* __restrict__ v_copy, float* __restrict__ r,
+                                                 float* __restrict__ rpart, int O, int I, float eps) {
+    __shared__ float sh[4];
+    const float inv = 1.f / fmaxf(sqrtf(sum_parts(tpart, ntp, sh)), eps);
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < I; i += THREADS) {
+            const float x = t[i] * inv;
+            v[i] = x;
+            if (v_copy) v_copy[i] = x;
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int o = blockIdx.x * 4 + wave;
+    float s = 0.f;
+    if (o < O) {
+        const float* wr = W + (long long)o * I;
+#pragma unroll 4
+        for (int i = lane; i < I; i += 64) s = fmaf(wr[i], t[i] * inv, s);
+    }
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (o < O && lane == 0) r[o] = s;
+    const float ss = block_reduce(lane == 0 && o < O ? s * s : 0.f, sh);
+    if (threadIdx.x == 0) rpart[blockIdx.x] = ss;
+}
+
+__global__ __launch_bounds__(THREADS) void sn_scale(const float* __restrict__ W, const float* __restrict__ r,
+                                                    const float* __restrict__ rpart, int nrp, float* __restrict__ u,
+                                                    float* __restrict__ u_copy, float* __restrict__ sigma,
+                                                    float* __restrict__ Wsn, int O, long long n, float eps) {
+    __shared__ float sh[4];
+    const float rr = sum_parts(rpart, nrp, sh);
+    const float inv = 1.f / fmaxf(sqrtf(rr), eps);
+    const float sg = rr * inv;                       // u . r with u = r * inv
+    if (blockIdx.x == 0) {
+        for (int o = threadIdx.x; o < O; o += THREADS) {
+            const float x = r[o] * inv;
+            u[o] = x;
+            if (u_copy) u_copy[o] = x;
+        }
+        if (threadIdx.x == 0) sigma[0] = sg;
+    }
+    const float is = 1.f / sg;
+    for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS)
+        Wsn[e] = W[e] * is;
+}
+
+__global__ __launch_bounds__(THREADS) void sn_gw(const float* __restrict__ g, const float* __restrict__ W,
+                                                 float* __restrict__ part, long long n) {
+    __shared__ float sh[4];
+    float s = 0.f;
+    for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS)
+        s = fmaf(g[e], W[e], s);
+    s = block_reduce(s, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(THREADS) void sn_dw(const float* __restrict__ g, const float* __restrict__ u,
+                                                 const float* __restrict__ v, const float* __restrict__ sigma,
+                                                 const float* __restrict__ part, int np, float* __restrict__ dW,
+                                                 int I, long long n) {
+    __shared__ float sh[4];
+    const float S = sum_parts(part, np, sh);
+    const float sg = sigma[0];
+    const float is = 1.f / sg, c = S / (sg * sg);
+    for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS) {
+        const long long o = e / I;
+        dW[e] = g[e] * is - c * u[o] * v[e - o * I];
+    }
+}
+
+constexpr int SCALE_BLOCKS = 512;
+
+}  // namespace
+
+// floats of workspace vfm_specnorm_fwd / _bwd need for an [O, I] weight
+extern "C" long long vfm_specnorm_workspace_floats(int O, int I) {
+    if (O <= 0 || I <= 0) return VFM_ERR_ARGS;
+    const long long tb = (I + 63) / 64, rb = (O + 3) / 4;
+    return (long long)I + O + tb + rb + SCALE_BLOCKS;
+}
+
+// One power iteration on (u [O], v [I]) in place, sigma [1] and Wsn = W / sigma for fp32 W [O, I];
+// u_copy / v_copy (optional) receive the new u / v too (the backward's constants: torch clones them,
+// since a later forward updates the buffers before this call's backward runs).
+extern "C" int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_copy, float* v_copy, float* sigma,
+                                float* Wsn, float* ws, int O, int I, float eps, void* stream) {
+    if (!W || !u || !v || !sigma || !Wsn || !ws || O <= 0 || I <= 0) return VFM_ERR_ARGS;
+    const int tb = (I + 63) / 64, rb = (O + 3) / 4;
+    float* t = ws;
+    float* r = t + I;
+    float* tpart = r + O;
+    float* rpart = tpart + tb;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(sn_wtu, dim3(tb), dim3(THREADS), 0, st, W, u, t, tpart, O, I);
+    hipLaunchKernelGGL(sn_wv, dim3(rb), dim3(THREADS), 0, st, W, t, tpart, tb, v, v_copy, r, rpart, O, I, eps);
+    const long long n = (long long)O * I;
+    const int sb = (int)std::min<long long>(SCALE_BLOCKS, (n + THREADS - 1) / THREADS);
+    hipLaunchKernelGGL(sn_scale, dim3(sb), dim3(THREADS), 0, st, W, r, rpart, rb, u, u_copy, sigma, Wsn, O, n, eps);
+    return launch_status();
+}
+
+// dW = g / sigma - (sum g W) / sigma^2 u v^T (u, v, sigma as left by the forward).
+extern "C" int vfm_specnorm_bwd(const float* g, const float* W, const float* u, const float* v, const float* sigma,
+                                float* dW, float* ws, int O, int I, void* stream) {
+    if (!g || !W || !u || !v || !sigma || !dW || !ws || O <= 0 || I <= 0) return VFM_ERR_ARGS;
+    const long long n = (long long)O * I;
+    const int nb = (int)std::min<long long>(SCALE_BLOCKS, (n + THREADS - 1) / THREADS);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(sn_gw, dim3(nb), dim3(THREADS), 0, st, g, W, ws, n);
+    hipLaunchKernelGGL(sn_dw, dim3(nb), dim3(THREADS), 0, st, g, u, v, sigma, ws, nb, dW, I, n);
+    return launch_status();
+}

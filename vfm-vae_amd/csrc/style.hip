@@ -15,9 +15,9 @@
 //              dA[j, k] = wg sum_b dm[b, j] w[b, k],   dab[j] = bg sum_b dm[b, j],
 //              dw[b, k] = wg sum_j dm[b, j] A[j, k]
 // The products are skinny (one side is the batch, <= a few dozen rows), so there are two job shapes:
-//  * long reductions (over WD, C, O or 3C): one wave per 4-row x CB-column output block, the 64 lanes
-//    striding over k (coalesced along k), each lane keeping 4 x CB partial sums that are then reduced
-//    across the wave with xor shuffles;
+//  * reductions over WD, C, O or 3C: 4-row x CB-column output tiles, one per wave (short K) or one per
+//    block (K >= 1024), the threads striding over k (coalesced along k), each keeping 4 x CB partial
+//    sums that are reduced across the wave with xor shuffles (and across the four waves in LDS);
 //  * reductions over the batch (dW1, dA, dab): one thread per 8-wide output strip of a row (the row's
 //    batch factor computed once per sample), a loop over the batch.
 // All sums are plain fp32 FMAs (the reference runs them in fp32 with TF32 off).
@@ -48,20 +48,25 @@ struct StyleArgs {
     float* dA;                            // [3C, WD] or null
     float* dab;                           // [3C] or null
     float* dw;                            // [B, WD] or null
-    long long units0;                     // work units (waves or threads) of the launch's first job
     int blocks0;                          // blocks of the first job
+    int tpb;                              // tiles per block of the launch's tile job (1 or WAVES)
 };
 
-// acc[r][c] = sum_k X(r, k) Y(c, k) over k < K for one wave: ldx(k, x[RB]) / ldy(k, y[CB]) load the
-// operand values of one k (zero outside the operand); the result is complete in every lane.
+// acc[r][c] = sum_k X(r, k) Y(c, k) over k < K: ldx(k, x[RB]) / ldy(k, y[CB]) load the operand values
+// of one k (zero outside the operand). tpb = 4 (short K): one tile per wave, its 64 lanes striding
+// over k, the partial sums reduced across the wave with xor shuffles (result in every lane).
+// tpb = 1 (long K): one tile per block, the 256 threads striding over k, the four waves' sums meeting
+// in LDS (result in wave 0). Loads are coalesced along k either way.
 template <int CB, class LX, class LY>
-__device__ __forceinline__ void wave_mm(int K, int lane, LX ldx, LY ldy, float (&acc)[RB][CB]) {
+__device__ __forceinline__ void tile_mm(int K, int tpb, LX ldx, LY ldy, float (&acc)[RB][CB], float* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int c = 0; c < CB; ++c) acc[r][c] = 0.f;
+    const int step = tpb == 1 ? THREADS : 64;
 #pragma unroll 2
-    for (int k = lane; k < K; k += 64) {
+    for (int k = tpb == 1 ? (int)threadIdx.x : lane; k < K; k += step) {
         float x[RB], y[CB];
         ldx(k, x);
         ldy(k, y);
@@ -76,6 +81,19 @@ __device__ __forceinline__ void wave_mm(int K, int lane, LX ldx, LY ldy, float (
         for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int c = 0; c < CB; ++c) acc[r][c] += __shfl_xor(acc[r][c], o, 64);
+    if (tpb != 1) return;
+    if (wave > 0 && lane == 0)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) red[((wave - 1) * RB + r) * CB + c] = acc[r][c];
+    __syncthreads();
+    if (wave == 0)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                acc[r][c] += (red[r * CB + c] + red[(RB + r) * CB + c]) + red[(2 * RB + r) * CB + c];
 }
 
 __device__ __forceinline__ float dm_at(const StyleArgs& a, int b, int j) {
@@ -91,16 +109,20 @@ __device__ __forceinline__ float q_at(const StyleArgs& a, int b, int o) {
     return -0.5f * a.dd[i] * dv * dv * dv;
 }
 
-// LAUNCH 0 (waves): m, s         — 4 samples x 4 channels (x 3 split parts) per wave, k < WD
-// LAUNCH 1 (waves): d            — 4 samples x 8 outputs per wave, k < C
-// LAUNCH 2: ds (waves: 4 samples x 8 channels, k < O) | dW1 (threads: 8-channel strips, b < B)
-// LAUNCH 3: dA + dab (threads: 8-column strips, b < B) | dw (waves: 4 samples x 8 columns, k < 3C)
+// LAUNCH 0 (tiles): m, s   — 4 samples x 4 channels (x 3 split parts) per tile, k < WD
+// LAUNCH 1 (tiles): d      — 4 samples x 8 outputs per tile, k < C
+// LAUNCH 2: ds (tiles: 4 samples x 8 channels, k < O) | dW1 (threads: 8-channel strips, b < B)
+// LAUNCH 3: dA + dab (threads: 8-column strips, b < B) | dw (tiles: 4 samples x 8 columns, k < 3C)
 template <int LAUNCH>
 __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ float red[(WAVES - 1) * RB * 3 * 4];
     const bool second = (int)blockIdx.x >= a.blocks0;
     const int blk = second ? blockIdx.x - a.blocks0 : blockIdx.x;
-    const long long wunit = (long long)blk * WAVES + wave;            // wave jobs
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // tile jobs: one tile per block (tpb = 1) or per wave (tpb = 4); the result sits in lane `idx` of
+    // wave 0 (tpb = 1) or of every wave (tpb = 4)
+    const long long wunit = a.tpb == 1 ? (long long)blk : (long long)blk * WAVES + wave;
+    const bool owner0 = a.tpb != 1 || wave == 0;
     const long long tunit = (long long)blk * THREADS + threadIdx.x;   // thread jobs
     const int C = a.C, C3 = 3 * a.C, WD = a.WD, O = a.O, B = a.B;
     const int nbg = (B + RB - 1) / RB;                                 // 4-sample groups
@@ -110,7 +132,7 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
         if (wunit >= (long long)nbg * ((C + CC - 1) / CC)) return;
         const int b0 = (int)(wunit % nbg) * RB, c0 = (int)(wunit / nbg) * CC;
         float acc[RB][3 * CC];
-        wave_mm<3 * CC>(WD, lane,
+        tile_mm<3 * CC>(WD, a.tpb,
             [&](int k, float (&x)[RB]) {
 #pragma unroll
                 for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? a.w[(long long)(b0 + r) * a.ldw + k] : 0.f;
@@ -121,13 +143,13 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
 #pragma unroll
                     for (int c = 0; c < CC; ++c)
                         y[p * CC + c] = c0 + c < C ? a.A[(long long)(p * C + c0 + c) * WD + k] : 0.f;
-            }, acc);
+            }, acc, red);
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int c = 0; c < CC; ++c) {
                 const int b = b0 + r, cc = c0 + c;
-                if (lane != r * CC + c || b >= B || cc >= C) continue;
+                if (!owner0 || lane != r * CC + c || b >= B || cc >= C) continue;
                 const float m1 = fmaf(a.wg, acc[r][c], a.bg * a.ab[cc]);
                 const float m2 = fmaf(a.wg, acc[r][CC + c], a.bg * a.ab[C + cc]);
                 const float m3 = fmaf(a.wg, acc[r][2 * CC + c], a.bg * a.ab[2 * C + cc]);
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
         if (wunit >= (long long)nbg * ((O + CB - 1) / CB)) return;
         const int b0 = (int)(wunit % nbg) * RB, o0 = (int)(wunit / nbg) * CB;
         float acc[RB][CB];
-        wave_mm<CB>(C, lane,
+        tile_mm<CB>(C, a.tpb,
             [&](int k, float (&x)[RB]) {
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {
@@ -154,12 +176,12 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
                     const float v = o0 + c < O ? a.W1[(long long)(o0 + c) * C + k] : 0.f;
                     y[c] = v * v;
                 }
-            }, acc);
+            }, acc, red);
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int c = 0; c < CB; ++c)
-                if (lane == r * CB + c && b0 + r < B && o0 + c < O)
+                if (owner0 && lane == r * CB + c && b0 + r < B && o0 + c < O)
                     a.d[(long long)(b0 + r) * O + o0 + c] = rsqrtf(acc[r][c] + a.eps);
     } else if (LAUNCH == 2) {
         if (!second) {            // ds [B, C]: waves, k < O
@@ -167,7 +189,7 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
             if (wunit >= (long long)nbg * ((C + CB - 1) / CB)) return;
             const int b0 = (int)(wunit % nbg) * RB, i0 = (int)(wunit / nbg) * CB;
             float acc[RB][CB];
-            wave_mm<CB>(O, lane,
+            tile_mm<CB>(O, a.tpb,
                 [&](int k, float (&x)[RB]) {
 #pragma unroll
                     for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? q_at(a, b0 + r, k) : 0.f;
@@ -179,13 +201,13 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
                         const float v = i0 + c < C ? row[c] : 0.f;
                         y[c] = v * v;
                     }
-                }, acc);
+                }, acc, red);
 #pragma unroll
             for (int r = 0; r < RB; ++r)
 #pragma unroll
                 for (int c = 0; c < CB; ++c) {
                     const int b = b0 + r, i = i0 + c;
-                    if (lane != r * CB + c || b >= B || i >= C) continue;
+                    if (!owner0 || lane != r * CB + c || b >= B || i >= C) continue;
                     const long long o = (long long)b * C + i;
                     a.ds[o] = (a.dsin ? a.dsin[o] : 0.f) + 2.f * a.s[o] * acc[r][c];
                 }
@@ -233,7 +255,7 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
             if (wunit >= (long long)nbg * ((WD + CB - 1) / CB)) return;
             const int b0 = (int)(wunit % nbg) * RB, n0 = (int)(wunit / nbg) * CB;
             float acc[RB][CB];
-            wave_mm<CB>(C3, lane,
+            tile_mm<CB>(C3, a.tpb,
                 [&](int k, float (&x)[RB]) {
 #pragma unroll
                     for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? dm_at(a, b0 + r, k) : 0.f;
@@ -242,18 +264,21 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
                     const float* row = a.A + (long long)k * WD + n0;
 #pragma unroll
                     for (int c = 0; c < CB; ++c) y[c] = n0 + c < WD ? row[c] : 0.f;
-                }, acc);
+                }, acc, red);
 #pragma unroll
             for (int r = 0; r < RB; ++r)
 #pragma unroll
                 for (int c = 0; c < CB; ++c)
-                    if (lane == r * CB + c && b0 + r < B && n0 + c < WD)
+                    if (owner0 && lane == r * CB + c && b0 + r < B && n0 + c < WD)
                         a.dw[(long long)(b0 + r) * WD + n0 + c] = a.wg * acc[r][c];
         }
     }
 }
 
 inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+
+// tiles per block for a reduction of length K: the whole block on one tile from K >= 1024 on
+inline int tiles_per_block(int K) { return K >= 1024 ? 1 : WAVES; }
 
 template <int L>
 int launch(StyleArgs& a, long long blocks, hipStream_t st) {
@@ -281,10 +306,12 @@ extern "C" int vfm_style_demod_fwd(const float* w, long long ldw, const float* A
     a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = m; a.s = s; a.d = d;
     hipStream_t st = (hipStream_t)stream;
     const long long nbg = cdiv(B, RB);
-    a.blocks0 = (int)cdiv(nbg * cdiv(C, 4), WAVES);
+    a.tpb = tiles_per_block(WD);
+    a.blocks0 = (int)cdiv(nbg * cdiv(C, 4), a.tpb);
     int rc = launch<0>(a, a.blocks0, st);
     if (rc || !W1) return rc;
-    a.blocks0 = (int)cdiv(nbg * cdiv(O, 8), WAVES);
+    a.tpb = tiles_per_block(C);
+    a.blocks0 = (int)cdiv(nbg * cdiv(O, 8), a.tpb);
     return launch<1>(a, a.blocks0, st);
 }
 
@@ -307,7 +334,8 @@ extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A
     hipStream_t st = (hipStream_t)stream;
     const long long nbg = cdiv(B, RB);
     if (demod) {
-        a.blocks0 = (int)cdiv(nbg * cdiv(C, 8), WAVES);
+        a.tpb = tiles_per_block(O);
+        a.blocks0 = (int)cdiv(nbg * cdiv(C, 8), a.tpb);
         const long long b1 = dW1 ? cdiv((long long)O * cdiv(C, 8), THREADS) : 0;
         const int rc = launch<2>(a, a.blocks0 + b1, st);
         if (rc) return rc;
@@ -317,6 +345,8 @@ extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A
     }
     if (!dA && !dab && !dw) return 0;
     a.blocks0 = (dA || dab) ? (int)cdiv(3LL * C * cdiv(WD, 8), THREADS) : 0;
-    const long long b1 = dw ? cdiv(nbg * cdiv(WD, 8), WAVES) : 0;
+    const int C3 = 3 * C;
+    a.tpb = tiles_per_block(C3);
+    const long long b1 = dw ? cdiv(nbg * cdiv(WD, 8), a.tpb) : 0;
     return launch<3>(a, a.blocks0 + b1, st);
 }

@@ -42,24 +42,36 @@ class SpectralConv1d(nn.Conv1d):
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)
         SpectralNorm.apply(self, name='weight', n_power_iterations=1, dim=0, eps=1e-12)
+        # training-mode power iteration + W / sigma on csrc/specnorm.hip for ROCm weights (same buffers,
+        # same state-dict keys; torch's hook runs otherwise)
+        from torch_utils.ops import specnorm
+        specnorm.install_fused_spectral_norm(self)
 
     def _conv_forward(self, x, weight, bias):
         if not x.is_cuda or self.groups != 1 or self.stride != (1,) or self.dilation != (1,) or x.dim() != 3:
             return super()._conv_forward(x, weight, bias)
         k = self.kernel_size[0]
-        O = weight.shape[0]
         if k > 1 or self.padding[0] > 0:
             p = self.padding[0]
+            from torch_utils.ops import patchgan_hip
+            circ = self.padding_mode == 'circular'
+            if self.padding_mode in ('zeros', 'circular') and patchgan_hip.im2col1d_supported(x, k, p, circ):
+                x = patchgan_hip.im2col1d(x, k, p, circ)             # one launch each way (csrc/im2col1d.hip)
+                return self._gemm_out(x, weight, bias)
             mode = 'constant' if self.padding_mode == 'zeros' else self.padding_mode
             xp = F.pad(x, (p, p), mode=mode) if p > 0 else x
             B, C, _ = xp.shape
             cols = xp.unfold(2, k, 1)                                  # [B, C, L, k]
             L = cols.shape[2]
             x = cols.permute(0, 1, 3, 2).reshape(B, C * k, L)
+        return self._gemm_out(x, weight, bias)
+
+    @staticmethod
+    def _gemm_out(x, weight, bias):
         # exact fp32 GEMM (hipBLASLt): the heads' BatchNormLocal over virtual batches of <= 8
         # samples amplifies GEMM rounding into the input gradient, so these stay on the vendor's
         # fp32 products; they are a few GFLOP per step
-        y = torch.matmul(weight.reshape(O, -1), x)
+        y = torch.matmul(weight.reshape(weight.shape[0], -1), x)
         if bias is not None:
             y = y + bias.to(y.dtype)[None, :, None]
         return y

@@ -83,9 +83,10 @@ class ConvNeXtSynthesisLayer(nn.Module):
     def _noise(self, H, W):
         if not self.legacy:
             return None
-        noise = (self.noise_const * self.noise_strength)[None, None]
-        if noise.shape[-2:] != (H, W):
-            noise = F.interpolate(noise, size=(H, W), mode='bilinear', align_corners=False)
+        noise = self.noise_const * self.noise_strength
+        if noise.shape[-2:] == (H, W):
+            return noise.float()              # no [None, None] / [0, 0] round trip: its backward is a zeros + copy
+        noise = F.interpolate(noise[None, None], size=(H, W), mode='bilinear', align_corners=False)
         return noise[0, 0].float()
 
     def forward(self, x, w, compute_dtype=None):

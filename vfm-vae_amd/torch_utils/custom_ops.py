@@ -80,6 +80,11 @@ SIGNATURES = {
     "vfm_dwconv2d_fwd_mfma_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_vp],
     "vfm_dwconv2d_wgrad_reduce": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
+    "vfm_specnorm_workspace_floats": [c_int, c_int],
+    "vfm_specnorm_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp],
+    "vfm_specnorm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
+    "vfm_im2col1d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_col2im1d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_shift2d": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_im2col_nhwc_f32": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_col2im_nhwc_f32": [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -163,6 +168,7 @@ def get_native():
             lib.vfm_version.restype = ctypes.c_char_p
             lib.vfm_bnl_workspace_floats.restype = c_ll
             lib.vfm_channel_rms_norm_rows.restype = c_ll
+            lib.vfm_specnorm_workspace_floats.restype = c_ll
             _lib = lib
     return _lib
 

@@ -219,3 +219,87 @@ def bias_lrelu(yh, bias, slope):
     C = yh.shape[-1]
     y2 = bias_act.bias_act(yh.reshape(-1, C), bias, dim=1, act='lrelu', alpha=slope, gain=1.0)
     return y2.reshape(yh.shape)
+
+
+# ---------------------------------------------------------------------------
+# Spectral normalisation of the D heads' SpectralConv1d weights in training mode (csrc/specnorm.hip;
+# torch.nn.utils.spectral_norm with one power iteration, dim 0): three launches forward, two backward.
+
+
+class _SpectralNormWeight(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, u, v, eps):
+        O = weight.shape[0]
+        W = weight.detach().reshape(O, -1)
+        if W.dtype != torch.float32 or not W.is_contiguous():
+            raise custom_ops.NativeError("spectral_norm_weight: fp32 contiguous weight expected")
+        I = W.shape[1]
+        dev = W.device
+        ws = torch.empty([_lib.vfm_specnorm_workspace_floats(O, I)], dtype=torch.float32, device=dev)
+        uc = torch.empty([O], dtype=torch.float32, device=dev)
+        vc = torch.empty([I], dtype=torch.float32, device=dev)
+        sigma = torch.empty([1], dtype=torch.float32, device=dev)
+        wsn = torch.empty_like(weight)
+        with kernel_timer.region('specnorm_fwd<f32>', 4 * (2 * O * I + O + I)):
+            _check(_lib.vfm_specnorm_fwd(W.data_ptr(), u.data_ptr(), v.data_ptr(), uc.data_ptr(), vc.data_ptr(),
+                                         sigma.data_ptr(), wsn.data_ptr(), ws.data_ptr(), O, I, float(eps), _stream()),
+                   'vfm_specnorm_fwd')
+        ctx.save_for_backward(W, uc, vc, sigma)
+        return wsn
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g):
+        W, uc, vc, sigma = ctx.saved_tensors
+        O, I = W.shape
+        g = _c16(g.float())
+        ws = torch.empty([_lib.vfm_specnorm_workspace_floats(O, I)], dtype=torch.float32, device=W.device)
+        dW = torch.empty_like(W)
+        with kernel_timer.region('specnorm_bwd<f32>', 4 * 3 * O * I):
+            _check(_lib.vfm_specnorm_bwd(g.data_ptr(), W.data_ptr(), uc.data_ptr(), vc.data_ptr(), sigma.data_ptr(),
+                                         dW.data_ptr(), ws.data_ptr(), O, I, _stream()), 'vfm_specnorm_bwd')
+        return dW.reshape(g.shape), None, None, None
+
+
+def spectral_norm_weight(weight, u, v, eps):
+    """W / sigma(W) with one in-place power iteration on (u, v) (training-mode torch spectral_norm, dim 0)."""
+    return _SpectralNormWeight.apply(weight, u, v, eps)
+
+
+# ---------------------------------------------------------------------------
+# im2col of the D heads' 1-D convs (csrc/im2col1d.hip): zero or circular padding, one launch each way.
+
+
+class _Im2col1d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, p, circular):
+        x = _c16(x)
+        B, C, L = x.shape
+        Lo = L + 2 * p - k + 1
+        cols = torch.empty([B, C * k, Lo], dtype=torch.float32, device=x.device)
+        with kernel_timer.region('im2col1d<f32>', 4 * (x.numel() + cols.numel())):
+            _check(_lib.vfm_im2col1d_f32(x.data_ptr(), cols.data_ptr(), B, C, L, k, p, int(circular), _stream()),
+                   'vfm_im2col1d_f32')
+        ctx.meta = (B, C, L, k, p, circular)
+        return cols
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dcols):
+        B, C, L, k, p, circular = ctx.meta
+        dcols = _c16(dcols.float())
+        dx = torch.empty([B, C, L], dtype=torch.float32, device=dcols.device)
+        with kernel_timer.region('col2im1d<f32>', 4 * (dx.numel() + dcols.numel())):
+            _check(_lib.vfm_col2im1d_f32(dcols.data_ptr(), dx.data_ptr(), B, C, L, k, p, int(circular), _stream()),
+                   'vfm_col2im1d_f32')
+        return dx, None, None, None
+
+
+def im2col1d_supported(x, k, p, circular):
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.numel() > 0
+            and (not circular or (2 * p == k - 1 and p <= x.shape[2])))
+
+
+def im2col1d(x, k, p, circular):
+    """[B, C, L] -> [B, C k, Lo]: F.pad(x, (p, p), circular / zeros).unfold(2, k, 1) in the GEMM layout."""
+    return _Im2col1d.apply(x, int(k), int(p), bool(circular))
