@@ -160,6 +160,12 @@ int vfm_specnorm_bwd(const float* g, const float* W, const float* u, const float
 int vfm_im2col1d_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular, void* stream);
 int vfm_col2im1d_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular, void* stream);
 
+/* Column sums of the per-sample [rows, cols] fp32 partials of the decoder backward kernels, two at a
+ * time in one launch: out_a = scale_a * sum_r a (scale_a optional), out_b = sum_r b (either output may
+ * be null); rows summed in order. */
+int vfm_colsum2_f32(const float* a, const float* b, const float* scale_a, float* out_a, float* out_b, int rows,
+                    int cols, void* stream);
+
 /* DiffAugment random translation (replaces the padded gather of reference training/diffaug.py
  * rand_translation and its indexing backward): y[b, c, i, j] = x[b, c, i + sign tx[b], j + sign ty[b]]
  * inside the image, else 0; x, y contiguous NCHW (VFM_F32 / VFM_BF16); tx, ty int64 [B] on the device.

@@ -1363,9 +1363,33 @@ __global__ __launch_bounds__(256) void dw_wgrad_reduce(const float* __restrict__
     }
 }
 
+// out_a[c] = scale_a[c] * sum_r a[r, c] (scale_a optional), out_b[c] = sum_r b[r, c] (b optional);
+// rows summed in order (deterministic): the per-sample partials of the norm / layer-scale backward
+__global__ __launch_bounds__(256) void colsum2(const float* __restrict__ a, const float* __restrict__ b,
+                                               const float* __restrict__ scale_a, float* __restrict__ out_a,
+                                               float* __restrict__ out_b, int rows, int cols) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cols) return;
+    float sa = 0.f, sb = 0.f;
+    for (int r = 0; r < rows; ++r) {
+        if (out_a) sa += a[(long long)r * cols + c];
+        if (out_b) sb += b[(long long)r * cols + c];
+    }
+    if (out_a) out_a[c] = scale_a ? sa * scale_a[c] : sa;
+    if (out_b) out_b[c] = sb;
+}
+
 }  // namespace
 
 // ============================== C ABI ==========================================================
+
+extern "C" int vfm_colsum2_f32(const float* a, const float* b, const float* scale_a, float* out_a, float* out_b,
+                               int rows, int cols, void* stream) {
+    if (rows <= 0 || cols <= 0 || (!out_a && !out_b) || (out_a && !a) || (out_b && !b)) return VFM_ERR_ARGS;
+    hipLaunchKernelGGL(colsum2, dim3((cols + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, b,
+                       scale_a, out_a, out_b, rows, cols);
+    return launch_status();
+}
 
 extern "C" int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float* db, int rows, int C, int KK,
                                          void* stream) {

@@ -354,6 +354,18 @@ def dwconv2d(x, weight, bias, padding, noise, slot=None):
 # (reference shared.py:165-167 GroupNorm32; convnext_utils.py:126-127).
 
 
+def _colsum2(a, b, scale_a, want_a, want_b, rows, cols):
+    """(scale_a * a.view(rows, cols).sum(0) if want_a, b.view(rows, cols).sum(0) if want_b) in one launch."""
+    if not (want_a or want_b):
+        return None, None
+    oa = torch.empty([cols], dtype=torch.float32, device=a.device) if want_a else None
+    ob = torch.empty([cols], dtype=torch.float32, device=a.device) if want_b else None
+    sc = None if scale_a is None else _f32(scale_a)
+    _check(_lib.vfm_colsum2_f32(a.data_ptr(), b.data_ptr(), _p(sc), _p(oa), _p(ob), rows, cols, _stream()),
+           'vfm_colsum2_f32')
+    return oa, ob
+
+
 class _GroupNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, style, groups, eps, out_dtype):
@@ -392,8 +404,9 @@ class _GroupNorm(torch.autograd.Function):
                                            _code(x), _code(dy), B, C, ctx.groups, HW, _stream()),
                    'vfm_group_norm_bwd')
         wdt, bdt, sdt = ctx.meta
-        dw = dwp.sum(0).to(wdt) if _wanted(ctx, 1) else None
-        db = dbp.sum(0).to(bdt) if _wanted(ctx, 2) else None
+        dw, db = _colsum2(dwp, dbp, None, _wanted(ctx, 1), _wanted(ctx, 2), B, C)
+        dw = None if dw is None else dw.to(wdt)
+        db = None if db is None else db.to(bdt)
         dst = ds.to(sdt) if _wanted(ctx, 3) else None
         return (dx if ctx.needs_input_grad[0] else None), dw, db, dst, None, None, None
 
@@ -485,12 +498,9 @@ class _LayerScaleResidual(torch.autograd.Function):
             _check(_lib.vfm_layer_scale_residual_bwd(y.data_ptr(), _p(b), _p(g), dout.data_ptr(), dy.data_ptr(),
                                                      r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout), B, C, P,
                                                      _stream()), 'vfm_layer_scale_residual_bwd')
-        db = dg = None
-        if b is not None and _wanted(ctx, 1):
-            s1 = r1.view(B, C).sum(0)
-            db = (s1 * g if g is not None else s1).to(bdt)
-        if g is not None and _wanted(ctx, 2):
-            dg = r0.view(B, C).sum(0).to(gdt)
+        db, dg = _colsum2(r1, r0, g, b is not None and _wanted(ctx, 1), g is not None and _wanted(ctx, 2), B, C)
+        db = None if db is None else db.to(bdt)
+        dg = None if dg is None else dg.to(gdt)
         dx = dout if ctx.needs_input_grad[3] and not _stash_residual(ctx.slot, dout) else None
         return (dy if ctx.needs_input_grad[0] else None), db, dg, dx, None
 
