@@ -336,6 +336,7 @@ def smoke_step():
     it = TrainingIteration(G, D, copy.deepcopy(G).eval(), loss, make_optimizer(G.parameters(), opt, dev),
                            make_optimizer(D.parameters(), opt, dev), batch_size=2)
     img = torch.rand(2, 3, 64, 64, device=dev)
+    print("smoke: networks built, running the iteration", flush=True)
     it([img], [['x', 'x']], 0)
     torch.cuda.synchronize()
     for n, p in G.named_parameters():
