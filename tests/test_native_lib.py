@@ -92,3 +92,16 @@ def test_torch_library_schemas():
     # CPU tensors: the ops are registered for the CUDA (ROCm) dispatch key only
     with pytest.raises(NotImplementedError):
         ops.upfirdn2d(torch.zeros(1, 1, 4, 4), torch.ones(1, 1), 1, 1, 1, 1, 0, 0, 0, 0, False, 1.0)
+
+
+def test_torch_ops_load_first_in_fresh_process():
+    """get_torch_ops() as the first native call of a process (what smoke() does through upfirdn2d)
+    returns: it takes the loader lock and loads the kernel library under it (a non-reentrant lock
+    deadlocked there)."""
+    import subprocess
+    import sys
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from torch_utils import custom_ops; "
+            "print(custom_ops.get_torch_ops() is not None)" % (root + "/vfm-vae_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("True"), r.stderr[-2000:]

@@ -17,7 +17,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
 # TORCH_LIBRARY(vfmvae) registration of the reference's plugin ops (csrc/torch_ops.cpp)
 _TORCH_LIB_PATH = os.path.join(os.path.dirname(_LIB_PATH), "libvfmvae_torch.so")
 _torch_ops = None
-_lock = threading.Lock()
+_lock = threading.RLock()          # get_torch_ops holds it while it calls get_native
 _lib = None
 
 c_int, c_ll, c_float, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
@@ -182,9 +182,9 @@ def get_torch_ops():
     global _torch_ops
     if _torch_ops is not None:
         return _torch_ops
+    get_native()                          # outside the lock: it takes the lock itself
     with _lock:
         if _torch_ops is None:
-            get_native()
             if not os.path.exists(_TORCH_LIB_PATH):
                 raise NativeError(f"torch op library not found at {_TORCH_LIB_PATH}; run the build "
                                   "(`make -C vfm-vae_amd/csrc`)")
