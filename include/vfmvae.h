@@ -51,6 +51,19 @@ enum {
 const char* vfm_version(void);
 
 /*
+ * Kernel timing (measurement only; no reference counterpart). While (start, stop) is armed on the
+ * calling thread, every kernel the library launches is dispatched with hipExtLaunchKernelGGL and the
+ * two events bound to the dispatch itself: start = the first launch's start, stop = the end of each
+ * launch. hipEventElapsedTime(start, stop) is then the kernels' own duration (no host launch gaps).
+ * vfm_timer_arm(NULL, NULL) disarms; every call returns the number of launches made under the
+ * previous arming (0: the events were not recorded). Events come from vfm_event_create.
+ */
+int vfm_timer_arm(void* start, void* stop);
+int vfm_event_create(void** ev);
+int vfm_event_destroy(void* ev);
+int vfm_event_elapsed(void* start, void* stop, float* ms);
+
+/*
  * upfirdn2d: upsample (zero insertion) -> pad/crop -> 2-D FIR -> downsample -> gain.
  * Replaces `upfirdn2d(x, f, upx, upy, downx, downy, padx0, padx1, pady0, pady1,
  * flip, gain)` of `torch_utils/ops/upfirdn2d.cpp:16` (kernels `upfirdn2d.cu:29-200`).

@@ -170,3 +170,45 @@ def test_wds_process_workers_batches(tmp_path):
         assert all(len(b[1]) == 4 and all(lab in ("zero", "one", "two") for lab in b[1]) for b in batches)
         got[procs] = sorted(bytes(x.numpy().tobytes()[:64]) for b in batches for x in b[0])
     assert len(got[True]) == 16 and got[True] == got[False]
+
+
+def test_wds_process_leftovers_pooled(tmp_path):
+    """One-epoch pass on worker processes: each worker's last partial batch goes to the parent, which
+    pools the leftovers into whole batches (only the final remainder is dropped, as on threads)."""
+    from training.data_wds import WdsWrapper
+    _write_shards(str(tmp_path / "wds"), n_shards=4, per_shard=3)
+    c2t = tmp_path / "c2t.json"
+    c2t.write_text(json.dumps({"0": "zero", "1": "one", "2": "two"}))
+    kw = dict(label_type="cls2text", cls_to_text_path=str(c2t), workers=2, one_epoch=True, sample_shuffle_size=2)
+    n = {}
+    for procs in (False, True):
+        ds = WdsWrapper(str(tmp_path / "wds"), 64, processes=procs, **kw)
+        batches = list(ds.iterate(batch_size=4, seed=3))
+        assert all(b[0].shape == (4, 3, 64, 64) and len(b[1]) == 4 for b in batches)
+        n[procs] = len(batches)
+    assert n[True] == n[False] == 3          # 12 samples: 2 workers x (1 whole batch + 2 leftovers)
+
+
+def test_wds_process_worker_death_raises(tmp_path):
+    """A decode worker killed without reaching its finally clause (SIGKILL) must surface as an error
+    in the training process, not as an endless wait for its end-of-stream sentinel."""
+    import multiprocessing as mp
+    import signal
+    import time
+    from training.data_wds import WdsWrapper
+    _write_shards(str(tmp_path / "wds"), n_shards=2, per_shard=4)
+    c2t = tmp_path / "c2t.json"
+    c2t.write_text(json.dumps({"0": "zero", "1": "one", "2": "two"}))
+    ds = WdsWrapper(str(tmp_path / "wds"), 64, processes=True, label_type="cls2text", cls_to_text_path=str(c2t),
+                    workers=2, one_epoch=False, sample_shuffle_size=2)
+    ds.worker_poll_s = 0.2
+    it = ds.iterate(batch_size=2, seed=3)
+    next(it)
+    victims = [p for p in mp.active_children() if "Process" in p.name]
+    assert victims
+    os.kill(victims[0].pid, signal.SIGKILL)
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="died without finishing"):
+        while time.time() - t0 < 60:
+            next(it)
+    it.close()

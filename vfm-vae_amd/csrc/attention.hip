@@ -254,6 +254,6 @@ extern "C" int vfm_attention_fwd(const void* q, const void* k, const void* v, vo
     a.H = H;
     a.c = scale * 1.4426950408889634f;
     dim3 grid((N + QB - 1) / QB, H, B);
-    hipLaunchKernelGGL(attn_fwd_d64, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    VFM_LAUNCH(attn_fwd_d64, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
     return launch_status();
 }

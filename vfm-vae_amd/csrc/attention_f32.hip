@@ -515,8 +515,8 @@ extern "C" int vfm_attention_f32_fwd(const void* q, const void* k, const void* v
     a.c = scale * 1.4426950408889634f;
     a.hd = head_dim;
     const dim3 grid((Nq + RB - 1) / RB, H, B);
-    if (precision == VFM_F32) hipLaunchKernelGGL(attn32_fwd<3>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(attn32_fwd<2>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    if (precision == VFM_F32) VFM_LAUNCH(attn32_fwd<3>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    else VFM_LAUNCH(attn32_fwd<2>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
     return launch_status();
 }
 
@@ -548,14 +548,14 @@ extern "C" int vfm_attention_f32_bwd(const void* q, const void* k, const void* v
     hipStream_t st = (hipStream_t)stream;
     const long long rows = (long long)B * H * Nq;
     if (rows > (1ll << 31) / 16) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(attn32_delta, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, st, a, (int)rows);
+    VFM_LAUNCH(attn32_delta, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, st, a, (int)rows);
     const dim3 gq((Nq + RB - 1) / RB, H, B), gk((Nk + RB - 1) / RB, H, B);
     if (precision == VFM_F32) {
-        hipLaunchKernelGGL(attn32_dq<3>, gq, dim3(64 * WAVES), 0, st, a);
-        hipLaunchKernelGGL(attn32_dkdv<3>, gk, dim3(64 * WAVES), 0, st, a);
+        VFM_LAUNCH(attn32_dq<3>, gq, dim3(64 * WAVES), 0, st, a);
+        VFM_LAUNCH(attn32_dkdv<3>, gk, dim3(64 * WAVES), 0, st, a);
     } else {
-        hipLaunchKernelGGL(attn32_dq<2>, gq, dim3(64 * WAVES), 0, st, a);
-        hipLaunchKernelGGL(attn32_dkdv<2>, gk, dim3(64 * WAVES), 0, st, a);
+        VFM_LAUNCH(attn32_dq<2>, gq, dim3(64 * WAVES), 0, st, a);
+        VFM_LAUNCH(attn32_dkdv<2>, gk, dim3(64 * WAVES), 0, st, a);
     }
     return launch_status();
 }

@@ -118,9 +118,9 @@ int launch_act(BiasActArgs& p, hipStream_t st) {
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
     dim3 g((unsigned)blocks), b(NT);
-    if (p.grad == 0) hipLaunchKernelGGL((bias_act_kernel<T, ACT, 0>), g, b, 0, st, p);
-    else if (p.grad == 1) hipLaunchKernelGGL((bias_act_kernel<T, ACT, 1>), g, b, 0, st, p);
-    else hipLaunchKernelGGL((bias_act_kernel<T, ACT, 2>), g, b, 0, st, p);
+    if (p.grad == 0) VFM_LAUNCH((bias_act_kernel<T, ACT, 0>), g, b, 0, st, p);
+    else if (p.grad == 1) VFM_LAUNCH((bias_act_kernel<T, ACT, 1>), g, b, 0, st, p);
+    else VFM_LAUNCH((bias_act_kernel<T, ACT, 2>), g, b, 0, st, p);
     return launch_status();
 }
 

@@ -299,7 +299,7 @@ int launch(const ConvArgs& a, hipStream_t st) {
     }
     const long long tiles = (long long)((a.M + BM - 1) / BM) * (a.Cout / BN);
     if (tiles > 0x7fffffff) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NP>), dim3((unsigned)tiles), dim3(2 * BM), lds, st, a);
+    VFM_LAUNCH((conv3x3_kernel<BM, BN, NP>), dim3((unsigned)tiles), dim3(2 * BM), lds, st, a);
     return launch_status();
 }
 
@@ -419,7 +419,7 @@ int launch_dgrad(const float* dz, const float* w, float* dx, int B, int H, int W
                                   (3 * (DG_PX + 2) * (128 + 4) + 9 * 4 * 128) * 4);
         attr = true;
     }
-    hipLaunchKernelGGL((conv3x3_dgrad_small<C>), dim3((W + DG_PX - 1) / DG_PX, H, B), dim3(256), lds, st, dz, w, dx, H, W,
+    VFM_LAUNCH((conv3x3_dgrad_small<C>), dim3((W + DG_PX - 1) / DG_PX, H, B), dim3(256), lds, st, dz, w, dx, H, W,
                        K);
     return launch_status();
 }

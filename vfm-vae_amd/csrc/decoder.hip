@@ -220,10 +220,10 @@ int dw_launch(DwArgs& a, int mode, const void* dy, float* partial, hipStream_t s
     const size_t red = sizeof(float) * 4 * a.ppw * (K * K + 1);
     if (mode == 0) {
         const long long blocks = (long long)a.tilesX * a.tilesY * a.planeGroups;
-        hipLaunchKernelGGL((dw_fwd<T, K>), dim3((unsigned)blocks), dim3(NT), lds, st, a);
+        VFM_LAUNCH((dw_fwd<T, K>), dim3((unsigned)blocks), dim3(NT), lds, st, a);
     } else {
         const long long blocks = (long long)a.tilesX * a.planeGroups;
-        hipLaunchKernelGGL((dw_bwd_w<T, K>), dim3((unsigned)blocks), dim3(NT), lds > red ? lds : red, st, a, dy,
+        VFM_LAUNCH((dw_bwd_w<T, K>), dim3((unsigned)blocks), dim3(NT), lds > red ? lds : red, st, a, dy,
                            partial);
     }
     return launch_status();
@@ -528,8 +528,8 @@ int dwr_launch(DwRowArgs& a, int K, int mode, hipStream_t st) {
     const dim3 grid((unsigned)((waves + 3) / 4));
 #define DWR_CASE(KK)                                                                   \
     case KK:                                                                           \
-        if (mode == 0) hipLaunchKernelGGL((dwr_fwd<T, KK>), grid, dim3(NT), 0, st, a); \
-        else hipLaunchKernelGGL((dwr_bwd_w<T, KK>), grid, dim3(NT), 0, st, a);         \
+        if (mode == 0) VFM_LAUNCH((dwr_fwd<T, KK>), grid, dim3(NT), 0, st, a); \
+        else VFM_LAUNCH((dwr_bwd_w<T, KK>), grid, dim3(NT), 0, st, a);         \
         break;
     switch (K) {
         DWR_CASE(3)
@@ -1321,8 +1321,8 @@ template <class T, int R>
 int blur_launch_r(BlurArgs& a, int mode, const void* dout, void* dx, const dim3& g, hipStream_t st) {
 #define BLUR_CASE(KK)                                                                        \
     case KK:                                                                                 \
-        if (mode == 0) hipLaunchKernelGGL((blur_fwd<T, R, KK>), g, dim3(NT), 0, st, a);      \
-        else hipLaunchKernelGGL((blur_bwd<T, R, KK>), g, dim3(NT), 0, st, a, dout, dx);      \
+        if (mode == 0) VFM_LAUNCH((blur_fwd<T, R, KK>), g, dim3(NT), 0, st, a);      \
+        else VFM_LAUNCH((blur_bwd<T, R, KK>), g, dim3(NT), 0, st, a, dout, dx);      \
         break;
     switch (a.K) {
         BLUR_CASE(1) BLUR_CASE(2) BLUR_CASE(3) BLUR_CASE(4) BLUR_CASE(5) BLUR_CASE(6) BLUR_CASE(7) BLUR_CASE(8)
@@ -1386,7 +1386,7 @@ __global__ __launch_bounds__(256) void colsum2(const float* __restrict__ a, cons
 extern "C" int vfm_colsum2_f32(const float* a, const float* b, const float* scale_a, float* out_a, float* out_b,
                                int rows, int cols, void* stream) {
     if (rows <= 0 || cols <= 0 || (!out_a && !out_b) || (out_a && !a) || (out_b && !b)) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(colsum2, dim3((cols + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, b,
+    VFM_LAUNCH(colsum2, dim3((cols + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, b,
                        scale_a, out_a, out_b, rows, cols);
     return launch_status();
 }
@@ -1395,7 +1395,7 @@ extern "C" int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float*
                                          void* stream) {
     if (!partial || rows <= 0 || C <= 0 || KK <= 0 || (!dw && !db)) return VFM_ERR_ARGS;
     const long long n = (long long)C * (KK + 1);
-    hipLaunchKernelGGL(dw_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+    VFM_LAUNCH(dw_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), partial, dw, db, rows, C, KK);
     return launch_status();
 }
@@ -1475,7 +1475,7 @@ extern "C" int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* par
 
 template <class TI, class TO>
 static int gn_fwd_launch(GnArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((gn_fwd<TI, TO>), dim3(a.B * a.G), dim3(NT), 0, st, a);
+    VFM_LAUNCH((gn_fwd<TI, TO>), dim3(a.B * a.G), dim3(NT), 0, st, a);
     return launch_status();
 }
 
@@ -1500,7 +1500,7 @@ extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b,
 
 template <class TX, class TY>
 static int gn_bwd_launch(GnBwdArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((gn_bwd<TX, TY>), dim3(a.B * a.G), dim3(NT), 0, st, a);
+    VFM_LAUNCH((gn_bwd<TX, TY>), dim3(a.B * a.G), dim3(NT), 0, st, a);
     return launch_status();
 }
 
@@ -1531,9 +1531,9 @@ extern "C" int vfm_scale_bias_gelu_fwd(const void* h, const float* scale, const 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid((a.R + 3) / 4);
     switch (dtype) {
-    case VFM_F32: hipLaunchKernelGGL((gelu_fwd<float>), grid, dim3(NT), 0, st, a); break;
-    case VFM_BF16: hipLaunchKernelGGL((gelu_fwd<__hip_bfloat16>), grid, dim3(NT), 0, st, a); break;
-    case VFM_F16: hipLaunchKernelGGL((gelu_fwd<__half>), grid, dim3(NT), 0, st, a); break;
+    case VFM_F32: VFM_LAUNCH((gelu_fwd<float>), grid, dim3(NT), 0, st, a); break;
+    case VFM_BF16: VFM_LAUNCH((gelu_fwd<__hip_bfloat16>), grid, dim3(NT), 0, st, a); break;
+    case VFM_F16: VFM_LAUNCH((gelu_fwd<__half>), grid, dim3(NT), 0, st, a); break;
     default: return VFM_ERR_ARGS;
     }
     return launch_status();
@@ -1549,20 +1549,20 @@ extern "C" int vfm_scale_bias_gelu_bwd(const void* h, const void* dg, const floa
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid((a.R + 3) / 4);
     switch (dtype) {
-    case VFM_F32: hipLaunchKernelGGL((gelu_bwd<float>), grid, dim3(NT), 0, st, a); break;
-    case VFM_BF16: hipLaunchKernelGGL((gelu_bwd<__hip_bfloat16>), grid, dim3(NT), 0, st, a); break;
-    case VFM_F16: hipLaunchKernelGGL((gelu_bwd<__half>), grid, dim3(NT), 0, st, a); break;
+    case VFM_F32: VFM_LAUNCH((gelu_bwd<float>), grid, dim3(NT), 0, st, a); break;
+    case VFM_BF16: VFM_LAUNCH((gelu_bwd<__hip_bfloat16>), grid, dim3(NT), 0, st, a); break;
+    case VFM_F16: VFM_LAUNCH((gelu_bwd<__half>), grid, dim3(NT), 0, st, a); break;
     default: return VFM_ERR_ARGS;
     }
     return launch_status();
 }
 
 #define LSR_DISPATCH(KERNEL)                                                                       \
-    if (dtype_y == VFM_F32 && dtype_x == VFM_F32) hipLaunchKernelGGL((KERNEL<float, float>), grid, dim3(NT), 0, st, a); \
-    else if (dtype_y == VFM_BF16 && dtype_x == VFM_BF16) hipLaunchKernelGGL((KERNEL<__hip_bfloat16, __hip_bfloat16>), grid, dim3(NT), 0, st, a); \
-    else if (dtype_y == VFM_BF16 && dtype_x == VFM_F32) hipLaunchKernelGGL((KERNEL<__hip_bfloat16, float>), grid, dim3(NT), 0, st, a); \
-    else if (dtype_y == VFM_F16 && dtype_x == VFM_F16) hipLaunchKernelGGL((KERNEL<__half, __half>), grid, dim3(NT), 0, st, a); \
-    else if (dtype_y == VFM_F16 && dtype_x == VFM_F32) hipLaunchKernelGGL((KERNEL<__half, float>), grid, dim3(NT), 0, st, a); \
+    if (dtype_y == VFM_F32 && dtype_x == VFM_F32) VFM_LAUNCH((KERNEL<float, float>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_BF16 && dtype_x == VFM_BF16) VFM_LAUNCH((KERNEL<__hip_bfloat16, __hip_bfloat16>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_BF16 && dtype_x == VFM_F32) VFM_LAUNCH((KERNEL<__hip_bfloat16, float>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_F16 && dtype_x == VFM_F16) VFM_LAUNCH((KERNEL<__half, __half>), grid, dim3(NT), 0, st, a); \
+    else if (dtype_y == VFM_F16 && dtype_x == VFM_F32) VFM_LAUNCH((KERNEL<__half, float>), grid, dim3(NT), 0, st, a); \
     else return VFM_ERR_ARGS;
 
 extern "C" int vfm_layer_scale_residual_fwd(const void* y, const float* bias, const float* gamma, const void* x_in,

@@ -40,11 +40,11 @@ extern "C" int vfm_shift2d(const void* x, void* y, const long long* tx, const lo
     hipStream_t st = (hipStream_t)stream;
     switch (dtype) {
     case VFM_F32:
-        hipLaunchKernelGGL(shift2d_kernel<float>, grid, dim3(256), 0, st, (const float*)x, (float*)y, tx, ty, C, H, W,
+        VFM_LAUNCH(shift2d_kernel<float>, grid, dim3(256), 0, st, (const float*)x, (float*)y, tx, ty, C, H, W,
                            sign);
         break;
     case VFM_BF16:
-        hipLaunchKernelGGL(shift2d_kernel<__hip_bfloat16>, grid, dim3(256), 0, st, (const __hip_bfloat16*)x,
+        VFM_LAUNCH(shift2d_kernel<__hip_bfloat16>, grid, dim3(256), 0, st, (const __hip_bfloat16*)x,
                            (__hip_bfloat16*)y, tx, ty, C, H, W, sign);
         break;
     default:

@@ -168,8 +168,8 @@ template <int K>
 int dwm_launch(DwmArgs& a, hipStream_t st) {
     const long long blocks = (a.units + WAVES - 1) / WAVES;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    if (a.XW == 64) hipLaunchKernelGGL((dwm_fwd<K, 64>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
-    else hipLaunchKernelGGL((dwm_fwd<K, 16>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+    if (a.XW == 64) VFM_LAUNCH((dwm_fwd<K, 64>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+    else VFM_LAUNCH((dwm_fwd<K, 16>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
     return launch_status();
 }
 
@@ -318,8 +318,8 @@ int dwm_bw_launch(DwmBwArgs& a, int XW, hipStream_t st) {
     const long long waves = (long long)a.C * a.tiles;
     const long long blocks = (waves + 1) / 2;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    if (XW == 64) hipLaunchKernelGGL((dwm_bwd_w<K, 64>), dim3((unsigned)blocks), dim3(128), 0, st, a);
-    else hipLaunchKernelGGL((dwm_bwd_w<K, 16>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+    if (XW == 64) VFM_LAUNCH((dwm_bwd_w<K, 64>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+    else VFM_LAUNCH((dwm_bwd_w<K, 16>), dim3((unsigned)blocks), dim3(128), 0, st, a);
     return launch_status();
 }
 

@@ -154,9 +154,9 @@ template <class T, int UP, int DOWN>
 int launch_ud(FlreluArgs& a, int mode, size_t lds, hipStream_t st) {
     long long blocks = (long long)a.tilesX * a.tilesY * a.N * a.C;
     dim3 g((unsigned)blocks), b(NT);
-    if (mode == 0) hipLaunchKernelGGL((flrelu_fused<T, UP, DOWN, 0>), g, b, lds, st, a);
-    else if (mode == 1) hipLaunchKernelGGL((flrelu_fused<T, UP, DOWN, 1>), g, b, lds, st, a);
-    else hipLaunchKernelGGL((flrelu_fused<T, UP, DOWN, 2>), g, b, lds, st, a);
+    if (mode == 0) VFM_LAUNCH((flrelu_fused<T, UP, DOWN, 0>), g, b, lds, st, a);
+    else if (mode == 1) VFM_LAUNCH((flrelu_fused<T, UP, DOWN, 1>), g, b, lds, st, a);
+    else VFM_LAUNCH((flrelu_fused<T, UP, DOWN, 2>), g, b, lds, st, a);
     return launch_status();
 }
 
@@ -249,9 +249,9 @@ int run_act(FlActArgs& a, int mode, hipStream_t st) {
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
     dim3 g((unsigned)blocks), b(NT);
-    if (mode == 0) hipLaunchKernelGGL((flrelu_act<T, 0>), g, b, 0, st, a, gridW, gridH);
-    else if (mode == 1) hipLaunchKernelGGL((flrelu_act<T, 1>), g, b, 0, st, a, gridW, gridH);
-    else hipLaunchKernelGGL((flrelu_act<T, 2>), g, b, 0, st, a, gridW, gridH);
+    if (mode == 0) VFM_LAUNCH((flrelu_act<T, 0>), g, b, 0, st, a, gridW, gridH);
+    else if (mode == 1) VFM_LAUNCH((flrelu_act<T, 1>), g, b, 0, st, a, gridW, gridH);
+    else VFM_LAUNCH((flrelu_act<T, 2>), g, b, 0, st, a, gridW, gridH);
     return launch_status();
 }
 

@@ -295,7 +295,7 @@ int launch(const GemmArgs& a, int batch, hipStream_t st) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm_kernel<AK, BKC, NP, OUTF32>), dim3(tiles, batch * a.splits), dim3(THREADS), lds, st, a);
+    VFM_LAUNCH((gemm_kernel<AK, BKC, NP, OUTF32>), dim3(tiles, batch * a.splits), dim3(THREADS), lds, st, a);
     return launch_status();
 }
 
@@ -355,7 +355,7 @@ extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias
     const int J = reduce_batch ? batch * splits : splits;
     const int zc = reduce_batch ? 1 : batch;
     dim3 grid((unsigned)((MN + 255) / 256), zc);
-    if (of32) hipLaunchKernelGGL(gemm_reduce_kernel<true>, grid, dim3(256), 0, st, a, J, zc);
-    else      hipLaunchKernelGGL(gemm_reduce_kernel<false>, grid, dim3(256), 0, st, a, J, zc);
+    if (of32) VFM_LAUNCH(gemm_reduce_kernel<true>, grid, dim3(256), 0, st, a, J, zc);
+    else      VFM_LAUNCH(gemm_reduce_kernel<false>, grid, dim3(256), 0, st, a, J, zc);
     return launch_status();
 }

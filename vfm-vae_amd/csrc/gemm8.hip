@@ -618,7 +618,7 @@ void launch8d(const G8Args& a, int nwg, int ny, hipStream_t st) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm8_kernel<AK, BKC, OUTF32, DEEP, EPI>), dim3(nwg, ny), dim3(THREADS), 2 * BUF, st, a);
+    VFM_LAUNCH((gemm8_kernel<AK, BKC, OUTF32, DEEP, EPI>), dim3(nwg, ny), dim3(THREADS), 2 * BUF, st, a);
 }
 
 template <bool AK, bool BKC, bool OUTF32, int EPI = 0>
@@ -634,7 +634,7 @@ int launch8(const G8Args& a, int batch, hipStream_t st) {
     launch8k<AK, BKC, OUTF32>(a, nwg, zo * a.S, st);
     if (a.ws) {
         const long long MN = (long long)a.M * a.N;
-        hipLaunchKernelGGL(gemm8_reduce<OUTF32>, dim3((unsigned)((MN + 255) / 256), zo), dim3(256), 0, st, a);
+        VFM_LAUNCH(gemm8_reduce<OUTF32>, dim3((unsigned)((MN + 255) / 256), zo), dim3(256), 0, st, a);
     }
     return launch_status();
 }
@@ -688,10 +688,10 @@ extern "C" int vfm_split_f32(const float* src, void* dst, int R, int K, long lon
     const long long total4 = ((long long)R * K) / 4;
     dim3 grid((unsigned)((total4 + 255) / 256), batch);
     if (precision == VFM_F32)
-        hipLaunchKernelGGL(split_f32_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, src, (__hip_bfloat16*)dst, R, K,
+        VFM_LAUNCH(split_f32_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, src, (__hip_bfloat16*)dst, R, K,
                            ld, sb, db, kcont);
     else
-        hipLaunchKernelGGL(split_f32_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, src, (__hip_bfloat16*)dst, R, K,
+        VFM_LAUNCH(split_f32_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, src, (__hip_bfloat16*)dst, R, K,
                            ld, sb, db, kcont);
     return launch_status();
 }

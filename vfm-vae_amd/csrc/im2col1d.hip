@@ -62,7 +62,7 @@ extern "C" int vfm_im2col1d_f32(const float* x, float* cols, int B, int C, int L
     const int Lo = L + 2 * p - k + 1;
     if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
     const long long n = (long long)B * C * k * Lo;
-    hipLaunchKernelGGL(im2col1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, C, L, k, p, Lo,
+    VFM_LAUNCH(im2col1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, C, L, k, p, Lo,
                        circular ? 1 : 0, n);
     return launch_status();
 }
@@ -74,7 +74,7 @@ extern "C" int vfm_col2im1d_f32(const float* dcols, float* dx, int B, int C, int
     const int Lo = L + 2 * p - k + 1;
     if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
     const long long n = (long long)B * C * L;
-    hipLaunchKernelGGL(col2im1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, C, L, k, p, Lo,
+    VFM_LAUNCH(col2im1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, C, L, k, p, Lo,
                        circular ? 1 : 0, n);
     return launch_status();
 }

@@ -224,7 +224,7 @@ extern "C" int vfm_lpips_head_fwd(const float* f0, const float* f1, const float*
     if (!f0 || !f1 || !w || !r || !n0 || !n1) return VFM_ERR_ARGS;
     if (grid_of(total) <= 0 || (long long)C * HW * B > (1ll << 40)) return VFM_ERR_ARGS;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(lpips_head_fwd, dim3(grid_of(total)), dim3(LP_NT), 0, st, f0, f1, w, r, n0, n1, C, HW, total);
+    VFM_LAUNCH(lpips_head_fwd, dim3(grid_of(total)), dim3(LP_NT), 0, st, f0, f1, w, r, n0, n1, C, HW, total);
     return (int)hipGetLastError();
 }
 
@@ -235,7 +235,7 @@ extern "C" int vfm_lpips_head_bwd(const float* f0, const float* f1, const float*
     if (total == 0 || (!g0 && !g1)) return VFM_OK;
     if (!f0 || !f1 || !w || !n0 || !n1 || !gs) return VFM_ERR_ARGS;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(lpips_head_bwd, dim3(grid_of(total)), dim3(LP_NT), 0, st, f0, f1, w, n0, n1, gs, g0, g1, C, HW,
+    VFM_LAUNCH(lpips_head_bwd, dim3(grid_of(total)), dim3(LP_NT), 0, st, f0, f1, w, n0, n1, gs, g0, g1, C, HW,
                        total);
     return (int)hipGetLastError();
 }
@@ -251,10 +251,10 @@ extern "C" int vfm_lpips_head_fwd_nhwc(const float* f0, const float* f1, const f
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 g(nhwc_grid(total)), b(LP_NT);
     switch (C) {
-        case 64: hipLaunchKernelGGL(lpips_head_fwd_nhwc<1>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
-        case 128: hipLaunchKernelGGL(lpips_head_fwd_nhwc<2>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
-        case 256: hipLaunchKernelGGL(lpips_head_fwd_nhwc<4>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
-        default: hipLaunchKernelGGL(lpips_head_fwd_nhwc<8>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        case 64: VFM_LAUNCH(lpips_head_fwd_nhwc<1>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        case 128: VFM_LAUNCH(lpips_head_fwd_nhwc<2>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        case 256: VFM_LAUNCH(lpips_head_fwd_nhwc<4>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
+        default: VFM_LAUNCH(lpips_head_fwd_nhwc<8>, g, b, 0, st, f0, f1, w, r, n0, n1, total); break;
     }
     return (int)hipGetLastError();
 }
@@ -271,10 +271,10 @@ extern "C" int vfm_lpips_head_bwd_nhwc(const float* f0, const float* f1, const f
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 g(nhwc_grid(total)), b(LP_NT);
     switch (C) {
-        case 64: hipLaunchKernelGGL(lpips_head_bwd_nhwc<1>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
-        case 128: hipLaunchKernelGGL(lpips_head_bwd_nhwc<2>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
-        case 256: hipLaunchKernelGGL(lpips_head_bwd_nhwc<4>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
-        default: hipLaunchKernelGGL(lpips_head_bwd_nhwc<8>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        case 64: VFM_LAUNCH(lpips_head_bwd_nhwc<1>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        case 128: VFM_LAUNCH(lpips_head_bwd_nhwc<2>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        case 256: VFM_LAUNCH(lpips_head_bwd_nhwc<4>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
+        default: VFM_LAUNCH(lpips_head_bwd_nhwc<8>, g, b, 0, st, f0, f1, w, n0, n1, gs, g0, g1, HW, total); break;
     }
     return (int)hipGetLastError();
 }

@@ -385,8 +385,8 @@ extern "C" int vfm_im2col_nhwc_f32(const float* x, float* A, long long ldA, int 
     const long long blocks = (total + 255) / 256;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;
-    if (v4) hipLaunchKernelGGL(im2col_nhwc<true>, dim3((unsigned)blocks), dim3(256), 0, st, x, A, g, total);
-    else hipLaunchKernelGGL(im2col_nhwc<false>, dim3((unsigned)blocks), dim3(256), 0, st, x, A, g, total);
+    if (v4) VFM_LAUNCH(im2col_nhwc<true>, dim3((unsigned)blocks), dim3(256), 0, st, x, A, g, total);
+    else VFM_LAUNCH(im2col_nhwc<false>, dim3((unsigned)blocks), dim3(256), 0, st, x, A, g, total);
     return launch_status();
 }
 
@@ -404,8 +404,8 @@ extern "C" int vfm_col2im_nhwc_f32(const float* dA, long long ldA, const float* 
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;
     const float* a = (dy1 && w1) ? nullptr : dA;
-    if (v4) hipLaunchKernelGGL(col2im_nhwc<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, dy1, w1, dX, g, total);
-    else hipLaunchKernelGGL(col2im_nhwc<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, dy1, w1, dX, g, total);
+    if (v4) VFM_LAUNCH(col2im_nhwc<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, dy1, w1, dX, g, total);
+    else VFM_LAUNCH(col2im_nhwc<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, dy1, w1, dX, g, total);
     return launch_status();
 }
 
@@ -413,7 +413,7 @@ extern "C" int vfm_rowdot_f32(const float* A, long long ldA, const float* w, con
                               void* stream) {
     if (!A || !w || !y || M <= 0 || K <= 0 || ldA < K) return VFM_ERR_ARGS;
     if (K % 4 || ldA % 4 || ((uintptr_t)A | (uintptr_t)w) % 16) return VFM_NO_KERNEL;
-    hipLaunchKernelGGL(rowdot, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, A, ldA, w, bias, y, M,
+    VFM_LAUNCH(rowdot, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, A, ldA, w, bias, y, M,
                        K);
     return launch_status();
 }
@@ -434,7 +434,7 @@ extern "C" int vfm_coldot_f32(const float* A, long long ldA, const float* v, flo
     if (!A || !v || !part || M <= 0 || K <= 0 || S <= 0 || S > 65535 || ldA < K) return VFM_ERR_ARGS;
     if (K % 4 || ldA % 4 || ((uintptr_t)A | (uintptr_t)part) % 16) return VFM_NO_KERNEL;
     const int span = (M + S - 1) / S;
-    hipLaunchKernelGGL(coldot, dim3((unsigned)((K + 1023) / 1024), S), dim3(256), 0, (hipStream_t)stream, A, ldA, v,
+    VFM_LAUNCH(coldot, dim3((unsigned)((K + 1023) / 1024), S), dim3(256), 0, (hipStream_t)stream, A, ldA, v,
                        part, M, K, span);
     return launch_status();
 }
@@ -458,16 +458,16 @@ extern "C" int vfm_bnl_lrelu_fwd(const float* x, const float* w, const float* b,
     a.x = x; a.w = w; a.b = b; a.mean = mean; a.rstd = rstd; a.out = y; a.part = ws; a.slope = slope;
     hipStream_t st = (hipStream_t)stream;
     const dim3 rg(a.chunks, G), fg((C + 255) / 256);
-    hipLaunchKernelGGL(bn_reduce<0>, rg, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_finalize<0>, fg, dim3(256), 0, st, a, mean, (float*)nullptr, (float*)nullptr,
+    VFM_LAUNCH(bn_reduce<0>, rg, dim3(256), 0, st, a);
+    VFM_LAUNCH(bn_finalize<0>, fg, dim3(256), 0, st, a, mean, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, eps);
-    hipLaunchKernelGGL(bn_reduce<1>, rg, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_finalize<1>, fg, dim3(256), 0, st, a, rstd, (float*)nullptr, (float*)nullptr,
+    VFM_LAUNCH(bn_reduce<1>, rg, dim3(256), 0, st, a);
+    VFM_LAUNCH(bn_finalize<1>, fg, dim3(256), 0, st, a, rstd, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, eps);
     const long long total4 = (long long)B * P * C / 4;
     const long long blocks = (total4 + 255) / 256;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(bn_apply<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, (const float*)nullptr,
+    VFM_LAUNCH(bn_apply<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, (const float*)nullptr,
                        (const float*)nullptr, total4);
     return launch_status();
 }
@@ -486,12 +486,12 @@ extern "C" int vfm_bnl_lrelu_bwd(const float* x, const float* dy, const float* w
     float* c0 = ws + (long long)G * a.chunks * 2 * C;
     float* c1 = c0 + (long long)G * C;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(bn_reduce<2>, dim3(a.chunks, G), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_finalize<2>, dim3((C + 255) / 256), dim3(256), 0, st, a, c0, c1, dw, db, 0.f);
+    VFM_LAUNCH(bn_reduce<2>, dim3(a.chunks, G), dim3(256), 0, st, a);
+    VFM_LAUNCH(bn_finalize<2>, dim3((C + 255) / 256), dim3(256), 0, st, a, c0, c1, dw, db, 0.f);
     const long long total4 = (long long)B * P * C / 4;
     const long long blocks = (total4 + 255) / 256;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(bn_apply<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, (const float*)c0,
+    VFM_LAUNCH(bn_apply<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, (const float*)c0,
                        (const float*)c1, total4);
     return launch_status();
 }
@@ -503,7 +503,7 @@ extern "C" int vfm_bnl1d_lrelu_fwd(const float* x, const float* w, const float* 
     if (!x || !y || !mean || !rstd || B <= 0 || C <= 0 || L <= 0 || G <= 0 || B % G || C > 65535 || G > 65535)
         return VFM_ERR_ARGS;
     if ((long long)(B / G) * L > 0x7fffffffLL) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(bn1d_fwd, dim3(C, G), dim3(256), 0, (hipStream_t)stream, x, w, b, y, mean, rstd, C, L, B / G,
+    VFM_LAUNCH(bn1d_fwd, dim3(C, G), dim3(256), 0, (hipStream_t)stream, x, w, b, y, mean, rstd, C, L, B / G,
                        eps, slope);
     return launch_status();
 }
@@ -514,7 +514,7 @@ extern "C" int vfm_bnl1d_lrelu_bwd(const float* x, const float* dy, const float*
     if (!x || !dy || !dx || !part || !mean || !rstd || B <= 0 || C <= 0 || L <= 0 || G <= 0 || B % G ||
         C > 65535 || G > 65535)
         return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(bn1d_bwd, dim3(C, G), dim3(256), 0, (hipStream_t)stream, x, dy, w, b, mean, rstd, dx, part, C,
+    VFM_LAUNCH(bn1d_bwd, dim3(C, G), dim3(256), 0, (hipStream_t)stream, x, dy, w, b, mean, rstd, dx, part, C,
                        L, B / G, slope);
     return launch_status();
 }

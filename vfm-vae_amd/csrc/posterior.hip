@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void posterior_bwd(const float* __restrict__ p
 extern "C" int vfm_posterior_fwd(const float* params, const float* eps, float* z, float* kl, int B, int C, long long P,
                                  void* stream) {
     if (!params || B <= 0 || B > 0x7fffffff || C <= 0 || P <= 0 || (!z && !kl)) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(posterior_fwd, dim3(B), dim3(256), 0, (hipStream_t)stream, params, eps, z, kl, C, P);
+    VFM_LAUNCH(posterior_fwd, dim3(B), dim3(256), 0, (hipStream_t)stream, params, eps, z, kl, C, P);
     return launch_status();
 }
 
@@ -74,7 +74,7 @@ extern "C" int vfm_posterior_bwd(const float* params, const float* eps, const fl
     const long long total = (long long)B * C * P;
     const long long blocks = (total + 255) / 256;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(posterior_bwd, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, params, eps, dz, dkl,
+    VFM_LAUNCH(posterior_bwd, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, params, eps, dz, dkl,
                        dparams, C, P, total);
     return launch_status();
 }

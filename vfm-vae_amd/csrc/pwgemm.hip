@@ -282,7 +282,7 @@ int launch(const PwArgs& a, int B, hipStream_t st) {
                                   K * 256 + 8 * 2048);
         attr = true;
     }
-    hipLaunchKernelGGL((pw_gemm_gelu<MODE, K>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
+    VFM_LAUNCH((pw_gemm_gelu<MODE, K>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
     return launch_status();
 }
 
@@ -493,7 +493,7 @@ void launch_mlp(const MlpArgs& a, int B, size_t lds, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)mlp_fwd<C, SAVE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((mlp_fwd<C, SAVE>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
+    VFM_LAUNCH((mlp_fwd<C, SAVE>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
 }
 }  // namespace
 

@@ -123,7 +123,7 @@ extern "C" int vfm_channel_rms_norm_fwd(const float* x, const float* gamma, floa
     int tiles;
     long long blocks;
     if (!x || !gamma || !y || !crms_grid(B, C, P, tiles, blocks)) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(crms_fwd, dim3((unsigned)blocks), dim3(THREADS), 0, (hipStream_t)stream, x, gamma, y, rinv, C,
+    VFM_LAUNCH(crms_fwd, dim3((unsigned)blocks), dim3(THREADS), 0, (hipStream_t)stream, x, gamma, y, rinv, C,
                        P, tiles, scale);
     return vfm::launch_status();
 }
@@ -137,9 +137,9 @@ extern "C" int vfm_channel_rms_norm_bwd(const float* x, const float* gamma, cons
     if (!x || !gamma || !rinv || !dy || !dx || !crms_grid(B, C, P, tiles, blocks)) return VFM_ERR_ARGS;
     if ((gpart == nullptr) != (dgamma == nullptr)) return VFM_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(crms_bwd, dim3((unsigned)blocks), dim3(THREADS), 0, st, x, gamma, rinv, dy, dx, gpart, C, P,
+    VFM_LAUNCH(crms_bwd, dim3((unsigned)blocks), dim3(THREADS), 0, st, x, gamma, rinv, dy, dx, gpart, C, P,
                        tiles, scale);
     if (dgamma)
-        hipLaunchKernelGGL(crms_gamma, dim3((C + 255) / 256), dim3(256), 0, st, gpart, dgamma, C, (int)blocks, scale);
+        VFM_LAUNCH(crms_gamma, dim3((C + 255) / 256), dim3(256), 0, st, gpart, dgamma, C, (int)blocks, scale);
     return vfm::launch_status();
 }

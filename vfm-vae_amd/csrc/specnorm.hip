@@ -151,11 +151,11 @@ extern "C" int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_cop
     float* tpart = r + O;
     float* rpart = tpart + tb;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(sn_wtu, dim3(tb), dim3(THREADS), 0, st, W, u, t, tpart, O, I);
-    hipLaunchKernelGGL(sn_wv, dim3(rb), dim3(THREADS), 0, st, W, t, tpart, tb, v, v_copy, r, rpart, O, I, eps);
+    VFM_LAUNCH(sn_wtu, dim3(tb), dim3(THREADS), 0, st, W, u, t, tpart, O, I);
+    VFM_LAUNCH(sn_wv, dim3(rb), dim3(THREADS), 0, st, W, t, tpart, tb, v, v_copy, r, rpart, O, I, eps);
     const long long n = (long long)O * I;
     const int sb = (int)std::min<long long>(SCALE_BLOCKS, (n + THREADS - 1) / THREADS);
-    hipLaunchKernelGGL(sn_scale, dim3(sb), dim3(THREADS), 0, st, W, r, rpart, rb, u, u_copy, sigma, Wsn, O, n, eps);
+    VFM_LAUNCH(sn_scale, dim3(sb), dim3(THREADS), 0, st, W, r, rpart, rb, u, u_copy, sigma, Wsn, O, n, eps);
     return launch_status();
 }
 
@@ -166,7 +166,7 @@ extern "C" int vfm_specnorm_bwd(const float* g, const float* W, const float* u, 
     const long long n = (long long)O * I;
     const int nb = (int)std::min<long long>(SCALE_BLOCKS, (n + THREADS - 1) / THREADS);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(sn_gw, dim3(nb), dim3(THREADS), 0, st, g, W, ws, n);
-    hipLaunchKernelGGL(sn_dw, dim3(nb), dim3(THREADS), 0, st, g, u, v, sigma, ws, nb, dW, I, n);
+    VFM_LAUNCH(sn_gw, dim3(nb), dim3(THREADS), 0, st, g, W, ws, n);
+    VFM_LAUNCH(sn_dw, dim3(nb), dim3(THREADS), 0, st, g, u, v, sigma, ws, nb, dW, I, n);
     return launch_status();
 }

@@ -284,7 +284,7 @@ template <int L>
 int launch(StyleArgs& a, long long blocks, hipStream_t st) {
     if (blocks <= 0) return 0;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    hipLaunchKernelGGL(style_kernel<L>, dim3((unsigned)blocks), dim3(THREADS), 0, st, a);
+    VFM_LAUNCH(style_kernel<L>, dim3((unsigned)blocks), dim3(THREADS), 0, st, a);
     return launch_status();
 }
 

@@ -175,7 +175,7 @@ int fwd_launch(const void* x, const float* wm, const float* bias, float* y, int 
     int PL = 8;
     while (PL < 256 && PL < P / 8) PL *= 2;
     dim3 grid((unsigned)((P / 8 + PL - 1) / PL), B);
-#define VFM_TF(OO) hipLaunchKernelGGL((torgb_fwd<T, OO>), grid, dim3(256), 0, st, (const T*)x, wm, bias, y, C, P, PL)
+#define VFM_TF(OO) VFM_LAUNCH((torgb_fwd<T, OO>), grid, dim3(256), 0, st, (const T*)x, wm, bias, y, C, P, PL)
     switch (O) {
     case 1: VFM_TF(1); break;
     case 2: VFM_TF(2); break;
@@ -192,7 +192,7 @@ int bwd_launch(const void* x, const float* dy, const float* wm, void* dx, float*
     const int span = ((P + S - 1) / S + 511) / 512 * 512;
     dim3 grid(S, C / 16, B);
 #define VFM_TB(OO) \
-    hipLaunchKernelGGL((torgb_bwd<T, OO>), grid, dim3(256), 0, st, (const T*)x, dy, wm, (T*)dx, tpart, C, P, span)
+    VFM_LAUNCH((torgb_bwd<T, OO>), grid, dim3(256), 0, st, (const T*)x, dy, wm, (T*)dx, tpart, C, P, span)
     switch (O) {
     case 1: VFM_TB(1); break;
     case 2: VFM_TB(2); break;

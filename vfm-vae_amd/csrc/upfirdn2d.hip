@@ -149,7 +149,7 @@ __global__ __launch_bounds__(NT) void updn_generic(UpfirdnArgs a, long long tota
 template <class T, int UPX, int UPY, int DX, int DY>
 int launch_tile(UpfirdnArgs& a, size_t lds, hipStream_t st) {
     long long blocks = (long long)a.tilesX * a.tilesY * a.N * a.C;
-    hipLaunchKernelGGL((updn_tile<T, UPX, UPY, DX, DY>), dim3((unsigned)blocks), dim3(NT), lds, st, a);
+    VFM_LAUNCH((updn_tile<T, UPX, UPY, DX, DY>), dim3((unsigned)blocks), dim3(NT), lds, st, a);
     return launch_status();
 }
 
@@ -180,7 +180,7 @@ int run(UpfirdnArgs& a, hipStream_t st) {
     const int chan_fastest = (a.xs[1] == 1 && a.C > 1) ? 1 : 0;
     long long blocks = (total + NT - 1) / NT;
     if (blocks > 2048 * 8) blocks = 2048 * 8;
-    hipLaunchKernelGGL((updn_generic<T>), dim3((unsigned)blocks), dim3(NT), 0, st, a, total, chan_fastest);
+    VFM_LAUNCH((updn_generic<T>), dim3((unsigned)blocks), dim3(NT), 0, st, a, total, chan_fastest);
     return launch_status();
 }
 

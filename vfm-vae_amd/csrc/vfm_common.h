@@ -6,6 +6,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
@@ -127,6 +128,16 @@ __device__ __forceinline__ GeluParts gelu_parts(float z) {
     r.zpdf = z * 0.39894228040143268f * e;
     return r;
 }
+// Kernel timing for bench.py's roofline object (vfm_timer_arm, version.hip): while a pair of events
+// is armed, every launch goes through hipExtLaunchKernelGGL, which binds the events to the kernel
+// dispatch itself: `start` to the first launch's start, `stop` to the end of each launch (the last
+// one wins). The elapsed time is the kernels' own duration, not host launch gaps around them.
+struct TimerArm {
+    hipEvent_t start = nullptr, stop = nullptr;
+    int launches = 0;
+};
+TimerArm& timer_arm();
+
 inline int launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? VFM_OK : (int)e;
@@ -143,3 +154,16 @@ inline int launch_status() {
     case VFM_F64: { typedef double T; __VA_ARGS__; break; }                    \
     default: return VFM_ERR_ARGS;                                              \
     }
+
+// Every kernel launch of the library (see TimerArm).
+#define VFM_LAUNCH(kern, grid, block, shm, stream, ...)                                                     \
+    do {                                                                                                    \
+        ::vfm::TimerArm& vfm_ta_ = ::vfm::timer_arm();                                                      \
+        if (vfm_ta_.stop) {                                                                                 \
+            hipExtLaunchKernelGGL(kern, grid, block, shm, stream, vfm_ta_.start, vfm_ta_.stop, 0, __VA_ARGS__); \
+            vfm_ta_.start = nullptr;                                                                        \
+            ++vfm_ta_.launches;                                                                             \
+        } else {                                                                                            \
+            hipLaunchKernelGGL(kern, grid, block, shm, stream, __VA_ARGS__);                               \
+        }                                                                                                   \
+    } while (0)

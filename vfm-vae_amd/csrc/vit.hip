@@ -120,13 +120,13 @@ template <class TD, class TO>
 int ln_dispatch(LnArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.rows + 3) / 4)), blk(256);
     switch (a.D / 256) {
-    case 1: hipLaunchKernelGGL((ln_rows<TD, TO, 1>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((ln_rows<TD, TO, 2>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((ln_rows<TD, TO, 3>), grid, blk, 0, st, a); break;
-    case 4: hipLaunchKernelGGL((ln_rows<TD, TO, 4>), grid, blk, 0, st, a); break;
-    case 5: hipLaunchKernelGGL((ln_rows<TD, TO, 5>), grid, blk, 0, st, a); break;
-    case 6: hipLaunchKernelGGL((ln_rows<TD, TO, 6>), grid, blk, 0, st, a); break;
-    case 8: hipLaunchKernelGGL((ln_rows<TD, TO, 8>), grid, blk, 0, st, a); break;
+    case 1: VFM_LAUNCH((ln_rows<TD, TO, 1>), grid, blk, 0, st, a); break;
+    case 2: VFM_LAUNCH((ln_rows<TD, TO, 2>), grid, blk, 0, st, a); break;
+    case 3: VFM_LAUNCH((ln_rows<TD, TO, 3>), grid, blk, 0, st, a); break;
+    case 4: VFM_LAUNCH((ln_rows<TD, TO, 4>), grid, blk, 0, st, a); break;
+    case 5: VFM_LAUNCH((ln_rows<TD, TO, 5>), grid, blk, 0, st, a); break;
+    case 6: VFM_LAUNCH((ln_rows<TD, TO, 6>), grid, blk, 0, st, a); break;
+    case 8: VFM_LAUNCH((ln_rows<TD, TO, 8>), grid, blk, 0, st, a); break;
     default: return VFM_NO_KERNEL;
     }
     return launch_status();

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(VQ_NT) void codebook_argmax_kernel(const float* __r
 template <int C>
 int vq_launch(const float* f, long long ldf, const float* w, int N, int V, long long* idx, hipStream_t st) {
     const dim3 grid((unsigned)((N + VQ_NT - 1) / VQ_NT));
-    hipLaunchKernelGGL((codebook_argmax_kernel<C>), grid, dim3(VQ_NT), 0, st, f, ldf, w, N, V, idx);
+    VFM_LAUNCH((codebook_argmax_kernel<C>), grid, dim3(VQ_NT), 0, st, f, ldf, w, N, V, idx);
     return vfm::launch_status();
 }
 

@@ -1,13 +1,23 @@
-"""Per-launch HIP-event timing of named kernels inside a timed region.
+"""Per-launch timing of named kernels inside a timed region.
 
 bench.py enables the timer around its timed steps; every native op wrapper
-brackets its launch with a pair of events recorded on the stream the kernel is
-launched on, and reports the launch's ALGORITHMIC bytes (unique inputs +
-outputs + weights at the op boundary) and flops. `dominant_roofline()` picks
-the kernel with the largest total time and returns the bench.py `roofline`
-object (achieved = algorithmic bytes or flops per launch / average launch time).
+opens a region around its launch and reports the launch's ALGORITHMIC bytes
+(unique inputs + outputs + weights at the op boundary) and flops.
+
+Native regions (our kernels) arm a pair of HIP events in the kernel library
+(`vfm_timer_arm`, include/vfmvae.h): the library then launches through
+hipExtLaunchKernelGGL, which binds the events to the kernel dispatch itself, so a
+region's time is the kernels' own duration -- the number rocprofv3's kernel trace
+reports -- and not the host launch gaps that events recorded around a launch also
+enclose when the stream runs dry. Library GEMM regions (hipBLASLt through torch)
+still record events around the call on the launch stream.
+
+`dominant_roofline()` picks the kernel with the largest total time and returns the
+bench.py `roofline` object (achieved = algorithmic bytes or flops per launch /
+average launch time).
 """
 import contextlib
+import ctypes
 import os
 
 import torch
@@ -46,17 +56,69 @@ class _Null:
 _NULL = _Null()
 
 
+class _TorchPair:
+    """Events recorded around a (library) call on the launch stream."""
+
+    def __init__(self):
+        self.s = torch.cuda.Event(enable_timing=True)
+        self.e = torch.cuda.Event(enable_timing=True)
+
+    def ms(self):
+        return self.s.elapsed_time(self.e)
+
+
+class _KernelPair:
+    """Events bound to our kernels' dispatches (vfm_timer_arm); pooled, since a timed region creates
+    one pair per timed launch."""
+    _pool = []
+
+    def __init__(self, lib):
+        self.lib = lib
+        if _KernelPair._pool:
+            self.s, self.e = _KernelPair._pool.pop()
+        else:
+            s, e = ctypes.c_void_p(), ctypes.c_void_p()
+            if lib.vfm_event_create(ctypes.byref(s)) or lib.vfm_event_create(ctypes.byref(e)):
+                raise RuntimeError("vfm_event_create failed")
+            self.s, self.e = s.value, e.value
+        self.launched = False
+
+    def ms(self):
+        if not self.launched:
+            return None
+        out = ctypes.c_float()
+        rc = self.lib.vfm_event_elapsed(self.s, self.e, ctypes.byref(out))
+        _KernelPair._pool.append((self.s, self.e))
+        return float(out.value) if rc == 0 else None
+
+
+def _native():
+    from torch_utils import custom_ops
+    return custom_ops.get_native()
+
+
 @contextlib.contextmanager
-def _timed(name, nbytes, flops, bound):
+def _timed(name, nbytes, flops, bound, native):
+    if native:
+        lib = _native()
+        pair = _KernelPair(lib)
+        lib.vfm_timer_arm(pair.s, pair.e)
+        try:
+            yield
+        finally:
+            pair.launched = lib.vfm_timer_arm(None, None) > 0
+            if not pair.launched:
+                _KernelPair._pool.append((pair.s, pair.e))
+            _records.setdefault(name, []).append((pair, nbytes, flops, bound))
+        return
     st = torch.cuda.current_stream()
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
-    s.record(st)
+    pair = _TorchPair()
+    pair.s.record(st)
     try:
         yield
     finally:
-        e.record(st)
-        _records.setdefault(name, []).append((s, e, nbytes, flops, bound))
+        pair.e.record(st)
+        _records.setdefault(name, []).append((pair, nbytes, flops, bound))
 
 
 @contextlib.contextmanager
@@ -80,9 +142,10 @@ def _mix(c):
     return x ^ (x >> 16)
 
 
-def region(name, nbytes=0, flops=0, bound="hbm"):
-    """Context manager around one native launch; a shared no-op object when timing is off
-    (this is on every launch's host path)."""
+def region(name, nbytes=0, flops=0, bound="hbm", native=True):
+    """Context manager around one launch (native = our kernel library, timed by the kernel dispatch;
+    otherwise events around the call); a shared no-op object when timing is off (this is on every
+    launch's host path)."""
     if not _enabled:
         return _NULL
     c = _counts.get(name, 0)
@@ -91,7 +154,7 @@ def region(name, nbytes=0, flops=0, bound="hbm"):
     # stride aliases with the region's launches per step (every 4th of 10 per step = even ones only)
     if _every > 1 and _mix(c) % _every:
         return _NULL
-    return _timed(name, nbytes, flops, bound)
+    return _timed(name, nbytes, flops, bound, native)
 
 
 def vendor_gemm(tag, M, N, K, z=1, esize=2):
@@ -100,19 +163,24 @@ def vendor_gemm(tag, M, N, K, z=1, esize=2):
     to ours; names start with `vendor_gemm<`."""
     if not _enabled:
         return _NULL
-    return region(f"vendor_gemm<{tag}>", esize * z * (M * K + K * N + M * N), 2.0 * z * M * N * K, "mfma")
+    return region(f"vendor_gemm<{tag}>", esize * z * (M * K + K * N + M * N), 2.0 * z * M * N * K, "mfma",
+                  native=False)
 
 
 def summary():
     torch.cuda.synchronize()
     out = {}
     for name, recs in _records.items():
-        ms = sum(s.elapsed_time(e) for s, e, *_ in recs)
-        n = _counts.get(name, len(recs))
-        scale = n / len(recs)               # every n-th launch timed: totals extrapolated to all launches
-        out[name] = dict(launches=n, timed_launches=len(recs), total_ms=ms * scale,
-                         bytes=sum(r[2] for r in recs) * scale, flops=sum(r[3] for r in recs) * scale,
-                         bound=recs[0][4])
+        timed = [(p.ms(), b, f, bd) for p, b, f, bd in recs]
+        timed = [t for t in timed if t[0] is not None]      # a region that launched nothing has no time
+        if not timed:
+            continue
+        ms = sum(t[0] for t in timed)
+        n = _counts.get(name, len(timed))
+        scale = n / len(timed)              # every n-th launch timed: totals extrapolated to all launches
+        out[name] = dict(launches=n, timed_launches=len(timed), total_ms=ms * scale,
+                         bytes=sum(t[1] for t in timed) * scale, flops=sum(t[2] for t in timed) * scale,
+                         bound=timed[0][3])
     return out
 
 

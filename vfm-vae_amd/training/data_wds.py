@@ -177,6 +177,13 @@ class _WorkerError:
         self.exc = exc
 
 
+class _Leftover:
+    """A worker's last partial batch (fewer than batch_size samples)."""
+
+    def __init__(self, arr, labels):
+        self.arr, self.labels = arr, labels
+
+
 def _batch_worker(ds, rank, world, seed, w, batch_size, out_q, stop):
     """Process entry of WdsWrapper._iterate_processes: worker w's shard stream -> whole batches
     (uint8 [B, 3, R, R] numpy, labels); the same per-worker seeds as the thread workers."""
@@ -192,6 +199,10 @@ def _batch_worker(ds, rank, world, seed, w, batch_size, out_q, stop):
             if len(labels) == batch_size:
                 out_q.put((arr, labels))
                 arr, labels = np.empty([batch_size, 3, R, R], dtype=np.uint8), []
+        if labels and not stop.is_set():
+            # this worker's leftover samples: the parent pools the leftovers of all workers into whole
+            # batches, so only the final remainder of the epoch is dropped (as with threads / wds.batched)
+            out_q.put(_Leftover(arr[:len(labels)].copy(), labels))
     except Exception as e:                            # surfaced in iterate(), not swallowed
         out_q.put(_WorkerError(e))
     finally:
@@ -224,6 +235,7 @@ class WdsWrapper:
         # decode in processes on a GPU host (see the module docstring); threads for the one-epoch
         # shard log (a per-rank file the workers append to) and by request
         self.processes = bool(torch.cuda.is_available() if processes is None else processes)
+        self.worker_poll_s = 5.0             # watchdog period of the process workers (dead-worker check)
 
     def _get_urls(self, path):
         if self.label_type in ("cls2text", "cls2id"):
@@ -366,9 +378,20 @@ class WdsWrapper:
             p.start()
         live = len(procs)
         pin = torch.cuda.is_available()
+        carry_arr, carry_lab = [], []          # pooled leftovers of finished workers
         try:
             while True:
-                item = out_q.get()
+                # watchdog: a worker killed before its finally clause (OOM kill, SIGKILL, a crash in the
+                # decoder) never posts its None sentinel; without this check live never reaches 0 and
+                # the loop waits forever (a normal exit is code 0, after the sentinel)
+                dead = [(i, p.exitcode) for i, p in enumerate(procs) if p.exitcode not in (None, 0)]
+                if dead:
+                    raise RuntimeError(f"WebDataset worker process(es) died without finishing: "
+                                       f"{', '.join(f'worker {i} exit code {c}' for i, c in dead)}")
+                try:
+                    item = out_q.get(timeout=self.worker_poll_s)
+                except queue.Empty:
+                    continue
                 if isinstance(item, _WorkerError):
                     raise RuntimeError("WebDataset worker failed") from item.exc
                 if item is None:
@@ -376,7 +399,17 @@ class WdsWrapper:
                     if live == 0:
                         return
                     continue
-                arr, labels = item
+                if isinstance(item, _Leftover):
+                    carry_arr.append(item.arr)
+                    carry_lab.extend(item.labels)
+                    if len(carry_lab) < batch_size:
+                        continue
+                    pooled = np.concatenate(carry_arr)
+                    arr, labels = pooled[:batch_size], carry_lab[:batch_size]
+                    carry_arr, carry_lab = ([pooled[batch_size:]] if len(carry_lab) > batch_size else []), \
+                        carry_lab[batch_size:]
+                else:
+                    arr, labels = item
                 imgs = torch.from_numpy(arr)
                 if pin:
                     imgs = imgs.pin_memory()

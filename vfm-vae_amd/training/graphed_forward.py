@@ -181,5 +181,16 @@ class _Entry:
         self.graph.replay()
         self.owner.replays += 1
         if self.vfm is not None:
-            self.owner.G.vfm_encoder.last_features = self.vfm
+            # the captured tower outputs are static buffers that the next replay overwrites: hand out
+            # copies, so features offered for one microbatch (VFMEncoder.offer_features keeps one entry
+            # per microbatch) are not replaced by a later microbatch's replay
+            self.owner.G.vfm_encoder.last_features = _clone_tree(self.vfm)
         return self.out
+
+
+def _clone_tree(x):
+    if isinstance(x, torch.Tensor):
+        return x.clone()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_clone_tree(v) for v in x)
+    return x
