@@ -358,6 +358,15 @@ int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int prec
               int kchunk, int reduce_batch, void* stream);
 int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
                                int reduce_batch);  /* -1: too large */
+/* bf16 form of the same contract with one wave per SIMD (csrc/gemm4.hip: 256 x 256 tiles, 4 waves of
+ * 128 x 128, register-staged operand tiles, C stored from the accumulators): the frozen SigLIP2
+ * tower's linears (reference networks/utils/vfms/siglip2_utils.py:120-121, HF SiglipMLP /
+ * SiglipAttention projections under bf16 autocast) and the decoder's bf16 1x1 convolutions
+ * (reference networks/utils/convnext_utils.py:135-138 pwconv1 / pwconv2 under autocast).
+ * bf16 A / B only; K % 64 == 0 (else VFM_NO_KERNEL); no split-K. */
+int vfm_gemm4(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+              int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 /* K-tile staging schedule of vfm_gemm8 / vfm_gemm8_gelu (process-wide A/B switch for microbenchmarks):
  * 1 = half-tile slots restaged two K-tiles ahead, 0 = one K-tile ahead (default). Returns the previous
  * setting. */
