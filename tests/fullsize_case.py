@@ -15,6 +15,7 @@ RECON_OVERRIDES = dict(img_resolution=256, conditional=False, label_type="cls2te
 TRAIN_OVERRIDES = dict(img_resolution=256, conditional=False, label_type="cls2text", num_fp16_res=0)
 TRAIN_GROUPS = ("synthesis", "mapping", "ldm_adapter")      # what the G phase updates (VFM tower frozen)
 R_SEED = 77
+VF_W, KL_W = 3.0, 1e-3        # loss = sum(gen_img R) + sum_i sum(ms_i R_i) + VF_W vf + KL_W kl (terms of similar size)
 HIDDEN_NAMES = ("h0", "h12", "hlast")      # patch_from_layers [0, 12, -1]
 ROW_STRIDE = 16
 IMG_SEED = 2024

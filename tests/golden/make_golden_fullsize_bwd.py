@@ -2,16 +2,16 @@
 
 Runs only in the build container (CPU, fp32): imports /root/reference with the stand-ins of
 tests/golden/ref_stubs (as make_golden_fullsize.py), builds the full f16d32 stage-0 Generator
-(configs/vfm_vae_f16d32_siglip2_stage_0_strong_alignment.yaml G_kwargs, img_resolution 256,
-unconditional, the training path's KL and VF losses on) on the full SigLIP2-L tower, overwrites every
+(configs/vfm_vae_f16d32_siglip2_stage_0_strong_alignment.yaml G_kwargs plus the use_* flags reference
+train.py:76-96 derives from loss_kwargs -- KL and VF losses on -- img_resolution 256, unconditional) on the full SigLIP2-L tower, overwrites every
 weight with tests/det_init.py, and runs one 256^2 image through Generator.forward(validation=True)
 in train mode (reference networks/generator.py:1152-1206; the equivariance draw is off under
 validation) with the posterior noise drawn from the CPU generator seeded 123. The scalar
 
-    loss = sum(gen_img * R) + sum_i sum(ms_i * R_i) + 3 vf_loss + 1e3 kl_loss
+    loss = sum(gen_img * R) + sum_i sum(ms_i * R_i) + 3 vf_loss + 1e-3 kl_loss
 
 (R, R_i: standard normal from a seeded CPU generator, regenerated on the GPU side; the same form as
-tests/golden/make_golden_networks.py's 64-px case) is back-propagated into the trainable groups the
+tests/golden/make_golden_networks.py's 64-px case, with a KL weight that keeps the three terms of similar size) is back-propagated into the trainable groups the
 reference's G phase updates -- synthesis, mapping, ldm_adapter (the VFM tower is frozen; reference
 training/loss.py:721-1001 accumulate_gradients and networks/generator.py set_train_mode). Stored:
 the loss terms, the per-parameter gradient norms and sums, per-group gradient norms, and per-image
@@ -51,8 +51,16 @@ vfm_dir = os.path.join(work, fc.VFM_DIRNAME)
 torch.manual_seed(0)
 SiglipVisionModel(SiglipVisionConfig(**fc.SIGLIP_L_CFG)).save_pretrained(vfm_dir)
 
-g_kwargs = yaml.safe_load(open(os.path.join(REF, "configs", fc.REF_YAML)))["G_kwargs"]
+cfg = yaml.safe_load(open(os.path.join(REF, "configs", fc.REF_YAML)))
+g_kwargs, loss_kwargs = cfg["G_kwargs"], cfg["loss_kwargs"]
 g_kwargs.pop("class_name")
+# the G_kwargs reference train.py:76-96 derives from loss_kwargs for training (KL / VF losses on, adaptive
+# VF weight, equivariance regulariser, multiscale outputs)
+g_kwargs.setdefault("use_kl_loss", loss_kwargs.get("kl_loss_weight", 0.0) > 0.0)
+g_kwargs.setdefault("use_vf_loss", loss_kwargs.get("vf_loss_weight", 0.0) > 0.0)
+g_kwargs.setdefault("use_adaptive_vf_loss", loss_kwargs.get("use_adaptive_vf_loss", False))
+g_kwargs.setdefault("use_equivariance_regularization", loss_kwargs.get("use_equivariance_regularization", False))
+g_kwargs.setdefault("use_multiscale_output", len(loss_kwargs.get("multiscale_block_indices", [])) > 0)
 g_kwargs.update(fc.TRAIN_OVERRIDES, vfm_name=vfm_dir)
 
 from networks.generator import Generator  # noqa: E402
@@ -68,7 +76,8 @@ torch.manual_seed(fc.EPS_SEED)
 out = G(img, ["x"], validation=True)
 R, Rs = fc.loss_weights(out.gen_img.shape, [m.shape for m in out.gen_multiscale_imgs])
 loss = (out.gen_img * R).sum() + sum((m * r).sum() for m, r in zip(out.gen_multiscale_imgs, Rs)) \
-    + 3.0 * out.vf_loss + 1e3 * out.kl_loss
+    + fc.VF_W * out.vf_loss + fc.KL_W * out.kl_loss
+assert float(out.vf_loss) != 0.0 and float(out.kl_loss) != 0.0, "KL / VF losses are off"
 meta["loss"] = float(loss)
 meta["vf_loss"] = float(out.vf_loss)
 meta["kl_loss"] = float(out.kl_loss)

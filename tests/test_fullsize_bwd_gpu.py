@@ -1,7 +1,7 @@
 """Full-size parity of the TRAINING backward on cuda:0 against vectors generated from the reference
 itself (tests/golden/make_golden_fullsize_bwd.py): the f16d32 stage-0 Generator on the full SigLIP2-L
 tower at 256^2, batch 1, KL / VF losses on, posterior noise from the CPU generator as the reference
-draws it, and loss = sum(gen_img R) + sum_i sum(ms_i R_i) + 3 vf + 1e3 kl back-propagated into the
+draws it, and loss = sum(gen_img R) + sum_i sum(ms_i R_i) + 3 vf + 1e-3 kl back-propagated into the
 groups the G phase trains (synthesis, mapping, ldm_adapter; reference networks/generator.py:1152-1206,
 training/loss.py:721-1001). The reference side is fp32 (CPU).
 
@@ -62,7 +62,7 @@ def _run(vfm_dir, meta, precision):
     out = G(img.to(DEV), ["x"], validation=True)
     R, Rs = fc.loss_weights(out.gen_img.shape, [m.shape for m in out.gen_multiscale_imgs])
     loss = (out.gen_img * R.to(DEV)).sum() + sum((m * r.to(DEV)).sum() for m, r in zip(out.gen_multiscale_imgs, Rs)) \
-        + 3.0 * out.vf_loss + 1e3 * out.kl_loss
+        + fc.VF_W * out.vf_loss + fc.KL_W * out.kl_loss
     loss.backward()
     torch.cuda.synchronize()
     return G, out, loss

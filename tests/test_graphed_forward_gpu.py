@@ -94,3 +94,42 @@ def test_graph_runner_passes_grad_mode_through(gen):
     with torch.enable_grad():
         assert not runner.eligible(img, ['x'])
     assert not runner.eligible(img.cpu(), ['x']) or not torch.is_grad_enabled()
+
+
+def test_graph_replay_features_per_microbatch(gen):
+    """Two microbatches in one D phase, both through graph replay: the tower features each one offers for
+    reuse (VFMEncoder.offer_features, one entry per microbatch) must be that microbatch's own -- a later
+    replay overwrites the graph's static output buffers, so the offered features must be copies -- and
+    equal a fresh tower pass of the same image."""
+    from training.graphed_forward import GraphedNoGradForward
+    G = gen
+    enc = G.vfm_encoder
+    prev = enc.reuse_features
+    enc.reuse_features = True
+    try:
+        runner = GraphedNoGradForward(G)
+        imgs = [torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(s)).cuda() for s in (21, 22)]
+        for img in imgs:                         # warm-up + capture (first call of a variant may run eagerly)
+            _graphed(runner, img, 7)
+        enc.clear_features()
+        for img in imgs:                         # the D phase: one replay per microbatch, each offers its own
+            enc.last_features = None
+            _graphed(runner, img, 7)
+            assert enc.last_features is not None
+            enc.offer_features(img, *enc.last_features)
+        assert runner.replays >= 2
+        for img in imgs:
+            tr = enc._reuse[id(img)][2]
+            hit = enc._take(img, tr)
+            assert hit is not None
+            feats, _ = hit
+            enc.reuse_features = False
+            with torch.no_grad():
+                fresh, _ = enc.encode_image(img, tr, tr < 1.0)
+            enc.reuse_features = True
+            for a, b in zip(feats, fresh):
+                d = float((a.float() - b.float()).abs().max())
+                assert d <= 1e-3 * max(1.0, float(b.float().abs().max())), d
+    finally:
+        enc.reuse_features = prev
+        enc.clear_features()

@@ -31,6 +31,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int BM = 256, BN = 256, BK = 64, THREADS = 256;
+#ifndef G4_SCHED
+#define G4_SCHED 1
+#endif
 constexpr int OPB = 256 * BK * 2;          // bytes of one operand tile image (32 KB)
 constexpr int STAGE = 2 * OPB;             // A + B images of one K-tile (64 KB)
 
@@ -76,24 +79,25 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int t,
     }
 }
 
-// Per-thread chunk i (0..7) of an operand tile: global byte offset relative to the K-tile origin and
-// the LDS byte offset inside the operand image. K-contiguous: row (tid >> 3) + 32 i, 16-B chunk tid & 7
-// (rows beyond outer_n clamped: their results are never stored). MN-contiguous: k-row (tid >> 5) + 8 i,
-// chunk tid & 31 of the 256 columns (columns beyond outer_n read chunk 0: outer_n % 8 == 0).
+// Per-thread chunks i = 0..7 of an operand tile: global byte offset (relative to the K-tile origin) and LDS byte
+// offset (inside the operand image) of chunk 0, and the per-chunk steps -- uniform, so the global step rides in
+// the scalar offset of the buffer load and the LDS step in the ds_write's immediate.
+//   K-contiguous: row (tid >> 3) + 32 i, 16-B chunk tid & 7: global += 32 ld per i, LDS += 4096 per i.
+//   MN-contiguous: k-row (tid >> 5) + 8 i, 16-B chunk tid & 31 of the 256 columns: global += 8 ld per i, LDS +=
+//   2048 per i with the 4 x 4 swizzle's k-row bits alternating between even and odd i (lofs[0] / lofs[1]).
+// No clamping: rows / columns past the operand read what follows (their outputs are never stored) or, past the
+// buffer descriptor's range, zeros.
 template <bool KCONT>
-__device__ __forceinline__ void chunk_offsets(long long ld, int outer0, int outer_n, int i, int tid, unsigned& gofs,
-                                              int& lofs) {
+__device__ __forceinline__ void chunk_base(long long ld, int outer0, int tid, unsigned& gofs, int (&lofs)[2]) {
     if (KCONT) {
-        const int row = (tid >> 3) + 32 * i, ch = tid & 7;
-        const int o = min(outer0 + row, outer_n - 1);
-        gofs = (unsigned)(((long long)o * ld + 8 * ch) * 2);
-        lofs = kc_off(row, ch);
+        const int row = tid >> 3, ch = tid & 7;
+        gofs = (unsigned)(((long long)(outer0 + row) * ld + 8 * ch) * 2);
+        lofs[0] = lofs[1] = kc_off(row, ch);
     } else {
-        const int krow = (tid >> 5) + 8 * i, ch = tid & 31;
-        int o = outer0 + 8 * ch;
-        if (o >= outer_n) o = 0;
-        gofs = (unsigned)(((long long)krow * ld + o) * 2);
-        lofs = (ch >> 4) * (OPB / 2) + mc_off(krow, ch & 15);
+        const int krow = tid >> 5, ch = tid & 31;
+        gofs = (unsigned)(((long long)krow * ld + outer0 + 8 * ch) * 2);
+        lofs[0] = (ch >> 4) * (OPB / 2) + mc_off(krow, ch & 15);
+        lofs[1] = (ch >> 4) * (OPB / 2) + mc_off(krow + 8, ch & 15) - 2048;
     }
 }
 
@@ -104,36 +108,93 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, b2));
 }
 
-// alpha, beta C, bias and activation of 4 consecutive columns n.. of row m (rolled: the epilogue's
-// 64 tiles stay small code)
-__device__ __forceinline__ f32x4 epi4(const G4Args& a, f32x4 v, const void* rowp, int m, int n) {
-    const float brow = (a.bias_mode == 2 && m < a.M) ? a.bias[m] : 0.f;
-#pragma unroll 1
-    for (int r = 0; r < 4; ++r) {
-        const bool in = n + r < a.N && m < a.M;
-        float x = a.alpha * v[r];
-        if (a.beta != 0.f && in) {
-            const float c = a.out_f32 ? reinterpret_cast<const float*>(rowp)[n + r]
-                                      : ld(reinterpret_cast<const __hip_bfloat16*>(rowp) + n + r);
-            x = fmaf(a.beta, c, x);
+// Epilogue through the wave's 32 KB of LDS: acc[i][j][r] = C[mw + 16 i + (lane & 15)][nw + 16 j + 4 (lane >> 4) + r].
+// The block's rows go to LDS as row-major [rows][128] images -- STF = 0: bf16 (plain bf16 output: all 128 rows,
+// 256-B rows); STF = 1: fp32 (two halves of 64 rows, 512-B rows; fp32 output, or bf16 output with an epilogue,
+// which is applied to the fp32 sums before the one rounding) -- XOR-swizzled so the 8-B / 16-B writes in the
+// accumulator layout and the 16-B row reads are conflict-free, and leave as whole 16-B row pieces.
+template <bool STF, bool OUTF32>
+__device__ __forceinline__ void epilogue(const G4Args& a, const f32x4 (&acc)[8][8], unsigned char* wl, int lane, int mw,
+                                         int nw, int z, bool plain) {
+    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
+    constexpr int H = STF ? 2 : 1, RH = 128 / H;                 // halves, rows per half
+    constexpr int RB = STF ? 512 : 256;                          // bytes per image row
+    constexpr int PPR = RB / 16;                                 // 16-B pieces per row
+    constexpr int VPP = STF ? 4 : 8;                             // values per piece
+    TC* Cz = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
+    const bool vec = (a.ldc % 8) == 0 && (a.sC % 8) == 0 && (reinterpret_cast<uintptr_t>(a.C) % 16) == 0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+#pragma unroll
+        for (int ii = 0; ii < 8 / H; ++ii) {
+            const int i = h * (8 / H) + ii;
+            const int ml = 16 * ii + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = 4 * j + (lane >> 4);              // 4-value chunk of the row (0..31)
+                const f32x4 v = acc[i][j];
+                if (STF) {
+                    *reinterpret_cast<f32x4*>(wl + ml * RB + 16 * (c ^ (ml & 15))) = v;
+                } else {
+                    *reinterpret_cast<uint2*>(wl + ml * RB + 8 * (c ^ ((ml & 15) << 1))) =
+                        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                }
+            }
         }
-        x += (a.bias_mode == 1) ? (in ? a.bias[n + r] : 0.f) : brow;
-        if (a.act == 1) x = gelu_tanh(x);
-        else if (a.act == 2) x = x * gelu_parts(x).cdf;
-        v[r] = x;
-    }
-    return v;
-}
-
-template <bool OUTF32, class TC>
-__device__ __forceinline__ void store4(TC* row, int n, f32x4 v, bool mok, bool whole, int N) {
-    if (!mok) return;
-    if (whole) {
-        if (OUTF32) *reinterpret_cast<f32x4*>(row + n) = v;
-        else *reinterpret_cast<uint2*>(row + n) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-    } else {
-        for (int r = 0; r < 4; ++r)
-            if (n + r < N) st(row + n + r, v[r]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 2
+        for (int q = lane; q < RH * PPR; q += 64) {
+            const int ml = q / PPR, p = q % PPR;
+            const int m = mw + h * RH + ml;
+            const uint4 raw = *reinterpret_cast<const uint4*>(wl + ml * RB + 16 * (p ^ (ml & 15)));
+            const int n = nw + VPP * p;
+            if (m >= a.M || n >= a.N) continue;
+            TC* dst = Cz + (long long)m * a.ldc + n;
+            const bool whole = n + VPP <= a.N && vec;
+            if (!STF && whole) {                                 // plain bf16: the staged bytes as they are
+                *reinterpret_cast<uint4*>(dst) = raw;
+                continue;
+            }
+            float v[VPP];
+            if (STF) {
+                const float4 f = __builtin_bit_cast(float4, raw);
+                v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+            } else {
+                const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[2 * e] = __uint_as_float(w[e] << 16);
+                    v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+                }
+            }
+            if (!plain) {
+                const float brow = (a.bias_mode == 2) ? a.bias[m] : 0.f;
+#pragma unroll
+                for (int e = 0; e < VPP; ++e) {
+                    const bool in = n + e < a.N;
+                    float x = a.alpha * v[e];
+                    if (a.beta != 0.f && in) x = fmaf(a.beta, ld(dst + e), x);
+                    x += (a.bias_mode == 1) ? (in ? a.bias[n + e] : 0.f) : brow;
+                    if (a.act == 1) x = gelu_tanh(x);
+                    else if (a.act == 2) x = x * gelu_parts(x).cdf;
+                    v[e] = x;
+                }
+            }
+            if (whole) {
+                if (OUTF32) {
+                    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+                } else {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                }
+            } else {
+                for (int e = 0; e < VPP && n + e < a.N; ++e) st(dst + e, v[e]);
+            }
+        }
+        if (H > 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
     }
 }
 
@@ -159,14 +220,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm4_kernel(G4Args a) {
     const int z = blockIdx.y;
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.spanA, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.spanB, 0x00020000);
-    unsigned gA[8], gB[8];
-    int lA[8], lB[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        chunk_offsets<AK>(a.lda, m0, a.M, i, tid, gA[i], lA[i]);
-        chunk_offsets<BKC>(a.ldb, n0, a.N, i, tid, gB[i], lB[i]);
-    }
+    unsigned gA, gB;
+    int lA[2], lB[2];
+    chunk_base<AK>(a.lda, m0, tid, gA, lA);
+    chunk_base<BKC>(a.ldb, n0, tid, gB, lB);
     const long long zA = (long long)z * a.sA * 2, zB = (long long)z * a.sB * 2;
+    const unsigned stA = (unsigned)((AK ? 32 : 8) * a.lda * 2), stB = (unsigned)((BKC ? 32 : 8) * a.ldb * 2);
     const int KT = a.K / BK;
     uint4 stg[16];
     auto gload = [&](int kt) {
@@ -174,17 +233,19 @@ __global__ __launch_bounds__(THREADS, 1) void gemm4_kernel(G4Args a) {
         const unsigned sb = (unsigned)(zB + (BKC ? (long long)kt * BK * 2 : (long long)kt * BK * a.ldb * 2));
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            stg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rA, gA[i], sa, 0));
+            stg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rA, gA, sa + i * stA, 0));
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            stg[8 + i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rB, gB[i], sb, 0));
+            stg[8 + i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rB, gB, sb + i * stB, 0));
     };
     auto swrite = [&](int buf) {
         unsigned char* base = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(base + lA[i]) = stg[i];
+        for (int i = 0; i < 8; ++i)
+            *reinterpret_cast<uint4*>(base + lA[i & 1] + (AK ? 4096 : 2048) * i) = stg[i];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(base + OPB + lB[i]) = stg[8 + i];
+        for (int i = 0; i < 8; ++i)
+            *reinterpret_cast<uint4*>(base + OPB + lB[i & 1] + (BKC ? 4096 : 2048) * i) = stg[8 + i];
     };
 
     f32x4 acc[8][8];
@@ -193,55 +254,77 @@ __global__ __launch_bounds__(THREADS, 1) void gemm4_kernel(G4Args a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
 
-    gload(0);
-    swrite(0);
-    if (KT > 1) gload(1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
     // A blocks of this wave: rows 128 wm + 16 bi -> image block 8 wm + bi (both layouts); same for B
     const int ablk = 8 * wm, bblk = 8 * wn;
+    bf16x8 a0[8], b0[8], a1[8], b1[8];          // fragments of k32 step 0 / 1
+    auto reads = [&](const unsigned char* buf, int t, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = frag<AK>(buf, ablk + i, t, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bf[j] = frag<BKC>(buf + OPB, bblk + j, t, lane);
+    };
+    auto mfmas = [&](const bf16x8 (&af)[8], const bf16x8 (&bf)[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    };
+    // LDS reads per k32 step: a K-contiguous fragment is one ds_read_b128, a transposed one two ds_read_b64_tr
+    constexpr int NRD = (AK ? 8 : 16) + (BKC ? 8 : 16);
+
+    // Pipeline (one barrier per K-tile, placed mid-tile):
+    //   step 0 of K-tile t: MFMAs on (a0, b0) = step 0 of t, beside the reads of step 1 of t (a1, b1), the LDS
+    //     write of K-tile t+1 (register stage, loaded during K-tile t-1) and the loads of K-tile t+2;
+    //   lgkmcnt(0) + barrier: K-tile t+1 is in LDS for every wave, and every wave's reads of K-tile t-1's
+    //     buffer are done (the next step 0 overwrites it);
+    //   step 1 of K-tile t: MFMAs on (a1, b1) beside the reads of step 0 of K-tile t+1 (a0, b0).
+    // K-tiles past the end are clamped (reloaded; written to the buffer nobody reads any more).
+    gload(0);
+    swrite(0);
+    gload(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    reads(lds, 0, a0, b0);
     for (int kt = 0; kt < KT; ++kt) {
-        const unsigned char* buf = lds + (kt & 1) * STAGE;
+        const int cur = kt & 1, nxt = cur ^ 1;
+        reads(lds + cur * STAGE, 1, a1, b1);
+        mfmas(a0, b0);
+        swrite(nxt);
+        gload(min(kt + 2, KT - 1));
+        if (G4_SCHED) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            bf16x8 af[8], bf[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) af[i] = frag<AK>(buf, ablk + i, t, lane);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bf[j] = frag<BKC>(buf + OPB, bblk + j, t, lane);
-            if (t == 1 && kt + 1 < KT) {
-                swrite((kt + 1) & 1);
-                if (kt + 2 < KT) gload(kt + 2);
+            for (int g = 0; g < 16; ++g) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);         // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, NRD / 16, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);         // DS write
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         // VMEM read
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             }
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-    }
-
-    // epilogue: acc[i][j][r] = C[m0 + 128 wm + 16 i + (lane & 15)][n0 + 128 wn + 16 j + 4 (lane >> 4) + r]
-    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
-    TC* Cz = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
-    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
-    const bool vec = (a.ldc % 4) == 0 && (a.sC % 4) == 0 && (reinterpret_cast<uintptr_t>(a.C) % 16) == 0;
-    const int mb = m0 + 128 * wm + (lane & 15), nb = n0 + 128 * wn + 4 * (lane >> 4);
+        reads(lds + nxt * STAGE, 0, a0, b0);
+        mfmas(a1, b1);
+        if (G4_SCHED) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = mb + 16 * i;
-        const bool mok = m < a.M;
-        TC* row = Cz + (long long)min(m, a.M - 1) * a.ldc;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int n = nb + 16 * j;
-            f32x4 v = acc[i][j];
-            if (!plain) v = epi4(a, v, row, m, n);
-            store4<OUTF32>(row, n, v, mok, vec && n + 4 <= a.N, a.N);
+            for (int g = 0; g < 16; ++g) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, NRD / 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            }
         }
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();               // every wave's LDS reads are done: the epilogue reuses LDS
+
+    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
+    unsigned char* wl = lds + wave * 32768;
+    const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
+    if (!OUTF32 && plain) epilogue<false, false>(a, acc, wl, lane, mw, nw, z, true);
+    else epilogue<true, OUTF32>(a, acc, wl, lane, mw, nw, z, plain);
 }
 
 template <bool AK, bool BKC, bool OUTF32>

@@ -18,8 +18,11 @@
 //  * reductions over WD, C, O or 3C: 4-row x CB-column output tiles, one per wave (short K) or one per
 //    block (K >= 1024), the threads striding over k (coalesced along k), each keeping 4 x CB partial
 //    sums that are reduced across the wave with xor shuffles (and across the four waves in LDS);
-//  * reductions over the batch (dW1, dA, dab): one thread per 8-wide output strip of a row (the row's
-//    batch factor computed once per sample), a loop over the batch.
+//  * reductions over the batch (dW1, dA, dab: K = B, outputs O x C and 3C x WD): 32-row x 128-column
+//    output tiles per block, the batch factors of the tile's rows (q or dm) and columns (s^2 or w) staged
+//    in LDS 32 samples at a time, each thread a 4 x 4 register tile fed by two float4 LDS reads per
+//    sample (the row factors a broadcast), float4 stores. (Round 3 had one thread per 8-wide strip
+//    looping over the batch with guarded scalar loads: 50 us per launch, 1 % of HBM.)
 // All sums are plain fp32 FMAs (the reference runs them in fp32 with TF32 off).
 #include "vfm_common.h"
 
@@ -109,6 +112,70 @@ __device__ __forceinline__ float q_at(const StyleArgs& a, int b, int o) {
     return -0.5f * a.dd[i] * dv * dv * dv;
 }
 
+// out[r][c] = sum_b X(b, r) Y(b, c) over b < B for the block's 32 x 128 tile (r0, c0): X / Y give the
+// batch factors (zero outside). Thread t owns rows r0 + 4 (t >> 5) .. + 3, columns c0 + 4 (t & 31) .. + 3;
+// rsum (if non-null) gets sum_b X(b, r) of the thread's 4 rows. Staging: xs [32 b][32 r], ys [32 b][128 c].
+constexpr int OT_R = 32, OT_C = 128, OT_B = 32;
+template <class FX, class FY>
+__device__ __forceinline__ void outer_tile(int B, FX X, FY Y, float (&acc)[4][4], float (&rsum)[4], float* xs,
+                                           float* ys) {
+    const int t = threadIdx.x, ty = t >> 5, tx = t & 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        rsum[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    }
+    for (int b0 = 0; b0 < B; b0 += OT_B) {
+        __syncthreads();
+        // X: 32 x 32 values, 4 per thread (b = t >> 3, r = 4 (t & 7) ..); Y: 32 x 128, 16 per thread
+        {
+            const int b = t >> 3, r = 4 * (t & 7);
+            float4 v = X(b0 + b, r);
+            *reinterpret_cast<float4*>(xs + b * OT_R + r) = v;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = t + 256 * u, b = e >> 5, c = 4 * (e & 31);
+            *reinterpret_cast<float4*>(ys + b * OT_C + c) = Y(b0 + b, c);
+        }
+        __syncthreads();
+        const int nb = min(OT_B, B - b0);
+        for (int b = 0; b < nb; ++b) {
+            const float4 x = *reinterpret_cast<const float4*>(xs + b * OT_R + 4 * ty);
+            const float4 y = *reinterpret_cast<const float4*>(ys + b * OT_C + 4 * tx);
+            const float xv[4] = {x.x, x.y, x.z, x.w}, yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                rsum[i] += xv[i];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xv[i], yv[j], acc[i][j]);
+            }
+        }
+    }
+}
+
+// four consecutive values of a [rows][cols] fp32 matrix (row stride ld) at (r, c..c+3), zero outside; one
+// 16-B load when the row is whole and aligned
+__device__ __forceinline__ float4 load4(const float* p, long long ld, int r, int rows, int c, int cols, bool vec) {
+    if (r >= rows) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* q = p + (long long)r * ld + c;
+    if (vec && c + 4 <= cols) return *reinterpret_cast<const float4*>(q);
+    return make_float4(c < cols ? q[0] : 0.f, c + 1 < cols ? q[1] : 0.f, c + 2 < cols ? q[2] : 0.f,
+                       c + 3 < cols ? q[3] : 0.f);
+}
+
+__device__ __forceinline__ void store4(float* p, long long ld, int r, int rows, int c, int cols, bool vec, float4 v) {
+    if (r >= rows) return;
+    float* q = p + (long long)r * ld + c;
+    if (vec && c + 4 <= cols) {
+        *reinterpret_cast<float4*>(q) = v;
+        return;
+    }
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    for (int j = 0; j < 4 && c + j < cols; ++j) q[j] = vv[j];
+}
+
 // LAUNCH 0 (tiles): m, s   — 4 samples x 4 channels (x 3 split parts) per tile, k < WD
 // LAUNCH 1 (tiles): d      — 4 samples x 8 outputs per tile, k < C
 // LAUNCH 2: ds (tiles: 4 samples x 8 channels, k < O) | dW1 (threads: 8-channel strips, b < B)
@@ -123,7 +190,6 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
     // wave 0 (tpb = 1) or of every wave (tpb = 4)
     const long long wunit = a.tpb == 1 ? (long long)blk : (long long)blk * WAVES + wave;
     const bool owner0 = a.tpb != 1 || wave == 0;
-    const long long tunit = (long long)blk * THREADS + threadIdx.x;   // thread jobs
     const int C = a.C, C3 = 3 * a.C, WD = a.WD, O = a.O, B = a.B;
     const int nbg = (B + RB - 1) / RB;                                 // 4-sample groups
 
@@ -211,45 +277,59 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
                     const long long o = (long long)b * C + i;
                     a.ds[o] = (a.dsin ? a.dsin[o] : 0.f) + 2.f * a.s[o] * acc[r][c];
                 }
-        } else {                  // dW1 [O, C]: one thread per 8-channel strip of a row, b < B
-            const int strips = (C + 7) / 8;
-            if (tunit >= (long long)O * strips) return;
-            const int o = (int)(tunit / strips), i0 = (int)(tunit - (long long)o * strips) * 8;
-            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            for (int b = 0; b < B; ++b) {
-                const float q = q_at(a, b, o);
-                const float* sr = a.s + (long long)b * C + i0;
+        } else {                  // dW1 [O, C] = 2 W1 (Q^T S^2): outer tiles over the batch
+            __shared__ __attribute__((aligned(16))) float xs[OT_B * OT_R], ys[OT_B * OT_C];
+            const int tn = (C + OT_C - 1) / OT_C;
+            const int o0 = (blk / tn) * OT_R, i0 = (blk % tn) * OT_C;
+            const bool vec = (C % 4) == 0;
+            float acc[4][4], rs[4];
+            outer_tile(B,
+                [&](int b, int r) {
+                    float v[4];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float v = i0 + e < C ? sr[e] : 0.f;
-                    acc[e] = fmaf(q, v * v, acc[e]);
-                }
+                    for (int j = 0; j < 4; ++j) v[j] = (b < B && o0 + r + j < O) ? q_at(a, b, o0 + r + j) : 0.f;
+                    return make_float4(v[0], v[1], v[2], v[3]);
+                },
+                [&](int b, int c) {
+                    float4 v = b < B ? load4(a.s, C, b, B, i0 + c, C, vec) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    return make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
+                }, acc, rs, xs, ys);
+            const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int o = o0 + 4 * ty + i, c = i0 + 4 * tx;
+                const float4 w = load4(a.W1, C, o, O, c, C, vec);
+                store4(a.dW1, C, o, O, c, C, vec,
+                       make_float4(2.f * w.x * acc[i][0], 2.f * w.y * acc[i][1], 2.f * w.z * acc[i][2],
+                                   2.f * w.w * acc[i][3]));
             }
-            const long long row = (long long)o * C;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                if (i0 + e < C) a.dW1[row + i0 + e] = 2.f * a.W1[row + i0 + e] * acc[e];
         }
     } else {
-        if (!second) {            // dA [3C, WD] and dab [3C]: one thread per 8-column strip of a row, b < B
-            const int strips = (WD + 7) / 8;
-            if (tunit >= (long long)C3 * strips) return;
-            const int j = (int)(tunit / strips), k0 = (int)(tunit - (long long)j * strips) * 8;
-            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            float sb = 0.f;
-            for (int b = 0; b < B; ++b) {
-                const float g = dm_at(a, b, j);
-                const float* wr = a.w + (long long)b * a.ldw + k0;
+        if (!second) {            // dA [3C, WD] = wg dm^T w, dab [3C] = bg sum_b dm: outer tiles over the batch
+            __shared__ __attribute__((aligned(16))) float xs[OT_B * OT_R], ys[OT_B * OT_C];
+            const int tn = (WD + OT_C - 1) / OT_C;
+            const int j0 = (blk / tn) * OT_R, k0 = (blk % tn) * OT_C;
+            const bool vec = (WD % 4) == 0 && (a.ldw % 4) == 0 && (reinterpret_cast<uintptr_t>(a.w) % 16) == 0;
+            float acc[4][4], rs[4];
+            outer_tile(B,
+                [&](int b, int r) {
+                    float v[4];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) acc[e] = fmaf(g, k0 + e < WD ? wr[e] : 0.f, acc[e]);
-                sb += g;
-            }
-            if (a.dA) {
+                    for (int j = 0; j < 4; ++j) v[j] = (b < B && j0 + r + j < C3) ? dm_at(a, b, j0 + r + j) : 0.f;
+                    return make_float4(v[0], v[1], v[2], v[3]);
+                },
+                [&](int b, int c) { return b < B ? load4(a.w, a.ldw, b, B, k0 + c, WD, vec) : make_float4(0.f, 0.f, 0.f, 0.f); },
+                acc, rs, xs, ys);
+            const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+            const bool dvec = (WD % 4) == 0;
 #pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (k0 + e < WD) a.dA[(long long)j * WD + k0 + e] = a.wg * acc[e];
+            for (int i = 0; i < 4; ++i) {
+                const int j = j0 + 4 * ty + i;
+                if (a.dA)
+                    store4(a.dA, WD, j, C3, k0 + 4 * tx, WD, dvec,
+                           make_float4(a.wg * acc[i][0], a.wg * acc[i][1], a.wg * acc[i][2], a.wg * acc[i][3]));
+                if (a.dab && k0 == 0 && tx == 0 && j < C3) a.dab[j] = a.bg * rs[i];
             }
-            if (a.dab && k0 == 0) a.dab[j] = a.bg * sb;
         } else {                  // dw [B, WD]: waves, k < 3C
             constexpr int CB = 8;
             if (wunit >= (long long)nbg * ((WD + CB - 1) / CB)) return;
@@ -336,7 +416,7 @@ extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A
     if (demod) {
         a.tpb = tiles_per_block(O);
         a.blocks0 = (int)cdiv(nbg * cdiv(C, 8), a.tpb);
-        const long long b1 = dW1 ? cdiv((long long)O * cdiv(C, 8), THREADS) : 0;
+        const long long b1 = dW1 ? cdiv(O, OT_R) * cdiv(C, OT_C) : 0;
         const int rc = launch<2>(a, a.blocks0 + b1, st);
         if (rc) return rc;
         a.dsv = ds_ws;
@@ -344,7 +424,7 @@ extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A
         a.dsv = ds_in;
     }
     if (!dA && !dab && !dw) return 0;
-    a.blocks0 = (dA || dab) ? (int)cdiv(3LL * C * cdiv(WD, 8), THREADS) : 0;
+    a.blocks0 = (dA || dab) ? (int)(cdiv(3LL * C, OT_R) * cdiv(WD, OT_C)) : 0;
     const int C3 = 3 * C;
     a.tpb = tiles_per_block(C3);
     const long long b1 = dw ? cdiv(nbg * cdiv(WD, 8), a.tpb) : 0;
