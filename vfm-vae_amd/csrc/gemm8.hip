@@ -402,12 +402,15 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     }
     const unsigned lds0 =
         __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void*)lds + (unsigned)wave * 64 * 16);
-    // virtual K-tile iterator: term (piece pair), batch zt (batch-reduced products), K-tile kk of the batch
+    // virtual K-tile iterator, term-fastest (v = T * real K-tile + term): the T piece products of one real
+    // K-tile run back to back, so the piece tiles a term re-reads (hi of A for three terms, ...) are still
+    // in L2 from the term before -- one HBM read of each piece instead of one per term. Then batch zt
+    // (batch-reduced products) and K-tile kk of the batch.
     int term, zt, kk;
     {
         const int v = it.v0;
-        term = v / VT;
-        const int rest = v - term * VT;
+        const int rest = v / a.T;
+        term = v - rest * a.T;
         zt = a.reduce ? rest / KTz : it.z;
         kk = a.reduce ? rest - (rest / KTz) * KTz : rest;
     }
@@ -419,12 +422,11 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
         sb = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sB + (BKC ? kb : kb * a.ldb)) * 2));
     };
     auto advance = [&]() {                               // branch-free: selects on wave-uniform values
-        const bool w1 = ++kk == KTz;
+        const bool w0 = ++term == a.T;
+        term = w0 ? 0 : term;
+        const bool w1 = w0 && ++kk == KTz;
         kk = w1 ? 0 : kk;
-        const int zn = zt + (a.reduce && w1 ? 1 : 0);
-        const bool w2 = a.reduce ? zn == a.Z : w1;
-        zt = (a.reduce && w2) ? 0 : zn;
-        term += w2 ? 1 : 0;
+        zt += (a.reduce && w1) ? 1 : 0;
     };
     auto issue = [&](unsigned sa, unsigned sb, int bsel, int h) {
         const unsigned m0 = lds0 + bsel * BUF + (h == 0 ? OFF_ALO : h == 1 ? OFF_BLO : h == 2 ? OFF_BHI : OFF_AHI);
