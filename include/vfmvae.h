@@ -342,6 +342,16 @@ int vfm_gemm(const void* A, const void* B, void* C, const float* bias, float* wo
              int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,
              int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
              int bias_mode, int act, int splits, int reduce_batch, void* stream);
+/* Batch-folded form of vfm_gemm for a shared A (sA = 0, either layout): C[z] = epi(alpha A B[z] + beta C[z]),
+ * z < batch, B[z] MN-contiguous [K][P] (row stride ldb, batch stride sB), C[z] [M][P] (row stride ldc,
+ * batch stride sC), P = 2^lgp >= 8 columns per sample, run as ONE product over N = batch * P columns
+ * (column n -> sample n >> lgp): per-sample planes narrower than a 128-wide tile -- the 1x1
+ * convolutions of the 8 x 8 decoder block (reference networks/utils/convnext_utils.py:36-142,
+ * gigagan_utils.py:53-185 at 8 x 8) -- fill whole tiles. bias_mode 2: per row; 1: per column of the
+ * P-wide plane. No split-K, no workspace. */
+int vfm_gemm_fold(const void* A, const void* B, void* C, const float* bias, int in_dtype, int out_dtype, int M,
+                  int lgp, int K, int batch, int a_kcont, long long lda, long long ldb, long long sB, long long ldc,
+                  long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 
 /* Large-tile form (csrc/gemm8.hip: 256 x 256 tiles, 4-phase LDS-DMA pipeline) of the same contract,
  * K % 64 == 0 (else VFM_NO_KERNEL). precision VFM_BF16: A / B are bf16 matrices as above. precision

@@ -315,3 +315,28 @@ def test_gemm8_split_k_ragged_chunks(g8_schedule):
     B = _make((2432, 2304), torch.bfloat16, g)
     out = gemm_hip.try_gemm(A, B, out_dtype=torch.float32, route=("g8", 10))
     assert _rel(out, A.float() @ B.float()) < 1e-5
+
+
+@pytest.mark.parametrize("a_t", [False, True])
+@pytest.mark.parametrize("O,I,P,Bn", [(512, 512, 64, 32), (2048, 512, 64, 5), (200, 136, 16, 9), (3, 40, 8, 17)])
+@pytest.mark.parametrize("bias_dim", [None, 0])
+def test_gemm_batch_folded_narrow_planes(a_t, O, I, P, Bn, bias_dim):
+    """Shared A (1x1-conv weight, or its transpose for the data gradient) times per-sample planes of
+    P < 128 columns: one batch-folded product (vfm_gemm_fold, kernel timer region gemm_fold), f32x6
+    products against the fp32 reference at the fp32 tolerance."""
+    from torch_utils.ops import gemm_hip, kernel_timer
+    g = torch.Generator().manual_seed(O + I + P + Bn)
+    W = torch.randn(I, O, generator=g).to(DEV) if a_t else torch.randn(O, I, generator=g).to(DEV)
+    Wv = W.t() if a_t else W
+    x = torch.randn(Bn, I, P, generator=g).to(DEV)
+    bias = torch.randn(O, generator=g).to(DEV) if bias_dim is not None else None
+    kernel_timer.enable(True)
+    out = gemm_hip.try_gemm(Wv, x, bias=bias, bias_dim=bias_dim, auto=True)
+    names = set(kernel_timer.summary())
+    kernel_timer.enable(False)
+    assert out is not None and out.shape == (Bn, O, P)
+    assert any(n.startswith("gemm_fold<") for n in names), names
+    ref = torch.matmul(Wv.double(), x.double())
+    if bias is not None:
+        ref = ref + bias.double()[None, :, None]
+    assert _rel(out, ref) < F32_TOL

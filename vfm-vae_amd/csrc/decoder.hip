@@ -1371,12 +1371,26 @@ __global__ __launch_bounds__(256) void colsum2(const float* __restrict__ a, cons
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= cols) return;
     float sa = 0.f, sb = 0.f;
-    for (int r = 0; r < rows; ++r) {
-        if (out_a) sa += a[(long long)r * cols + c];
-        if (out_b) sb += b[(long long)r * cols + c];
+    const bool wa = out_a != nullptr, wb = out_b != nullptr;
+    // 16 rows' loads in flight per thread before they are summed (in row order): the loop was one
+    // dependent L2 round trip per row
+    for (int r0 = 0; r0 < rows; r0 += 16) {
+        float va[16], vb[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const bool in = r0 + k < rows;
+            const long long o = (long long)(r0 + k) * cols + c;
+            va[k] = (wa && in) ? a[o] : 0.f;
+            vb[k] = (wb && in) ? b[o] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            sa += va[k];
+            sb += vb[k];
+        }
     }
-    if (out_a) out_a[c] = scale_a ? sa * scale_a[c] : sa;
-    if (out_b) out_b[c] = sb;
+    if (wa) out_a[c] = scale_a ? sa * scale_a[c] : sa;
+    if (wb) out_b[c] = sb;
 }
 
 }  // namespace

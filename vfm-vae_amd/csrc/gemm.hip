@@ -59,6 +59,11 @@ struct GemmArgs {
     float alpha, beta;
     int bias_mode;             // 0 none, 1 per column (n), 2 per row (m)
     int act;                   // 0 none, 1 gelu tanh, 2 gelu erf
+    // batch folding (vfm_gemm_fold): the z products of a shared A with MN-contiguous B[z] / C[z] of
+    // P = 2^lgp columns each run as ONE product over N = z P columns, column n -> (batch n >> lgp,
+    // column n & (P - 1)) -- per-sample planes narrower than a tile (the 8 x 8 decoder block's 1x1
+    // convolutions: P = 64) fill whole tiles. 0 = off.
+    int lgp;
 };
 
 // K-contiguous image [128 rows][64 k]: byte offset of 16-B chunk ch (0..7) of row
@@ -92,9 +97,10 @@ struct Stage {
     static constexpr int ROWCH = (KCONT ? 64 : 128) / EPC;   // chunks per global row of the tile
     uint4 r[PER];
 
-    // outer0: first outer index of the tile, k0: first k, outer_n / K: bounds
+    // outer0: first outer index of the tile, k0: first k, outer_n / K: bounds; lgp / sb: batch folding of
+    // an MN-contiguous operand (outer index o -> batch o >> lgp at element stride sb, column o & (2^lgp - 1))
     __device__ __forceinline__ void load(const unsigned char* base, long long ld, int outer0, int k0, int outer_n,
-                                         int K, int tid) {
+                                         int K, int tid, int lgp = 0, long long sb = 0) {
         const int esz = F32 ? 4 : 2;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
@@ -104,7 +110,8 @@ struct Stage {
             if (KCONT) { o = outer0 + row; k = k0 + col; }
             else       { k = k0 + row; o = outer0 + col; }
             const bool ok = (o < outer_n) && (k < K);
-            const long long off = KCONT ? ((long long)o * ld + k) : ((long long)k * ld + o);
+            long long off = KCONT ? ((long long)o * ld + k) : ((long long)k * ld + o);
+            if (!KCONT && lgp) off = (long long)(o >> lgp) * sb + (long long)k * ld + (o & ((1 << lgp) - 1));
             r[u] = ok ? *reinterpret_cast<const uint4*>(base + off * esz) : make_uint4(0, 0, 0, 0);
         }
     }
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
 
     const int esz = F32 ? 4 : 2;
     const unsigned char* Ab = reinterpret_cast<const unsigned char*>(a.A) + (long long)z * a.sA * esz;
-    const unsigned char* Bb = reinterpret_cast<const unsigned char*>(a.B) + (long long)z * a.sB * esz;
+    const unsigned char* Bb = reinterpret_cast<const unsigned char*>(a.B) + (a.lgp ? 0LL : (long long)z * a.sB * esz);
 
     Stage<AK, NP> sa;
     Stage<BKC, NP> sb;
@@ -178,14 +185,14 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
         for (int j = 0; j < 2; ++j) acc[i][j] = accs[i][j] = f32x16{};
 
     sa.load(Ab, a.lda, m0, kbeg, a.M, kend, tid);
-    sb.load(Bb, a.ldb, n0, kbeg, a.N, kend, tid);
+    sb.load(Bb, a.ldb, n0, kbeg, a.N, kend, tid, a.lgp, a.sB);
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
         sa.store(a_img, tid);
         sb.store(b_img, tid);
         __syncthreads();
         if (k0 + BK < kend) {
             sa.load(Ab, a.lda, m0, k0 + BK, a.M, kend, tid);
-            sb.load(Bb, a.ldb, n0, k0 + BK, a.N, kend, tid);
+            sb.load(Bb, a.ldb, n0, k0 + BK, a.N, kend, tid, a.lgp, a.sB);
         }
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
@@ -240,19 +247,20 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
         return;
     }
     typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
-    TC* Cb = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
+    TC* Cb = reinterpret_cast<TC*>(a.C) + (a.lgp ? 0LL : (long long)z * a.sC);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int n = n0 + 64 * wn + 32 * j + r;
         if (n >= a.N) continue;
-        const float bcol = (a.bias_mode == 1) ? a.bias[n] : 0.f;
+        const float bcol = (a.bias_mode == 1) ? a.bias[a.lgp ? (n & ((1 << a.lgp) - 1)) : n] : 0.f;
+        TC* Cn = a.lgp ? Cb + (long long)(n >> a.lgp) * a.sC + (n & ((1 << a.lgp) - 1)) - n : Cb;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int m = m0 + 64 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * hh;
                 if (m >= a.M) continue;
-                TC* cp = Cb + (long long)m * a.ldc + n;
+                TC* cp = Cn + (long long)m * a.ldc + n;
                 float v = a.alpha * acc[i][j][e];
                 if (a.beta != 0.f) v = fmaf(a.beta, ld(cp), v);
                 v += (a.bias_mode == 2) ? a.bias[m] : bcol;
@@ -315,10 +323,10 @@ extern "C" int vfm_gemm_workspace_floats(int M, int N, int batch, int splits, in
     return M * N * batch * (splits < 1 ? 1 : splits);
 }
 
-extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias, float* workspace, int in_dtype,
-                        int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,
-                        int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
-                        int bias_mode, int act, int splits, int reduce_batch, void* stream) {
+static int gemm_impl(const void* A, const void* B, void* C, const float* bias, float* workspace, int in_dtype,
+                     int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,
+                     int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
+                     int bias_mode, int act, int splits, int reduce_batch, int lgp, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
     if (in_dtype != VFM_BF16 && in_dtype != VFM_F32 && in_dtype != VFM_F32X3) return VFM_NO_KERNEL;
     if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
@@ -326,10 +334,12 @@ extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias
     if (splits < 1) splits = 1;
     // 16-B chunks along every contiguous dimension; row starts 16-B aligned
     const int epc = in_dtype == VFM_BF16 ? 8 : 4;
-    const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
+    const int Nrow = lgp ? (1 << lgp) : N;                      // columns of one C / B row (folded: P)
+    const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : Nrow;
     if (a_c % epc || b_c % epc || lda % epc || ldb % epc || sA % epc || sB % epc) return VFM_NO_KERNEL;
     if (((uintptr_t)A | (uintptr_t)B) % 16) return VFM_NO_KERNEL;
-    if (lda < (a_kcont ? K : M) || ldb < (b_kcont ? K : N) || ldc < N) return VFM_ERR_ARGS;
+    if (lgp && (b_kcont || reduce_batch || splits > 1)) return VFM_ERR_ARGS;
+    if (lda < (a_kcont ? K : M) || ldb < (b_kcont ? K : Nrow) || ldc < Nrow) return VFM_ERR_ARGS;
     if ((long long)batch * splits > 65535) return VFM_ERR_ARGS;
     const bool use_ws = splits > 1 || reduce_batch;
     if (use_ws && !workspace) return VFM_ERR_ARGS;
@@ -341,6 +351,7 @@ extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias
     a.splits = splits;
     a.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
     a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
+    a.lgp = lgp;
     hipStream_t st = (hipStream_t)stream;
     const bool of32 = out_dtype == VFM_F32;
     int rc;
@@ -358,4 +369,28 @@ extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias
     if (of32) VFM_LAUNCH(gemm_reduce_kernel<true>, grid, dim3(256), 0, st, a, J, zc);
     else      VFM_LAUNCH(gemm_reduce_kernel<false>, grid, dim3(256), 0, st, a, J, zc);
     return launch_status();
+}
+
+extern "C" int vfm_gemm(const void* A, const void* B, void* C, const float* bias, float* workspace, int in_dtype,
+                        int out_dtype, int M, int N, int K, int batch, int a_kcont, long long lda, long long sA,
+                        int b_kcont, long long ldb, long long sB, long long ldc, long long sC, float alpha, float beta,
+                        int bias_mode, int act, int splits, int reduce_batch, void* stream) {
+    return gemm_impl(A, B, C, bias, workspace, in_dtype, out_dtype, M, N, K, batch, a_kcont, lda, sA, b_kcont, ldb, sB,
+                     ldc, sC, alpha, beta, bias_mode, act, splits, reduce_batch, 0, stream);
+}
+
+// Batch-folded form: C[z] = epi(alpha A B[z] + beta C[z]) for z < batch with A shared (either layout), B[z]
+// MN-contiguous [K][P] (row stride ldb, batch stride sB) and C[z] [M][P] (ldc, sC), P = 2^lgp columns
+// (lgp >= 2), run as one product of N = batch * P columns. bias per row (bias_mode 2) or per column of
+// the P-wide plane (1). No split-K.
+extern "C" int vfm_gemm_fold(const void* A, const void* B, void* C, const float* bias, int in_dtype, int out_dtype,
+                             int M, int lgp, int K, int batch, int a_kcont, long long lda, long long ldb, long long sB,
+                             long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream) {
+    if (lgp < 2 || lgp > 20 || batch <= 0) return VFM_ERR_ARGS;
+    const long long N = (long long)batch << lgp;
+    if (N > 0x7fffffffLL) return VFM_ERR_ARGS;
+    const int P = 1 << lgp;
+    if (ldb < P || ldc < P || sB % 8 || sC % 4) return VFM_NO_KERNEL;
+    return gemm_impl(A, B, C, bias, nullptr, in_dtype, out_dtype, M, (int)N, K, 1, a_kcont, lda, 0, 0, ldb, sB, ldc, sC,
+                     alpha, beta, bias_mode, act, 1, 0, lgp, stream);
 }

@@ -139,6 +139,13 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     K2, N = b3.shape[1], b3.shape[2]
     if K != K2:
         raise RuntimeError(f"gemm: inner dims differ ({K} vs {K2})")
+    if (auto and A.dtype == torch.float32 and not reduce_batch and splits == 1 and a3.shape[0] == 1 and z > 1
+            and FOLD_MIN <= N < 128 and (N & (N - 1)) == 0):
+        # per-sample planes narrower than a tile (the 8 x 8 decoder block's 1x1 convs): one product over
+        # the batch-folded N = z P columns (csrc/gemm.hip vfm_gemm_fold)
+        out = _try_fold(a3, b3, M, N, K, z, out, bias, bias_dim, act, alpha, beta, out_dtype)
+        if out is not None:
+            return out
     if auto and not preferred(A, M, N, reduce_batch):
         return None
     if auto and splits == 1:
@@ -245,6 +252,45 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     if rc == custom_ops.VFM_NO_KERNEL:
         return None
     custom_ops.check(rc, "vfm_gemm")
+    return out
+
+
+FOLD_MIN = 8                # narrowest per-sample plane the batch-folded product takes
+
+
+def _try_fold(a3, b3, M, N, K, z, out, bias, bias_dim, act, alpha, beta, out_dtype):
+    """C[z] = epi(alpha A B[z] + beta C[z]) as one batch-folded product, or None (layout not covered)."""
+    if b3.stride(2) != 1 or b3.shape[0] != z:
+        return None
+    la = _layout(a3, True)
+    if la is None:
+        return None
+    a_kc, lda, _ = la
+    out_dtype = out_dtype or a3.dtype
+    if out is None:
+        if beta != 0.0:
+            raise RuntimeError("gemm: beta != 0 needs `out`")
+        out = torch.empty((z, M, N), dtype=out_dtype, device=a3.device)
+    if out.dim() != 3 or out.stride(2) != 1 or out.dtype != out_dtype:
+        return None
+    bias_mode = 0
+    if bias is not None:
+        bias = bias.detach().float().contiguous()
+        bias_mode = 1 if bias_dim in (None, 1) else 2
+    prec, _, tag = custom_ops.f32_precision()
+    lgp = N.bit_length() - 1
+    tb = lambda v: "true" if v else "false"
+    region = f"gemm_fold<{tag},{tb(a_kc)},{tb(out_dtype == torch.float32)}>"
+    if kernel_timer.SHAPES:
+        region += f"[{M}x{N}x{K}x{z}]"
+    with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype), 2.0 * z * M * N * K, "mfma"):
+        rc = _lib.vfm_gemm_fold(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), prec,
+                                _CODES[out_dtype], M, lgp, K, z, int(a_kc), lda, b3.stride(1), b3.stride(0),
+                                out.stride(1), out.stride(0), float(alpha), float(beta), bias_mode, ACTS[act],
+                                custom_ops.stream_ptr(a3.device))
+    if rc == custom_ops.VFM_NO_KERNEL:
+        return None
+    custom_ops.check(rc, "vfm_gemm_fold")
     return out
 
 

@@ -213,6 +213,10 @@ def rocprof_name(region):
         return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}, false, 0>"
     if base == "gemm8_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2)
         return f"gemm8_kernel<true, false, false, false, {args[0]}>"
+    if base == "gemm_fold" and len(args) == 3:                 # batch-folded: gemm_kernel<AK, false, NP, OUTF32>
+        return f"gemm_kernel<{args[1]}, false, {_NP.get(args[0], 1)}, {args[2]}>"
+    if base == "gemm4" and len(args) == 4:                     # gemm4_kernel<AK, BK, OUTF32>
+        return f"gemm4_kernel<{args[1]}, {args[2]}, {args[3]}>"
     if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32>
         return f"gemm_kernel<{args[1]}, {args[2]}, {_NP.get(args[0], 1)}, {args[3]}>"
     if base == "conv3x3_nhwc" and len(args) == 2:              # conv3x3_kernel<BM, BN, NP>
