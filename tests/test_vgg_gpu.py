@@ -47,10 +47,11 @@ def test_conv3x3_layer(B, H, W, Cin, Cout):
 
 
 def _conv64(x, w, bias=None, relu=False, mask=None):
-    """fp64 torch stand-in for vgg_hip.conv3x3 (same NHWC / tap-major conventions; w = the bf16
-    pieces, whose sum is the fp32 weight exactly)."""
+    """fp64 torch stand-in for vgg_hip.conv3x3 (same NHWC conventions; w = the bf16 pieces in the kernel's
+    k order, whose sum is the fp32 weight exactly)."""
+    from torch_utils.ops import vgg_hip
     B, H, W, Cin = x.shape
-    w = w.double().sum(0)[:, :9 * Cin]
+    w = vgg_hip.tap_major(w.double().sum(0)[:, :9 * Cin], Cin)
     y = F.conv2d(x.permute(0, 3, 1, 2).double(), w.reshape(w.shape[0], 3, 3, Cin).permute(0, 3, 1, 2),
                  None if bias is None else bias.double(), padding=1)
     y = (y.relu() if relu else y).permute(0, 2, 3, 1)

@@ -7,9 +7,10 @@
 //   epi: + bias[n], ReLU, and/or x (mask[p, n] > 0) (the ReLU derivative of the layer below, for
 //   the data-gradient pass), fp32 out.
 //
-// Layout: activations NHWC fp32 ([B, H, W, C] contiguous: channels_last), weights [Cout][9][Cin]
-// (tap-major, channels contiguous) pre-split into NP bf16 piece arrays [NP][Cout][ldw] with rows
-// padded to ldw. Cin is a power of two >= 4 (the 3-channel image is padded to 4), Cout a multiple
+// Layout: activations NHWC fp32 ([B, H, W, C] contiguous: channels_last), weights pre-split into NP bf16
+// piece arrays [NP][Cout][ldw] (rows padded to ldw), k ordered tap-major (k = tap Cin + c) for Cin < 32 and
+// channel-chunk-major for Cin >= 32 (k = (c / 32) 288 + tap 32 + c % 32: a K-tile is one tap of one
+// 32-channel chunk, and the 9 taps of a chunk are consecutive K-tiles -- StageA::load_wide). Cin is a power of two >= 4 (the 3-channel image is padded to 4), Cout a multiple
 // of 64. The data gradient of the same conv is this kernel with the flipped, transposed weights
 // w'[cin, tap, cout] = w[cout, 8 - tap, cin] over dZ.
 //
@@ -120,10 +121,14 @@ struct StageA {
         }
         cur_tap = tap;
     }
+    // K order for Cin >= 32 is channel-chunk-major, tap-minor: K-tile kt = 32 channels (kt / 9) x tap kt % 9,
+    // so the 9 shifted reads of a pixel's channel chunk are 9 consecutive K-tiles and hit L2 (tap-major
+    // order re-read them Cin / 32 K-tiles apart, from HBM: 3.75x the algorithmic traffic in round 3)
     __device__ __forceinline__ void load_wide(const ConvArgs& a, int k0, int tid) {
-        const int tap = k0 >> a.lc;                      // uniform
+        const int kt = k0 >> 5;                          // uniform
+        const int cc = kt / 9, tap = kt - 9 * cc;
         if (tap != cur_tap) tap_setup(a, tap);
-        const int c = (k0 & (a.Cin - 1)) + 4 * (tid & 7);
+        const int c = 32 * cc + 4 * (tid & 7);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             r[u] = ((okm >> u) & 1)

@@ -56,9 +56,26 @@ def split_weight(w2d, npieces=None):
     return out
 
 
+def chunk_major(w2d, cin):
+    """[Cout, 9 cin] tap-major (k = tap cin + c) -> the kernel's order for cin >= 32: channel-chunk-major,
+    tap-minor (k = (c // 32) 288 + tap 32 + c % 32; csrc/conv.hip StageA::load_wide). cin < 32 stays."""
+    if cin < 32:
+        return w2d
+    Cout = w2d.shape[0]
+    return w2d.reshape(Cout, 9, cin // 32, 32).permute(0, 2, 1, 3).reshape(Cout, 9 * cin)
+
+
+def tap_major(w2d, cin):
+    """Inverse of chunk_major."""
+    if cin < 32:
+        return w2d
+    Cout = w2d.shape[0]
+    return w2d.reshape(Cout, cin // 32, 9, 32).permute(0, 2, 1, 3).reshape(Cout, 9 * cin)
+
+
 def conv3x3(x, w, bias=None, relu=False, mask=None):
     """x: NHWC fp32 [B, H, W, Cin] contiguous; w: [np, Cout, Kp] pieces from split_weight of the
-    [Cout, 9*Cin] tap-major weights -> [B, H, W, Cout] = relu?(conv(x) + bias) (x (mask > 0) when
+    [Cout, 9*Cin] weights in the kernel's k order (chunk_major) -> [B, H, W, Cout] = relu?(conv(x) + bias) (x (mask > 0) when
     given)."""
     B, H, W, Cin = x.shape
     npc, Cout, Kp = w.shape
@@ -94,9 +111,9 @@ def prepare(convs):
             cp = max(Cin, 4)
             wf = torch.zeros(Cout, 3, 3, cp, dtype=torch.float32, device=w.device)
             wf[..., :Cin] = w.permute(0, 2, 3, 1)
-            wb = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9 * Cout).contiguous()
-            hit = (key, (split_weight(wf.reshape(Cout, 9 * cp)), split_weight(wb), m.bias.detach().float().contiguous(),
-                         w))
+            wb = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9 * Cout)
+            hit = (key, (split_weight(chunk_major(wf.reshape(Cout, 9 * cp), cp).contiguous()),
+                         split_weight(chunk_major(wb, Cout).contiguous()), m.bias.detach().float().contiguous(), w))
             m._vfm_vgg_prep = hit
         out.append(hit[1])
     return out
