@@ -11,8 +11,8 @@
 //
 // Block = 16 columns (consecutive p) x 16 channel groups; a thread sums every 16th channel of its
 // column, the 16 partial sums meet in LDS, then the same threads write their channels. The gamma
-// gradient: each block reduces dy x / n over its 16 columns per channel into one partial row,
-// and a second kernel sums the rows of every channel in a fixed order (deterministic).
+// gradient: each block reduces dy x / n over its 16 columns per channel into one partial (channel-major
+// [C][blocks]), and a second kernel sums every channel's partials in a fixed order (deterministic).
 #include "vfm_common.h"
 
 namespace {
@@ -85,19 +85,39 @@ __global__ __launch_bounds__(THREADS) void crms_bwd(const float* __restrict__ x,
             // sum over the block's 16 columns: lanes col = 0..15 of one channel group are 16 consecutive lanes
 #pragma unroll
             for (int o = 8; o >= 1; o >>= 1) gx += __shfl_xor(gx, o, 16);
-            if (col == 0) gpart[(long long)blockIdx.x * C + c] = gx;
+            if (col == 0) gpart[(long long)c * gridDim.x + blockIdx.x] = gx;     // channel-major: [C][rows]
         }
     }
 }
 
-// dgamma[c] = scale * sum_rows gpart[row, c], rows in order
+// dgamma[c] = scale * sum_rows gpart[c, row]: one block per channel over its contiguous row partials (one per
+// crms_bwd block), every thread's loads in flight before its strided sum, then a fixed-order tree over the
+// block (deterministic). Round 3 summed the rows serially per channel (2048 dependent L2 round trips at
+// 32 x 32^2 pixels: ~100 us per launch).
 __global__ __launch_bounds__(256) void crms_gamma(const float* __restrict__ gpart, float* __restrict__ dgamma, int C,
                                                   int rows, float scale) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= C) return;
+    __shared__ float red[256];
+    const int c = blockIdx.x, t = threadIdx.x;
+    const float* row = gpart + (long long)c * rows;
     float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += gpart[(long long)r * C + c];
-    dgamma[c] = scale * s;
+    for (int r0 = 0; r0 < rows; r0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = r0 + t + 256 * k;
+            v[k] = r < rows ? row[r] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    red[t] = s;
+    __syncthreads();
+#pragma unroll
+    for (int w = 128; w >= 1; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    if (t == 0) dgamma[c] = scale * red[0];
 }
 
 bool crms_grid(int B, int C, int P, int& tiles, long long& blocks) {
@@ -140,6 +160,6 @@ extern "C" int vfm_channel_rms_norm_bwd(const float* x, const float* gamma, cons
     VFM_LAUNCH(crms_bwd, dim3((unsigned)blocks), dim3(THREADS), 0, st, x, gamma, rinv, dy, dx, gpart, C, P,
                        tiles, scale);
     if (dgamma)
-        VFM_LAUNCH(crms_gamma, dim3((C + 255) / 256), dim3(256), 0, st, gpart, dgamma, C, (int)blocks, scale);
+        VFM_LAUNCH(crms_gamma, dim3(C), dim3(256), 0, st, gpart, dgamma, C, (int)blocks, scale);
     return vfm::launch_status();
 }
