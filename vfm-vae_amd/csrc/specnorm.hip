@@ -8,7 +8,7 @@
 //   sigma = u . (W v) = ||W v||^2 / max(||W v||, eps),  W_sn = W / sigma
 // backward (u, v constants, as torch detaches them):
 //   dW = g / sigma - (sum_ij g_ij W_ij) / sigma^2 * u v^T
-// Launches (fwd): K1 t = W^T u (64 columns x 4 row groups per block) + per-block ||t||^2 partials;
+// Launches (fwd): K1 t = W^T u (16 columns x 16 row groups per block) + per-block ||t||^2 partials;
 // K2 r = W v (one row per wave, v = t / max(||t||, eps) formed from the K1 partials on the fly; block 0
 // stores v) + per-block ||r||^2 partials; K3 W_sn = W / sigma (grid-stride; block 0 stores u and sigma).
 // (bwd): K4 per-block partials of sum g W; K5 dW. Partial sums are added in a fixed order.
@@ -36,21 +36,26 @@ __device__ __forceinline__ float sum_parts(const float* p, int n, float* sh) {
     return block_reduce(s, sh);
 }
 
+// 16 columns x 16 row groups per block (4x the blocks of a 64-column tile, a quarter of the serial row loop
+// per thread: the heads' W is only 384 x 3456, so the 64-column form ran 54 blocks of 96-row loops)
+constexpr int TU_COLS = 16, TU_RG = THREADS / TU_COLS;
+
 __global__ __launch_bounds__(THREADS) void sn_wtu(const float* __restrict__ W, const float* __restrict__ u,
                                                   float* __restrict__ t, float* __restrict__ part, int O, int I) {
-    __shared__ float red[4][65];
+    __shared__ float red[TU_RG][TU_COLS + 1];
     __shared__ float sh[4];
-    const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const int i = blockIdx.x * 64 + col;
+    const int col = threadIdx.x % TU_COLS, rg = threadIdx.x / TU_COLS;
+    const int i = blockIdx.x * TU_COLS + col;
     float s = 0.f;
     if (i < I)
 #pragma unroll 4
-        for (int o = rg; o < O; o += 4) s = fmaf(W[(long long)o * I + i], u[o], s);
+        for (int o = rg; o < O; o += TU_RG) s = fmaf(W[(long long)o * I + i], u[o], s);
     red[rg][col] = s;
     __syncthreads();
     float tv = 0.f;
     if (rg == 0) {
-        tv = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+#pragma unroll
+        for (int g = 0; g < TU_RG; ++g) tv += red[g][col];
         if (i < I) t[i] = tv;
     }
     const float ss = block_reduce(rg == 0 && i < I ? tv * tv : 0.f, sh);
@@ -135,7 +140,7 @@ constexpr int SCALE_BLOCKS = 512;
 // floats of workspace vfm_specnorm_fwd / _bwd need for an [O, I] weight
 extern "C" long long vfm_specnorm_workspace_floats(int O, int I) {
     if (O <= 0 || I <= 0) return VFM_ERR_ARGS;
-    const long long tb = (I + 63) / 64, rb = (O + 3) / 4;
+    const long long tb = (I + TU_COLS - 1) / TU_COLS, rb = (O + 3) / 4;
     return (long long)I + O + tb + rb + SCALE_BLOCKS;
 }
 
@@ -145,7 +150,7 @@ extern "C" long long vfm_specnorm_workspace_floats(int O, int I) {
 extern "C" int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_copy, float* v_copy, float* sigma,
                                 float* Wsn, float* ws, int O, int I, float eps, void* stream) {
     if (!W || !u || !v || !sigma || !Wsn || !ws || O <= 0 || I <= 0) return VFM_ERR_ARGS;
-    const int tb = (I + 63) / 64, rb = (O + 3) / 4;
+    const int tb = (I + TU_COLS - 1) / TU_COLS, rb = (O + 3) / 4;
     float* t = ws;
     float* r = t + I;
     float* tpart = r + O;
