@@ -366,6 +366,19 @@ int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int prec
               int K, int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
               long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
               int kchunk, int reduce_batch, void* stream);
+/* vfm_gemm8 with explicit piece strides psA / psB (elements from piece 0 to piece 1 of an operand; 0 =
+ * the stacked layouts above). Planar pieces [np][numel] of a whole fp32 tensor (vfm_split_f32 with R = 1,
+ * K = numel) are addressed through any strided view of the tensor with the view's own lda / sA (in
+ * elements, rows of K, not np K): one split of an activation serves its forward product and the
+ * weight-gradient product of the backward, one split of a weight its forward and data-gradient
+ * products (the fp32 1x1 convolutions and linears of reference networks/utils/convnext_utils.py:36-142,
+ * ldm_utils.py:55-166 with TF32 off, training/training_loop.py:504-505). Same results as vfm_gemm8 on
+ * the same pieces, bit for bit. */
+int vfm_gemm8_pieces(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype, int M,
+                     int N, int K, int batch, int a_kcont, long long lda, long long sA, long long psA, int b_kcont,
+                     long long ldb, long long sB, long long psB, long long ldc, long long sC, float alpha,
+                     float beta, int bias_mode, int act, float* workspace, int kchunk, int reduce_batch,
+                     void* stream);
 int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
                                int reduce_batch);  /* -1: too large */
 /* bf16 form of the same contract with one wave per SIMD (csrc/gemm4.hip: 256 x 256 tiles, 4 waves of

@@ -334,9 +334,43 @@ def test_gemm_batch_folded_narrow_planes(a_t, O, I, P, Bn, bias_dim):
     out = gemm_hip.try_gemm(Wv, x, bias=bias, bias_dim=bias_dim, auto=True)
     names = set(kernel_timer.summary())
     kernel_timer.enable(False)
+    if a_t and O % 4:
+        # an MN-contiguous A needs its contiguous extent (M) % 4 == 0: the caller takes its torch path
+        assert out is None
+        return
     assert out is not None and out.shape == (Bn, O, P)
     assert any(n.startswith("gemm_fold<") for n in names), names
     ref = torch.matmul(Wv.double(), x.double())
     if bias is not None:
         ref = ref + bias.double()[None, :, None]
     assert _rel(out, ref) < F32_TOL
+
+
+@pytest.mark.parametrize("a_t,b_t", [(False, True), (False, False), (True, True), (True, False)])
+@pytest.mark.parametrize("M,N,K,Z,reduce", [(520, 776, 128, 3, False), (512, 256, 1024, 4, True),
+                                            (256, 1000, 192, 1, False)])
+def test_gemm8_planar_pieces_bit_identical(a_t, b_t, M, N, K, Z, reduce, monkeypatch):
+    """Planar pieces ([3][tensor], one split per fp32 tensor, vfm_gemm8_pieces) against the per-product
+    stacked split (vfm_split_f32 along K): the same pieces and term order, so bit-identical outputs;
+    the split is reused by the transposed view and redone after an in-place update."""
+    from torch_utils.ops import gemm_hip
+    g = torch.Generator().manual_seed(M + N + K + Z)
+    A = _make((Z, K, M) if a_t else (Z, M, K), torch.float32, g)
+    B = _make((Z, N, K) if b_t else (Z, K, N), torch.float32, g)
+    Av = A.transpose(1, 2) if a_t else A
+    Bv = B.transpose(1, 2) if b_t else B
+    route = ("g8", 4) if reduce else ("g8", 0)
+    monkeypatch.setattr(gemm_hip, "PLANAR", True)
+    planar = gemm_hip.try_gemm(Av, Bv, out_dtype=torch.float32, reduce_batch=reduce, route=route)
+    assert getattr(A, "_vfm_planar", None) is not None and getattr(B, "_vfm_planar", None) is not None
+    monkeypatch.setattr(gemm_hip, "PLANAR", False)
+    stacked = gemm_hip.try_gemm(Av, Bv, out_dtype=torch.float32, reduce_batch=reduce, route=route)
+    assert torch.equal(planar, stacked)
+    ref = torch.bmm(Av.double(), Bv.double())
+    ref = ref.sum(0) if reduce else ref
+    assert _rel(planar, ref) < F32_TOL
+    # the cached split follows the tensor's version
+    monkeypatch.setattr(gemm_hip, "PLANAR", True)
+    A.mul_(0.5)
+    again = gemm_hip.try_gemm(Av, Bv, out_dtype=torch.float32, reduce_batch=reduce, route=route)
+    assert torch.equal(again, planar * 0.5)

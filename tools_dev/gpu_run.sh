@@ -32,7 +32,8 @@ for s in "$@"; do
     pwpmc)   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex pw_gemm_gelu -d $out/pwpmc -o run --output-format csv -- python3 tools_dev/pwbench.py > $out/pwpmc.log 2>&1 ;;
     g8pmc) timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $out/g8kt -o run --output-format csv -- python3 tools_dev/g8prof.py > $out/g8kt.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex gemm8_kernel -d $out/g8pmc -o run --output-format csv -- python3 tools_dev/g8prof.py > $out/g8pmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAVES TCC_HIT_sum TCC_MISS_sum --kernel-include-regex gemm8_kernel -d $out/g8pmc2 -o run --output-format csv -- python3 tools_dev/g8prof.py > $out/g8pmc2.log 2>&1 ;;
     dwmpmc) timeout -k 10 120 python tools_dev/decbench.py --only dw > $out/dwm_bench.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex dwm_fwd -d $out/dwmpmc -o run --output-format csv -- python3 tools_dev/decbench.py --only dw > $out/dwmpmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VMEM TCC_HIT_sum TCC_MISS_sum --kernel-include-regex dwm_fwd -d $out/dwmpmc2 -o run --output-format csv -- python3 tools_dev/decbench.py --only dw > $out/dwmpmc2.log 2>&1 ;;
-    r4tests) timeout -k 10 900 python -u -m pytest tests/test_gemm_gpu.py tests/test_vgg_gpu.py tests/test_style_rmsnorm_gpu.py tests/test_graphed_forward_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_decoder_gpu.py tests/test_gemm_shapes_gpu.py -m gpu -x -v --timeout 240 --timeout-method thread > $out/r4tests.log 2>&1 ;;
+    r4tests) timeout -k 10 900 python -u -m pytest tests/test_gemm_gpu.py tests/test_vgg_gpu.py tests/test_style_rmsnorm_gpu.py tests/test_graphed_forward_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_decoder_gpu.py tests/test_gemm_shapes_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests.log 2>&1 ;;
+    r4tests2) timeout -k 10 900 python -u -m pytest tests/test_graphed_forward_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_decoder_gpu.py tests/test_gemm_shapes_gpu.py -m gpu --maxfail=10 -v -s --timeout 240 --timeout-method thread > $out/r4tests2.log 2>&1 ;;
     vggbench) timeout -k 10 300 python tools_dev/vggbench.py > $out/vggbench.log 2>&1 ;;
     benchab) VFM_LPIPS_VGG=torch timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_a.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_b.log 2>&1 && VFM_LPIPS_VGG=torch timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_c.log 2>&1 ;;
     convpmc) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex conv3x3_kernel -d $out/convpmc -o run --output-format csv -- python3 tools_dev/vggbench.py > $out/convpmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-include-regex conv3x3_kernel -d $out/convpmc2 -o run --output-format csv -- python3 tools_dev/vggbench.py > $out/convpmc2.log 2>&1 ;;
@@ -70,6 +71,7 @@ for s in "$@"; do
     mlpbench) timeout -k 10 300 python tools_dev/mlpbench.py > $out/mlpbench.log 2>&1 ;;
     gc1) timeout -k 10 400 python tools_dev/graph_c1.py > $out/gc1.log 2>&1 && GC1_NORM=mm timeout -k 10 400 python tools_dev/graph_c1.py > $out/gc1_mm.log 2>&1 ;;
     opsites) timeout -k 10 600 python tools_dev/opsites.py > $out/opsites.log 2>&1 ;;
+    opsitest) OPSITES_TIME=1 timeout -k 10 600 python tools_dev/opsites.py > $out/opsites_timed.log 2>&1 ;;
     benchg) VFM_EXPERIMENTAL_GRAPHS=1 timeout -k 10 600 python bench.py --graphs --no-cpu-baseline > $out/benchg.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_e.log 2>&1 ;;
     benchst) VFM_STYLE_HIP=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_st1.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_st0.log 2>&1 ;;
     styleprof) timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $out/styleprof -o run --output-format csv -- python3 tools_dev/stylebench.py > $out/styleprof.log 2>&1 ;;

@@ -3,7 +3,7 @@
 # failure before anything ran (status=transient / exit 3). Never re-runs a
 # command that actually ran on the GPU.  Usage: gpurun_retry.sh <log> <timeout> <cmd>
 log=$1; to=$2; shift 2
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
   if [ $rc -eq 3 ] || grep -q "status=transient" "$log"; then

@@ -1,7 +1,10 @@
 """Call sites of the torch (aten) ops one training iteration runs on the GPU, by count: a
 TorchDispatchMode sees every aten call; forward calls are attributed to the innermost repo frames
 of the Python stack, backward calls to the autograd node being run and the forward stack that made
-it (anomaly mode keeps it). Ops from our own kernel library are not aten calls and do not show."""
+it (anomaly mode keeps it). Ops from our own kernel library are not aten calls and do not show.
+With OPSITES_TIME=1 each aten call is also timed on the GPU (the stream synchronised before the
+call, HIP events around it: kernel time plus ~10 us of launch latency per call) and the call sites
+are ranked by that time."""
 import collections
 import re
 import os
@@ -37,10 +40,19 @@ class Sites(TorchDispatchMode):
     def __init__(self):
         super().__init__()
         self.count = collections.Counter()
+        self.timed = os.environ.get("OPSITES_TIME") == "1"
+        self.events = collections.defaultdict(list)
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
-        out = func(*args, **(kwargs or {}))
         name = str(func)
+        ev = None
+        if self.timed and name not in SKIP:
+            torch.cuda.synchronize()
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        out = func(*args, **(kwargs or {}))
+        if ev is not None:
+            ev[1].record()
         if name in SKIP:
             return out
         t = out[0] if isinstance(out, (tuple, list)) and out else out
@@ -59,6 +71,8 @@ class Sites(TorchDispatchMode):
         else:
             where = "fwd " + _repo_frames(traceback.extract_stack())
         self.count[(name, where)] += 1
+        if ev is not None:
+            self.events[(name, where)].append(ev)
         return out
 
 
@@ -86,6 +100,17 @@ def main():
     print("by call site:", flush=True)
     for (name, where), n in mode.count.most_common(120):
         print(f"{n:5d}  {name:36s} {where}", flush=True)
+    if mode.timed:
+        ms = {k: sum(a.elapsed_time(b) for a, b in evs) for k, evs in mode.events.items()}
+        per_op_ms = collections.Counter()
+        for (name, _), t in ms.items():
+            per_op_ms[name] += t
+        print(f"GPU time of the timed aten calls: {sum(ms.values()):.2f} ms", flush=True)
+        for name, t in per_op_ms.most_common(30):
+            print(f"  {t:8.3f} ms  {name}", flush=True)
+        print("by call site (GPU ms, calls):", flush=True)
+        for (name, where), t in sorted(ms.items(), key=lambda kv: -kv[1])[:150]:
+            print(f"{t:8.3f} ms {mode.count[(name, where)]:5d}  {name:36s} {where}", flush=True)
 
 
 if __name__ == "__main__":

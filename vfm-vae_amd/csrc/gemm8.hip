@@ -67,8 +67,12 @@ struct G8Args {
     float* ws;
     int kchunk, S, reduce, Z;
     // fp32 emulation: T product terms over pieces of Kp columns (rows) each; term t reads piece
-    // (pa >> 2t) & 3 of A and (pb >> 2t) & 3 of B (T = 1, pa = pb = 0 for bf16 operands)
+    // (pa >> 2t) & 3 of A and (pb >> 2t) & 3 of B (T = 1, pa = pb = 0 for bf16 operands). Piece p of
+    // an operand starts p * psA (psB) elements after piece 0: Kp (K-contiguous [R][hi | mid | lo]),
+    // Kp * ld (MN-contiguous [hi ; mid ; lo][R]) or the element count of a whole tensor (planar
+    // pieces [NP][tensor], one split of an activation shared by its forward and backward products)
     int T, Kp, pa, pb;
+    long long psA, psB;
     // microbenchmark stamps (null in production): per block, s_memrealtime (100 MHz) at entry, after the first
     // K-tile's wait, then per item: main loop done, epilogue stores issued, stores drained
     long long* stamps;
@@ -416,10 +420,10 @@ __global__ __launch_bounds__(THREADS, 1) void gemm8_kernel(G8Args a) {
     }
     // scalar byte offsets of the current K-tile inside A / B
     auto soffs = [&](unsigned& sa, unsigned& sb) {
-        const long long ka = (long long)kk * BK + ((a.pa >> (2 * term)) & 3) * (long long)a.Kp;
-        const long long kb = (long long)kk * BK + ((a.pb >> (2 * term)) & 3) * (long long)a.Kp;
-        sa = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sA + (AK ? ka : ka * a.lda)) * 2));
-        sb = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sB + (BKC ? kb : kb * a.ldb)) * 2));
+        const long long ka = (long long)kk * BK, kb = ka;
+        const long long pofa = ((a.pa >> (2 * term)) & 3) * a.psA, pofb = ((a.pb >> (2 * term)) & 3) * a.psB;
+        sa = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sA + (AK ? ka : ka * a.lda) + pofa) * 2));
+        sb = __builtin_amdgcn_readfirstlane((unsigned)((zt * a.sB + (BKC ? kb : kb * a.ldb) + pofb) * 2));
     };
     auto advance = [&]() {                               // branch-free: selects on wave-uniform values
         const bool w0 = ++term == a.T;
@@ -719,31 +723,46 @@ static void terms_of(int np, int& T, int& pa, int& pb) {
     else pack_terms<1>(T, pa, pb);
 }
 
-extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype, int M,
-                         int N, int K, int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb,
-                         long long sB, long long ldc, long long sC, float alpha, float beta, int bias_mode, int act,
-                         float* workspace, int kchunk, int reduce_batch, void* stream) {
+// Bytes an operand with np pieces spans: the stacked layouts (ps = 0: pieces along K) or planar
+// pieces ps elements apart; -1 when the buffer descriptor cannot cover it (>= 2^31 bytes).
+static long long piece_span(int kcont, long long outer, int K, int np, long long ld, long long sb, int batch,
+                            long long ps) {
+    if (ps == 0) return span_bytes(kcont, outer, (long long)np * K, ld, sb, batch);
+    const long long one = span_bytes(kcont, outer, K, ld, sb, batch);
+    if (one < 0) return -1;
+    const long long bytes = one + (long long)(np - 1) * ps * 2;
+    return bytes >= (1LL << 31) ? -1 : bytes;
+}
+
+static int gemm8_impl(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype, int M,
+                      int N, int K, int batch, int a_kcont, long long lda, long long sA, long long psA, int b_kcont,
+                      long long ldb, long long sB, long long psB, long long ldc, long long sC, float alpha, float beta,
+                      int bias_mode, int act, float* workspace, int kchunk, int reduce_batch, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
     if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
     const int np = pieces_of(precision);
     if (!np) return VFM_ERR_ARGS;
     if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
+    if (psA < 0 || psB < 0) return VFM_ERR_ARGS;
     if (K % BK) return VFM_NO_KERNEL;
     const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
-    if (a_c % 8 || b_c % 8 || lda % 8 || ldb % 8 || sA % 8 || sB % 8) return VFM_NO_KERNEL;
+    if (a_c % 8 || b_c % 8 || lda % 8 || ldb % 8 || sA % 8 || sB % 8 || psA % 8 || psB % 8) return VFM_NO_KERNEL;
     if (((uintptr_t)A | (uintptr_t)B) % 16) return VFM_NO_KERNEL;
-    if (lda < (a_kcont ? (long long)np * K : M) || ldb < (b_kcont ? (long long)np * K : N) || ldc < N)
-        return VFM_ERR_ARGS;
+    // stacked pieces (ps = 0) lie along K inside a K-contiguous row: the row holds np K
+    const int kra = (a_kcont && !psA) ? np * K : K, krb = (b_kcont && !psB) ? np * K : K;
+    if (lda < (a_kcont ? (long long)kra : M) || ldb < (b_kcont ? (long long)krb : N) || ldc < N) return VFM_ERR_ARGS;
     const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
-    const long long spA = span_bytes(a_kcont, M, (long long)np * K, lda, sA, batch);
-    const long long spB = span_bytes(b_kcont, N, (long long)np * K, ldb, sB, batch);
+    const long long spA = piece_span(a_kcont, M, K, np, lda, sA, batch, psA);
+    const long long spB = piece_span(b_kcont, N, K, np, ldb, sB, batch, psB);
     if (spA < 0 || spB < 0) return VFM_NO_KERNEL;
     G8Args a{};
     a.stamps = g_stamps;
     a.spanA = (unsigned)spA;
     a.spanB = (unsigned)spB;
     a.Kp = K;
+    a.psA = psA ? psA : (a_kcont ? (long long)K : (long long)K * lda);
+    a.psB = psB ? psB : (b_kcont ? (long long)K : (long long)K * ldb);
     terms_of(np, a.T, a.pa, a.pb);
     a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
@@ -765,6 +784,26 @@ extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bia
     if (!a_kcont && b_kcont) VFM_G8(false, true);
     VFM_G8(false, false);
 #undef VFM_G8
+}
+
+extern "C" int vfm_gemm8(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype, int M,
+                         int N, int K, int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb,
+                         long long sB, long long ldc, long long sC, float alpha, float beta, int bias_mode, int act,
+                         float* workspace, int kchunk, int reduce_batch, void* stream) {
+    return gemm8_impl(A, B, C, bias, precision, out_dtype, M, N, K, batch, a_kcont, lda, sA, 0, b_kcont, ldb, sB, 0,
+                      ldc, sC, alpha, beta, bias_mode, act, workspace, kchunk, reduce_batch, stream);
+}
+
+// vfm_gemm8 with explicit piece strides (elements; 0 = the stacked layouts of vfm_split_f32): planar
+// pieces [NP][tensor] of an fp32 tensor (vfm_split_f32 with R = 1 over the whole tensor) addressed
+// through any strided view of it, so one split serves every product the tensor enters.
+extern "C" int vfm_gemm8_pieces(const void* A, const void* B, void* C, const float* bias, int precision, int out_dtype,
+                                int M, int N, int K, int batch, int a_kcont, long long lda, long long sA, long long psA,
+                                int b_kcont, long long ldb, long long sB, long long psB, long long ldc, long long sC,
+                                float alpha, float beta, int bias_mode, int act, float* workspace, int kchunk,
+                                int reduce_batch, void* stream) {
+    return gemm8_impl(A, B, C, bias, precision, out_dtype, M, N, K, batch, a_kcont, lda, sA, psA, b_kcont, ldb, sB,
+                      psB, ldc, sC, alpha, beta, bias_mode, act, workspace, kchunk, reduce_batch, stream);
 }
 
 // ConvNeXt-MLP 1x1 GEMMs with the GELU epilogues (gelu_epilogue above), bf16 operands and outputs:
@@ -789,7 +828,7 @@ extern "C" int vfm_gemm8_gelu(const void* W, const void* X, void* C, void* C2, c
     a.H = (const __hip_bfloat16*)H; a.rscale = rscale; a.bias = bias; a.rs0 = rsum0; a.rs1 = rsum1;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = 0; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = 1.f; a.beta = 0.f; a.bias_mode = 0; a.act = 0;
-    a.Kp = K; a.T = 1; a.pa = a.pb = 0;
+    a.Kp = K; a.T = 1; a.pa = a.pb = 0; a.psA = K; a.psB = (long long)K * ldb;
     a.Z = batch; a.reduce = 0; a.kchunk = K / BK; a.S = 1; a.ws = nullptr;
     a.stamps = g_stamps;
     const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);

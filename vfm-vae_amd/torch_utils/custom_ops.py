@@ -62,6 +62,9 @@ SIGNATURES = {
     "vfm_lpips_head_bwd_nhwc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp],
     "vfm_gemm8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
                   c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    "vfm_gemm8_pieces": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll,
+                         c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp, c_int, c_int,
+                         c_vp],
     "vfm_gemm8_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm8_set_schedule": [c_int],
     "vfm_gemm8_gelu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,

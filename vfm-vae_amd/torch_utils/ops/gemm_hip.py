@@ -75,6 +75,43 @@ def _split_f32(t3, R, K, kc, ld, sb, cache, stream):
     return res
 
 
+PLANAR = __import__("os").environ.get("VFM_PLANAR_PIECES", "1") == "1"
+
+
+def _planar(t3, stream):
+    """Planar bf16 pieces [np][numel] of the contiguous fp32 tensor that the operand view t3 covers
+    whole (a transpose / unsqueeze of it), cached on that tensor until its version moves, so one
+    split serves every product the tensor enters (an activation's forward product and the backward's
+    weight gradient, a weight's forward and data-gradient products) -> (pieces, element offset of
+    t3's origin, piece stride) or None (the per-product stacked split then applies)."""
+    if not PLANAR:
+        return None
+    base = t3._base if t3._base is not None else t3
+    n = base.numel()
+    if base.dtype != torch.float32 or not base.is_contiguous() or t3.numel() != n:
+        return None
+    prec, npc, _ = custom_ops.f32_precision()
+    off = (t3.data_ptr() - base.data_ptr()) // 4
+    if n % 8 or off % 8 or n * npc * 2 >= (1 << 31):
+        return None
+    capturing = torch.cuda.is_current_stream_capturing()
+    key = (base.data_ptr(), n, base._version, prec)
+    hit = getattr(base, "_vfm_planar", None)
+    if hit is not None and hit[0] == key and not capturing:
+        return hit[1], off, n
+    dst = torch.empty((npc, n), dtype=torch.bfloat16, device=base.device)
+    rc = _lib.vfm_split_f32(base.data_ptr(), dst.data_ptr(), 1, n, n, 0, 0, 1, prec, 1, stream)
+    if rc == custom_ops.VFM_NO_KERNEL:
+        return None
+    custom_ops.check(rc, "vfm_split_f32")
+    if not capturing:
+        try:
+            base._vfm_planar = (key, dst)
+        except AttributeError:
+            pass
+    return dst, off, n
+
+
 def preferred(A, M, N, reduce_batch=False):
     """Where this kernel family is routed (tools_dev/gemmbench.py, MI355X): fp32 operands (the
     fp32-equivalent split at >= 128-wide tiles, and the batch-reduced weight gradients at any
@@ -200,13 +237,25 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     if kern == "g8":
         # 256 tiles + LDS-DMA pipeline (csrc/gemm8.hip); fp32 operands as their bf16 pieces along
         # K, the kernel accumulating the piece products of every K-tile
+        psA = psB = 0
         if A.dtype == torch.float32:
             prec, _, tag = custom_ops.f32_precision()
-            Ak, fa_kc, flda, fsA = _split_f32(a3, M, K, a_kc, lda, sA, cache_a, stream)
-            Bk, fb_kc, fldb, fsB = _split_f32(b3, N, K, b_kc, ldb, sB, cache_b, stream)
+            # planar pieces of the whole tensor where the view covers one (shared with the other
+            # products of that tensor), else the per-product stacked split
+            pl = _planar(a3, stream)
+            if pl is not None:
+                Ak, fa_kc, flda, fsA, psA, a_off = pl[0], a_kc, lda, sA, pl[2], pl[1]
+            else:
+                (Ak, fa_kc, flda, fsA), a_off = _split_f32(a3, M, K, a_kc, lda, sA, cache_a, stream), 0
+            pl = _planar(b3, stream)
+            if pl is not None:
+                Bk, fb_kc, fldb, fsB, psB, b_off = pl[0], b_kc, ldb, sB, pl[2], pl[1]
+            else:
+                (Bk, fb_kc, fldb, fsB), b_off = _split_f32(b3, N, K, b_kc, ldb, sB, cache_b, stream), 0
         else:
             prec, tag = custom_ops.VFM_BF16, "bf16"
             Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB = a3, a_kc, lda, sA, b3, b_kc, ldb, sB
+            a_off = b_off = 0
         if Ak is not None and Bk is not None:
             kchunk = int(arg)
             ws = None
@@ -220,10 +269,10 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             if kernel_timer.SHAPES:
                 region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'k%d' % kchunk if kchunk else ''}]"
             with kernel_timer.region(region, nbytes, flops, "mfma"):
-                rc = _lib.vfm_gemm8(Ak.data_ptr(), Bk.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), prec,
-                                    _CODES[out_dtype], M, N, K, z, int(fa_kc), flda, fsA, int(fb_kc), fldb, fsB, ldc,
-                                    sC, float(alpha), float(beta), bias_mode, ACTS[act], custom_ops.ptr(ws), kchunk,
-                                    int(reduce_batch), stream)
+                rc = _lib.vfm_gemm8_pieces(Ak.data_ptr() + 2 * a_off, Bk.data_ptr() + 2 * b_off, out.data_ptr(),
+                                           custom_ops.ptr(bias), prec, _CODES[out_dtype], M, N, K, z, int(fa_kc), flda,
+                                           fsA, psA, int(fb_kc), fldb, fsB, psB, ldc, sC, float(alpha), float(beta),
+                                           bias_mode, ACTS[act], custom_ops.ptr(ws), kchunk, int(reduce_batch), stream)
             if rc != custom_ops.VFM_NO_KERNEL:
                 custom_ops.check(rc, "vfm_gemm8")
                 return out
