@@ -320,11 +320,12 @@ def test_gemm8_split_k_ragged_chunks(g8_schedule):
 @pytest.mark.parametrize("a_t", [False, True])
 @pytest.mark.parametrize("O,I,P,Bn", [(512, 512, 64, 32), (2048, 512, 64, 5), (200, 136, 16, 9), (3, 40, 8, 17)])
 @pytest.mark.parametrize("bias_dim", [None, 0])
-def test_gemm_batch_folded_narrow_planes(a_t, O, I, P, Bn, bias_dim):
+def test_gemm_batch_folded_narrow_planes(a_t, O, I, P, Bn, bias_dim, monkeypatch):
     """Shared A (1x1-conv weight, or its transpose for the data gradient) times per-sample planes of
     P < 128 columns: one batch-folded product (vfm_gemm_fold, kernel timer region gemm_fold), f32x6
     products against the fp32 reference at the fp32 tolerance."""
     from torch_utils.ops import gemm_hip, kernel_timer
+    monkeypatch.setattr(gemm_hip, "FOLD", True)          # opt-in on the network path (VFM_GEMM_FOLD=1)
     g = torch.Generator().manual_seed(O + I + P + Bn)
     W = torch.randn(I, O, generator=g).to(DEV) if a_t else torch.randn(O, I, generator=g).to(DEV)
     Wv = W.t() if a_t else W

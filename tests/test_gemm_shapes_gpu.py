@@ -15,7 +15,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("B,O,I,P", [(2, 64, 384, 196), (2, 64, 576, 196), (2, 384, 3456, 196), (3, 256, 512, 1024),
-                                     (2, 2048, 512, 64), (2, 512, 2048, 256)])
+                                     (2, 2048, 512, 64), (2, 512, 2048, 256), (4, 512, 256, 16), (4, 256, 512, 144),
+                                     (32, 2048, 512, 4)])
 def test_pointwise_autograd_shapes(B, O, I, P):
     from torch_utils.ops import decoder_ops
     g = torch.Generator().manual_seed(O + I + P)

@@ -79,6 +79,7 @@ for s in "$@"; do
     decgn) timeout -k 10 300 python tools_dev/decbench.py --only gn,dw > $out/decgn.log 2>&1 ;;
     g4abl) timeout -k 10 300 python tools_dev/g4abl.py > $out/g4abl.log 2>&1 ;;
     g4bench) timeout -k 10 400 python tools_dev/g4bench.py > $out/g4bench.log 2>&1 ;;
+    bf16bench) timeout -k 10 300 python tools_dev/bf16bench.py > $out/bf16bench.log 2>&1 ;;
     timerchk) timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $out/tchk -o run --output-format csv -- python3 tools_dev/timer_check.py > $out/timerchk.log 2>&1 ;;
     smoke)   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -45,3 +45,28 @@ for C in (512, 256, 128):
         res.append((bench(fwd), bench(fb)))
     print(f"C={C}: hip fwd {res[0][0]:7.1f} us  fwd+bwd {res[0][1]:7.1f} us | torch fwd {res[1][0]:7.1f} us  "
           f"fwd+bwd {res[1][1]:7.1f} us", flush=True)
+
+# backward per job (direct C-ABI calls, outputs switched off one at a time): launch 2 = ds tiles | dW1 outer
+# tiles, launch 3 = dA/dab outer tiles | dw tiles
+from torch_utils import custom_ops  # noqa: E402
+
+lib = custom_ops.get_native()
+st = custom_ops.stream_ptr(torch.device("cuda", 0))
+P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+for C in (512, 256, 128):
+    B, WD, O = 32, 512, 4 * C
+    f = lambda *s: torch.randn(*s, device="cuda")  # noqa: E731
+    w, A, ab, W1 = f(B, WD), f(3 * C, WD) * 0.05, f(3 * C), f(O, C) * 0.02
+    m, s, d = f(B, 3 * C), f(B, C), f(B, O).abs() + 0.5
+    ds_in, dd = f(B, C), f(B, O)
+    ds_ws, dW1, dA, dab, dw = f(B, C), f(O, C), f(3 * C, WD), f(3 * C), f(B, WD)
+    res = []
+    for tag, outs in [("all", (dW1, dA, dab, dw)), ("no dW1", (None, dA, dab, dw)), ("ds only", (None, None, None, None)),
+                      ("no dA/dab", (dW1, None, None, dw)), ("no dw", (dW1, dA, dab, None))]:
+        def fn(outs=outs):
+            rc = lib.vfm_style_demod_bwd(w.data_ptr(), WD, A.data_ptr(), W1.data_ptr(), m.data_ptr(), s.data_ptr(),
+                                         d.data_ptr(), ds_in.data_ptr(), dd.data_ptr(), 1.0, 1.0, B, C, WD, O,
+                                         ds_ws.data_ptr(), P(outs[0]), P(outs[1]), P(outs[2]), P(outs[3]), st)
+            assert rc == 0, rc
+        res.append(f"{tag} {bench(fn):6.1f}")
+    print(f"C={C} bwd us: " + " | ".join(res), flush=True)

@@ -156,7 +156,17 @@ def _tn(t):
 
 
 def weight_grad_1x1(dy, x, wdt):
-    """sum_b dy[b] @ x[b]^T in fp32 -> wdt ([O, P] x [I, P] per sample)."""
+    """sum_b dy[b] @ x[b]^T in fp32 -> wdt ([O, P] x [I, P] per sample). Planes whose P is not a
+    multiple of the 64-deep K-tile (the 2x2 .. 12x12 maps: P = 4, 16, 36, 144) would fill a fraction
+    P / 64 of every K-tile of the batch-reduced kernel (3-60 TF/s in the step, r4g shape table): those
+    are gathered once into [O, B P] / [I, B P] (a few MB) and run as one product over K = B P."""
+    B, O, P = dy.shape
+    if dy.dtype == torch.float32 and P % 64 and (B * P) % 64 == 0 and _USE_HIP_GEMM:
+        dyc = dy.permute(1, 0, 2).reshape(O, B * P)
+        xc = x.permute(1, 0, 2).reshape(x.shape[1], B * P)
+        dw = _gemm(dyc, xc.t(), out_dtype=torch.float32)
+        if dw is not None:
+            return dw.to(wdt)
     dw = _gemm(dy, x.transpose(1, 2), out_dtype=torch.float32, reduce_batch=True,
                splits=_splits(dy.shape[1], x.shape[1], dy.shape[2], dy.shape[0]))
     if dw is None:

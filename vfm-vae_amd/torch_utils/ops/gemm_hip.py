@@ -176,8 +176,8 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     K2, N = b3.shape[1], b3.shape[2]
     if K != K2:
         raise RuntimeError(f"gemm: inner dims differ ({K} vs {K2})")
-    if (auto and A.dtype == torch.float32 and not reduce_batch and splits == 1 and a3.shape[0] == 1 and z > 1
-            and FOLD_MIN <= N < 128 and (N & (N - 1)) == 0):
+    if (FOLD and auto and A.dtype == torch.float32 and not reduce_batch and splits == 1 and a3.shape[0] == 1
+            and z > 1 and FOLD_MIN <= N < 128 and (N & (N - 1)) == 0):
         # per-sample planes narrower than a tile (the 8 x 8 decoder block's 1x1 convs): one product over
         # the batch-folded N = z P columns (csrc/gemm.hip vfm_gemm_fold)
         out = _try_fold(a3, b3, M, N, K, z, out, bias, bias_dim, act, alpha, beta, out_dtype)
@@ -305,6 +305,9 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
 
 
 FOLD_MIN = 8                # narrowest per-sample plane the batch-folded product takes
+# Off by default: on the 8 x 8 block's shapes the folded product leaves 64-256 128-tiles and measured
+# 34-40 TF/s in the step against hipBLASLt's exact fp32 bmm at 43-61 (r4g bench: 10.6 vs 6.4 ms/step)
+FOLD = __import__("os").environ.get("VFM_GEMM_FOLD", "0") == "1"
 
 
 def _try_fold(a3, b3, M, N, K, z, out, bias, bias_dim, act, alpha, beta, out_dtype):
