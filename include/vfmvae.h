@@ -298,6 +298,16 @@ int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int precision, in
  * the forward weight), dx NCHW fp32 [B, C, H, W], C <= 4 (else VFM_NO_KERNEL). Deterministic. */
 int vfm_conv3x3_dgrad_small_f32(const float* dz, const float* w, float* dx, int B, int H, int W, int C, int K,
                                 void* stream);
+/* 2x2 / stride-2 max pooling of the LPIPS VGG16 stack (torchvision vgg16().features nn.MaxPool2d(2, 2),
+ * reference training/lpips.py:126-163) on NHWC fp32 [B, H, W, C] (C % 4 == 0, H and W even, 16-B
+ * aligned; else VFM_NO_KERNEL): forward without indices (torch's rule: strictly greater or NaN replaces
+ * the running max, rows then columns), and the backward fused with the tap gradient gt (NHWC, may be
+ * NULL) and the ReLU derivative of the conv below: dx = (argmax ? g : 0 + gt) * (x > 0), the argmax
+ * recomputed from the pool input x. Bit-identical to torch's max_pool2d_with_indices(_backward) + add
+ * + mask chain. */
+int vfm_maxpool2x2_nhwc_f32(const float* x, float* y, int B, int H, int W, int C, void* stream);
+int vfm_maxpool2x2_bwd_nhwc_f32(const float* g, const float* x, const float* gt, float* dx, int B, int H, int W,
+                                int C, void* stream);
 
 /* fp32 attention with gradients (replaces F.scaled_dot_product_attention on the fp32 paths of the
  * generator: fusion-adapter AttnProjection, reference networks/utils/ldm_utils.py:55-93 (encode,

@@ -109,3 +109,29 @@ def test_image_layer_input_gradient(B, H, W):
     e = _rel(out, ref)
     assert e < 2e-6, e
     assert e <= 2 * _rel(t32, ref) + 1e-7, (e, _rel(t32, ref))
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 16, 16, 64), (3, 8, 12, 128), (1, 2, 2, 4)])
+@pytest.mark.parametrize("with_tap", [True, False])
+def test_maxpool2x2_fused_bit_exact(B, H, W, C, with_tap):
+    """csrc/pool.hip against torch: the forward (no indices) equals F.max_pool2d, and the fused backward
+    (pool backward + tap gradient + ReLU derivative, argmax recomputed from the input) equals torch's
+    max_pool2d_with_indices_backward -> add -> * (x > 0) chain bit for bit, ties (ReLU zeros, repeated
+    values) included."""
+    from torch_utils.ops import vgg_hip
+    g0 = torch.Generator().manual_seed(B * H + W * C)
+    x = torch.randn(B, H, W, C, generator=g0).relu()                     # ~half zeros: all-zero windows
+    x[:, ::2, ::2, : C // 2] = x[:, 1::2, 1::2, : C // 2]                # exact ties inside windows
+    x = x.to(DEV)
+    out = vgg_hip.maxpool2x2(x)
+    ref, idx = F.max_pool2d(x.permute(0, 3, 1, 2), 2, 2, return_indices=True)
+    assert torch.equal(out, ref.permute(0, 2, 3, 1))
+    g = torch.randn(B, H // 2, W // 2, C, generator=g0).to(DEV)
+    gt = torch.randn(B, H, W, C, generator=g0).to(DEV) if with_tap else None
+    got = vgg_hip.maxpool2x2_bwd(g, x, gt)
+    r = torch.ops.aten.max_pool2d_with_indices_backward(g.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), [2, 2], [2, 2],
+                                                        [0, 0], [1, 1], False, idx).permute(0, 2, 3, 1)
+    if gt is not None:
+        r = r + gt
+    r = r * (x > 0)
+    assert torch.equal(got, r)

@@ -118,6 +118,8 @@ SIGNATURES = {
     "vfm_attention_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp, c_llp, c_float,
                           c_vp],
     "vfm_conv3x3_dgrad_small_f32": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_maxpool2x2_nhwc_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_maxpool2x2_bwd_nhwc_f32": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
     "vfm_conv3x3_nhwc_f32": [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_vp],
     "vfm_attention_f32_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp,

@@ -141,10 +141,44 @@ def forward_chain(x, prep):
         elif op[0] == 'tap':
             taps.append(h)
         else:
-            p, idx = F.max_pool2d(_nchw(h), 2, 2, return_indices=True)
-            pools.append(idx)
-            h = _nhwc(p)
+            p = maxpool2x2(h)
+            if p is not None:
+                pools.append(None)        # the backward recomputes the argmax from the pool input
+                h = p
+            else:
+                p, idx = F.max_pool2d(_nchw(h), 2, 2, return_indices=True)
+                pools.append(idx)
+                h = _nhwc(p)
     return taps, ys, pools
+
+
+def maxpool2x2(h):
+    """NHWC fp32 2x2 / stride-2 max pool on csrc/pool.hip (no indices), or None when the kernel does
+    not take the shape (odd sizes, C % 4)."""
+    B, H, W, C = h.shape
+    if not (h.is_contiguous() and h.dtype == torch.float32 and C % 4 == 0 and H % 2 == 0 and W % 2 == 0):
+        return None
+    out = torch.empty(B, H // 2, W // 2, C, dtype=torch.float32, device=h.device)
+    with kernel_timer.region("maxpool2x2_fwd<f32>", 4 * (h.numel() + out.numel())):
+        rc = _lib.vfm_maxpool2x2_nhwc_f32(h.data_ptr(), out.data_ptr(), B, H, W, C, custom_ops.stream_ptr(h.device))
+    if rc == custom_ops.VFM_NO_KERNEL:
+        return None
+    custom_ops.check(rc, "vfm_maxpool2x2_nhwc_f32")
+    return out
+
+
+def maxpool2x2_bwd(g, x, gt):
+    """(max-pool backward of g [B, H/2, W/2, C] + gt [B, H, W, C] or None) * (x > 0), NHWC fp32, with
+    the argmax recomputed from the pool input x (csrc/pool.hip; bit-identical to the torch chain)."""
+    g = g.contiguous()
+    B, H, W, C = x.shape
+    out = torch.empty_like(x)
+    nb = 4 * (2 * x.numel() + g.numel() + (x.numel() if gt is not None else 0))
+    with kernel_timer.region("maxpool2x2_bwd<f32>", nb):
+        rc = _lib.vfm_maxpool2x2_bwd_nhwc_f32(g.data_ptr(), x.data_ptr(), None if gt is None else gt.data_ptr(),
+                                              out.data_ptr(), B, H, W, C, custom_ops.stream_ptr(x.device))
+    custom_ops.check(rc, "vfm_maxpool2x2_bwd_nhwc_f32")
+    return out
 
 
 class _VGG16Taps(torch.autograd.Function):
@@ -171,9 +205,13 @@ def backward_chain(ys, pools, prep, in_shape, gtaps, conv=None):
     g = None           # gradient wrt the current NHWC activation (walking the plan backwards)
     masked = False     # g already carries the ReLU derivative of the conv that produced it
     pi = len(pools)
+    skip_tap = False   # the tap below a pool was added by the fused pool backward
     for at in range(len(PLAN) - 1, -1, -1):
         op = PLAN[at]
         if op[0] == 'tap':
+            if skip_tap:
+                skip_tap = False
+                continue
             gt = gtaps[op[1]]
             if gt is not None:
                 gt = _nhwc(gt)
@@ -181,8 +219,20 @@ def backward_chain(ys, pools, prep, in_shape, gtaps, conv=None):
                 masked = False
         elif op[0] == 'pool':
             pi -= 1
+            if (pools[pi] is None and g is not None and g.dtype == torch.float32 and PLAN[at - 1][0] == 'tap'
+                    and PLAN[at - 2][0] == 'conv'):
+                # pool backward + the tap gradient + the ReLU derivative of the conv below, one pass
+                gt = gtaps[PLAN[at - 1][1]]
+                g = maxpool2x2_bwd(g, _pool_input(ys, pi), None if gt is None else _nhwc(gt))
+                skip_tap, masked = True, True
+                continue
+            if g is None:
+                continue
+            idx = pools[pi]
+            if idx is None:    # (a plan without the tap below) the indices from the pool input
+                _, idx = F.max_pool2d(_nchw(_pool_input(ys, pi)), 2, 2, return_indices=True)
             g = _nhwc(torch.ops.aten.max_pool2d_with_indices_backward(
-                _nchw(g), _nchw(_pool_input(ys, pi)), [2, 2], [2, 2], [0, 0], [1, 1], False, pools[pi]))
+                _nchw(g), _nchw(_pool_input(ys, pi)), [2, 2], [2, 2], [0, 0], [1, 1], False, idx))
             masked = False
         elif g is not None:
             ci = op[1]
