@@ -147,12 +147,14 @@ int vfm_channel_rms_norm_bwd(const float* x, const float* gamma, const float* ri
  * networks/utils/convnext_utils.py:60-66): m = wg w A^T + bg ab [B, 3C], s = m1 m2 + m3 [B, C],
  * d = rsqrt(s^2 (W1^2)^T + eps) [B, O] (W1 null: no d). fp32; w rows ldw apart. The backward takes
  * dL/ds (ds_in) and dL/dd (dd) and writes any of dw [B, WD], dA [3C, WD], dab [3C], dW1 [O, C]
- * (null: skipped); ds_ws [B, C] is its workspace. */
+ * (null: skipped); ws is its workspace of vfm_style_demod_bwd_workspace_floats(B, C, WD, O) floats
+ * (ds and the fixed-order partial sums of the column reductions; required). */
+int vfm_style_demod_bwd_workspace_floats(int B, int C, int WD, int O);
 int vfm_style_demod_fwd(const float* w, long long ldw, const float* A, const float* ab, const float* W1, float wg,
                         float bg, float eps, int B, int C, int WD, int O, float* m, float* s, float* d, void* stream);
 int vfm_style_demod_bwd(const float* w, long long ldw, const float* A, const float* W1, const float* m,
                         const float* s, const float* d, const float* ds_in, const float* dd, float wg, float bg,
-                        int B, int C, int WD, int O, float* ds_ws, float* dW1, float* dA, float* dab, float* dw,
+                        int B, int C, int WD, int O, float* ws, float* dW1, float* dA, float* dab, float* dw,
                         void* stream);
 
 /* Spectral normalisation in training mode (torch.nn.utils.spectral_norm, one power iteration, dim 0: the

@@ -59,7 +59,7 @@ for C in (512, 256, 128):
     w, A, ab, W1 = f(B, WD), f(3 * C, WD) * 0.05, f(3 * C), f(O, C) * 0.02
     m, s, d = f(B, 3 * C), f(B, C), f(B, O).abs() + 0.5
     ds_in, dd = f(B, C), f(B, O)
-    ds_ws, dW1, dA, dab, dw = f(B, C), f(O, C), f(3 * C, WD), f(3 * C), f(B, WD)
+    ds_ws, dW1, dA, dab, dw = f(lib.vfm_style_demod_bwd_workspace_floats(B, C, WD, O)), f(O, C), f(3 * C, WD), f(3 * C), f(B, WD)
     res = []
     for tag, outs in [("all", (dW1, dA, dab, dw)), ("no dW1", (None, dA, dab, dw)), ("ds only", (None, None, None, None)),
                       ("no dA/dab", (dW1, None, None, dw)), ("no dw", (dW1, dA, dab, None))]:

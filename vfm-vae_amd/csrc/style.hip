@@ -1,5 +1,5 @@
 // Style affine + demodulation coefficients of a ConvNeXt synthesis layer, forward (two launches)
-// and backward (two launches), fp32. Reference: networks/utils/convnext_utils.py ConvNeXtBlock
+// and backward (four launches), fp32. Reference: networks/utils/convnext_utils.py ConvNeXtBlock
 // (affine_pw1 = StyleSplit(FullyConnectedLayer(w_dim, 3C)), networks/utils/shared.py StyleSplit /
 // FullyConnectedLayer, and the demodulation of ModulatedPointwiseConv2DLayer, convnext_utils.py:60-66):
 //
@@ -9,28 +9,40 @@
 //
 // torch runs this as ~9 kernels per layer forward (gain scalings, addmm, split products, squares, the
 // mm, eps, rsqrt) and ~25 in its backward. Backward, with q = -dd d^3 / 2:
-//   launch 1:  ds[b, i]  = ds_in[b, i] + 2 s[b, i] sum_o q[b, o] W1[o, i]^2
-//              dW1[o, i] = 2 W1[o, i] sum_b q[b, o] s[b, i]^2
-//   launch 2:  dm = (ds m2, ds m1, ds)  (per split part),
-//              dA[j, k] = wg sum_b dm[b, j] w[b, k],   dab[j] = bg sum_b dm[b, j],
-//              dw[b, k] = wg sum_j dm[b, j] A[j, k]
-// The products are skinny (one side is the batch, <= a few dozen rows), so there are two job shapes:
-//  * reductions over WD, C, O or 3C: 4-row x CB-column output tiles, one per wave (short K) or one per
-//    block (K >= 1024), the threads striding over k (coalesced along k), each keeping 4 x CB partial
-//    sums that are reduced across the wave with xor shuffles (and across the four waves in LDS);
-//  * reductions over the batch (dW1, dA, dab: K = B, outputs O x C and 3C x WD): 32-row x 128-column
-//    output tiles per block, the batch factors of the tile's rows (q or dm) and columns (s^2 or w) staged
-//    in LDS 32 samples at a time, each thread a 4 x 4 register tile fed by two float4 LDS reads per
-//    sample (the row factors a broadcast), float4 stores. (Round 3 had one thread per 8-wide strip
-//    looping over the batch with guarded scalar loads: 50 us per launch, 1 % of HBM.)
+//   ds[b, i]  = ds_in[b, i] + 2 s[b, i] sum_o q[b, o] W1[o, i]^2
+//   dW1[o, i] = 2 W1[o, i] sum_b q[b, o] s[b, i]^2
+//   dm = (ds m2, ds m1, ds)  (per split part),
+//   dA[j, k] = wg sum_b dm[b, j] w[b, k],   dab[j] = bg sum_b dm[b, j],
+//   dw[b, k] = wg sum_j dm[b, j] A[j, k]
+//
+// Every product is skinny: one side is the batch (B <= a few dozen), the other a weight matrix of up to
+// 2048 x 512. The kernels read each weight matrix once for the whole batch (32 samples per pass):
+//  * row dots (forward: m over the rows of A, d over the rows of W1; the reduction runs along the
+//    matrix's contiguous rows): a block owns 16 rows (48 for m: the three split parts of 16 channels) and
+//    walks K in 64-wide chunks staged in LDS (the weight rows and the batch's factors, both padded to
+//    65 floats per row: conflict-free column reads); thread (row, sample pair) keeps its sums in
+//    registers. No cross-lane reductions.
+//  * column sums over the contiguous axis (backward ds over the rows of W1^2, dw over the rows of A):
+//    a block owns 64 columns (lane = column: coalesced rows) and a 64-deep K chunk, each wave 8 samples
+//    whose factors it reads from LDS as broadcasts; the K chunks' partial sums [KS][B][N] are added in a
+//    fixed order by a small second launch (deterministic; no atomics).
+//  * outer products over the batch (dW1, dA, dab): 32-row x 128-column output tiles per block, the
+//    batch factors staged in LDS 32 samples at a time, 4 x 4 register tiles, float4 stores.
 // All sums are plain fp32 FMAs (the reference runs them in fp32 with TF32 off).
+// Round-4 per-job timings before this layout (tools_dev/stylebench.py, C = 512, B = 32): the backward's
+// ds job 30 us and dw job 20 us of 58 us (one 4-sample x 8-column tile per block: the weight matrix
+// re-read per sample group and ~200 cross-lane shuffles per tile).
 #include "vfm_common.h"
 
 namespace {
 
 using namespace vfm;
 
-constexpr int THREADS = 256, WAVES = THREADS / 64, RB = 4;
+constexpr int THREADS = 256;
+constexpr int RD_ROWS = 16;              // rows per block of the row-dot jobs
+constexpr int KCH = 64;                  // K chunk (row dots: staged; column sums: one block's K range)
+constexpr int LDP = KCH + 1;             // padded LDS row (floats)
+constexpr int SPASS = 32;                // samples per pass
 
 struct StyleArgs {
     const float* w;
@@ -45,58 +57,89 @@ struct StyleArgs {
     float* d;                             // [B, O]
     const float* dsin;                    // [B, C] or null
     const float* dd;                      // [B, O]
-    const float* dsv;                     // ds for launch 2 (the workspace of launch 1, or dsin)
-    float* ds;                            // [B, C] workspace written by launch 1
+    const float* dsv;                     // ds for the dm factors (the workspace's ds, or dsin)
+    float* ds;                            // [B, C] (workspace)
+    float* part;                          // [KS][B][N] column-sum partials (workspace)
     float* dW1;                           // [O, C] or null
     float* dA;                            // [3C, WD] or null
     float* dab;                           // [3C] or null
     float* dw;                            // [B, WD] or null
-    int blocks0;                          // blocks of the first job
-    int tpb;                              // tiles per block of the launch's tile job (1 or WAVES)
+    int blocks0;                          // blocks of the launch's first job
+    int ks;                               // K chunks of the column-sum job
 };
 
-// acc[r][c] = sum_k X(r, k) Y(c, k) over k < K: ldx(k, x[RB]) / ldy(k, y[CB]) load the operand values
-// of one k (zero outside the operand). tpb = 4 (short K): one tile per wave, its 64 lanes striding
-// over k, the partial sums reduced across the wave with xor shuffles (result in every lane).
-// tpb = 1 (long K): one tile per block, the 256 threads striding over k, the four waves' sums meeting
-// in LDS (result in wave 0). Loads are coalesced along k either way.
-template <int CB, class LX, class LY>
-__device__ __forceinline__ void tile_mm(int K, int tpb, LX ldx, LY ldy, float (&acc)[RB][CB], float* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__host__ __device__ inline int cdiv_i(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------------------------------
+// Row dots: acc[p][i] = sum_k X(b_i, k) R(rowp, k) for the block's rows, samples b_i = bp + 2 sg + i.
+// LR(row, k) / LX(b, k) give the (transformed) operand values, zero outside. NR = row groups (3 for m).
+template <int NR, class LR, class LX>
+__device__ __forceinline__ void row_dots(int K, int bp, LR lr, LX lx, float (&acc)[NR][2], float* rs, float* xs) {
+    const int t = threadIdx.x, r = t & (RD_ROWS - 1), sg = t >> 4;
 #pragma unroll
-    for (int r = 0; r < RB; ++r)
+    for (int p = 0; p < NR; ++p) acc[p][0] = acc[p][1] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += KCH) {
+        __syncthreads();
+        // weight rows: NR * 16 rows x 64 k; batch factors: 32 samples x 64 k (consecutive threads along k)
+        for (int e = t; e < NR * RD_ROWS * KCH; e += THREADS) {
+            const int row = e / KCH, k = e - row * KCH;
+            rs[row * LDP + k] = lr(row, k0 + k);
+        }
+        for (int e = t; e < SPASS * KCH; e += THREADS) {
+            const int b = e / KCH, k = e - b * KCH;
+            xs[b * LDP + k] = lx(bp + b, k0 + k);
+        }
+        __syncthreads();
+        const int kn = min(KCH, K - k0);
+#pragma unroll 4
+        for (int k = 0; k < kn; ++k) {
+            const float x0 = xs[(2 * sg) * LDP + k], x1 = xs[(2 * sg + 1) * LDP + k];
 #pragma unroll
-        for (int c = 0; c < CB; ++c) acc[r][c] = 0.f;
-    const int step = tpb == 1 ? THREADS : 64;
-#pragma unroll 2
-    for (int k = tpb == 1 ? (int)threadIdx.x : lane; k < K; k += step) {
-        float x[RB], y[CB];
-        ldx(k, x);
-        ldy(k, y);
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int c = 0; c < CB; ++c) acc[r][c] = fmaf(x[r], y[c], acc[r][c]);
+            for (int p = 0; p < NR; ++p) {
+                const float v = rs[(p * RD_ROWS + r) * LDP + k];
+                acc[p][0] = fmaf(x0, v, acc[p][0]);
+                acc[p][1] = fmaf(x1, v, acc[p][1]);
+            }
+        }
     }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Column sums: part[ks][b][n] = sum_{k in chunk ks} X(b, k) Y(k, n) for the block's 64 columns, all samples
+// (passes of 32: wave wv takes samples bp + 8 wv .. + 7). LX(b, k) / LY(k, n) as above.
+template <class LX, class LY>
+__device__ __forceinline__ void col_sums(int K, int N, int B, int strip, int ks, LX lx, LY ly, float* part,
+                                         float* xs) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int n = strip * 64 + lane, k0 = ks * KCH, kn = min(KCH, K - k0);
+    for (int bp = 0; bp < B; bp += SPASS) {
+        __syncthreads();
+        for (int e = t; e < SPASS * KCH; e += THREADS) {        // xs[k][b]: a wave's 8 samples contiguous
+            const int b = e / KCH, k = e - b * KCH;
+            xs[k * (SPASS + 4) + b] = k < kn ? lx(bp + b, k0 + k) : 0.f;
+        }
+        __syncthreads();
+        float acc[8];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        if (n < N) {
+#pragma unroll 8
+            for (int k = 0; k < kn; ++k) {
+                const float y = ly(k0 + k, n);
+                const float4 xa = *reinterpret_cast<const float4*>(xs + k * (SPASS + 4) + 8 * wv);
+                const float4 xb = *reinterpret_cast<const float4*>(xs + k * (SPASS + 4) + 8 * wv + 4);
+                acc[0] = fmaf(xa.x, y, acc[0]); acc[1] = fmaf(xa.y, y, acc[1]);
+                acc[2] = fmaf(xa.z, y, acc[2]); acc[3] = fmaf(xa.w, y, acc[3]);
+                acc[4] = fmaf(xb.x, y, acc[4]); acc[5] = fmaf(xb.y, y, acc[5]);
+                acc[6] = fmaf(xb.z, y, acc[6]); acc[7] = fmaf(xb.w, y, acc[7]);
+            }
 #pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int c = 0; c < CB; ++c) acc[r][c] += __shfl_xor(acc[r][c], o, 64);
-    if (tpb != 1) return;
-    if (wave > 0 && lane == 0)
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int c = 0; c < CB; ++c) red[((wave - 1) * RB + r) * CB + c] = acc[r][c];
-    __syncthreads();
-    if (wave == 0)
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int c = 0; c < CB; ++c)
-                acc[r][c] += (red[r * CB + c] + red[(RB + r) * CB + c]) + red[(2 * RB + r) * CB + c];
+            for (int i = 0; i < 8; ++i) {
+                const int b = bp + 8 * wv + i;
+                if (b < B) part[((long long)ks * B + b) * N + n] = acc[i];
+            }
+        }
+    }
 }
 
 __device__ __forceinline__ float dm_at(const StyleArgs& a, int b, int j) {
@@ -112,6 +155,7 @@ __device__ __forceinline__ float q_at(const StyleArgs& a, int b, int o) {
     return -0.5f * a.dd[i] * dv * dv * dv;
 }
 
+// ---------------------------------------------------------------------------------------------------
 // out[r][c] = sum_b X(b, r) Y(b, c) over b < B for the block's 32 x 128 tile (r0, c0): X / Y give the
 // batch factors (zero outside). Thread t owns rows r0 + 4 (t >> 5) .. + 3, columns c0 + 4 (t & 31) .. + 3;
 // rsum (if non-null) gets sum_b X(b, r) of the thread's 4 rows. Staging: xs [32 b][32 r], ys [32 b][128 c].
@@ -128,7 +172,6 @@ __device__ __forceinline__ void outer_tile(int B, FX X, FY Y, float (&acc)[4][4]
     }
     for (int b0 = 0; b0 < B; b0 += OT_B) {
         __syncthreads();
-        // X: 32 x 32 values, 4 per thread (b = t >> 3, r = 4 (t & 7) ..); Y: 32 x 128, 16 per thread
         {
             const int b = t >> 3, r = 4 * (t & 7);
             float4 v = X(b0 + b, r);
@@ -176,151 +219,121 @@ __device__ __forceinline__ void store4(float* p, long long ld, int r, int rows, 
     for (int j = 0; j < 4 && c + j < cols; ++j) q[j] = vv[j];
 }
 
-// LAUNCH 0 (tiles): m, s   — 4 samples x 4 channels (x 3 split parts) per tile, k < WD
-// LAUNCH 1 (tiles): d      — 4 samples x 8 outputs per tile, k < C
-// LAUNCH 2: ds (tiles: 4 samples x 8 channels, k < O) | dW1 (threads: 8-channel strips, b < B)
-// LAUNCH 3: dA + dab (threads: 8-column strips, b < B) | dw (tiles: 4 samples x 8 columns, k < 3C)
+// LAUNCH 0: m, s   — row dots over A's three split parts of 16 channels (blocks: C / 16)
+// LAUNCH 1: d      — row dots over 16 rows of W1 (blocks: O / 16)
+// LAUNCH 2: ds partials (column sums over W1^2, blocks0 = strips x K chunks) | dW1 (outer tiles)
+// LAUNCH 3: dA + dab (outer tiles, blocks0) | dw partials (column sums over A)
+// LAUNCH 4: ds = ds_in + 2 s sum(partials)          LAUNCH 5: dw = wg sum(partials)
 template <int LAUNCH>
 __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
-    __shared__ float red[(WAVES - 1) * RB * 3 * 4];
+    __shared__ __attribute__((aligned(16))) float smem[3 * RD_ROWS * LDP + SPASS * LDP];
     const bool second = (int)blockIdx.x >= a.blocks0;
     const int blk = second ? blockIdx.x - a.blocks0 : blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // tile jobs: one tile per block (tpb = 1) or per wave (tpb = 4); the result sits in lane `idx` of
-    // wave 0 (tpb = 1) or of every wave (tpb = 4)
-    const long long wunit = a.tpb == 1 ? (long long)blk : (long long)blk * WAVES + wave;
-    const bool owner0 = a.tpb != 1 || wave == 0;
     const int C = a.C, C3 = 3 * a.C, WD = a.WD, O = a.O, B = a.B;
-    const int nbg = (B + RB - 1) / RB;                                 // 4-sample groups
+    const int t = threadIdx.x, r = t & (RD_ROWS - 1), sg = t >> 4;
 
     if (LAUNCH == 0) {
-        constexpr int CC = 4;
-        if (wunit >= (long long)nbg * ((C + CC - 1) / CC)) return;
-        const int b0 = (int)(wunit % nbg) * RB, c0 = (int)(wunit / nbg) * CC;
-        float acc[RB][3 * CC];
-        tile_mm<3 * CC>(WD, a.tpb,
-            [&](int k, float (&x)[RB]) {
-#pragma unroll
-                for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? a.w[(long long)(b0 + r) * a.ldw + k] : 0.f;
-            },
-            [&](int k, float (&y)[3 * CC]) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-#pragma unroll
-                    for (int c = 0; c < CC; ++c)
-                        y[p * CC + c] = c0 + c < C ? a.A[(long long)(p * C + c0 + c) * WD + k] : 0.f;
-            }, acc, red);
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int c = 0; c < CC; ++c) {
-                const int b = b0 + r, cc = c0 + c;
-                if (!owner0 || lane != r * CC + c || b >= B || cc >= C) continue;
-                const float m1 = fmaf(a.wg, acc[r][c], a.bg * a.ab[cc]);
-                const float m2 = fmaf(a.wg, acc[r][CC + c], a.bg * a.ab[C + cc]);
-                const float m3 = fmaf(a.wg, acc[r][2 * CC + c], a.bg * a.ab[2 * C + cc]);
-                float* mb = a.m + (long long)b * C3;
-                mb[cc] = m1; mb[C + cc] = m2; mb[2 * C + cc] = m3;
-                a.s[(long long)b * C + cc] = fmaf(m1, m2, m3);
-            }
-    } else if (LAUNCH == 1) {
-        constexpr int CB = 8;
-        if (wunit >= (long long)nbg * ((O + CB - 1) / CB)) return;
-        const int b0 = (int)(wunit % nbg) * RB, o0 = (int)(wunit / nbg) * CB;
-        float acc[RB][CB];
-        tile_mm<CB>(C, a.tpb,
-            [&](int k, float (&x)[RB]) {
-#pragma unroll
-                for (int r = 0; r < RB; ++r) {
-                    const float v = b0 + r < B ? a.s[(long long)(b0 + r) * C + k] : 0.f;
-                    x[r] = v * v;
-                }
-            },
-            [&](int k, float (&y)[CB]) {
-#pragma unroll
-                for (int c = 0; c < CB; ++c) {
-                    const float v = o0 + c < O ? a.W1[(long long)(o0 + c) * C + k] : 0.f;
-                    y[c] = v * v;
-                }
-            }, acc, red);
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int c = 0; c < CB; ++c)
-                if (owner0 && lane == r * CB + c && b0 + r < B && o0 + c < O)
-                    a.d[(long long)(b0 + r) * O + o0 + c] = rsqrtf(acc[r][c] + a.eps);
-    } else if (LAUNCH == 2) {
-        if (!second) {            // ds [B, C]: waves, k < O
-            constexpr int CB = 8;
-            if (wunit >= (long long)nbg * ((C + CB - 1) / CB)) return;
-            const int b0 = (int)(wunit % nbg) * RB, i0 = (int)(wunit / nbg) * CB;
-            float acc[RB][CB];
-            tile_mm<CB>(O, a.tpb,
-                [&](int k, float (&x)[RB]) {
-#pragma unroll
-                    for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? q_at(a, b0 + r, k) : 0.f;
+        const int c0 = blk * RD_ROWS;
+        float* rs = smem;
+        float* xs = smem + 3 * RD_ROWS * LDP;
+        for (int bp = 0; bp < B; bp += SPASS) {
+            float acc[3][2];
+            row_dots<3>(WD, bp,
+                [&](int row, int k) {
+                    const int p = row / RD_ROWS, c = c0 + row - p * RD_ROWS;
+                    return (c < C && k < WD) ? a.A[(long long)(p * C + c) * WD + k] : 0.f;
                 },
-                [&](int k, float (&y)[CB]) {
-                    const float* row = a.W1 + (long long)k * C + i0;
+                [&](int b, int k) { return (b < B && k < WD) ? a.w[(long long)b * a.ldw + k] : 0.f; }, acc, rs, xs);
+            const int c = c0 + r;
 #pragma unroll
-                    for (int c = 0; c < CB; ++c) {
-                        const float v = i0 + c < C ? row[c] : 0.f;
-                        y[c] = v * v;
-                    }
-                }, acc, red);
+            for (int i = 0; i < 2; ++i) {
+                const int b = bp + 2 * sg + i;
+                if (b >= B || c >= C) continue;
+                const float m1 = fmaf(a.wg, acc[0][i], a.bg * a.ab[c]);
+                const float m2 = fmaf(a.wg, acc[1][i], a.bg * a.ab[C + c]);
+                const float m3 = fmaf(a.wg, acc[2][i], a.bg * a.ab[2 * C + c]);
+                float* mb = a.m + (long long)b * C3;
+                mb[c] = m1; mb[C + c] = m2; mb[2 * C + c] = m3;
+                a.s[(long long)b * C + c] = fmaf(m1, m2, m3);
+            }
+        }
+    } else if (LAUNCH == 1) {
+        const int o0 = blk * RD_ROWS;
+        float* rs = smem;
+        float* xs = smem + RD_ROWS * LDP;
+        for (int bp = 0; bp < B; bp += SPASS) {
+            float acc[1][2];
+            row_dots<1>(C, bp,
+                [&](int row, int k) {
+                    const float v = (o0 + row < O && k < C) ? a.W1[(long long)(o0 + row) * C + k] : 0.f;
+                    return v * v;
+                },
+                [&](int b, int k) {
+                    const float v = (b < B && k < C) ? a.s[(long long)b * C + k] : 0.f;
+                    return v * v;
+                }, acc, rs, xs);
+            const int o = o0 + r;
 #pragma unroll
-            for (int r = 0; r < RB; ++r)
-#pragma unroll
-                for (int c = 0; c < CB; ++c) {
-                    const int b = b0 + r, i = i0 + c;
-                    if (!owner0 || lane != r * CB + c || b >= B || i >= C) continue;
-                    const long long o = (long long)b * C + i;
-                    a.ds[o] = (a.dsin ? a.dsin[o] : 0.f) + 2.f * a.s[o] * acc[r][c];
-                }
+            for (int i = 0; i < 2; ++i) {
+                const int b = bp + 2 * sg + i;
+                if (b < B && o < O) a.d[(long long)b * O + o] = rsqrtf(acc[0][i] + a.eps);
+            }
+        }
+    } else if (LAUNCH == 2) {
+        if (!second) {            // ds partials: sum_o q[b, o] W1[o, i]^2 over the block's 64-deep o chunk
+            const int strips = cdiv_i(C, 64);
+            col_sums(O, C, B, blk % strips, blk / strips,
+                [&](int b, int k) { return b < B ? q_at(a, b, k) : 0.f; },
+                [&](int k, int n) {
+                    const float v = a.W1[(long long)k * C + n];
+                    return v * v;
+                }, a.part, smem);
         } else {                  // dW1 [O, C] = 2 W1 (Q^T S^2): outer tiles over the batch
-            __shared__ __attribute__((aligned(16))) float xs[OT_B * OT_R], ys[OT_B * OT_C];
+            float* xs = smem;
+            float* ys = smem + OT_B * OT_R;
             const int tn = (C + OT_C - 1) / OT_C;
             const int o0 = (blk / tn) * OT_R, i0 = (blk % tn) * OT_C;
             const bool vec = (C % 4) == 0;
-            float acc[4][4], rs[4];
+            float acc[4][4], rsm[4];
             outer_tile(B,
-                [&](int b, int r) {
+                [&](int b, int rr) {
                     float v[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = (b < B && o0 + r + j < O) ? q_at(a, b, o0 + r + j) : 0.f;
+                    for (int j = 0; j < 4; ++j) v[j] = (b < B && o0 + rr + j < O) ? q_at(a, b, o0 + rr + j) : 0.f;
                     return make_float4(v[0], v[1], v[2], v[3]);
                 },
                 [&](int b, int c) {
                     float4 v = b < B ? load4(a.s, C, b, B, i0 + c, C, vec) : make_float4(0.f, 0.f, 0.f, 0.f);
                     return make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
-                }, acc, rs, xs, ys);
-            const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+                }, acc, rsm, xs, ys);
+            const int ty = t >> 5, tx = t & 31;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int o = o0 + 4 * ty + i, c = i0 + 4 * tx;
-                const float4 w = load4(a.W1, C, o, O, c, C, vec);
+                const float4 wv = load4(a.W1, C, o, O, c, C, vec);
                 store4(a.dW1, C, o, O, c, C, vec,
-                       make_float4(2.f * w.x * acc[i][0], 2.f * w.y * acc[i][1], 2.f * w.z * acc[i][2],
-                                   2.f * w.w * acc[i][3]));
+                       make_float4(2.f * wv.x * acc[i][0], 2.f * wv.y * acc[i][1], 2.f * wv.z * acc[i][2],
+                                   2.f * wv.w * acc[i][3]));
             }
         }
-    } else {
+    } else if (LAUNCH == 3) {
         if (!second) {            // dA [3C, WD] = wg dm^T w, dab [3C] = bg sum_b dm: outer tiles over the batch
-            __shared__ __attribute__((aligned(16))) float xs[OT_B * OT_R], ys[OT_B * OT_C];
+            float* xs = smem;
+            float* ys = smem + OT_B * OT_R;
             const int tn = (WD + OT_C - 1) / OT_C;
             const int j0 = (blk / tn) * OT_R, k0 = (blk % tn) * OT_C;
             const bool vec = (WD % 4) == 0 && (a.ldw % 4) == 0 && (reinterpret_cast<uintptr_t>(a.w) % 16) == 0;
-            float acc[4][4], rs[4];
+            float acc[4][4], rsm[4];
             outer_tile(B,
-                [&](int b, int r) {
+                [&](int b, int rr) {
                     float v[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = (b < B && j0 + r + j < C3) ? dm_at(a, b, j0 + r + j) : 0.f;
+                    for (int j = 0; j < 4; ++j) v[j] = (b < B && j0 + rr + j < C3) ? dm_at(a, b, j0 + rr + j) : 0.f;
                     return make_float4(v[0], v[1], v[2], v[3]);
                 },
                 [&](int b, int c) { return b < B ? load4(a.w, a.ldw, b, B, k0 + c, WD, vec) : make_float4(0.f, 0.f, 0.f, 0.f); },
-                acc, rs, xs, ys);
-            const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+                acc, rsm, xs, ys);
+            const int ty = t >> 5, tx = t & 31;
             const bool dvec = (WD % 4) == 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -328,37 +341,29 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
                 if (a.dA)
                     store4(a.dA, WD, j, C3, k0 + 4 * tx, WD, dvec,
                            make_float4(a.wg * acc[i][0], a.wg * acc[i][1], a.wg * acc[i][2], a.wg * acc[i][3]));
-                if (a.dab && k0 == 0 && tx == 0 && j < C3) a.dab[j] = a.bg * rs[i];
+                if (a.dab && k0 == 0 && tx == 0 && j < C3) a.dab[j] = a.bg * rsm[i];
             }
-        } else {                  // dw [B, WD]: waves, k < 3C
-            constexpr int CB = 8;
-            if (wunit >= (long long)nbg * ((WD + CB - 1) / CB)) return;
-            const int b0 = (int)(wunit % nbg) * RB, n0 = (int)(wunit / nbg) * CB;
-            float acc[RB][CB];
-            tile_mm<CB>(C3, a.tpb,
-                [&](int k, float (&x)[RB]) {
-#pragma unroll
-                    for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? dm_at(a, b0 + r, k) : 0.f;
-                },
-                [&](int k, float (&y)[CB]) {
-                    const float* row = a.A + (long long)k * WD + n0;
-#pragma unroll
-                    for (int c = 0; c < CB; ++c) y[c] = n0 + c < WD ? row[c] : 0.f;
-                }, acc, red);
-#pragma unroll
-            for (int r = 0; r < RB; ++r)
-#pragma unroll
-                for (int c = 0; c < CB; ++c)
-                    if (owner0 && lane == r * CB + c && b0 + r < B && n0 + c < WD)
-                        a.dw[(long long)(b0 + r) * WD + n0 + c] = a.wg * acc[r][c];
+        } else {                  // dw partials: sum_j dm[b, j] A[j, n] over the block's 64-deep j chunk
+            const int strips = cdiv_i(WD, 64);
+            col_sums(C3, WD, B, blk % strips, blk / strips,
+                [&](int b, int k) { return b < B ? dm_at(a, b, k) : 0.f; },
+                [&](int k, int n) { return a.A[(long long)k * WD + n]; }, a.part, smem);
         }
+    } else if (LAUNCH == 4) {     // ds = ds_in + 2 s sum_ks part (fixed order)
+        const long long i = (long long)blockIdx.x * THREADS + t;
+        if (i >= (long long)B * C) return;
+        float acc = 0.f;
+        for (int k = 0; k < a.ks; ++k) acc += a.part[(long long)k * B * C + i];
+        a.ds[i] = (a.dsin ? a.dsin[i] : 0.f) + 2.f * a.s[i] * acc;
+    } else {                      // dw = wg sum_ks part (fixed order)
+        const long long i = (long long)blockIdx.x * THREADS + t;
+        if (i >= (long long)B * WD) return;
+        float acc = 0.f;
+        for (int k = 0; k < a.ks; ++k) acc += a.part[(long long)k * B * WD + i];
+        const long long b = i / WD, n = i - b * WD;
+        a.dw[b * WD + n] = a.wg * acc;
     }
 }
-
-inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
-
-// tiles per block for a reduction of length K: the whole block on one tile from K >= 1024 on
-inline int tiles_per_block(int K) { return K >= 1024 ? 1 : WAVES; }
 
 template <int L>
 int launch(StyleArgs& a, long long blocks, hipStream_t st) {
@@ -373,6 +378,14 @@ bool sizes_ok(int B, int C, int WD, int O) {
            (long long)O * C < (1LL << 31) && (long long)3 * C * WD < (1LL << 31);
 }
 
+// K chunks of the backward's column sums and the floats of their partials
+inline int ks_ds(int O) { return cdiv_i(O, KCH); }
+inline int ks_dw(int C) { return cdiv_i(3LL * C, KCH); }
+inline long long part_floats(int B, int C, int WD, int O) {
+    const long long pds = O > 0 ? (long long)ks_ds(O) * B * C : 0, pdw = (long long)ks_dw(C) * B * WD;
+    return pds > pdw ? pds : pdw;
+}
+
 }  // namespace
 
 // m [B, 3C], s [B, C] and (W1 given) d [B, O] of the layer's style path (see the header).
@@ -385,48 +398,56 @@ extern "C" int vfm_style_demod_fwd(const float* w, long long ldw, const float* A
     a.w = w; a.ldw = ldw; a.A = A; a.ab = ab; a.W1 = W1; a.wg = wg; a.bg = bg; a.eps = eps;
     a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = m; a.s = s; a.d = d;
     hipStream_t st = (hipStream_t)stream;
-    const long long nbg = cdiv(B, RB);
-    a.tpb = tiles_per_block(WD);
-    a.blocks0 = (int)cdiv(nbg * cdiv(C, 4), a.tpb);
+    a.blocks0 = cdiv_i(C, RD_ROWS);
     int rc = launch<0>(a, a.blocks0, st);
     if (rc || !W1) return rc;
-    a.tpb = tiles_per_block(C);
-    a.blocks0 = (int)cdiv(nbg * cdiv(O, 8), a.tpb);
+    a.blocks0 = cdiv_i(O, RD_ROWS);
     return launch<1>(a, a.blocks0, st);
 }
 
+// Workspace floats of vfm_style_demod_bwd: ds [B, C] and the column-sum partials.
+extern "C" int vfm_style_demod_bwd_workspace_floats(int B, int C, int WD, int O) {
+    if (!sizes_ok(B, C, WD, O)) return -1;
+    const long long n = (long long)B * C + part_floats(B, C, WD, O);
+    return n > 0x7fffffffLL ? -1 : (int)n;
+}
+
 // Gradients of the style path from ds_in = dL/ds (or null) and dd = dL/dd (null without demodulation):
-// dw [B, WD], dA [3C, WD], dab [3C], dW1 [O, C], each optional (null: not computed). ds_ws [B, C] is a
-// workspace (required when dd is given).
+// dw [B, WD], dA [3C, WD], dab [3C], dW1 [O, C], each optional (null: not computed). ws: workspace of
+// vfm_style_demod_bwd_workspace_floats floats (required).
 extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A, const float* W1, const float* m,
                                    const float* s, const float* d, const float* ds_in, const float* dd, float wg,
-                                   float bg, int B, int C, int WD, int O, float* ds_ws, float* dW1, float* dA,
+                                   float bg, int B, int C, int WD, int O, float* ws, float* dW1, float* dA,
                                    float* dab, float* dw, void* stream) {
-    if (!w || !A || !m || !s || !sizes_ok(B, C, WD, O) || ldw < WD) return VFM_ERR_ARGS;
+    if (!w || !A || !m || !s || !ws || !sizes_ok(B, C, WD, O) || ldw < WD) return VFM_ERR_ARGS;
     const bool demod = dd != nullptr;
-    if (demod && (!W1 || !d || !ds_ws || O <= 0)) return VFM_ERR_ARGS;
+    if (demod && (!W1 || !d || O <= 0)) return VFM_ERR_ARGS;
     if (!demod && (dW1 || !ds_in)) return VFM_ERR_ARGS;
     StyleArgs a{};
     a.w = w; a.ldw = ldw; a.A = A; a.W1 = W1; a.wg = wg; a.bg = bg;
     a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = const_cast<float*>(m); a.s = const_cast<float*>(s);
-    a.d = const_cast<float*>(d); a.dsin = ds_in; a.dd = dd; a.ds = ds_ws; a.dW1 = dW1; a.dA = dA; a.dab = dab;
-    a.dw = dw;
+    a.d = const_cast<float*>(d); a.dsin = ds_in; a.dd = dd; a.ds = ws; a.part = ws + (long long)B * C;
+    a.dW1 = dW1; a.dA = dA; a.dab = dab; a.dw = dw;
     hipStream_t st = (hipStream_t)stream;
-    const long long nbg = cdiv(B, RB);
     if (demod) {
-        a.tpb = tiles_per_block(O);
-        a.blocks0 = (int)cdiv(nbg * cdiv(C, 8), a.tpb);
-        const long long b1 = dW1 ? cdiv(O, OT_R) * cdiv(C, OT_C) : 0;
-        const int rc = launch<2>(a, a.blocks0 + b1, st);
+        a.ks = ks_ds(O);
+        a.blocks0 = cdiv_i(C, 64) * a.ks;
+        const long long b1 = dW1 ? (long long)cdiv_i(O, OT_R) * cdiv_i(C, OT_C) : 0;
+        int rc = launch<2>(a, a.blocks0 + b1, st);
         if (rc) return rc;
-        a.dsv = ds_ws;
+        a.blocks0 = 0;
+        rc = launch<4>(a, cdiv_i((long long)B * C, THREADS), st);
+        if (rc) return rc;
+        a.dsv = a.ds;
     } else {
         a.dsv = ds_in;
     }
     if (!dA && !dab && !dw) return 0;
-    a.blocks0 = (dA || dab) ? (int)(cdiv(3LL * C, OT_R) * cdiv(WD, OT_C)) : 0;
-    const int C3 = 3 * C;
-    a.tpb = tiles_per_block(C3);
-    const long long b1 = dw ? cdiv(nbg * cdiv(WD, 8), a.tpb) : 0;
-    return launch<3>(a, a.blocks0 + b1, st);
+    a.ks = ks_dw(C);
+    a.blocks0 = (dA || dab) ? cdiv_i(3LL * C, OT_R) * cdiv_i(WD, OT_C) : 0;
+    const long long b1 = dw ? (long long)cdiv_i(WD, 64) * a.ks : 0;
+    int rc = launch<3>(a, a.blocks0 + b1, st);
+    if (rc || !dw) return rc;
+    a.blocks0 = 0;
+    return launch<5>(a, cdiv_i((long long)B * WD, THREADS), st);
 }

@@ -76,6 +76,7 @@ SIGNATURES = {
     "vfm_channel_rms_norm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp],
     "vfm_style_demod_fwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_float, c_float, c_float, c_int, c_int, c_int, c_int,
                             c_vp, c_vp, c_vp, c_vp],
+    "vfm_style_demod_bwd_workspace_floats": [c_int, c_int, c_int, c_int],
     "vfm_style_demod_bwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_int, c_int,
                             c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "vfm_dwconv2d_fwd_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

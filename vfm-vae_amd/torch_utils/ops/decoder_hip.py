@@ -977,7 +977,7 @@ class _StyleDemod(torch.autograd.Function):
         ds_in = _c(ds_in.float()) if ds_in is not None else torch.zeros([B, C], **f32)
         if d is not None:
             dd = _c(dd.float()) if dd is not None else torch.zeros([B, O], **f32)
-        ds_ws = torch.empty([B, C], **f32) if d is not None else None
+        ds_ws = torch.empty([max(1, _lib.vfm_style_demod_bwd_workspace_floats(B, C, WD, O))], **f32)
         dW1 = torch.empty([O, C], **f32) if want_W1 else None
         dA = torch.empty([3 * C, WD], **f32) if want_A else None
         dab = torch.empty([3 * C], **f32) if want_ab else None
