@@ -45,6 +45,8 @@ def analyse(path, steps):
     tr = json.load(open(path))
     evs = tr["traceEvents"] if isinstance(tr, dict) else tr
     gpu, py = [], collections.defaultdict(list)
+    cats = collections.Counter(e.get("cat", "") for e in evs if e.get("ph") == "X")
+    print("event categories:", dict(cats.most_common(12)), flush=True)
     for e in evs:
         if e.get("ph") != "X":
             continue
@@ -52,8 +54,9 @@ def analyse(path, steps):
         ts, dur = float(e.get("ts", 0)), float(e.get("dur", 0))
         if cat in ("kernel", "gpu_memcpy", "gpu_memset"):
             gpu.append((ts, ts + dur))
-        elif cat == "python_function":
-            py[e.get("tid")].append((ts, ts + dur, e.get("name", "")))
+        elif cat in ("python_function", "cpu_op", "user_annotation"):
+            name = e.get("name", "")
+            py[e.get("tid")].append((ts, ts + dur, name if cat == "python_function" else f"[{cat}] {name}"))
     gpu.sort()
     busy, merged = 0.0, []
     for s, t in gpu:
@@ -75,6 +78,7 @@ def analyse(path, steps):
             samples.append(t)
             t += DT
     repo = lambda n: ("vfm-vae_amd" in n or "bench.py" in n or "/training/" in n) and "tools_dev" not in n  # noqa: E731
+    print("host events per thread:", {t: len(v) for t, v in py.items()}, flush=True)
     for tid, lst in py.items():
         lst.sort(key=lambda x: (x[0], -x[1]))
         incl, excl = collections.Counter(), collections.Counter()
@@ -88,7 +92,10 @@ def analyse(path, steps):
                 i += 1
             while stack and stack[-1][1] < t:
                 stack.pop()
-            frames = [e[2] for e in stack if e[1] >= t and repo(e[2])]
+            live = [e[2] for e in stack if e[1] >= t]
+            frames = [f for f in live if repo(f)]
+            if live and live[-1].startswith("["):       # the innermost event is an op: keep it as the leaf
+                frames.append(live[-1])
             if not frames:
                 continue
             hit += 1

@@ -17,11 +17,11 @@
 //
 // Every product is skinny: one side is the batch (B <= a few dozen), the other a weight matrix of up to
 // 2048 x 512. The kernels read each weight matrix once for the whole batch (32 samples per pass):
-//  * row dots (forward: m over the rows of A, d over the rows of W1; the reduction runs along the
-//    matrix's contiguous rows): a block owns 16 rows (48 for m: the three split parts of 16 channels) and
-//    walks K in 64-wide chunks staged in LDS (the weight rows and the batch's factors, both padded to
-//    65 floats per row: conflict-free column reads); thread (row, sample pair) keeps its sums in
-//    registers. No cross-lane reductions.
+//  * forward reductions along the contiguous rows (m over the rows of A, d over the rows of W1): 4-sample
+//    x CB-row tiles, one per wave (K < 1024) or per block, lanes striding over k (coalesced), the
+//    partial sums reduced across the wave with xor shuffles. (A whole-batch form with the rows staged
+//    in LDS, 32 blocks at C = 512, measured 74 us against this form's 24 us: too few waves in flight
+//    to cover the load latency.)
 //  * column sums over the contiguous axis (backward ds over the rows of W1^2, dw over the rows of A):
 //    a block owns 64 columns (lane = column: coalesced rows) and a 64-deep K chunk, each wave 8 samples
 //    whose factors it reads from LDS as broadcasts; the K chunks' partial sums [KS][B][N] are added in a
@@ -29,20 +29,18 @@
 //  * outer products over the batch (dW1, dA, dab): 32-row x 128-column output tiles per block, the
 //    batch factors staged in LDS 32 samples at a time, 4 x 4 register tiles, float4 stores.
 // All sums are plain fp32 FMAs (the reference runs them in fp32 with TF32 off).
-// Round-4 per-job timings before this layout (tools_dev/stylebench.py, C = 512, B = 32): the backward's
-// ds job 30 us and dw job 20 us of 58 us (one 4-sample x 8-column tile per block: the weight matrix
-// re-read per sample group and ~200 cross-lane shuffles per tile).
+// Backward at C = 512, B = 32 (tools_dev/stylebench.py, profiles/r4_h / r4_i): 58 -> 44 us (ds job 30 -> 21
+// us, dw job 20 -> 16 us; they had one 4-sample x 8-column tile per block: the weight matrix re-read
+// per sample group and ~200 cross-lane shuffles per tile).
 #include "vfm_common.h"
 
 namespace {
 
 using namespace vfm;
 
-constexpr int THREADS = 256;
-constexpr int RD_ROWS = 16;              // rows per block of the row-dot jobs
-constexpr int KCH = 64;                  // K chunk (row dots: staged; column sums: one block's K range)
-constexpr int LDP = KCH + 1;             // padded LDS row (floats)
-constexpr int SPASS = 32;                // samples per pass
+constexpr int THREADS = 256, WAVES = THREADS / 64, RB = 4;
+constexpr int KCH = 64;                  // K range of one column-sum block
+constexpr int SPASS = 32;                // samples per pass of the column sums
 
 struct StyleArgs {
     const float* w;
@@ -65,43 +63,54 @@ struct StyleArgs {
     float* dab;                           // [3C] or null
     float* dw;                            // [B, WD] or null
     int blocks0;                          // blocks of the launch's first job
+    int tpb;                              // tiles per block of the forward's tile jobs (1 or WAVES)
     int ks;                               // K chunks of the column-sum job
 };
 
 __host__ __device__ inline int cdiv_i(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-// ---------------------------------------------------------------------------------------------------
-// Row dots: acc[p][i] = sum_k X(b_i, k) R(rowp, k) for the block's rows, samples b_i = bp + 2 sg + i.
-// LR(row, k) / LX(b, k) give the (transformed) operand values, zero outside. NR = row groups (3 for m).
-template <int NR, class LR, class LX>
-__device__ __forceinline__ void row_dots(int K, int bp, LR lr, LX lx, float (&acc)[NR][2], float* rs, float* xs) {
-    const int t = threadIdx.x, r = t & (RD_ROWS - 1), sg = t >> 4;
+// acc[r][c] = sum_k X(r, k) Y(c, k) over k < K: ldx(k, x[RB]) / ldy(k, y[CB]) load the operand values
+// of one k (zero outside the operand). tpb = 4 (short K): one tile per wave, its 64 lanes striding
+// over k, the partial sums reduced across the wave with xor shuffles (result in every lane).
+// tpb = 1 (long K): one tile per block, the 256 threads striding over k, the four waves' sums meeting
+// in LDS (result in wave 0). Loads are coalesced along k either way.
+template <int CB, class LX, class LY>
+__device__ __forceinline__ void tile_mm(int K, int tpb, LX ldx, LY ldy, float (&acc)[RB][CB], float* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int p = 0; p < NR; ++p) acc[p][0] = acc[p][1] = 0.f;
-    for (int k0 = 0; k0 < K; k0 += KCH) {
-        __syncthreads();
-        // weight rows: NR * 16 rows x 64 k; batch factors: 32 samples x 64 k (consecutive threads along k)
-        for (int e = t; e < NR * RD_ROWS * KCH; e += THREADS) {
-            const int row = e / KCH, k = e - row * KCH;
-            rs[row * LDP + k] = lr(row, k0 + k);
-        }
-        for (int e = t; e < SPASS * KCH; e += THREADS) {
-            const int b = e / KCH, k = e - b * KCH;
-            xs[b * LDP + k] = lx(bp + b, k0 + k);
-        }
-        __syncthreads();
-        const int kn = min(KCH, K - k0);
-#pragma unroll 4
-        for (int k = 0; k < kn; ++k) {
-            const float x0 = xs[(2 * sg) * LDP + k], x1 = xs[(2 * sg + 1) * LDP + k];
+    for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int p = 0; p < NR; ++p) {
-                const float v = rs[(p * RD_ROWS + r) * LDP + k];
-                acc[p][0] = fmaf(x0, v, acc[p][0]);
-                acc[p][1] = fmaf(x1, v, acc[p][1]);
-            }
-        }
+        for (int c = 0; c < CB; ++c) acc[r][c] = 0.f;
+    const int step = tpb == 1 ? THREADS : 64;
+#pragma unroll 2
+    for (int k = tpb == 1 ? (int)threadIdx.x : lane; k < K; k += step) {
+        float x[RB], y[CB];
+        ldx(k, x);
+        ldy(k, y);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[r][c] = fmaf(x[r], y[c], acc[r][c]);
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[r][c] += __shfl_xor(acc[r][c], o, 64);
+    if (tpb != 1) return;
+    if (wave > 0 && lane == 0)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) red[((wave - 1) * RB + r) * CB + c] = acc[r][c];
+    __syncthreads();
+    if (wave == 0)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                acc[r][c] += (red[r * CB + c] + red[(RB + r) * CB + c]) + red[(2 * RB + r) * CB + c];
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -226,59 +235,74 @@ __device__ __forceinline__ void store4(float* p, long long ld, int r, int rows, 
 // LAUNCH 4: ds = ds_in + 2 s sum(partials)          LAUNCH 5: dw = wg sum(partials)
 template <int LAUNCH>
 __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
-    __shared__ __attribute__((aligned(16))) float smem[3 * RD_ROWS * LDP + SPASS * LDP];
+    __shared__ __attribute__((aligned(16))) float smem[OT_B * OT_R + OT_B * OT_C];
+    float* red = smem;
     const bool second = (int)blockIdx.x >= a.blocks0;
     const int blk = second ? blockIdx.x - a.blocks0 : blockIdx.x;
     const int C = a.C, C3 = 3 * a.C, WD = a.WD, O = a.O, B = a.B;
-    const int t = threadIdx.x, r = t & (RD_ROWS - 1), sg = t >> 4;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // forward tile jobs: one tile per block (tpb = 1) or per wave (tpb = 4); the result sits in lane
+    // `idx` of wave 0 (tpb = 1) or of every wave (tpb = 4)
+    const long long wunit = a.tpb == 1 ? (long long)blk : (long long)blk * WAVES + wave;
+    const bool owner0 = a.tpb != 1 || wave == 0;
+    const int nbg = (B + RB - 1) / RB;                                 // 4-sample groups
 
     if (LAUNCH == 0) {
-        const int c0 = blk * RD_ROWS;
-        float* rs = smem;
-        float* xs = smem + 3 * RD_ROWS * LDP;
-        for (int bp = 0; bp < B; bp += SPASS) {
-            float acc[3][2];
-            row_dots<3>(WD, bp,
-                [&](int row, int k) {
-                    const int p = row / RD_ROWS, c = c0 + row - p * RD_ROWS;
-                    return (c < C && k < WD) ? a.A[(long long)(p * C + c) * WD + k] : 0.f;
-                },
-                [&](int b, int k) { return (b < B && k < WD) ? a.w[(long long)b * a.ldw + k] : 0.f; }, acc, rs, xs);
-            const int c = c0 + r;
+        constexpr int CC = 4;
+        if (wunit >= (long long)nbg * ((C + CC - 1) / CC)) return;
+        const int b0 = (int)(wunit % nbg) * RB, c0 = (int)(wunit / nbg) * CC;
+        float acc[RB][3 * CC];
+        tile_mm<3 * CC>(WD, a.tpb,
+            [&](int k, float (&x)[RB]) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int b = bp + 2 * sg + i;
-                if (b >= B || c >= C) continue;
-                const float m1 = fmaf(a.wg, acc[0][i], a.bg * a.ab[c]);
-                const float m2 = fmaf(a.wg, acc[1][i], a.bg * a.ab[C + c]);
-                const float m3 = fmaf(a.wg, acc[2][i], a.bg * a.ab[2 * C + c]);
+                for (int r = 0; r < RB; ++r) x[r] = b0 + r < B ? a.w[(long long)(b0 + r) * a.ldw + k] : 0.f;
+            },
+            [&](int k, float (&y)[3 * CC]) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+#pragma unroll
+                    for (int c = 0; c < CC; ++c)
+                        y[p * CC + c] = c0 + c < C ? a.A[(long long)(p * C + c0 + c) * WD + k] : 0.f;
+            }, acc, red);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CC; ++c) {
+                const int b = b0 + r, cc = c0 + c;
+                if (!owner0 || lane != r * CC + c || b >= B || cc >= C) continue;
+                const float m1 = fmaf(a.wg, acc[r][c], a.bg * a.ab[cc]);
+                const float m2 = fmaf(a.wg, acc[r][CC + c], a.bg * a.ab[C + cc]);
+                const float m3 = fmaf(a.wg, acc[r][2 * CC + c], a.bg * a.ab[2 * C + cc]);
                 float* mb = a.m + (long long)b * C3;
-                mb[c] = m1; mb[C + c] = m2; mb[2 * C + c] = m3;
-                a.s[(long long)b * C + c] = fmaf(m1, m2, m3);
+                mb[cc] = m1; mb[C + cc] = m2; mb[2 * C + cc] = m3;
+                a.s[(long long)b * C + cc] = fmaf(m1, m2, m3);
             }
-        }
     } else if (LAUNCH == 1) {
-        const int o0 = blk * RD_ROWS;
-        float* rs = smem;
-        float* xs = smem + RD_ROWS * LDP;
-        for (int bp = 0; bp < B; bp += SPASS) {
-            float acc[1][2];
-            row_dots<1>(C, bp,
-                [&](int row, int k) {
-                    const float v = (o0 + row < O && k < C) ? a.W1[(long long)(o0 + row) * C + k] : 0.f;
-                    return v * v;
-                },
-                [&](int b, int k) {
-                    const float v = (b < B && k < C) ? a.s[(long long)b * C + k] : 0.f;
-                    return v * v;
-                }, acc, rs, xs);
-            const int o = o0 + r;
+        constexpr int CB = 8;
+        if (wunit >= (long long)nbg * ((O + CB - 1) / CB)) return;
+        const int b0 = (int)(wunit % nbg) * RB, o0 = (int)(wunit / nbg) * CB;
+        float acc[RB][CB];
+        tile_mm<CB>(C, a.tpb,
+            [&](int k, float (&x)[RB]) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int b = bp + 2 * sg + i;
-                if (b < B && o < O) a.d[(long long)b * O + o] = rsqrtf(acc[0][i] + a.eps);
-            }
-        }
+                for (int r = 0; r < RB; ++r) {
+                    const float v = b0 + r < B ? a.s[(long long)(b0 + r) * C + k] : 0.f;
+                    x[r] = v * v;
+                }
+            },
+            [&](int k, float (&y)[CB]) {
+#pragma unroll
+                for (int c = 0; c < CB; ++c) {
+                    const float v = o0 + c < O ? a.W1[(long long)(o0 + c) * C + k] : 0.f;
+                    y[c] = v * v;
+                }
+            }, acc, red);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                if (owner0 && lane == r * CB + c && b0 + r < B && o0 + c < O)
+                    a.d[(long long)(b0 + r) * O + o0 + c] = rsqrtf(acc[r][c] + a.eps);
     } else if (LAUNCH == 2) {
         if (!second) {            // ds partials: sum_o q[b, o] W1[o, i]^2 over the block's 64-deep o chunk
             const int strips = cdiv_i(C, 64);
@@ -378,6 +402,10 @@ bool sizes_ok(int B, int C, int WD, int O) {
            (long long)O * C < (1LL << 31) && (long long)3 * C * WD < (1LL << 31);
 }
 
+// tiles per block of a forward tile job with a reduction of length K: the whole block on one tile from
+// K >= 1024 on
+inline int tiles_per_block(int K) { return K >= 1024 ? 1 : WAVES; }
+
 // K chunks of the backward's column sums and the floats of their partials
 inline int ks_ds(int O) { return cdiv_i(O, KCH); }
 inline int ks_dw(int C) { return cdiv_i(3LL * C, KCH); }
@@ -398,10 +426,13 @@ extern "C" int vfm_style_demod_fwd(const float* w, long long ldw, const float* A
     a.w = w; a.ldw = ldw; a.A = A; a.ab = ab; a.W1 = W1; a.wg = wg; a.bg = bg; a.eps = eps;
     a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = m; a.s = s; a.d = d;
     hipStream_t st = (hipStream_t)stream;
-    a.blocks0 = cdiv_i(C, RD_ROWS);
+    const long long nbg = cdiv_i(B, RB);
+    a.tpb = tiles_per_block(WD);
+    a.blocks0 = cdiv_i(nbg * cdiv_i(C, 4), a.tpb);
     int rc = launch<0>(a, a.blocks0, st);
     if (rc || !W1) return rc;
-    a.blocks0 = cdiv_i(O, RD_ROWS);
+    a.tpb = tiles_per_block(C);
+    a.blocks0 = cdiv_i(nbg * cdiv_i(O, 8), a.tpb);
     return launch<1>(a, a.blocks0, st);
 }
 
