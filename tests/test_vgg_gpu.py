@@ -135,3 +135,27 @@ def test_maxpool2x2_fused_bit_exact(B, H, W, C, with_tap):
         r = r + gt
     r = r * (x > 0)
     assert torch.equal(got, r)
+
+
+@pytest.mark.parametrize("res", [64, 48])
+def test_vgg16_taps_pair_matches_two_passes(res):
+    """LPIPS's input and target through one VGG16 pass of 2B images (vgg_hip.vgg16_taps_pair): taps bit-
+    identical to two single-batch passes (every layer is per-sample), the input gradient identical to the
+    single-batch backward, and no gradient work for the target (no grad requested)."""
+    from training.lpips import vgg16
+    from torch_utils.ops import vgg_hip
+    net = vgg16(pretrained=False).to(DEV)
+    convs = [m for k in range(1, 6) for m in getattr(net, f"slice{k}") if isinstance(m, torch.nn.Conv2d)]
+    g = torch.Generator(device=DEV).manual_seed(res + 1)
+    x0 = torch.randn(3, 3, res, res, generator=g, device=DEV).requires_grad_(True)
+    x1 = torch.randn(3, 3, res, res, generator=g, device=DEV)
+    t0, t1 = vgg_hip.vgg16_taps_pair(x0, x1, convs)
+    r0 = vgg_hip.vgg16_taps(x0.detach().requires_grad_(True), convs)
+    r1 = vgg_hip.vgg16_taps(x1, convs)
+    for a, b in zip(list(t0) + list(t1), list(r0) + list(r1)):
+        assert torch.equal(a, b)
+    gs = [torch.randn(o.shape, generator=g, device=DEV) for o in t0]
+    gx, = torch.autograd.grad(list(t0), [x0], gs)
+    xr = x0.detach().requires_grad_(True)
+    gr, = torch.autograd.grad(list(vgg_hip.vgg16_taps(xr, convs)), [xr], gs)
+    assert torch.equal(gx, gr)

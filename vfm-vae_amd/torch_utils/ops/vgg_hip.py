@@ -128,10 +128,14 @@ def _nhwc(t):
 
 
 def forward_chain(x, prep):
-    """(taps, ReLU outputs, pool indices) of the stack on x (NCHW fp32): taps / outputs NHWC."""
-    B, C, H, W = x.shape
-    h = torch.zeros(B, H, W, 4, dtype=torch.float32, device=x.device)
-    h[..., :C] = x.permute(0, 2, 3, 1)
+    """(taps, ReLU outputs, pool indices) of the stack on x (NCHW fp32, or a tuple of same-shape NCHW
+    batches stacked along the batch on the way into the first layer): taps / outputs NHWC."""
+    xs = x if isinstance(x, (tuple, list)) else (x,)
+    B1, C, H, W = xs[0].shape
+    B = B1 * len(xs)
+    h = torch.zeros(B, H, W, 4, dtype=torch.float32, device=xs[0].device)
+    for i, xi in enumerate(xs):
+        h[i * B1:(i + 1) * B1, :, :, :C] = xi.permute(0, 2, 3, 1)
     ys, pools, taps = [], [], []
     for op in PLAN:
         if op[0] == 'conv':
@@ -195,6 +199,49 @@ class _VGG16Taps(torch.autograd.Function):
     def backward(ctx, *gtaps):
         saved = ctx.saved_tensors
         return backward_chain(saved[:13], saved[13:], ctx.prep, ctx.in_shape, gtaps), None
+
+
+class _VGG16TapsPair(torch.autograd.Function):
+    """The stack over two same-shape batches (LPIPS's input and target) in ONE pass of 2B images: every
+    layer is per-sample, so the taps are bit-identical to two separate passes, and the deep layers
+    (16 x 16 / 32 x 32 planes) get twice the tiles. The backward runs only for the batch whose input
+    needs a gradient (the generated image; the target is a data batch)."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, prep):
+        taps, ys, pools = forward_chain((x0, x1), prep)
+        B = x0.shape[0]
+        ctx.prep, ctx.in_shape, ctx.B = prep, x0.shape, B
+        need = ctx.needs_input_grad[:2]
+        if any(need):
+            ctx.save_for_backward(*ys, *[p for p in pools if p is not None])
+            ctx.pool_none = [p is None for p in pools]
+        outs = [_nchw(t) for t in taps]
+        return tuple(t[:B] for t in outs) + tuple(t[B:] for t in outs)
+
+    @staticmethod
+    def backward(ctx, *g):
+        saved = ctx.saved_tensors
+        ys = saved[:13]
+        it = iter(saved[13:])
+        pools = [None if none else next(it) for none in ctx.pool_none]
+        B = ctx.B
+        grads = []
+        for half, need in enumerate(ctx.needs_input_grad[:2]):
+            gt = g[5 * half:5 * half + 5]
+            if not need or all(t is None for t in gt):
+                grads.append(None)
+                continue
+            sl = slice(half * B, (half + 1) * B)
+            grads.append(backward_chain([y[sl] for y in ys], [None if p is None else p[sl] for p in pools],
+                                        ctx.prep, ctx.in_shape, gt))
+        return grads[0], grads[1], None
+
+
+def vgg16_taps_pair(x0, x1, convs):
+    """(taps of x0, taps of x1) from one pass over both batches (see _VGG16TapsPair)."""
+    outs = _VGG16TapsPair.apply(x0, x1, prepare(convs))
+    return outs[:5], outs[5:]
 
 
 def backward_chain(ys, pools, prep, in_shape, gtaps, conv=None):

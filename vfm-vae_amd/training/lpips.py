@@ -140,8 +140,16 @@ class LPIPS(nn.Module):
             dist.print0(f"loaded pretrained LPIPS loss from {ckpt}")
 
     def forward(self, input, target):
-        outs0 = self.net(self.scaling_layer(input))
-        outs1 = self.net(self.scaling_layer(target))
+        net = self.net
+        if (input.is_cuda and input.dtype == torch.float32 and target.dtype == torch.float32
+                and input.shape == target.shape and net.impl == 'hip'):
+            # both batches through the VGG16 stack in one pass (per-sample layers: same taps as two passes)
+            from torch_utils.ops import vgg_hip
+            convs = [m for k in range(1, 6) for m in getattr(net, f"slice{k}") if isinstance(m, nn.Conv2d)]
+            outs0, outs1 = vgg_hip.vgg16_taps_pair(self.scaling_layer(input), self.scaling_layer(target), convs)
+        else:
+            outs0 = self.net(self.scaling_layer(input))
+            outs1 = self.net(self.scaling_layer(target))
         val = None
         for kk in range(len(self.chns)):
             lin = getattr(self, f"lin{kk}").model
