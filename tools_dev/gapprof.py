@@ -77,8 +77,11 @@ def analyse(path, steps):
         while t < b:
             samples.append(t)
             t += DT
-    repo = lambda n: ("vfm-vae_amd" in n or "bench.py" in n or "/training/" in n) and "tools_dev" not in n  # noqa: E731
+    keys = ("vfm-vae_amd", "bench.py", "training/", "torch_utils/", "networks/")
+    repo = lambda n: any(k in n for k in keys) and "tools_dev" not in n and "site-packages" not in n  # noqa: E731
     print("host events per thread:", {t: len(v) for t, v in py.items()}, flush=True)
+    names = collections.Counter(e[2] for v in py.values() for e in v if not e[2].startswith("["))
+    print("sample python frames:", [n for n, _ in names.most_common(8)], flush=True)
     for tid, lst in py.items():
         lst.sort(key=lambda x: (x[0], -x[1]))
         incl, excl = collections.Counter(), collections.Counter()
