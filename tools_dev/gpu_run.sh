@@ -38,6 +38,7 @@ for s in "$@"; do
     r4tests4) timeout -k 10 600 python -u -m pytest tests/test_vgg_gpu.py tests/test_lpips_gpu.py tests/test_gemm_shapes_gpu.py tests/test_networks_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests4.log 2>&1 ;;
     r4tests5) timeout -k 10 600 python -u -m pytest tests/test_style_rmsnorm_gpu.py tests/test_vgg_gpu.py tests/test_lpips_gpu.py tests/test_decoder_gpu.py tests/test_networks_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests5.log 2>&1 ;;
     r4tests6) timeout -k 10 600 python -u -m pytest tests/test_style_rmsnorm_gpu.py tests/test_decoder_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests6.log 2>&1 ;;
+    r4tests7) timeout -k 10 600 python -u -m pytest tests/test_vgg_gpu.py tests/test_lpips_gpu.py tests/test_networks_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests7.log 2>&1 ;;
     vggbench) timeout -k 10 300 python tools_dev/vggbench.py > $out/vggbench.log 2>&1 ;;
     benchab) VFM_LPIPS_VGG=torch timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_a.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_b.log 2>&1 && VFM_LPIPS_VGG=torch timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_c.log 2>&1 ;;
     convpmc) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex conv3x3_kernel -d $out/convpmc -o run --output-format csv -- python3 tools_dev/vggbench.py > $out/convpmc.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-include-regex conv3x3_kernel -d $out/convpmc2 -o run --output-format csv -- python3 tools_dev/vggbench.py > $out/convpmc2.log 2>&1 ;;
