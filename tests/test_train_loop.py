@@ -212,3 +212,36 @@ def test_wds_process_worker_death_raises(tmp_path):
         while time.time() - t0 < 60:
             next(it)
     it.close()
+
+
+def test_fast_adam_step_matches_torch_fused_adam():
+    """training_loop.fast_adam_step (cached tensor lists -> torch._fused_adam_) against torch.optim.Adam
+    (fused=True).step() on a twin model: bit-identical parameters after every step, including a step where
+    one parameter has no gradient (the cache is rebuilt) and the first step (regular path creates state)."""
+    import dnnlib
+    from training.training_loop import fast_adam_step
+
+    def mk():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4))
+    a, b = mk(), mk()
+    kw = dict(lr=1e-2, betas=(0.0, 0.99), eps=1e-8, fused=True)
+    oa, ob = torch.optim.Adam(a.parameters(), **kw), torch.optim.Adam(b.parameters(), **kw)
+    phase = dnnlib.EasyDict(opt=ob)
+    used = []
+    g = torch.Generator().manual_seed(1)
+    for i in range(4):
+        x = torch.randn(5, 8, generator=g)
+        for m in (a, b):
+            m.zero_grad(set_to_none=True)
+            m(x).square().sum().backward()
+        if i == 2:
+            a[1].bias.grad = None
+            b[1].bias.grad = None
+        oa.step()
+        u = fast_adam_step(phase)
+        if not u:
+            ob.step()
+        used.append(u)
+        assert all(torch.equal(p, q) for p, q in zip(a.parameters(), b.parameters())), i
+    assert used == [False, True, True, True]
