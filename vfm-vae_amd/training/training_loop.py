@@ -22,6 +22,7 @@ import copy
 import gc
 import json
 import math
+import operator
 import os
 import random
 import time
@@ -261,24 +262,24 @@ def fast_adam_step(phase):
     plist = phase.__dict__.get('adam_params')
     if plist is None:
         plist = phase.adam_params = list(g['params'])
-    with_grad = [p for p in plist if p.grad is not None]
-    if not with_grad:
-        return True
-    key = tuple(id(p) for p in with_grad)
+    now = [p.grad for p in plist]                       # the one Python pass over the parameters
     cache = phase.__dict__.get('adam_cache')
-    if cache is None or cache[0] != key:
+    if cache is not None and all(map(operator.is_, now, cache[0])):
+        _, params, grads, m1, m2, steps = cache         # same grad tensors as last time (flat-buffer views)
+    else:
+        with_grad = [p for p, gr in zip(plist, now) if gr is not None]
+        if not with_grad:
+            return True
         st = opt.state
         dev = with_grad[0].device
         if any(p not in st or p.dtype != torch.float32 or p.device != dev or p.grad.dtype != torch.float32
                for p in with_grad):
             phase.adam_cache = None
             return False                 # first step of these parameters: the regular path creates state
-        grads = [p.grad for p in with_grad]
-        cache = phase.adam_cache = (key, with_grad, grads, [st[p]['exp_avg'] for p in with_grad],
-                                    [st[p]['exp_avg_sq'] for p in with_grad], [st[p]['step'] for p in with_grad])
-    _, params, grads, m1, m2, steps = cache
-    if any(p.grad is not gr for p, gr in zip(params, grads)):
-        grads = [p.grad for p in params]   # a grad tensor was replaced (not the flat-buffer views)
+        params, grads = with_grad, [p.grad for p in with_grad]
+        m1, m2 = [st[p]['exp_avg'] for p in with_grad], [st[p]['exp_avg_sq'] for p in with_grad]
+        steps = [st[p]['step'] for p in with_grad]
+        phase.adam_cache = (now, params, grads, m1, m2, steps)
     beta1, beta2 = g['betas']
     with torch.no_grad():
         torch._foreach_add_(steps, 1)
