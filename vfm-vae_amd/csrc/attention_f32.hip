@@ -34,6 +34,8 @@
 // current tile's math.
 #include "vfm_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace vfm;
@@ -211,8 +213,11 @@ __device__ __forceinline__ void store_tr(float* p, const f32x16* acc, int hh, fl
 __device__ __forceinline__ float xchg32(float v) { return __int_as_float(__shfl_xor(__float_as_int(v), 32)); }
 
 // ---------------------------------------------------------------------------------------------
-template <int NP>
-__global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
+// OCC = 1: the next K/V tile prefetched into registers during the current tile's math (one wave per
+// SIMD: 292 registers); OCC = 2: no register prefetch, <= 256 registers and two workgroups per CU, so
+// one workgroup's softmax / piece splits / loads overlap the other's MFMAs.
+template <int NP, int OCC>
+__global__ __launch_bounds__(64 * WAVES, OCC) void attn32_fwd(Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG];
     unsigned char *kimg = lds, *vimg = lds + NP * IMG;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -232,13 +237,19 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_fwd(Args a) {
     float m_run = -INFINITY, l_run = 0.f;
     const float c = a.c;
     const int T = (Nk + TT - 1) / TT;
-    stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
-    stage_load(sv, vb, a.sv.n, 0, Nk, hd, tid);
+    if (OCC == 1) {
+        stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
+        stage_load(sv, vb, a.sv.n, 0, Nk, hd, tid);
+    }
     for (int t = 0; t < T; ++t) {
+        if (OCC != 1) {
+            stage_load(sk, kb, a.sk.n, t * TT, Nk, hd, tid);
+            stage_load(sv, vb, a.sv.n, t * TT, Nk, hd, tid);
+        }
         stage_store<NP>(sk, kimg, tid);
         stage_store<NP>(sv, vimg, tid);
         __syncthreads();
-        if (t + 1 < T) {
+        if (OCC == 1 && t + 1 < T) {
             stage_load(sk, kb, a.sk.n, (t + 1) * TT, Nk, hd, tid);
             stage_load(sv, vb, a.sv.n, (t + 1) * TT, Nk, hd, tid);
         }
@@ -515,8 +526,16 @@ extern "C" int vfm_attention_f32_fwd(const void* q, const void* k, const void* v
     a.c = scale * 1.4426950408889634f;
     a.hd = head_dim;
     const dim3 grid((Nq + RB - 1) / RB, H, B);
-    if (precision == VFM_F32) VFM_LAUNCH(attn32_fwd<3>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
-    else VFM_LAUNCH(attn32_fwd<2>, grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    static const int occ = [] {
+        const char* e = getenv("VFM_ATTN32_OCC");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    if (precision == VFM_F32) {
+        if (occ == 2) VFM_LAUNCH((attn32_fwd<3, 2>), grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+        else VFM_LAUNCH((attn32_fwd<3, 1>), grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    } else {
+        VFM_LAUNCH((attn32_fwd<2, 1>), grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    }
     return launch_status();
 }
 
