@@ -214,8 +214,10 @@ __device__ __forceinline__ float xchg32(float v) { return __int_as_float(__shfl_
 
 // ---------------------------------------------------------------------------------------------
 // OCC = 1: the next K/V tile prefetched into registers during the current tile's math (one wave per
-// SIMD: 292 registers); OCC = 2: no register prefetch, <= 256 registers and two workgroups per CU, so
-// one workgroup's softmax / piece splits / loads overlap the other's MFMAs.
+// SIMD: 292 registers); OCC = 2 (default): no register prefetch, 220 registers and two workgroups per
+// CU, so one workgroup's softmax / piece splits / loads overlap the other's MFMAs (PMC: 6.6 VALU
+// instructions per 32x32x16 MFMA; MI355X: adapter shape 1110 -> 965 us, decoder 32 x 32 489 -> 398 us,
+// DINO 38 -> 29.5 us, profiles/r4_o_attn32_occ.txt). VFM_ATTN32_OCC=1 selects the prefetch form.
 template <int NP, int OCC>
 __global__ __launch_bounds__(64 * WAVES, OCC) void attn32_fwd(Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG];
@@ -528,7 +530,7 @@ extern "C" int vfm_attention_f32_fwd(const void* q, const void* k, const void* v
     const dim3 grid((Nq + RB - 1) / RB, H, B);
     static const int occ = [] {
         const char* e = getenv("VFM_ATTN32_OCC");
-        return e && e[0] == '2' ? 2 : 1;
+        return e && e[0] == '1' ? 1 : 2;
     }();
     if (precision == VFM_F32) {
         if (occ == 2) VFM_LAUNCH((attn32_fwd<3, 2>), grid, dim3(64 * WAVES), 0, (hipStream_t)stream, a);

@@ -36,6 +36,8 @@
 // and applies the epilogue.
 #include "vfm_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace vfm;
@@ -88,12 +90,12 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 //   KCONT: global rows are outer (m or n), contiguous along k (lead = ld between rows)
 //   !KCONT: global rows are k, contiguous along the outer index
 // NP > 1: fp32 input split into NP bf16 images (hi, [mid,] lo), else bf16 input.
-template <bool KCONT, int NP>
+template <bool KCONT, int NP, int NT = THREADS>
 struct Stage {
     static constexpr bool F32 = NP > 1;
     static constexpr int EPC = F32 ? 4 : 8;                  // elements per 16-B chunk
     static constexpr int CHUNKS = 128 * 64 / EPC;            // chunks per tile
-    static constexpr int PER = CHUNKS / THREADS;             // chunks per thread
+    static constexpr int PER = CHUNKS / NT;                  // chunks per thread
     static constexpr int ROWCH = (KCONT ? 64 : 128) / EPC;   // chunks per global row of the tile
     uint4 r[PER];
 
@@ -104,7 +106,7 @@ struct Stage {
         const int esz = F32 ? 4 : 2;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int c = tid + THREADS * u;
+            const int c = tid + NT * u;
             const int row = c / ROWCH, col = (c % ROWCH) * EPC;
             int o, k;
             if (KCONT) { o = outer0 + row; k = k0 + col; }
@@ -120,7 +122,7 @@ struct Stage {
     __device__ __forceinline__ void store(unsigned char* img, int tid) const {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int c = tid + THREADS * u;
+            const int c = tid + NT * u;
             const int row = c / ROWCH, cc = c % ROWCH;
             if (!F32) {
                 const int off = KCONT ? kc_off(row, cc) : mc_off(row, cc);
@@ -156,8 +158,12 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int s,
     }
 }
 
-template <bool AK, bool BKC, int NP, bool OUTF32>
-__global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs a) {
+// NW = 4: 2 x 2 waves of 64 x 64 (one wave per SIMD for the fp32 splits: 310 registers); NW = 8: 2 x 4
+// waves of 64 x 32, two waves per SIMD (<= 256 registers), so one wave's fp32 -> piece split and LDS
+// stores overlap the other's MFMAs (the VGG conv's 8-wave form: 146 -> 196 TF/s there).
+template <bool AK, bool BKC, int NP, bool OUTF32, int NW = 4>
+__global__ __launch_bounds__(64 * NW, (NP == 3 || NW == 8) ? 1 : 2) void gemm_kernel(GemmArgs a) {
+    constexpr int NT = 64 * NW, JB = NW == 8 ? 1 : 2;      // threads; 32-column blocks per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr bool F32 = NP > 1;
     unsigned char* a_img = lds;               // A pieces at a_img + p IMG
@@ -176,13 +182,13 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
     const unsigned char* Ab = reinterpret_cast<const unsigned char*>(a.A) + (long long)z * a.sA * esz;
     const unsigned char* Bb = reinterpret_cast<const unsigned char*>(a.B) + (a.lgp ? 0LL : (long long)z * a.sB * esz);
 
-    Stage<AK, NP> sa;
-    Stage<BKC, NP> sb;
-    f32x16 acc[2][2], accs[2][2];              // hi.hi products / the smaller piece products (NP > 1)
+    Stage<AK, NP, NT> sa;
+    Stage<BKC, NP, NT> sb;
+    f32x16 acc[2][JB], accs[2][JB];            // hi.hi products / the smaller piece products (NP > 1)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = accs[i][j] = f32x16{};
+        for (int j = 0; j < JB; ++j) acc[i][j] = accs[i][j] = f32x16{};
 
     sa.load(Ab, a.lda, m0, kbeg, a.M, kend, tid);
     sb.load(Bb, a.ldb, n0, kbeg, a.N, kend, tid, a.lgp, a.sB);
@@ -196,13 +202,13 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
         }
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
-            bf16x8 af[NP][2], bfr[NP][2];
+            bf16x8 af[NP][2], bfr[NP][JB];
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) af[p][i] = frag<AK>(a_img + p * IMG, 2 * wm + i, s, lane);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) bfr[p][j] = frag<BKC>(b_img + p * IMG, 2 * wn + j, s, lane);
+                for (int j = 0; j < JB; ++j) bfr[p][j] = frag<BKC>(b_img + p * IMG, JB * wn + j, s, lane);
             }
             // the piece products (Terms<NP>): the smaller ones into their own accumulator (rounded
             // at their ~2^-8 scale), hi.hi alone into acc -- as many full-magnitude roundings as an
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
+                    for (int j = 0; j < JB; ++j) {
                         f32x16& c = (t == Terms<NP>::N - 1) ? acc[i][j] : accs[i][j];
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[Terms<NP>::a(t)][i], bfr[Terms<NP>::b(t)][j], c,
                                                                     0, 0, 0);
@@ -225,16 +231,16 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] += accs[i][j];
+            for (int j = 0; j < JB; ++j) acc[i][j] += accs[i][j];
     }
 
-    // ---- epilogue: acc[i][j][e] = C[m][n], m = m0 + 64wm + 32i + (e&3) + 8(e>>2) + 4hh, n = n0 + 64wn + 32j + r
+    // ---- epilogue: acc[i][j][e] = C[m][n], m = m0 + 64wm + 32i + (e&3) + 8(e>>2) + 4hh, n = n0 + 32(JB wn + j) + r
     const int r = lane & 31, hh = lane >> 5;
     if (a.ws) {   // split-K partials, raw fp32
         float* w = a.ws + ((long long)z * a.splits + split) * a.M * a.N;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + 64 * wn + 32 * j + r;
+        for (int j = 0; j < JB; ++j) {
+            const int n = n0 + 32 * (JB * wn + j) + r;
             if (n >= a.N) continue;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -249,8 +255,8 @@ __global__ __launch_bounds__(THREADS, NP == 3 ? 1 : 2) void gemm_kernel(GemmArgs
     typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
     TC* Cb = reinterpret_cast<TC*>(a.C) + (a.lgp ? 0LL : (long long)z * a.sC);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = n0 + 64 * wn + 32 * j + r;
+    for (int j = 0; j < JB; ++j) {
+        const int n = n0 + 32 * (JB * wn + j) + r;
         if (n >= a.N) continue;
         const float bcol = (a.bias_mode == 1) ? a.bias[a.lgp ? (n & ((1 << a.lgp) - 1)) : n] : 0.f;
         TC* Cn = a.lgp ? Cb + (long long)(n >> a.lgp) * a.sC + (n & ((1 << a.lgp) - 1)) - n : Cb;
@@ -293,18 +299,33 @@ __global__ void gemm_reduce_kernel(GemmArgs a, int J, int zcount) {
     (void)zcount;
 }
 
-template <bool AK, bool BKC, int NP, bool OUTF32>
-int launch(const GemmArgs& a, int batch, hipStream_t st) {
+template <bool AK, bool BKC, int NP, bool OUTF32, int NW>
+int launch_nw(const GemmArgs& a, int batch, hipStream_t st) {
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const size_t lds = 2 * NP * IMG;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, NP, OUTF32>,
+        (void)hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, NP, OUTF32, NW>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    VFM_LAUNCH((gemm_kernel<AK, BKC, NP, OUTF32>), dim3(tiles, batch * a.splits), dim3(THREADS), lds, st, a);
+    VFM_LAUNCH((gemm_kernel<AK, BKC, NP, OUTF32, NW>), dim3(tiles, batch * a.splits), dim3(64 * NW), lds, st, a);
     return launch_status();
+}
+
+// waves per 128-tile workgroup for the fp32-equivalent products (8 by default; VFM_GEMM128_WAVES=4 for A/B)
+int f32_waves() {
+    static const int w = [] {
+        const char* e = getenv("VFM_GEMM128_WAVES");
+        return e && e[0] == '4' ? 4 : 8;
+    }();
+    return w;
+}
+
+template <bool AK, bool BKC, int NP, bool OUTF32>
+int launch(const GemmArgs& a, int batch, hipStream_t st) {
+    if (NP == 3 && f32_waves() == 8) return launch_nw<AK, BKC, NP, OUTF32, 8>(a, batch, st);
+    return launch_nw<AK, BKC, NP, OUTF32, 4>(a, batch, st);
 }
 
 template <int NP, bool OUTF32>
