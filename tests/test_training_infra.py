@@ -123,15 +123,15 @@ def test_kernel_timer_rocprof_names():
     """Timer regions map onto the kernel names rocprofv3 prints, so the bench's roofline
     average can be checked against the committed profile."""
     from torch_utils.ops import kernel_timer as kt
-    assert kt.rocprof_name("gemm<f32x6,true,false,true>") == "gemm_kernel<true, false, 3, true>"
-    assert kt.rocprof_name("gemm<f32x3,true,false,true>") == "gemm_kernel<true, false, 2, true>"
-    assert kt.rocprof_name("gemm<bf16,false,true,false>[4x8x16x1]") == "gemm_kernel<false, true, 1, false>"
+    assert kt.rocprof_name("gemm<f32x6,true,false,true>") == "gemm_kernel<true, false, 3, true, 8>"
+    assert kt.rocprof_name("gemm<f32x3,true,false,true>") == "gemm_kernel<true, false, 2, true, 4>"
+    assert kt.rocprof_name("gemm<bf16,false,true,false>[4x8x16x1]") == "gemm_kernel<false, true, 1, false, 4>"
     assert kt.rocprof_name("gemm8<f32x6,true,true,true>") == "gemm8_kernel<true, true, true, false, 0>"
     assert kt.rocprof_name("gemm8_gelu<2>") == "gemm8_kernel<true, false, false, false, 2>"
     assert kt.rocprof_name("conv3x3_nhwc<f32x6,128>") == "conv3x3_kernel<256, 128, 3>"
     assert kt.rocprof_name("conv3x3_nhwc<f32x3,64>") == "conv3x3_kernel<128, 64, 2>"
-    assert kt.rocprof_name("conv3x3_nhwc<f32x6,64>") == "conv3x3_kernel<128, 64, 3>"
-    assert kt.rocprof_name("attention_fwd<f32x6,64>") == "attn32_fwd<3>"
+    assert kt.rocprof_name("conv3x3_nhwc<f32x6,64>") == "conv3x3_kernel<256, 64, 3>"
+    assert kt.rocprof_name("attention_fwd<f32x6,64>") == "attn32_fwd<3, 2>"
     assert kt.rocprof_name("attention_fwd<bf16,64>") == "attn_fwd_d64"
     assert kt.rocprof_name("dwconv2d_fwd<bf16,7>") == "dwr_fwd<__hip_bfloat16, 7>"
     assert kt.rocprof_name("gemm_ws<f32x6,true,true,true>") is None

@@ -28,6 +28,8 @@
 // (p + dy*W + dx)*Cin + c, zero outside the image. The 9 shifted reads of a pixel hit L2.
 #include "vfm_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace vfm;
@@ -335,7 +337,16 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int pr
     a.fH = make_fastdiv((uint32_t)H);
     a.relu = relu;
     hipStream_t st = (hipStream_t)stream;
-    if (np == 3) return (Cout % 128 == 0) ? launch<256, 128, 3>(a, st) : launch<128, 64, 3>(a, st);
+    // Cout = 64 layers (conv1_x) on 256 x 64 tiles with 8 waves (two per SIMD, 32 columns each) like the
+    // 256 x 128 form; VFM_CONV_N64=128 keeps the 4-wave 128 x 64 tile (A/B)
+    static const bool wide64 = [] {
+        const char* e = getenv("VFM_CONV_N64");
+        return !(e && e[0] == '1');
+    }();
+    if (np == 3) {
+        if (Cout % 128 == 0) return launch<256, 128, 3>(a, st);
+        return wide64 ? launch<256, 64, 3>(a, st) : launch<128, 64, 3>(a, st);
+    }
     return (Cout % 128 == 0) ? launch<128, 128, 2>(a, st) : launch<128, 64, 2>(a, st);
 }
 

@@ -213,19 +213,25 @@ def rocprof_name(region):
         return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}, false, 0>"
     if base == "gemm8_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2)
         return f"gemm8_kernel<true, false, false, false, {args[0]}>"
-    if base == "gemm_fold" and len(args) == 3:                 # batch-folded: gemm_kernel<AK, false, NP, OUTF32>
-        return f"gemm_kernel<{args[1]}, false, {_NP.get(args[0], 1)}, {args[2]}>"
+    if base == "gemm_fold" and len(args) == 3:                 # batch-folded: gemm_kernel<AK, false, NP, OUTF32, NW>
+        np_ = _NP.get(args[0], 1)
+        nw = 8 if (np_ == 3 and os.environ.get("VFM_GEMM128_WAVES", "8") != "4") else 4
+        return f"gemm_kernel<{args[1]}, false, {np_}, {args[2]}, {nw}>"
     if base == "gemm4" and len(args) == 4:                     # gemm4_kernel<AK, BK, OUTF32>
         return f"gemm4_kernel<{args[1]}, {args[2]}, {args[3]}>"
-    if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32>
-        return f"gemm_kernel<{args[1]}, {args[2]}, {_NP.get(args[0], 1)}, {args[3]}>"
+    if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32, NW>
+        np_ = _NP.get(args[0], 1)
+        nw = 8 if (np_ == 3 and os.environ.get("VFM_GEMM128_WAVES", "8") != "4") else 4
+        return f"gemm_kernel<{args[1]}, {args[2]}, {np_}, {args[3]}, {nw}>"
     if base == "conv3x3_nhwc" and len(args) == 2:              # conv3x3_kernel<BM, BN, NP>
         np_ = _NP.get(args[0], 3)
-        bm = 256 if (np_ == 3 and args[1] == "128") else 128
+        wide64 = os.environ.get("VFM_CONV_N64", "256") != "128"
+        bm = 256 if (np_ == 3 and (args[1] == "128" or wide64)) else 128
         return f"conv3x3_kernel<{bm}, {args[1]}, {np_}>"
     if base in ("attention_fwd", "attention_bwd") and args and args[0] in ("f32x6", "f32x3"):
         np_ = _NP[args[0]]
-        return f"attn32_fwd<{np_}>" if base == "attention_fwd" else f"attn32_dkdv<{np_}>"
+        occ = 2 if (np_ == 3 and os.environ.get("VFM_ATTN32_OCC", "2") != "1") else 1
+        return f"attn32_fwd<{np_}, {occ}>" if base == "attention_fwd" else f"attn32_dkdv<{np_}>"
     if base == "convnext_mlp_fwd" and len(args) == 3:          # mlp_fwd<C, SAVE>
         return f"mlp_fwd<{args[1]}, {args[2]}>"
     pat = _ROC.get(base)
