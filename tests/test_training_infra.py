@@ -130,7 +130,7 @@ def test_kernel_timer_rocprof_names():
     assert kt.rocprof_name("gemm8_gelu<2>") == "gemm8_kernel<true, false, false, false, 2>"
     assert kt.rocprof_name("conv3x3_nhwc<f32x6,128>") == "conv3x3_kernel<256, 128, 3>"
     assert kt.rocprof_name("conv3x3_nhwc<f32x3,64>") == "conv3x3_kernel<128, 64, 2>"
-    assert kt.rocprof_name("conv3x3_nhwc<f32x6,64>") == "conv3x3_kernel<256, 64, 3>"
+    assert kt.rocprof_name("conv3x3_nhwc<f32x6,64>") == "conv3x3_kernel<128, 64, 3>"
     assert kt.rocprof_name("attention_fwd<f32x6,64>") == "attn32_fwd<3, 2>"
     assert kt.rocprof_name("attention_fwd<bf16,64>") == "attn_fwd_d64"
     assert kt.rocprof_name("dwconv2d_fwd<bf16,7>") == "dwr_fwd<__hip_bfloat16, 7>"

@@ -337,11 +337,12 @@ extern "C" int vfm_conv3x3_nhwc_f32(const float* x, const void* w_pieces, int pr
     a.fH = make_fastdiv((uint32_t)H);
     a.relu = relu;
     hipStream_t st = (hipStream_t)stream;
-    // Cout = 64 layers (conv1_x) on 256 x 64 tiles with 8 waves (two per SIMD, 32 columns each) like the
-    // 256 x 128 form; VFM_CONV_N64=128 keeps the 4-wave 128 x 64 tile (A/B)
+    // Cout = 64 layers (conv1_x): 128 x 64 tiles with 4 waves, two workgroups per CU; VFM_CONV_N64=256 runs
+    // them on 256 x 64 tiles with 8 waves (A/B: 3.10 vs 2.96 ms for the 64-image forward,
+    // profiles/r4_q_conv_n64_ab.txt -- the larger tile does not pay)
     static const bool wide64 = [] {
         const char* e = getenv("VFM_CONV_N64");
-        return !(e && e[0] == '1');
+        return e && e[0] == '2';
     }();
     if (np == 3) {
         if (Cout % 128 == 0) return launch<256, 128, 3>(a, st);

@@ -225,7 +225,7 @@ def rocprof_name(region):
         return f"gemm_kernel<{args[1]}, {args[2]}, {np_}, {args[3]}, {nw}>"
     if base == "conv3x3_nhwc" and len(args) == 2:              # conv3x3_kernel<BM, BN, NP>
         np_ = _NP.get(args[0], 3)
-        wide64 = os.environ.get("VFM_CONV_N64", "256") != "128"
+        wide64 = os.environ.get("VFM_CONV_N64", "128") == "256"
         bm = 256 if (np_ == 3 and (args[1] == "128" or wide64)) else 128
         return f"conv3x3_kernel<{bm}, {args[1]}, {np_}>"
     if base in ("attention_fwd", "attention_bwd") and args and args[0] in ("f32x6", "f32x3"):
