@@ -185,6 +185,31 @@ def _splits(M, N, K, z):
     return max(1, min(want, K // 512, 64))
 
 
+# The backward's weight-gradient and data-gradient GEMMs are independent; on the bf16 (hipBLASLt) path they
+# are ridge-shaped (K = 512-2048 against 4096-65536-column planes: MFMA-bound K-loops, then output-write-
+# bound epilogues in synchronized tile rounds), so the weight gradient runs on a side stream next to the
+# data gradient and one kernel's write phase overlaps the other's K-loop. VFM_DW_STREAM=0 serialises them.
+_DW_STREAM = os.environ.get("VFM_DW_STREAM", "1") == "1"
+_side_streams = {}
+
+
+def _overlapped(side_fn, main_fn, dev):
+    """(side_fn(), main_fn()) with side_fn enqueued on a side stream of `dev` (after everything queued so
+    far on the current stream) and the current stream waiting for it before anything later runs."""
+    if not (_DW_STREAM and dev.type == 'cuda') or torch.cuda.is_current_stream_capturing():
+        return side_fn(), main_fn()
+    side = _side_streams.get(dev.index)
+    if side is None:
+        side = _side_streams[dev.index] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        a = side_fn()
+    b = main_fn()
+    cur.wait_stream(side)
+    return a, b
+
+
 class _Pointwise(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, x):
@@ -208,15 +233,23 @@ class _Pointwise(torch.autograd.Function):
         B, I, P = x.shape
         O = wc.shape[0]
         dy = dy.contiguous()
-        dw = dx = None
-        if _wanted(ctx, 0):
-            # sum_b dy[b] @ x[b]^T with fp32 per-sample products, summed in fp32
-            dw = weight_grad_1x1(dy, x, ctx.wdt)
-        if _wanted(ctx, 1):
+
+        def wgrad():      # sum_b dy[b] @ x[b]^T with fp32 per-sample products, summed in fp32
+            return weight_grad_1x1(dy, x, ctx.wdt)
+
+        def dgrad():
             dx = _gemm(wc.t(), dy, cache_a=True)
             if dx is None:
                 with kernel_timer.vendor_gemm(f"{_tn(dy)},1x1_dx", I, P, O, B, dy.element_size()):
                     dx = torch.bmm(wc.t().expand(B, I, O), dy)
+            return dx
+        want_w, want_x = _wanted(ctx, 0), _wanted(ctx, 1)
+        if want_w and want_x and dy.dtype != torch.float32:
+            # (fp32 operands stay on one stream: their piece splits are shared between the two products)
+            dw, dx = _overlapped(wgrad, dgrad, dy.device)
+        else:
+            dw = wgrad() if want_w else None
+            dx = dgrad() if want_x else None
         return dw, dx
 
 
@@ -717,29 +750,41 @@ class _ConvNeXtMLP(torch.autograd.Function):
             db2 = (s1 * fg if fg is not None else s1).to(b2dt)
         if fg is not None and _wanted(ctx, 6):
             dgm = r0.view(B, C).sum(0).to(gdt)
-        if _wanted(ctx, 4):
-            dw2 = weight_grad_1x1(dy, g, w2dt)
-        # dh = (W2^T dy) * GELU'(h*s+b1) * s, with the per-(b, o) sums for d_s and d_b1
+        # dh = (W2^T dy) * GELU'(h*s+b1) * s, with the per-(b, o) sums for d_s and d_b1 (next to dW2 on
+        # the side stream, _overlapped)
         tiles = _lib.vfm_pw_gemm_gelu_tiles(P)
         w2t = w2c.t().contiguous()
-        dh = torch.empty_like(h)
-        p0 = torch.empty([B, tiles, O], dtype=torch.float32, device=m.device)
-        p1 = torch.empty_like(p0)
-        with kernel_timer.region(_rn('pw_gemm_gelu_bwd', h), _nb(dy, h, dh)):
-            _check(_lib.vfm_pw_gemm_gelu(w2t.data_ptr(), dy.data_ptr(), _p(s), _p(fb1), h.data_ptr(), dh.data_ptr(),
-                                         None, p0.data_ptr(), p1.data_ptr(), 1, B, O, C, P, _stream()),
-                   'vfm_pw_gemm_gelu')
+
+        def dh_kernel():
+            dh = torch.empty_like(h)
+            p0 = torch.empty([B, tiles, O], dtype=torch.float32, device=m.device)
+            p1 = torch.empty_like(p0)
+            with kernel_timer.region(_rn('pw_gemm_gelu_bwd', h), _nb(dy, h, dh)):
+                _check(_lib.vfm_pw_gemm_gelu(w2t.data_ptr(), dy.data_ptr(), _p(s), _p(fb1), h.data_ptr(),
+                                             dh.data_ptr(), None, p0.data_ptr(), p1.data_ptr(), 1, B, O, C, P,
+                                             _stream()), 'vfm_pw_gemm_gelu')
+            return dh, p0, p1
+        if _wanted(ctx, 4):
+            dw2, (dh, p0, p1) = _overlapped(lambda: weight_grad_1x1(dy, g, w2dt), dh_kernel, dy.device)
+        else:
+            dh, p0, p1 = dh_kernel()
         if s is not None and _wanted(ctx, 2):
             ds = p0.sum(1).to(sdt)
         if fb1 is not None and _wanted(ctx, 3):
             db1 = p1.sum((0, 1)).to(b1dt)
-        if _wanted(ctx, 1):
-            dw1 = weight_grad_1x1(dh, m, w1dt)
-        if ctx.needs_input_grad[0]:
+
+        def dm_gemm():
             dm = _gemm(w1c.t(), dh)
             if dm is None:
                 with kernel_timer.vendor_gemm(f"{_tn(dh)},1x1_dx", C, dh.shape[2], O, B, dh.element_size()):
                     dm = torch.bmm(w1c.t().expand(B, C, O), dh)
+            return dm
+        want_w1, want_m = _wanted(ctx, 1), ctx.needs_input_grad[0]
+        if want_w1 and want_m:
+            dw1, dm = _overlapped(lambda: weight_grad_1x1(dh, m, w1dt), dm_gemm, dh.device)
+        else:
+            dw1 = weight_grad_1x1(dh, m, w1dt) if want_w1 else None
+            dm = dm_gemm() if want_m else None
         dx = dout if ctx.needs_input_grad[7] and not _stash_residual(ctx.slot, dout) else None
         return dm, dw1, ds, db1, dw2, db2, dgm, dx, None
 
