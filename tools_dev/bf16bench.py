@@ -40,12 +40,23 @@ dev = "cuda"
 bf = torch.bfloat16
 Bn = 32
 print("TF/s = FLOPs / time", flush=True)
-for name, O, I, P in [("b3 W1 512->2048 @64^2", 2048, 512, 4096), ("b3 W2 2048->512 @64^2", 512, 2048, 4096),
-                      ("b4 W1 256->1024 @128^2", 1024, 256, 16384), ("b4 W2 1024->256 @128^2", 256, 1024, 16384)]:
+SHAPES = [("b3 W1 512->2048 @64^2", 2048, 512, 4096), ("b3 W2 2048->512 @64^2", 512, 2048, 4096),
+          ("b4 W1 256->1024 @128^2", 1024, 256, 16384), ("b4 W2 1024->256 @128^2", 256, 1024, 16384),
+          ("b5 W1 128->512 @256^2", 512, 128, 65536), ("b5 W2 512->128 @256^2", 128, 512, 65536)]
+only_dw = os.environ.get("BF16BENCH_DW_ONLY") == "1"
+for name, O, I, P in SHAPES:
     W = (torch.randn(O, I, device=dev) * 0.05).to(bf)
     x = torch.randn(Bn, I, P, device=dev).to(bf)
     dy = torch.randn(Bn, O, P, device=dev).to(bf)
     fl = 2.0 * Bn * O * I * P
+    if only_dw:
+        V = Bn * (P // 64)
+        vs = [("blas", lambda: torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32).sum(0))]
+        for S in (16, 32, 64, 128, 256):
+            vs.append((f"g8r{S}", (lambda S=S: gemm_hip.try_gemm(dy, x.transpose(1, 2), out_dtype=torch.float32,
+                                                                  reduce_batch=True, route=("g8", -(-V // S))))))
+        line(f"dW  {name}", fl, vs)
+        continue
     line(f"fwd {name}", fl, [("blas", lambda: torch.bmm(W.expand(Bn, O, I), x)),
                              ("g8", lambda: gemm_hip.try_gemm(W, x, route=("g8", 0))),
                              ("g4", lambda: gemm_hip.try_gemm(W, x, route=("g4", 0)))])
