@@ -187,9 +187,11 @@ def _splits(M, N, K, z):
 
 # The backward's weight-gradient and data-gradient GEMMs are independent; on the bf16 (hipBLASLt) path they
 # are ridge-shaped (K = 512-2048 against 4096-65536-column planes: MFMA-bound K-loops, then output-write-
-# bound epilogues in synchronized tile rounds), so the weight gradient runs on a side stream next to the
-# data gradient and one kernel's write phase overlaps the other's K-loop. VFM_DW_STREAM=0 serialises them.
-_DW_STREAM = os.environ.get("VFM_DW_STREAM", "1") == "1"
+# bound epilogues in synchronized tile rounds). VFM_DW_STREAM=1 runs the weight gradient on a side stream
+# next to the data gradient so one kernel's write phase can overlap the other's K-loop; measured slower
+# (same-box A/B, profiles/r4_s_dw_stream_ab.txt: 95.95 / 95.61 img/s with it, 96.72 / 97.66 without), so
+# it is off by default.
+_DW_STREAM = os.environ.get("VFM_DW_STREAM", "0") == "1"
 _side_streams = {}
 
 
