@@ -101,3 +101,22 @@ def test_attention_f32_null_kv_cat():
     k = torch.cat([nk, torch.randn(B, h, P, 64, generator=g, device=DEV)], 2)
     v = torch.cat([nk * 0.5, torch.randn(B, h, P, 64, generator=g, device=DEV)], 2)
     _check(q, k, v)
+
+
+@pytest.mark.parametrize("B,N,H,d", [(2, 197, 6, 64), (3, 130, 4, 32)])
+def test_packed_qkv_attention_matches_unpacked(B, N, H, d):
+    """vit_ops.sdpa_packed (the packed-projection Function: q / k / v read in place, one packed gradient
+    buffer) against vit_ops.sdpa on the unpacked views: the same kernels, so identical outputs and
+    identical gradients of the projection."""
+    from torch_utils.ops import vit_ops
+    g = torch.Generator(device="cuda").manual_seed(N + d)
+    qkv = torch.randn(B, N, 3 * H * d, device="cuda", generator=g).requires_grad_(True)
+    do = torch.randn(B, H, N, d, device="cuda", generator=g)
+    out = vit_ops.sdpa_packed(qkv, H)
+    gp, = torch.autograd.grad(out, qkv, do)
+    ref_in = qkv.detach().clone().requires_grad_(True)
+    q, k, v = ref_in.reshape(B, N, 3, H, d).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = vit_ops.sdpa(q, k, v)
+    gr, = torch.autograd.grad(ref, ref_in, do)
+    assert torch.equal(out, ref)
+    assert torch.equal(gp, gr)

@@ -70,8 +70,11 @@ class SpectralConv1d(nn.Conv1d):
     def _gemm_out(x, weight, bias):
         # exact fp32 GEMM (hipBLASLt): the heads' BatchNormLocal over virtual batches of <= 8
         # samples amplifies GEMM rounding into the input gradient, so these stay on the vendor's
-        # fp32 products; they are a few GFLOP per step
-        y = torch.matmul(weight.reshape(weight.shape[0], -1), x)
+        # fp32 products. As a batched product with the weight broadcast (stride-0 batch): torch.matmul's
+        # 2-D x 3-D form folds the batch through x's transpose, which copies the [B, C k, L] columns
+        # forward and the gradient backward (~2.7 ms/step of copies, profiles/r4_h_opsites_timed.txt)
+        w2 = weight.reshape(weight.shape[0], -1)
+        y = torch.bmm(w2.expand(x.shape[0], *w2.shape), x) if x.dim() == 3 else torch.matmul(w2, x)
         if bias is not None:
             y = y + bias.to(y.dtype)[None, :, None]
         return y

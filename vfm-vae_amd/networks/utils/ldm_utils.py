@@ -74,8 +74,7 @@ class PlainAttention(nn.Module):
         B, N, C = x.shape
         bias = torch.cat((self.q_bias, self.zero_k_bias, self.v_bias))
         qkv = linear(x, self.qkv.weight, bias)
-        q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
-        x = vit_ops.sdpa(q, k, v)                                            # [B, h, N, d]
+        x = vit_ops.sdpa_packed(qkv, self.num_heads)                         # [B, h, N, d]
         if self.in_dim > self.out_dim:
             x = x.mean(dim=1)
             if self.in_dim // self.num_heads != self.out_dim:

@@ -40,8 +40,7 @@ class Attention(nn.Module):
     def forward(self, x):
         B, N, D = x.shape
         qkv = vit_ops.linear(x, self.qkv.weight.to(x.dtype), self.qkv.bias)
-        q, k, v = qkv.reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
-        o = vit_ops.sdpa(q, k, v).transpose(1, 2).reshape(B, N, D)
+        o = vit_ops.sdpa_packed(qkv, self.num_heads).transpose(1, 2).reshape(B, N, D)
         return vit_ops.linear(o, self.proj.weight.to(x.dtype), self.proj.bias)
 
 

@@ -119,6 +119,51 @@ class _Attention32(torch.autograd.Function):
         return dq, dk, dv
 
 
+class _Attention32Packed(torch.autograd.Function):
+    """The same kernels on a packed projection qkv [B, N, 3, H, d] (a view of a linear's [B, N, 3 H d]
+    output): q / k / v are read in place and the backward writes dq / dk / dv into ONE packed gradient
+    buffer, so autograd neither copies the strided views nor stacks three gradients back together."""
+
+    @staticmethod
+    def forward(ctx, qkv):
+        q, k, v = qkv.unbind(2)
+        o = _Attention32.forward(ctx, q, k, v)
+        ctx.packed_shape = qkv.shape
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        B, Nq, H, d = q.shape
+        do, sdo = _ready(do)
+        dqkv = torch.empty(ctx.packed_shape, dtype=torch.float32, device=q.device)
+        dq, dk, dv = dqkv.unbind(2)
+        delta = torch.empty(B, H, Nq, dtype=torch.float32, device=q.device)
+        flops = 10 * B * H * Nq * Nq * d
+        prec, _, tag = custom_ops.f32_precision()
+        with kernel_timer.region(f"attention_bwd<{tag},{d}>", 4 * 4 * 2 * B * Nq * H * d, flops, "mfma"):
+            rc = _lib.vfm_attention_f32_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(),
+                                            lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                                            dv.data_ptr(), B, H, Nq, Nq, d, _s4(q), _s4(k), _s4(v), _s4(o), sdo,
+                                            _s4(dq), _s4(dk), _s4(dv), float(d) ** -0.5, prec,
+                                            custom_ops.stream_ptr(q.device))
+        custom_ops.check(rc, "vfm_attention_f32_bwd")
+        return dqkv
+
+
+def sdpa_f32_packed(qkv, heads):
+    """sdpa over a packed fp32 projection qkv [B, N, 3 H d] (d = 64 or 32) -> [B, H, N, d] (a view of a
+    token-major tensor), or None when the layout does not fit the kernels (the caller unpacks)."""
+    B, N, D3 = qkv.shape
+    d = D3 // (3 * heads)
+    if not (qkv.is_cuda and qkv.dtype == torch.float32 and d in (32, HEAD_DIM) and 3 * heads * d == D3):
+        return None
+    q5 = qkv.reshape(B, N, 3, heads, d)
+    if _s4(q5[:, :, 0]) is None:
+        return None
+    return _Attention32Packed.apply(q5).transpose(1, 2)
+
+
 def supported_f32(q, k, v):
     return (q.is_cuda and q.dtype == torch.float32 and k.dtype == torch.float32 and v.dtype == torch.float32
             and q.shape[-1] in (32, HEAD_DIM) and k.shape == v.shape and q.shape[0] == k.shape[0]

@@ -146,6 +146,19 @@ def attention_packed(qkv, heads):
     return sdpa(q, k, v).transpose(1, 2).reshape(B, N, D)
 
 
+def sdpa_packed(qkv, heads):
+    """sdpa of the q / k / v packed in one projection output qkv [B, N, 3 heads d] -> [B, heads, N, d]:
+    fp32 ROCm operands on the packed HIP kernels (reads in place, one packed gradient), else unpacked."""
+    if qkv.is_cuda and qkv.dtype == torch.float32:
+        from . import attn_hip
+        out = attn_hip.sdpa_f32_packed(qkv, heads)
+        if out is not None:
+            return out
+    B, N, D3 = qkv.shape
+    q, k, v = qkv.reshape(B, N, 3, heads, D3 // (3 * heads)).permute(2, 0, 3, 1, 4).unbind(0)
+    return sdpa(q, k, v)
+
+
 def sdpa(q, k, v):
     """F.scaled_dot_product_attention(q, k, v) (no mask, default scale) on [B, H, N, d] operands.
     fp32 ROCm operands with head dim 64 run the HIP kernels (attn_hip.sdpa_f32, forward and
