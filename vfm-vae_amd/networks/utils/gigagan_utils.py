@@ -73,11 +73,21 @@ class SelfAttention(nn.Module):
         self.to_out = nn.Conv2d(inner, dim, 1, bias=False)
         nn.init.zeros_(self.to_out.weight)
 
+    # fp32 ROCm inputs: projections, attention with the null key / value and the output projection as one
+    # Function with no activation copies (torch_utils/ops/gigaattn_hip.py); VFM_GIGA_ATTN=0: unfused chain
+    fused = __import__("os").environ.get("VFM_GIGA_ATTN", "1") == "1"
+
     def forward(self, fmap):
         B, C, H, W = fmap.shape
         h, d = self.heads, self.dim_head
         x = self.norm(fmap).reshape(B, C, H * W)
         wqkv = torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], 0).reshape(3 * h * d, C)
+        if self.fused and self.to_out.bias is None:
+            from torch_utils.ops import gigaattn_hip
+            if gigaattn_hip.supported(x, h, d):
+                y = gigaattn_hip.null_kv_self_attention(x, wqkv, self.null_kv,
+                                                        self.to_out.weight.reshape(C, h * d), h)
+                return y.reshape(B, C, H, W)
         qkv = decoder_ops.pointwise(wqkv, x)                                   # [B, 3hd, P]
         q, k, v = qkv.reshape(B, 3, h, d, H * W).permute(1, 0, 2, 4, 3).unbind(0)  # [B, h, P, d]
         nk, nv = (t.to(q.dtype)[None, :, None, :].expand(B, h, 1, d) for t in self.null_kv.unbind(0))
