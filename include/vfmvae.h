@@ -174,6 +174,11 @@ int vfm_specnorm_bwd(const float* g, const float* W, const float* u, const float
  * for shapes not covered. */
 int vfm_im2col1d_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular, void* stream);
 int vfm_col2im1d_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular, void* stream);
+/* the same gather / adjoint with the batch folded into the columns, cols [C k, B, Lo]: the head conv of the
+   whole batch as one GEMM and its weight gradient as one GEMM with the batch in the reduction */
+int vfm_im2col1d_cbl_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular, void* stream);
+int vfm_col2im1d_cbl_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular,
+                         void* stream);
 
 /* Column sums of the per-sample [rows, cols] fp32 partials of the decoder backward kernels, two at a
  * time in one launch: out_a = scale_a * sum_r a (scale_a optional), out_b = sum_r b (either output may

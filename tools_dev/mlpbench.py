@@ -77,3 +77,9 @@ for C, H in [(512, 64), (256, 128)]:
     gb = (2 * B * 4 * C * P * 2) / 1e3
     print(f"   gelu-epilogue GEMMs: fwd(h,g) {t8:8.1f}us ({gb * 2 / t8:5.2f} TB/s out) | fwd(g) {t8n:8.1f}us | "
           f"bwd {t8b:8.1f}us", flush=True)
+    with torch.no_grad():
+        tgf = bench(lambda: decoder_hip.scale_bias_gelu(h, s_, b1))
+    hr = h.clone().requires_grad_(True)
+    dg = rnd(B, 4 * C, P)
+    tgb = bench(lambda: decoder_hip.scale_bias_gelu(hr, s_, b1).backward(dg)) - tgf
+    print(f"   unfused epilogue kernels: scale_bias_gelu fwd {tgf:8.1f}us | bwd {tgb:8.1f}us", flush=True)

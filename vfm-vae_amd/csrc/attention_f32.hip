@@ -336,8 +336,10 @@ __global__ __launch_bounds__(256) void attn32_delta(Args a, int rows) {
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int NP>
-__global__ __launch_bounds__(64 * WAVES, NP == 3 ? 1 : 2) void attn32_dq(Args a) {
+// OCC as in attn32_fwd: OCC = 1 prefetches the next K/V tile into registers (one wave per SIMD for
+// NP = 3), OCC = 2 loads it after the barrier and fits two workgroups per CU.
+template <int NP, int OCC>
+__global__ __launch_bounds__(64 * WAVES, OCC) void attn32_dq(Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG];
     unsigned char *kimg = lds, *vimg = lds + NP * IMG;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -360,13 +362,19 @@ __global__ __launch_bounds__(64 * WAVES, NP == 3 ? 1 : 2) void attn32_dq(Args a)
     f32x16 dq[2] = {f32x16{}, f32x16{}}, dqs[2] = {f32x16{}, f32x16{}};
     const float c = a.c;
     const int T = (Nk + TT - 1) / TT;
-    stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
-    stage_load(sv, vb, a.sv.n, 0, Nk, hd, tid);
+    if (OCC == 1) {
+        stage_load(sk, kb, a.sk.n, 0, Nk, hd, tid);
+        stage_load(sv, vb, a.sv.n, 0, Nk, hd, tid);
+    }
     for (int t = 0; t < T; ++t) {
+        if (OCC != 1) {
+            stage_load(sk, kb, a.sk.n, t * TT, Nk, hd, tid);
+            stage_load(sv, vb, a.sv.n, t * TT, Nk, hd, tid);
+        }
         stage_store<NP>(sk, kimg, tid);
         stage_store<NP>(sv, vimg, tid);
         __syncthreads();
-        if (t + 1 < T) {
+        if (OCC == 1 && t + 1 < T) {
             stage_load(sk, kb, a.sk.n, (t + 1) * TT, Nk, hd, tid);
             stage_load(sv, vb, a.sv.n, (t + 1) * TT, Nk, hd, tid);
         }
@@ -571,11 +579,16 @@ extern "C" int vfm_attention_f32_bwd(const void* q, const void* k, const void* v
     if (rows > (1ll << 31) / 16) return VFM_ERR_ARGS;
     VFM_LAUNCH(attn32_delta, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, st, a, (int)rows);
     const dim3 gq((Nq + RB - 1) / RB, H, B), gk((Nk + RB - 1) / RB, H, B);
+    static const int dq_occ = [] {
+        const char* e = getenv("VFM_ATTN32_DQ_OCC");
+        return e && e[0] == '1' ? 1 : 2;
+    }();
     if (precision == VFM_F32) {
-        VFM_LAUNCH(attn32_dq<3>, gq, dim3(64 * WAVES), 0, st, a);
+        if (dq_occ == 2) VFM_LAUNCH((attn32_dq<3, 2>), gq, dim3(64 * WAVES), 0, st, a);
+        else VFM_LAUNCH((attn32_dq<3, 1>), gq, dim3(64 * WAVES), 0, st, a);
         VFM_LAUNCH(attn32_dkdv<3>, gk, dim3(64 * WAVES), 0, st, a);
     } else {
-        VFM_LAUNCH(attn32_dq<2>, gq, dim3(64 * WAVES), 0, st, a);
+        VFM_LAUNCH((attn32_dq<2, 2>), gq, dim3(64 * WAVES), 0, st, a);
         VFM_LAUNCH(attn32_dkdv<2>, gk, dim3(64 * WAVES), 0, st, a);
     }
     return launch_status();

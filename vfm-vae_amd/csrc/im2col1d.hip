@@ -4,19 +4,32 @@
 // GEMM formulation, ~4 kernels forward and ~6 backward (CopySlices, slice / unfold backward)).
 //   cols[b, c k + j, l] = x[b, c, s],  s = l + j - p  (circular: mod L; zeros: 0 outside [0, L))
 //   dx[b, c, t]        = sum_j dcols[b, c k + j, l_j(t)]   over the l that read t
+// CBL = 1: the batch folded into the columns, cols[c k + j, b, l] ([C k, B Lo]): the whole batch's
+// convolution is then one GEMM W [O, C k] x cols with K = C k, and its weight gradient one GEMM
+// dY [O, B Lo] x cols^T with the batch in the reduction (no per-sample [O, C k] products to sum).
 #include "vfm_common.h"
 
 namespace {
 
 using namespace vfm;
 
-__global__ __launch_bounds__(256) void im2col1d(const float* __restrict__ x, float* __restrict__ cols, int C, int L,
-                                                int k, int p, int Lo, int circ, long long n) {
+template <int CBL>
+__global__ __launch_bounds__(256) void im2col1d(const float* __restrict__ x, float* __restrict__ cols, int B, int C,
+                                                int L, int k, int p, int Lo, int circ, long long n) {
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
         const int l = (int)(e % Lo);
-        const long long r = e / Lo;                  // (b C + c) k + j
-        const int j = (int)(r % k);
-        const long long bc = r / k;
+        const long long r = e / Lo;                  // CBL ? (c k + j) B + b : (b C + c) k + j
+        int j;
+        long long bc;
+        if (CBL) {
+            const int b = (int)(r % B);
+            const long long cj = r / B;
+            j = (int)(cj % k);
+            bc = (long long)b * C + cj / k;
+        } else {
+            j = (int)(r % k);
+            bc = r / k;
+        }
         int s = l + j - p;
         float v = 0.f;
         if (circ) {
@@ -30,12 +43,15 @@ __global__ __launch_bounds__(256) void im2col1d(const float* __restrict__ x, flo
     }
 }
 
-__global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols, float* __restrict__ dx, int C, int L,
-                                                int k, int p, int Lo, int circ, long long n) {
+template <int CBL>
+__global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols, float* __restrict__ dx, int B, int C,
+                                                int L, int k, int p, int Lo, int circ, long long n) {
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
         const int t = (int)(e % L);
         const long long bc = e / L;
-        const float* dr = dcols + bc * k * Lo;
+        // row j of (b, c): CBL ? ((c k + j) B + b) Lo : ((b C + c) k + j) Lo
+        const long long jstride = CBL ? (long long)B * Lo : Lo;
+        const float* dr = CBL ? dcols + (((bc % C) * k) * B + bc / C) * Lo : dcols + bc * k * Lo;
         float acc = 0.f;
         for (int j = 0; j < k; ++j) {
             int l = t - j + p;
@@ -45,7 +61,7 @@ __global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols,
             } else if (l < 0 || l >= Lo) {
                 continue;
             }
-            acc += dr[(long long)j * Lo + l];
+            acc += dr[(long long)j * jstride + l];
         }
         dx[e] = acc;
     }
@@ -53,28 +69,57 @@ __global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols,
 
 int grid_of(long long n) { return (int)std::min<long long>((n + 255) / 256, 16384); }
 
+int im2col_launch(const float* x, float* cols, int B, int C, int L, int k, int p, int circular, int cbl,
+                  void* stream) {
+    if (!x || !cols || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
+    const int Lo = L + 2 * p - k + 1;
+    if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
+    const long long n = (long long)B * C * k * Lo;
+    if (cbl)
+        VFM_LAUNCH(im2col1d<1>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo,
+                   circular ? 1 : 0, n);
+    else
+        VFM_LAUNCH(im2col1d<0>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo,
+                   circular ? 1 : 0, n);
+    return launch_status();
+}
+
+int col2im_launch(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular, int cbl,
+                  void* stream) {
+    if (!dcols || !dx || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
+    const int Lo = L + 2 * p - k + 1;
+    if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
+    const long long n = (long long)B * C * L;
+    if (cbl)
+        VFM_LAUNCH(col2im1d<1>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p, Lo,
+                   circular ? 1 : 0, n);
+    else
+        VFM_LAUNCH(col2im1d<0>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p, Lo,
+                   circular ? 1 : 0, n);
+    return launch_status();
+}
+
 }  // namespace
 
 // cols [B, C k, Lo] from x [B, C, L], Lo = L + 2 p - k + 1; circular padding needs Lo == L.
 extern "C" int vfm_im2col1d_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular,
                                 void* stream) {
-    if (!x || !cols || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
-    const int Lo = L + 2 * p - k + 1;
-    if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
-    const long long n = (long long)B * C * k * Lo;
-    VFM_LAUNCH(im2col1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, C, L, k, p, Lo,
-                       circular ? 1 : 0, n);
-    return launch_status();
+    return im2col_launch(x, cols, B, C, L, k, p, circular, 0, stream);
 }
 
 // dx [B, C, L] = the adjoint of vfm_im2col1d_f32 applied to dcols [B, C k, Lo].
 extern "C" int vfm_col2im1d_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular,
                                 void* stream) {
-    if (!dcols || !dx || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
-    const int Lo = L + 2 * p - k + 1;
-    if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
-    const long long n = (long long)B * C * L;
-    VFM_LAUNCH(col2im1d, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, C, L, k, p, Lo,
-                       circular ? 1 : 0, n);
-    return launch_status();
+    return col2im_launch(dcols, dx, B, C, L, k, p, circular, 0, stream);
+}
+
+// the same with the batch folded into the columns: cols [C k, B, Lo]
+extern "C" int vfm_im2col1d_cbl_f32(const float* x, float* cols, int B, int C, int L, int k, int p, int circular,
+                                    void* stream) {
+    return im2col_launch(x, cols, B, C, L, k, p, circular, 1, stream);
+}
+
+extern "C" int vfm_col2im1d_cbl_f32(const float* dcols, float* dx, int B, int C, int L, int k, int p, int circular,
+                                    void* stream) {
+    return col2im_launch(dcols, dx, B, C, L, k, p, circular, 1, stream);
 }

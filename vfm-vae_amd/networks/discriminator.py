@@ -28,6 +28,9 @@ from networks.utils.vit_utils import VisionTransformer, make_vit_backbone, forwa
 from networks.utils.vfm_utils import VFM2INTERPOLATION
 from training.diffaug import DiffAugment
 
+# VFM_DHEAD_FOLDED=0: the per-sample batched GEMMs (stride-0 weight) instead of the batch-folded GEMMs
+_FOLDED = os.environ.get("VFM_DHEAD_FOLDED", "1") == "1"
+
 IMAGENET_DEFAULT_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_DEFAULT_STD = (0.229, 0.224, 0.225)
 
@@ -35,8 +38,8 @@ IMAGENET_DEFAULT_STD = (0.229, 0.224, 0.225)
 class SpectralConv1d(nn.Conv1d):
     """Spectral-normalised Conv1d (reference discriminator.py:39-42).
 
-    On ROCm tensors the convolution runs as one GEMM over the whole batch
-    (k = 1: directly; k > 1: circular/zero pad + unfold to [B, C*k, L]) instead of
+    On ROCm fp32 tensors the convolution of the whole batch is one exact-fp32 GEMM each way, the
+    batch folded into the im2col columns ([C k, B L], patchgan_hip.conv1d_folded), instead of
     MIOpen's per-sample im2col + small-GEMM loop; same math."""
 
     def __init__(self, *args, **kwargs):
@@ -51,10 +54,14 @@ class SpectralConv1d(nn.Conv1d):
         if not x.is_cuda or self.groups != 1 or self.stride != (1,) or self.dilation != (1,) or x.dim() != 3:
             return super()._conv_forward(x, weight, bias)
         k = self.kernel_size[0]
-        if k > 1 or self.padding[0] > 0:
-            p = self.padding[0]
-            from torch_utils.ops import patchgan_hip
-            circ = self.padding_mode == 'circular'
+        p = self.padding[0]
+        circ = self.padding_mode == 'circular'
+        from torch_utils.ops import patchgan_hip
+        if (_FOLDED and self.padding_mode in ('zeros', 'circular')
+                and patchgan_hip.conv1d_folded_supported(x, k, p, circ)):
+            # the whole batch as one GEMM each way, batch folded into the columns (csrc/im2col1d.hip CBL)
+            return patchgan_hip.conv1d_folded(x, weight.reshape(weight.shape[0], -1), bias, k, p, circ)
+        if k > 1 or p > 0:
             if self.padding_mode in ('zeros', 'circular') and patchgan_hip.im2col1d_supported(x, k, p, circ):
                 x = patchgan_hip.im2col1d(x, k, p, circ)             # one launch each way (csrc/im2col1d.hip)
                 return self._gemm_out(x, weight, bias)

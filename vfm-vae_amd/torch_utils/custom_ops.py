@@ -89,6 +89,8 @@ SIGNATURES = {
     "vfm_specnorm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     "vfm_im2col1d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_col2im1d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_im2col1d_cbl_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_col2im1d_cbl_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_colsum2_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     "vfm_shift2d": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_im2col_nhwc_f32": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],

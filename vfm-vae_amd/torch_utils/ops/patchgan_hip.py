@@ -303,3 +303,66 @@ def im2col1d_supported(x, k, p, circular):
 def im2col1d(x, k, p, circular):
     """[B, C, L] -> [B, C k, Lo]: F.pad(x, (p, p), circular / zeros).unfold(2, k, 1) in the GEMM layout."""
     return _Im2col1d.apply(x, int(k), int(p), bool(circular))
+
+
+# ---------------------------------------------------------------------------
+# The D heads' SpectralConv1d over the whole batch as single GEMMs (reference networks/discriminator.py
+# :39-42, 116-142: nn.Conv1d, k = 1 or 9 with circular padding). The columns are gathered with the batch
+# folded in, cols [C k, B Lo] (vfm_im2col1d_cbl_f32), so
+#   forward   y [O, B Lo] = W [O, C k] cols (+ bias), one [B, O, Lo] transpose copy of the small output;
+#   backward  dW = dY [O, B Lo] cols^T  (the batch inside the reduction: no per-sample [O, C k] products
+#             and no batch sum), dcols = W^T dY, dx = the folded col2im; db = row sums of dY.
+# Exact fp32 products on the vendor GEMM (TF32 off), as the reference runs them: the heads' BatchNormLocal
+# over virtual batches of 8 samples amplifies GEMM rounding into the input gradient.
+
+
+class _Conv1dFolded(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w2, bias, k, p, circular):
+        x = _c16(x.float())
+        B, C, L = x.shape
+        O = w2.shape[0]
+        Lo = L + 2 * p - k + 1
+        cols = torch.empty([C * k, B * Lo], dtype=torch.float32, device=x.device)
+        with kernel_timer.region('im2col1d_cbl<f32>', 4 * (x.numel() + cols.numel())):
+            _check(_lib.vfm_im2col1d_cbl_f32(x.data_ptr(), cols.data_ptr(), B, C, L, k, p, int(circular), _stream()),
+                   'vfm_im2col1d_cbl_f32')
+        w = w2.detach().float()
+        if bias is not None:
+            y2 = torch.addmm(bias.detach().float()[:, None], w, cols)
+        else:
+            y2 = torch.mm(w, cols)
+        ctx.save_for_backward(cols, w)
+        ctx.meta = (B, C, L, k, p, circular, w2.dtype, None if bias is None else bias.dtype)
+        return y2.view(O, B, Lo).transpose(0, 1).contiguous()
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        cols, w = ctx.saved_tensors
+        B, C, L, k, p, circular, wdt, bdt = ctx.meta
+        O = w.shape[0]
+        gy2 = dy.float().transpose(0, 1).reshape(O, -1)                       # [O, B Lo]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dcols = _c16(torch.mm(w.t(), gy2))
+            dx = torch.empty([B, C, L], dtype=torch.float32, device=dy.device)
+            with kernel_timer.region('col2im1d_cbl<f32>', 4 * (dx.numel() + dcols.numel())):
+                _check(_lib.vfm_col2im1d_cbl_f32(dcols.data_ptr(), dx.data_ptr(), B, C, L, k, p, int(circular),
+                                                 _stream()), 'vfm_col2im1d_cbl_f32')
+        if ctx.needs_input_grad[1]:
+            dw = torch.mm(gy2, cols.t()).to(wdt)
+        if ctx.needs_input_grad[2]:
+            db = gy2.sum(1).to(bdt)
+        return dx, dw, db, None, None, None
+
+
+def conv1d_folded_supported(x, k, p, circular):
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.numel() > 0
+            and x.shape[2] + 2 * p - k + 1 > 0 and (not circular or (2 * p == k - 1 and p <= x.shape[2])))
+
+
+def conv1d_folded(x, w2, bias, k, p, circular):
+    """y [B, O, Lo] = conv1d(pad(x, p, circular / zeros), W) for x [B, C, L] fp32, w2 [O, C k] (the
+    Conv1d weight reshaped), stride 1, one group."""
+    return _Conv1dFolded.apply(x, w2, bias, int(k), int(p), bool(circular))
