@@ -511,6 +511,14 @@ int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* bias, const 
                         int B, int C, int H, int W, int K, int pad, int flip, void* stream);
 int vfm_dwconv2d_fwd_mfma_ex(const void* x, const float* w, const float* bias, const float* noise, const void* res,
                              void* y, int B, int C, int H, int W, int K, int pad, int flip, void* stream);
+/* vfm_dwconv2d_fwd_mfma_ex that also writes, when npart is given (with nplane fp32 [H, W], 16-B aligned),
+ * npart[u] = wave u's share of sum_{b,c,y,x} x[b,c,y,x] nplane[y,x] for u < vfm_dwconv2d_fwd_mfma_units(...):
+ * in the data-gradient call (x = dY) the gradient of the legacy noise strength (reference
+ * convnext_utils.py noise_const * noise_strength added after the dwconv) without another pass over dY. */
+int vfm_dwconv2d_fwd_mfma_nz(const void* x, const float* w, const float* bias, const float* noise, const void* res,
+                             void* y, const float* nplane, float* npart, int B, int C, int H, int W, int K, int pad,
+                             int flip, void* stream);
+long long vfm_dwconv2d_fwd_mfma_units(int B, int C, int H, int W, int K, int pad);
 /* dw[c, t] = sum_r partial[r, c, t] (t < KK), db[c] = sum_r partial[r, c, KK] over the [rows, C, KK + 1]
  * partials of the depthwise weight-gradient kernels (either output may be null). */
 int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float* db, int rows, int C, int KK, void* stream);

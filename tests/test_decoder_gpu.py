@@ -121,6 +121,50 @@ def test_dwconv2d_mfma(case):
     assert _rel(bg.grad, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 8, 16, 16, 3), (3, 4, 64, 64, 7), (2, 5, 37, 48, 7), (4, 6, 32, 128, 5),
+                                  (1, 3, 5, 16, 3)])
+def test_dwconv2d_noise_strength(case, dt):
+    """The legacy noise as plane * strength (reference convnext_utils.py: noise_const * noise_strength
+    added after the dwconv): the strength's gradient sum dY * plane comes from the data-gradient
+    kernel's per-wave partials on bf16 planes (vfm_dwconv2d_fwd_mfma_nz) and from a torch dot
+    otherwise; against an fp64 dot of the same dY within 1e-5 (fp32 partial sums), the forward and the
+    other gradients as the torch formulation (decoder tolerances), and the plane's own gradient
+    strength * sum_{b,c} dY when it is asked for."""
+    ops, kt = _ops()
+    B, C, H, W, K = case
+    torch.manual_seed(3)
+    x = torch.randn(B, C, H, W, device=DEV).to(dt)
+    w = (torch.randn(C, 1, K, K, device=DEV) * 0.2)
+    b = (torch.randn(C, device=DEV) * 0.1)
+    plane = torch.randn(H, W, device=DEV)
+    strength = torch.tensor(0.37, device=DEV)
+    dy = torch.randn(B, C, H, W, device=DEV).to(dt)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b, strength)]
+    kt.enable(True)
+    y = ops.dwconv2d(leaves[0], leaves[1], leaves[2], K // 2, noise=plane, noise_strength=leaves[3])
+    y.backward(dy)
+    torch.cuda.synchronize()
+    names = set(kt.summary())
+    kt.enable(False)
+    if dt == torch.bfloat16 and W % 16 == 0:
+        assert any(n.startswith("dwconv2d_mfma_bwd_data") for n in names), names
+    ref_leaves = [t.detach().float().clone().requires_grad_(True) for t in (x, w, b, strength)]
+    yr = ops.dwconv2d(ref_leaves[0], ref_leaves[1], ref_leaves[2], K // 2, noise=plane,
+                      noise_strength=ref_leaves[3], impl='ref')
+    yr.backward(dy.float())
+    tol = _tol(dt)
+    assert _rel(y.float(), yr) < tol
+    for a, r in zip(leaves[:3], ref_leaves[:3]):
+        assert _rel(a.grad.float(), r.grad) < 4 * tol
+    exact = (dy.double() * plane.double()).sum()
+    assert abs(float(leaves[3].grad) - float(exact)) <= 1e-5 * float((dy.double().abs() * plane.double().abs()).sum())
+    # the plane itself with a gradient (not the model's use): d plane = strength * sum_{b,c} dY
+    pl = plane.clone().requires_grad_(True)
+    ops.dwconv2d(x, w, b, K // 2, noise=pl, noise_strength=strength).backward(dy)
+    assert _rel(pl.grad, 0.37 * dy.float().sum((0, 1))) < 1e-5
+
+
 def test_dwconv2d_no_bias_valid_padding():
     ops, _ = _ops()
     torch.manual_seed(2)

@@ -20,7 +20,9 @@
 // block's loads in flight during the current block's MFMAs. Output: lane l holds
 // out[y0 + (l & 15)][x0 + 16 s + 4 (l >> 4) + r], r < 4 -> one 8-B store per tile (+ the fp32 noise
 // plane of the legacy noise path, and / or a residual tensor (the data gradient's other branch),
-// when given).
+// when given). With npart (the data gradient of a legacy-noise layer), each wave also writes
+// npart[unit] = sum over its output positions of x[b, c, y, x] * nplane[y, x] from the staged input
+// rows: the noise strength's gradient sum_{b,c,y,x} dY * noise_plane without another pass over dY.
 #include "vfm_common.h"
 
 namespace {
@@ -39,6 +41,8 @@ struct DwmArgs {
     const float* bias;                    // [C] or null
     const float* noise;                   // [H, W] fp32 added to every channel (legacy noise) or null
     const __hip_bfloat16* res;            // [B, C, H, W] bf16 added before the output rounding, or null
+    const float* nplane;                  // [H, W] fp32: with npart, sum x * nplane per wave (see below)
+    float* npart;                         // [units] or null
     __hip_bfloat16* y;
     int B, C, H, W, XW, nyb, nxs, rb;     // rb: 16-row blocks per wave
     int flip;                             // taps read rotated by 180 degrees (the data gradient)
@@ -129,6 +133,7 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     }
     const float bias = a.bias ? a.bias[c] : 0.f;
     const int n = lane & 15;                                // output row of this lane (B / C column)
+    float ndot = 0.f;
 
     for (int kb = 0; kb < nblk; ++kb) {
         const int y0 = 16 * (yb0 + kb);
@@ -159,8 +164,22 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
             if (oy < a.H) {
                 const uint2 o = make_uint2(pk_bf16(acc[0], acc[1]), pk_bf16(acc[2], acc[3]));   // 2 v_cvt_pk_bf16_f32
                 *reinterpret_cast<uint2*>(yp + 16 * s) = o;
+                if (a.npart) {     // input at the output position: staged row n + P, column 8 + 16 s + 4 g
+                    const uint2 xv = *reinterpret_cast<const uint2*>(img + (n + P) * RS + 16 + 32 * s + 8 * g);
+                    const float4 pl = *reinterpret_cast<const float4*>(a.nplane + (long long)oy * a.W + x0 +
+                                                                       16 * s + 4 * g);
+                    ndot = fmaf(__uint_as_float(xv.x << 16), pl.x, ndot);
+                    ndot = fmaf(__uint_as_float(xv.x & 0xffff0000u), pl.y, ndot);
+                    ndot = fmaf(__uint_as_float(xv.y << 16), pl.z, ndot);
+                    ndot = fmaf(__uint_as_float(xv.y & 0xffff0000u), pl.w, ndot);
+                }
             }
         }
+    }
+    if (a.npart) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) ndot += __shfl_xor(ndot, m);
+        if (lane == 0) a.npart[unit] = ndot;
     }
 }
 
@@ -338,33 +357,57 @@ bool dwm_bw_plan(DwmBwArgs& a, int B, int C, int H, int W, int& XW) {
     return true;
 }
 
-}  // namespace
-
-// y = dwconv(x, w) + bias on bf16 NCHW planes via MFMA (see the header). VFM_NO_KERNEL for shapes it
-// does not cover (W % 16, pad != (K - 1) / 2, K not in {3, 5, 7}, misaligned pointers): the caller
-// then uses vfm_dwconv2d_fwd.
-extern "C" int vfm_dwconv2d_fwd_mfma_ex(const void* x, const float* w, const float* bias, const float* noise,
-                                        const void* res, void* y, int B, int C, int H, int W, int K, int pad, int flip,
-                                        void* stream) {
-    if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
-    if ((K != 3 && K != 5 && K != 7) || pad != (K - 1) / 2 || W % 16) return VFM_NO_KERNEL;
-    if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)noise | (uintptr_t)res) % 16) return VFM_NO_KERNEL;
-    DwmArgs a;
-    a.x = (const __hip_bfloat16*)x; a.w = w; a.bias = bias; a.noise = noise; a.y = (__hip_bfloat16*)y;
-    a.res = (const __hip_bfloat16*)res;
-    a.B = B; a.C = C; a.H = H; a.W = W; a.flip = flip != 0;
+bool dwm_plan(DwmArgs& a, int B, int C, int H, int W, int K, int pad) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return false;
+    if ((K != 3 && K != 5 && K != 7) || pad != (K - 1) / 2 || W % 16) return false;
+    a.B = B; a.C = C; a.H = H; a.W = W;
     a.XW = W % 64 == 0 ? 64 : 16;
     const int rows16 = (H + 15) / 16;
     a.rb = rows16 < 4 ? rows16 : 4;                        // up to 64 output rows per wave
     a.nyb = (rows16 + a.rb - 1) / a.rb;
     a.nxs = W / a.XW;
     a.units = (long long)B * C * a.nyb * a.nxs;
+    return true;
+}
+
+}  // namespace
+
+// y = dwconv(x, w) + bias on bf16 NCHW planes via MFMA (see the header). VFM_NO_KERNEL for shapes it
+// does not cover (W % 16, pad != (K - 1) / 2, K not in {3, 5, 7}, misaligned pointers): the caller
+// then uses vfm_dwconv2d_fwd. With npart (vfm_dwconv2d_fwd_mfma_units entries) and nplane [H, W] fp32:
+// npart[u] = the wave's share of sum_{b, c, y, x} x[b, c, y, x] nplane[y, x].
+extern "C" int vfm_dwconv2d_fwd_mfma_nz(const void* x, const float* w, const float* bias, const float* noise,
+                                        const void* res, void* y, const float* nplane, float* npart, int B, int C,
+                                        int H, int W, int K, int pad, int flip, void* stream) {
+    if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
+    if (!npart != !nplane) return VFM_ERR_ARGS;
+    DwmArgs a;
+    if (!dwm_plan(a, B, C, H, W, K, pad)) return VFM_NO_KERNEL;
+    if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)noise | (uintptr_t)res | (uintptr_t)nplane) % 16)
+        return VFM_NO_KERNEL;
+    a.x = (const __hip_bfloat16*)x; a.w = w; a.bias = bias; a.noise = noise; a.y = (__hip_bfloat16*)y;
+    a.res = (const __hip_bfloat16*)res;
+    a.nplane = nplane; a.npart = npart;
+    a.flip = flip != 0;
     hipStream_t st = (hipStream_t)stream;
     switch (K) {
     case 3: return dwm_launch<3>(a, st);
     case 5: return dwm_launch<5>(a, st);
     default: return dwm_launch<7>(a, st);
     }
+}
+
+// entries of vfm_dwconv2d_fwd_mfma_nz's npart; VFM_NO_KERNEL if the shape is not covered
+extern "C" long long vfm_dwconv2d_fwd_mfma_units(int B, int C, int H, int W, int K, int pad) {
+    DwmArgs a;
+    if (!dwm_plan(a, B, C, H, W, K, pad)) return VFM_NO_KERNEL;
+    return a.units;
+}
+
+extern "C" int vfm_dwconv2d_fwd_mfma_ex(const void* x, const float* w, const float* bias, const float* noise,
+                                        const void* res, void* y, int B, int C, int H, int W, int K, int pad, int flip,
+                                        void* stream) {
+    return vfm_dwconv2d_fwd_mfma_nz(x, w, bias, noise, res, y, nullptr, nullptr, B, C, H, W, K, pad, flip, stream);
 }
 
 extern "C" int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, const float* noise,

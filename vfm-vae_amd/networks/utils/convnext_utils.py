@@ -80,14 +80,24 @@ class ConvNeXtSynthesisLayer(nn.Module):
         self.act = nn.GELU()
         self.gamma = nn.Parameter(layer_scale_init * torch.ones([1, channels, 1, 1])) if layer_scale_init > 0 else None
 
-    def _noise(self, H, W):
+    def _noise(self, H, W, split=False):
+        """The legacy noise added after the dwconv: noise_const * noise_strength, bilinearly resized to
+        H x W (reference convnext_utils.py:131-133). Returns (plane, None) with the product, or with
+        split (the GPU path) (resized noise_const, noise_strength) -- resizing is linear, so the same
+        math -- so that the dwconv's data-gradient pass over dY also yields the strength's gradient
+        sum dY * plane."""
         if not self.legacy:
-            return None
+            return None, None
+        if split:
+            plane = self.noise_const
+            if plane.shape[-2:] != (H, W):
+                plane = F.interpolate(plane[None, None], size=(H, W), mode='bilinear', align_corners=False)[0, 0]
+            return plane.float(), self.noise_strength
         noise = self.noise_const * self.noise_strength
         if noise.shape[-2:] == (H, W):
-            return noise.float()              # no [None, None] / [0, 0] round trip: its backward is a zeros + copy
+            return noise.float(), None        # no [None, None] / [0, 0] round trip: its backward is a zeros + copy
         noise = F.interpolate(noise[None, None], size=(H, W), mode='bilinear', align_corners=False)
-        return noise[0, 0].float()
+        return noise[0, 0].float(), None
 
     def forward(self, x, w, compute_dtype=None):
         cdt = compute_dtype or x.dtype
@@ -102,8 +112,9 @@ class ConvNeXtSynthesisLayer(nn.Module):
         if x.is_cuda and x.dtype == cdt and x.requires_grad and torch.is_grad_enabled():
             from torch_utils.ops import decoder_hip
             slot = decoder_hip.ResidualSlot() if decoder_hip.RESIDUAL_FUSION else None
+        plane, strength = self._noise(H, W, split=x.is_cuda)
         d = decoder_ops.dwconv2d(x.to(cdt), self.dwconv.weight, self.dwconv.bias, self.kernel_size // 2,
-                                 noise=self._noise(H, W), slot=slot)
+                                 noise=plane, slot=slot, noise_strength=strength)
         m = decoder_ops.group_norm(d, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps,
                                    out_dtype=cdt, style=style)                 # GN(d) * s_b
         gamma = self.gamma.reshape(-1) if self.gamma is not None else None

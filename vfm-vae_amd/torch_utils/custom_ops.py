@@ -83,6 +83,9 @@ SIGNATURES = {
                             c_vp],
     "vfm_dwconv2d_fwd_mfma_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_vp],
+    "vfm_dwconv2d_fwd_mfma_nz": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_int, c_vp],
+    "vfm_dwconv2d_fwd_mfma_units": [c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_dwconv2d_wgrad_reduce": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
     "vfm_specnorm_workspace_floats": [c_int, c_int],
     "vfm_specnorm_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp],
@@ -186,6 +189,7 @@ def get_native():
             lib.vfm_bnl_workspace_floats.restype = c_ll
             lib.vfm_channel_rms_norm_rows.restype = c_ll
             lib.vfm_specnorm_workspace_floats.restype = c_ll
+            lib.vfm_dwconv2d_fwd_mfma_units.restype = c_ll
             _lib = lib
     return _lib
 

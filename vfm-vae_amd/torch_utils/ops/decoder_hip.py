@@ -266,10 +266,12 @@ def pointwise(w, x):
 DW_MFMA = os.environ.get("VFM_DW_MFMA", "1") == "1"      # A/B switch for the banded-MFMA dwconv
 
 
-def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False):
+def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None):
     """y = dwconv(x) (+ bias, + noise plane) (+ res, a tensor of y's shape: the residual-branch
     gradient added in the MFMA kernel's epilogue, else by a torch add); flip: taps rotated by 180
-    degrees in the kernel (the data gradient)."""
+    degrees in the kernel (the data gradient). nplane ([H, W] fp32): also return sum x * nplane over
+    (b, c, y, x) as a 0-d fp32 tensor -- from per-wave partials of the MFMA kernel when it runs, else
+    by torch -- i.e. (y, dot)."""
     B, C, H, W = x.shape
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -280,16 +282,29 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False):
         # bf16 planes: the banded-MFMA kernel (csrc/dwconv_mfma.hip); taps rounded to bf16 as
         # the reference's autocast conv does
         r = None if res is None else _c(res.to(torch.bfloat16))
+        part = None
+        if nplane is not None and Ho == H and Wo == W:
+            units = _lib.vfm_dwconv2d_fwd_mfma_units(B, C, H, W, K, pad)
+            part = torch.empty([units], dtype=torch.float32, device=x.device) if units > 0 else None
         with kernel_timer.region(_rn(name.replace('dwconv2d', 'dwconv2d_mfma'), x, K), _nb(x, y, r)):
-            rc = _lib.vfm_dwconv2d_fwd_mfma_ex(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), _p(r), y.data_ptr(),
-                                               B, C, H, W, K, pad, int(flip), _stream())
+            rc = _lib.vfm_dwconv2d_fwd_mfma_nz(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), _p(r), y.data_ptr(),
+                                               _p(nplane if part is not None else None), _p(part), B, C, H, W, K,
+                                               pad, int(flip), _stream())
         if rc != custom_ops.VFM_NO_KERNEL:
             _check(rc, name)
-            return y
+            if nplane is None:
+                return y
+            return y, (part.sum() if part is not None else _plane_dot(x, nplane))
     with kernel_timer.region(_rn(name, x, K), _nb(x, y)):
         _check(_lib.vfm_dwconv2d_fwd_ex(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
                                         B, C, H, W, K, pad, int(flip), _stream()), name)
-    return y if res is None else y.add_(res.to(y.dtype))
+    y = y if res is None else y.add_(res.to(y.dtype))
+    return y if nplane is None else (y, _plane_dot(x, nplane))
+
+
+def _plane_dot(x, plane):
+    """sum_{b, c, y, x} x * plane[y, x] (fp32 accumulation, no fp32 copy of x)."""
+    return (x.sum(dim=(0, 1), dtype=torch.float32) * plane).sum()
 
 
 RESIDUAL_FUSION = os.environ.get("VFM_RESIDUAL_FUSION", "1") == "1"     # A/B switch (tests, benches)
@@ -331,38 +346,51 @@ def _dw_wgrad(part, want_w, want_b, C, K, wshape, wdt, bdt):
 
 
 class _DwConv2d(torch.autograd.Function):
+    """Depthwise conv (+ bias) (+ noise plane, or noise plane * strength for the legacy noise: then
+    `noise` is the constant plane and the strength's gradient sum dY * plane comes out of the data-
+    gradient kernel's pass over dY, decoder_hip._dw_fwd nplane)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, noise, pad, slot):
-        _edges(ctx, x, weight, bias, noise, pad, slot)
+    def forward(ctx, x, weight, bias, noise, pad, slot, strength=None):
+        _edges(ctx, x, weight, bias, noise, pad, slot, strength)
         ctx.slot = slot
         x = _c(x)
         C, K = weight.shape[0], weight.shape[-1]
         w3 = weight.detach().reshape(C, K, K).float().contiguous()
         b = _f32(bias)
         n = None if noise is None else noise.detach().float().contiguous()
+        plane = None
+        ctx.strength = None
+        if strength is not None:
+            plane = n
+            ctx.strength = strength.detach().float()
+            n = (n * ctx.strength).contiguous()
         y = _dw_fwd(x, w3, b, n, pad, 'dwconv2d_fwd')
-        ctx.save_for_backward(x, w3)
+        ctx.save_for_backward(x, w3, plane)
         ctx.pad = pad
         ctx.meta = (weight.dtype, weight.shape, None if bias is None else bias.dtype,
-                    None if noise is None else noise.dtype)
+                    None if noise is None else noise.dtype, None if strength is None else strength.dtype)
         return y
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, dy):
-        x, w3 = ctx.saved_tensors
+        x, w3, plane = ctx.saved_tensors
         pad = ctx.pad
-        wdt, wshape, bdt, ndt = ctx.meta
+        wdt, wshape, bdt, ndt, sdt = ctx.meta
         dy = _c(dy.to(x.dtype))
         B, C, H, W = x.shape
         K = w3.shape[-1]
-        dx = dw = db = dn = None
+        dx = dw = db = dn = dstr = None
         want_w, want_b = _wanted(ctx, 1), _wanted(ctx, 2)
+        want_s = plane is not None and _wanted(ctx, 6)
         res = None
         if ctx.slot is not None and ctx.slot.grad is not None:
             res, ctx.slot.grad = ctx.slot.grad, None
         if _wanted(ctx, 0):
-            dx = _dw_fwd(dy, w3, None, None, K - 1 - pad, 'dwconv2d_bwd_data', res, flip=True)
+            out = _dw_fwd(dy, w3, None, None, K - 1 - pad, 'dwconv2d_bwd_data', res, flip=True,
+                          nplane=plane if want_s else None)
+            dx, dstr = out if want_s else (out, None)
         # (res unused when dx is not wanted: then nothing consumes x's gradient in this pass)
         if (want_w or want_b) and DW_MFMA and x.dtype == torch.bfloat16 and \
                 _lib.vfm_dwconv2d_bwd_weight_mfma_tiles(B, C, H, W, K, pad) > 0:
@@ -382,13 +410,16 @@ class _DwConv2d(torch.autograd.Function):
                 _check(_lib.vfm_dwconv2d_bwd_weight(x.data_ptr(), dy.data_ptr(), part.data_ptr(), _code(x),
                                                     B, C, H, W, K, pad, _stream()), 'vfm_dwconv2d_bwd_weight')
             dw, db = _dw_wgrad(part, want_w, want_b, C, K, wshape, wdt, bdt)
+        if want_s and dstr is None:
+            dstr = _plane_dot(dy, plane)
         if _wanted(ctx, 3):
-            dn = dy.sum(dim=(0, 1), dtype=torch.float32).to(ndt)       # fp32 accumulation, no fp32 copy of dy
-        return dx, dw, db, dn, None, None
+            dn = dy.sum(dim=(0, 1), dtype=torch.float32)                  # fp32 accumulation, no fp32 copy of dy
+            dn = (dn if plane is None else dn * ctx.strength).to(ndt)      # d plane = strength * sum_{b,c} dy
+        return dx, dw, db, dn, None, None, (None if dstr is None else dstr.reshape(()).to(sdt))
 
 
-def dwconv2d(x, weight, bias, padding, noise, slot=None):
-    y = _DwConv2d.apply(x, weight, bias, noise, int(padding), slot)
+def dwconv2d(x, weight, bias, padding, noise, slot=None, noise_strength=None):
+    y = _DwConv2d.apply(x, weight, bias, noise, int(padding), slot, noise_strength)
     if slot is not None:
         slot.node = y.grad_fn
     return y

@@ -78,16 +78,19 @@ def pointwise(weight, x, impl='cuda'):
 # Depthwise k x k convolution (+bias, + optional additive [H, W] plane).
 
 
-def dwconv2d(x, weight, bias=None, padding=0, noise=None, impl='cuda', slot=None):
+def dwconv2d(x, weight, bias=None, padding=0, noise=None, impl='cuda', slot=None, noise_strength=None):
     """Depthwise conv: weight [C, 1, k, k], zero padding `padding`, stride 1.
-    `noise` ([H_out, W_out], fp32) is added to every channel (legacy noise path). `slot`
+    `noise` ([H_out, W_out], fp32) is added to every channel (legacy noise path); with
+    `noise_strength` (0-d) the added plane is noise * noise_strength. `slot`
     (decoder_hip.ResidualSlot, HIP path only) receives the layer's residual gradient."""
     if _use_hip('dwconv2d', x, impl, k=weight.shape[-1]):
         from . import decoder_hip
-        return decoder_hip.dwconv2d(x, weight, bias, padding, noise, slot)
+        return decoder_hip.dwconv2d(x, weight, bias, padding, noise, slot, noise_strength)
     y = F.conv2d(x, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None, padding=padding,
                  groups=x.shape[1])
     if noise is not None:
+        if noise_strength is not None:
+            noise = noise * noise_strength
         y = y + noise.to(y.dtype)
     return y
 
