@@ -1,0 +1,7 @@
+#!/bin/bash
+# Same-box A/B of a bench.py argument: ab_args.sh <tag> "<args A>" "<args B>"; A,B,A,B bench runs.
+out=gpurun_out/$1; mkdir -p $out
+for i in 1 2; do
+  timeout -k 10 600 python bench.py --no-cpu-baseline $2 > $out/a$i.log 2>&1 || exit $?
+  timeout -k 10 600 python bench.py --no-cpu-baseline $3 > $out/b$i.log 2>&1 || exit $?
+done

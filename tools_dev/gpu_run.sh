@@ -98,6 +98,8 @@ for s in "$@"; do
     r4tests11) timeout -k 10 900 python -u -m pytest tests/test_decoder_attention_gpu.py tests/test_networks_gpu.py tests/test_fullsize_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_graphed_forward_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests11.log 2>&1 ;;
     r4tests12) timeout -k 10 900 python -u -m pytest tests/test_specnorm_gpu.py tests/test_patchgan_gpu.py tests/test_networks_gpu.py tests/test_decoder_gpu.py tests/test_attention_f32_gpu.py tests/test_decoder_attention_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests12.log 2>&1 ;;
     r4tests13) timeout -k 10 900 python -u -m pytest tests/test_decoder_gpu.py tests/test_networks_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_fullsize_gpu.py tests/test_configs_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests13.log 2>&1 ;;
+    abtimer) bash tools_dev/ab_args.sh $tag/abtimer "" "--no-kernel-timer" ;;
+    dinobench) timeout -k 10 300 python tools_dev/dinobench.py > $out/dinobench.log 2>&1 ;;
     abfold) bash tools_dev/ab_env.sh $tag/abfold VFM_DHEAD_FOLDED 0 1 ;;
     abdw) bash tools_dev/ab_env.sh $tag/abdw VFM_DW_STREAM 0 1 ;;
     attn32pmc) ATTN32_ONLY=adapter timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU --kernel-include-regex attn32 -d $out/a1 -o run --output-format csv -- python3 tools_dev/attn32bench.py > $out/a1.log 2>&1 && ATTN32_ONLY=adapter timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex attn32 -d $out/a2 -o run --output-format csv -- python3 tools_dev/attn32bench.py > $out/a2.log 2>&1 ;;
