@@ -51,7 +51,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
-    ap.add_argument("--timer-every", type=int, default=4,
+    ap.add_argument("--timer-every", type=int, default=16,
                     help="per-launch HIP events on 1/n of each kernel region's launches (1 = all; on every "
                          "launch they cost ~5 %% of the step in host time)")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")

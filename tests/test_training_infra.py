@@ -209,3 +209,16 @@ def test_graphed_forward_refused_without_opt_in(monkeypatch):
         obj.enable_graphed_nograd_forward()
     obj.enable_graphed_nograd_forward(False)
     assert obj.graphed_nograd is None
+
+
+def test_kernel_timer_sampling_is_unbiased():
+    """region()'s launch sampling: exactly 1/every of each 2^16 launch indices, and every launch
+    position of a region with 10 launches per step sampled (a plain stride of 4 or 16 would only
+    ever time the even positions)."""
+    from torch_utils.ops import kernel_timer as kt
+    for every in (4, 16):
+        kt._every = every
+        hits = [c for c in range(1 << 16) if kt._sampled(c)]
+        assert len(hits) == (1 << 16) // every
+        assert {c % 10 for c in hits[:400]} == set(range(10))
+    kt._every = 1

@@ -161,6 +161,39 @@ def f32_precision():
     return (VFM_F32, 3, "f32x6") if F32_PRODUCTS == "f32x6" else (VFM_F32X3, 2, "f32x3")
 
 
+class _Never:
+    def __getitem__(self, i):
+        return False
+
+
+class _NoCtx:
+    """The ctx a FastFunction's forward gets when it runs outside autograd: saving is a no-op and no
+    input needs a gradient; attributes may be set (and are dropped with the object)."""
+    needs_input_grad = _Never()
+
+    def save_for_backward(self, *tensors):
+        pass
+
+    def mark_non_differentiable(self, *tensors):
+        pass
+
+    def set_materialize_grads(self, value):
+        pass
+
+
+class FastFunction(torch.autograd.Function):
+    """autograd.Function whose apply() with grad mode off calls forward directly: what apply would
+    do there too (no graph node, outputs without grad_fn), minus its ~8-10 us of host work per call,
+    which the no-grad generator forward of the D phase pays ~10^3 times per step while the GPU waits
+    for the host (tools_dev/gapprof.py)."""
+
+    @classmethod
+    def apply(cls, *args, **kwargs):
+        if torch.is_grad_enabled():
+            return super().apply(*args, **kwargs)
+        return cls.forward(_NoCtx(), *args, **kwargs)
+
+
 class NativeError(RuntimeError):
     pass
 

@@ -77,7 +77,7 @@ def _ready(t):
     return t, s
 
 
-class _Attention32(torch.autograd.Function):
+class _Attention32(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, q, k, v):
         B, Nq, H, d = q.shape
@@ -119,7 +119,7 @@ class _Attention32(torch.autograd.Function):
         return dq, dk, dv
 
 
-class _Attention32Packed(torch.autograd.Function):
+class _Attention32Packed(custom_ops.FastFunction):
     """The same kernels on a packed projection qkv [B, N, 3, H, d] (a view of a linear's [B, N, 3 H d]
     output): q / k / v are read in place and the backward writes dq / dk / dv into ONE packed gradient
     buffer, so autograd neither copies the strided views nor stacks three gradients back together."""

@@ -83,7 +83,7 @@ def _run(x, b, xref, yref, dy, grad, dim, spec, alpha, gain, clamp):
                                                int(dim), int(spec.cuda_idx), float(alpha), float(gain), float(clamp))
 
 
-class _BiasActHip(torch.autograd.Function):
+class _BiasActHip(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, b, dim, act, alpha, gain, clamp):
         spec = activation_funcs[act]
@@ -118,7 +118,7 @@ class _BiasActHip(torch.autograd.Function):
         return dx, db, None, None, None, None, None
 
 
-class _BiasActGradHip(torch.autograd.Function):
+class _BiasActGradHip(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, dy, x, b, y, cfg, memory_format):
         dim, act, alpha, gain, clamp = cfg

@@ -212,7 +212,7 @@ def _overlapped(side_fn, main_fn, dev):
     return a, b
 
 
-class _Pointwise(torch.autograd.Function):
+class _Pointwise(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, w, x):
         _edges(ctx, w, x)
@@ -345,7 +345,7 @@ def _dw_wgrad(part, want_w, want_b, C, K, wshape, wdt, bdt):
     return (None if dw is None else dw.to(wdt)), (None if db is None else db.to(bdt))
 
 
-class _DwConv2d(torch.autograd.Function):
+class _DwConv2d(custom_ops.FastFunction):
     """Depthwise conv (+ bias) (+ noise plane, or noise plane * strength for the legacy noise: then
     `noise` is the constant plane and the strength's gradient sum dY * plane comes out of the data-
     gradient kernel's pass over dY, decoder_hip._dw_fwd nplane)."""
@@ -442,7 +442,7 @@ def _colsum2(a, b, scale_a, want_a, want_b, rows, cols):
     return oa, ob
 
 
-class _GroupNorm(torch.autograd.Function):
+class _GroupNorm(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, weight, bias, style, groups, eps, out_dtype):
         _edges(ctx, x, weight, bias, style, groups, eps, out_dtype)
@@ -496,7 +496,7 @@ def group_norm(x, num_groups, weight, bias, eps, out_dtype, style):
 # (reference convnext_utils.py:60-66 demodulation, :129-130 bias + GELU).
 
 
-class _ScaleBiasGelu(torch.autograd.Function):
+class _ScaleBiasGelu(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, h, scale, bias):
         _edges(ctx, h, scale, bias)
@@ -541,7 +541,7 @@ def scale_bias_gelu(h, scale, bias):
 # pwconv2 bias + layer scale + residual (reference convnext_utils.py:131-142).
 
 
-class _LayerScaleResidual(torch.autograd.Function):
+class _LayerScaleResidual(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, y, bias, gamma, x_in, slot=None):
         _edges(ctx, y, bias, gamma, x_in, slot)
@@ -652,7 +652,7 @@ def gemm_gelu_bwd(w2t, dy, h, s, b1):
     return dh, (p0.sum(1) if p0 is not None else None), p1.sum((0, 1))
 
 
-class _ConvNeXtMLPGemm(torch.autograd.Function):
+class _ConvNeXtMLPGemm(custom_ops.FastFunction):
     """The ConvNeXt MLP of the wide bf16 blocks (reference convnext_utils.py:135-142) on the 256-tile
     GEMM: forward pwconv1 + scale/bias/GELU in one kernel (h and g written for the backward), pwconv2,
     the layer-scale residual kernel; backward: the residual kernel's dy, dW2 (batch-reduced fp32
@@ -731,7 +731,7 @@ def _mlp_gemm_nograd(m, w1, dcoef, b1, w2, b2, gamma, x_in):
     return out
 
 
-class _ConvNeXtMLP(torch.autograd.Function):
+class _ConvNeXtMLP(custom_ops.FastFunction):
     """pointwise(W1) -> GELU(h*s+b1) -> pointwise(W2) -> x_in + gamma*(y+b2) with autograd.
     Forward: one kernel that also writes h, g and y for the backward. Backward: the layer-
     scale residual kernel, then the 4C->C conv's data gradient with GELU' fused into its
@@ -860,7 +860,7 @@ def _taps(blur1d):
     return (ctypes.c_float * 8)(*(k + [0.0] * (8 - len(k)))), len(k)
 
 
-class _ShuffleBlur(torch.autograd.Function):
+class _ShuffleBlur(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, blur1d, r):
         x = _c(x)
@@ -901,7 +901,7 @@ def blur_replicate(x, blur1d):
 # partials on the host side (tiny).
 
 
-class _ToRGB(torch.autograd.Function):
+class _ToRGB(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, w2, style, bias):
         _edges(ctx, x, w2, style, bias)
@@ -961,7 +961,7 @@ def torgb(x, w2, style, bias):
 # networks/utils/gigagan_utils.py:31-39): one launch forward, one (+ the gamma row sum) backward.
 
 
-class _ChannelRMSNorm(torch.autograd.Function):
+class _ChannelRMSNorm(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, gamma, scale):
         _edges(ctx, x, gamma, scale)
@@ -1014,7 +1014,7 @@ def channel_rms_norm(x, gamma, scale):
 # two launches forward, two backward, instead of ~9 / ~25 torch kernels per layer.
 
 
-class _StyleDemod(torch.autograd.Function):
+class _StyleDemod(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, w, A, ab, W1, wg, bg, eps):
         _edges(ctx, w, A, ab, W1, wg, bg, eps)

@@ -126,7 +126,7 @@ def filtered_lrelu_act_(x, si, sx, sy, gain, slope, clamp, write_signs):
                                                           bool(write_signs))
 
 
-class _FilteredLReluHip(torch.autograd.Function):
+class _FilteredLReluHip(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, fu, fd, b, si, sx, sy, cfg):
         assert isinstance(x, torch.Tensor) and x.ndim == 4

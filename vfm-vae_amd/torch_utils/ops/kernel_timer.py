@@ -57,14 +57,21 @@ _NULL = _Null()
 
 
 class _TorchPair:
-    """Events recorded around a (library) call on the launch stream."""
+    """Events recorded around a (library) call on the launch stream; pooled like _KernelPair (creating
+    two events per timed call is host work inside the timed steps)."""
+    _pool = []
 
     def __init__(self):
-        self.s = torch.cuda.Event(enable_timing=True)
-        self.e = torch.cuda.Event(enable_timing=True)
+        if _TorchPair._pool:
+            self.s, self.e = _TorchPair._pool.pop()
+        else:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.e = torch.cuda.Event(enable_timing=True)
 
     def ms(self):
-        return self.s.elapsed_time(self.e)
+        out = self.s.elapsed_time(self.e)
+        _TorchPair._pool.append((self.s, self.e))
+        return out
 
 
 class _KernelPair:
@@ -92,33 +99,46 @@ class _KernelPair:
         return float(out.value) if rc == 0 else None
 
 
+_lib = None
+
+
 def _native():
-    from torch_utils import custom_ops
-    return custom_ops.get_native()
+    global _lib
+    if _lib is None:
+        from torch_utils import custom_ops
+        _lib = custom_ops.get_native()
+    return _lib
 
 
-@contextlib.contextmanager
-def _timed(name, nbytes, flops, bound, native):
-    if native:
-        lib = _native()
-        pair = _KernelPair(lib)
-        lib.vfm_timer_arm(pair.s, pair.e)
-        try:
-            yield
-        finally:
-            pair.launched = lib.vfm_timer_arm(None, None) > 0
+class _Timed:
+    """One sampled launch: native regions arm the kernel library's dispatch events around the launch,
+    library regions record torch events on the current stream. A plain context-manager class (a
+    generator-based one costs a few microseconds of host time per timed launch)."""
+    __slots__ = ("name", "nbytes", "flops", "bound", "native", "pair")
+
+    def __init__(self, name, nbytes, flops, bound, native):
+        self.name, self.nbytes, self.flops, self.bound, self.native = name, nbytes, flops, bound, native
+
+    def __enter__(self):
+        if self.native:
+            lib = _native()
+            self.pair = _KernelPair(lib)
+            lib.vfm_timer_arm(self.pair.s, self.pair.e)
+        else:
+            self.pair = _TorchPair()
+            self.pair.s.record(torch.cuda.current_stream())
+        return None
+
+    def __exit__(self, *exc):
+        pair = self.pair
+        if self.native:
+            pair.launched = pair.lib.vfm_timer_arm(None, None) > 0
             if not pair.launched:
                 _KernelPair._pool.append((pair.s, pair.e))
-            _records.setdefault(name, []).append((pair, nbytes, flops, bound))
-        return
-    st = torch.cuda.current_stream()
-    pair = _TorchPair()
-    pair.s.record(st)
-    try:
-        yield
-    finally:
-        pair.e.record(st)
-        _records.setdefault(name, []).append((pair, nbytes, flops, bound))
+        else:
+            pair.e.record(torch.cuda.current_stream())
+        _records.setdefault(self.name, []).append((pair, self.nbytes, self.flops, self.bound))
+        return False
 
 
 @contextlib.contextmanager
@@ -133,28 +153,25 @@ def suspended():
         _enabled = prev
 
 
-def _mix(c):
-    """32-bit integer hash (murmur3 finaliser) of a launch index."""
-    x = (c + 0x9E3779B9) & 0xFFFFFFFF
-    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
-    x ^= x >> 13
-    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
-    return x ^ (x >> 16)
+def _sampled(c):
+    """Launch index c of a region is timed: (c * 40503) mod 2^16 is a permutation of each block of
+    2^16 indices, so exactly 1/_every of them fall below the threshold, spread pseudo-randomly over a
+    step's launch positions (a plain stride aliases with the region's launches per step: every 4th of
+    10 per step = even ones only). Three integer operations on the host path of every launch."""
+    return ((c * 40503) & 0xFFFF) < 65536 // _every
 
 
 def region(name, nbytes=0, flops=0, bound="hbm", native=True):
     """Context manager around one launch (native = our kernel library, timed by the kernel dispatch;
-    otherwise events around the call); a shared no-op object when timing is off (this is on every
-    launch's host path)."""
+    otherwise events around the call); a shared no-op object when timing is off or the launch is not
+    sampled (this is on every launch's host path)."""
     if not _enabled:
         return _NULL
     c = _counts.get(name, 0)
     _counts[name] = c + 1
-    # a pseudo-random 1/_every of each region's launches (integer hash of the launch index): a plain
-    # stride aliases with the region's launches per step (every 4th of 10 per step = even ones only)
-    if _every > 1 and _mix(c) % _every:
+    if _every > 1 and not _sampled(c):
         return _NULL
-    return _timed(name, nbytes, flops, bound, native)
+    return _Timed(name, nbytes, flops, bound, native)
 
 
 def vendor_gemm(tag, M, N, K, z=1, esize=2):

@@ -52,7 +52,7 @@ def _im2col(xh, k, stride, pad, Ho, Wo):
     return A
 
 
-class _ConvNHWC(torch.autograd.Function):
+class _ConvNHWC(custom_ops.FastFunction):
     """y[b, oy, ox, o] = sum_{ky, kx, c} x[b, s oy - p + ky, s ox - p + kx, c] w[o, c, ky, kx] (+ bias[o])."""
 
     @staticmethod
@@ -115,7 +115,7 @@ class _ConvNHWC(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-class _BnLocalLReLU(torch.autograd.Function):
+class _BnLocalLReLU(custom_ops.FastFunction):
     """lrelu(BatchNormLocal2d(x)) over NHWC x [B, H, W, C], G virtual batches."""
 
     @staticmethod
@@ -159,7 +159,7 @@ class _BnLocalLReLU(torch.autograd.Function):
         return (dx, None if dw is None else dw.to(wdt), None if db is None else db.to(bdt), None, None, None)
 
 
-class _BnLocal1dLReLU(torch.autograd.Function):
+class _BnLocal1dLReLU(custom_ops.FastFunction):
     """lrelu(BatchNormLocal(x)) over [B, C, L] fp32, G virtual batches (the D heads' blocks)."""
 
     @staticmethod
@@ -226,7 +226,7 @@ def bias_lrelu(yh, bias, slope):
 # torch.nn.utils.spectral_norm with one power iteration, dim 0): three launches forward, two backward.
 
 
-class _SpectralNormWeight(torch.autograd.Function):
+class _SpectralNormWeight(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, weight, u, v, eps):
         O = weight.shape[0]
@@ -270,7 +270,7 @@ def spectral_norm_weight(weight, u, v, eps):
 # im2col of the D heads' 1-D convs (csrc/im2col1d.hip): zero or circular padding, one launch each way.
 
 
-class _Im2col1d(torch.autograd.Function):
+class _Im2col1d(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, k, p, circular):
         x = _c16(x)
@@ -316,7 +316,7 @@ def im2col1d(x, k, p, circular):
 # over virtual batches of 8 samples amplifies GEMM rounding into the input gradient.
 
 
-class _Conv1dFolded(torch.autograd.Function):
+class _Conv1dFolded(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, w2, bias, k, p, circular):
         x = _c16(x.float())

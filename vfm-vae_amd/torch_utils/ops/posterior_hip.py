@@ -10,7 +10,7 @@ from . import kernel_timer
 _lib = custom_ops.get_native()
 
 
-class _Posterior(torch.autograd.Function):
+class _Posterior(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, params, eps):
         params = params.contiguous()

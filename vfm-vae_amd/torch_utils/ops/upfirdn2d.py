@@ -174,7 +174,7 @@ def _upfirdn2d_hip_forward(x, f, up, down, pads, flip, gain):
     return _launch(y, f.unsqueeze(1), (1, up[1]), (1, down[1]), (0, 0, py0, py1), flip, gain)
 
 
-class _Upfirdn2dHip(torch.autograd.Function):
+class _Upfirdn2dHip(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, f, up, down, pads, flip, gain):
         assert x.ndim == 4

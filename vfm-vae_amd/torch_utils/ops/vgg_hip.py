@@ -185,7 +185,7 @@ def maxpool2x2_bwd(g, x, gt):
     return out
 
 
-class _VGG16Taps(torch.autograd.Function):
+class _VGG16Taps(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, x, prep):
         taps, ys, pools = forward_chain(x, prep)
@@ -201,7 +201,7 @@ class _VGG16Taps(torch.autograd.Function):
         return backward_chain(saved[:13], saved[13:], ctx.prep, ctx.in_shape, gtaps), None
 
 
-class _VGG16TapsPair(torch.autograd.Function):
+class _VGG16TapsPair(custom_ops.FastFunction):
     """The stack over two same-shape batches (LPIPS's input and target) in ONE pass of 2B images: every
     layer is per-sample, so the taps are bit-identical to two separate passes, and the deep layers
     (16 x 16 / 32 x 32 planes) get twice the tiles. The backward runs only for the batch whose input
