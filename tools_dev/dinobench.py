@@ -1,7 +1,8 @@
 """Microbench of the DINO ViT-S tower's fp32 linears (token-major, M = 32 images x 197 tokens = 6304)
 on the f32x6 routes: the 256-tile kernel direct / split-K, the 128-tile kernel direct / split-K, and
-hipBLASLt's exact fp32 GEMM. The activation's version is bumped before every call so the 256-tile
-kernel's planar piece split of it is re-done each time (as in the step); weights are cached."""
+hipBLASLt's exact fp32 GEMM. Calls cycle over 4 distinct activation tensors so the 256-tile kernel's
+planar piece split of the activation is re-done each time (as in the step: its cached pieces are dropped
+before each call); weights are cached."""
 import os
 import sys
 
@@ -30,13 +31,17 @@ print("TF/s = fp32 FLOPs / time", flush=True)
 M = 6304
 for name, N, K in [("qkv fwd / proj-in", 1152, 384), ("proj fwd / dx", 384, 384), ("fc1 fwd / fc2 dx", 1536, 384),
                    ("fc2 fwd / fc1 dx", 384, 1536), ("qkv dx", 384, 1152)]:
-    x = torch.randn(M, K, device="cuda")
+    xs = [torch.randn(M, K, device="cuda") for _ in range(4)]
+    x = xs[0]
     W = torch.randn(N, K, device="cuda")
     fl = 2.0 * M * N * K
+    it = [0]
 
     def call(route):
-        torch._C._increment_version(x)
-        return gemm_hip.gemm(x, W.t(), cache_b=True, auto=route is None, route=route)
+        it[0] += 1
+        xi = xs[it[0] % 4]
+        xi.__dict__.pop("_vfm_planar", None)
+        return gemm_hip.gemm(xi, W.t(), cache_b=True, auto=route is None, route=route)
 
     parts = []
     variants = [("auto", None), ("g8", ("g8", 0))]
