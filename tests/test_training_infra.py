@@ -222,3 +222,35 @@ def test_kernel_timer_sampling_is_unbiased():
         assert len(hits) == (1 << 16) // every
         assert {c % 10 for c in hits[:400]} == set(range(10))
     kt._every = 1
+
+
+def test_fast_function_bypasses_apply_only_without_grad():
+    """custom_ops.FastFunction: with grad mode off the forward runs directly (no graph node, the same
+    values, a stand-in ctx whose saves are no-ops and whose needs_input_grad is all False); with grad
+    mode on it is an ordinary autograd Function."""
+    import torch
+    from torch_utils import custom_ops
+
+    seen = []
+
+    class Twice(custom_ops.FastFunction):
+        @staticmethod
+        def forward(ctx, x, k):
+            ctx.save_for_backward(x)
+            ctx.k = k
+            seen.append(ctx.needs_input_grad[0])
+            return x * k
+
+        @staticmethod
+        def backward(ctx, g):
+            return g * ctx.k, None
+
+    x = torch.arange(4.0, requires_grad=True)
+    y = Twice.apply(x, 2.0)
+    assert y.grad_fn is not None and seen[-1] is True
+    y.sum().backward()
+    assert torch.equal(x.grad, torch.full((4,), 2.0))
+    with torch.no_grad():
+        z = Twice.apply(x, 3.0)
+    assert z.grad_fn is None and not z.requires_grad and seen[-1] is False
+    assert torch.equal(z, torch.arange(4.0) * 3)

@@ -53,14 +53,39 @@ def _p(t):
 _DT = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16", torch.float64: "f64"}
 
 
+_RN = {}
+
+
 def _rn(name, t, *extra):
     """kernel_timer region name: op + template parameters (dtype, tap count), so a timed
-    entry maps onto one kernel instantiation of the rocprofv3 trace."""
-    return f"{name}<{','.join([_DT.get(t.dtype, str(t.dtype))] + [str(e) for e in extra])}>"
+    entry maps onto one kernel instantiation of the rocprofv3 trace (memoised: this runs on every
+    launch's host path)."""
+    key = (name, t.dtype, extra)
+    out = _RN.get(key)
+    if out is None:
+        out = _RN[key] = f"{name}<{','.join([_DT.get(t.dtype, str(t.dtype))] + [str(e) for e in extra])}>"
+    return out
+
+
+class _LazyBytes:
+    """Algorithmic bytes of a launch's tensors, summed only when the timer samples the launch
+    (kernel_timer calls int()) -- the sum is host work on every launch otherwise."""
+    __slots__ = ("ts",)
+
+    def __init__(self, ts):
+        self.ts = ts
+
+    def __int__(self):
+        return sum(t.numel() * t.element_size() for t in self.ts if t is not None)
+
+    def __add__(self, other):
+        return int(self) + other
+
+    __radd__ = __add__
 
 
 def _nb(*ts):
-    return sum(t.numel() * t.element_size() for t in ts if t is not None)
+    return _LazyBytes(ts)
 
 
 def _check(rc, name):

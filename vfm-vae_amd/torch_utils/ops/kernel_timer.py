@@ -117,7 +117,8 @@ class _Timed:
     __slots__ = ("name", "nbytes", "flops", "bound", "native", "pair")
 
     def __init__(self, name, nbytes, flops, bound, native):
-        self.name, self.nbytes, self.flops, self.bound, self.native = name, nbytes, flops, bound, native
+        # nbytes may be lazy (decoder_hip._LazyBytes): evaluated for sampled launches only
+        self.name, self.nbytes, self.flops, self.bound, self.native = name, int(nbytes), flops, bound, native
 
     def __enter__(self):
         if self.native:
