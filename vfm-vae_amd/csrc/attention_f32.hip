@@ -409,8 +409,12 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attn32_dq(Args a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int NP>
-__global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
+// OCC = 1: Q / dO tile prefetch in registers, the small piece products of dK / dV in accumulators of
+// their own (420 registers, one wave per SIMD). OCC = 2 (VFM_ATTN32_DKDV_OCC=2, opt-in): no prefetch,
+// one accumulator per output block (all six piece products summed into it, as the S / dP products
+// are) and P's / dS's pieces live one after the other -- two workgroups per CU.
+template <int NP, int OCC>
+__global__ __launch_bounds__(64 * WAVES, OCC) void attn32_dkdv(Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG + 2 * TT * 4];
     unsigned char *qimg = lds, *oimg = lds + NP * IMG;
     float* lse_s = reinterpret_cast<float*>(lds + 2 * NP * IMG);
@@ -445,8 +449,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
     f32x16 dks[2] = {f32x16{}, f32x16{}}, dvs[2] = {f32x16{}, f32x16{}};
     const float c = a.c;
     const int T = (Nq + TT - 1) / TT;
-    load_rows(0);
+    if (OCC == 1) load_rows(0);
     for (int t = 0; t < T; ++t) {
+        if (OCC != 1) load_rows(t * TT);
         stage_store<NP>(sq, qimg, tid);
         stage_store<NP>(so, oimg, tid);
         if (tid < TT) {
@@ -454,7 +459,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
             dlt_s[tid] = dlt_r;
         }
         __syncthreads();
-        if (t + 1 < T) load_rows((t + 1) * TT);
+        if (OCC == 1 && t + 1 < T) load_rows((t + 1) * TT);
 #pragma unroll
         for (int qbk = 0; qbk < 2; ++qbk) {
             f32x16 s = f32x16{}, dp = f32x16{};
@@ -477,22 +482,39 @@ __global__ __launch_bounds__(64 * WAVES, 1) void attn32_dkdv(Args a) {
                     dp[i] = p * (dp[i] - Ds[j]);
                 }
             }
-            const Frag<NP> pf[2] = {split_acc<NP, 0>(s), split_acc<NP, 1>(s)};
-            const Frag<NP> df[2] = {split_acc<NP, 0>(dp), split_acc<NP, 1>(dp)};
+            if (OCC == 1) {
+                const Frag<NP> pf[2] = {split_acc<NP, 0>(s), split_acc<NP, 1>(s)};
+                const Frag<NP> df[2] = {split_acc<NP, 0>(dp), split_acc<NP, 1>(dp)};
 #pragma unroll
-            for (int st = 0; st < 2; ++st)
+                for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int d = 0; d < 2; ++d) {
-                    mfmaN2<NP>(rd_tr<NP>(oimg, tl, qbk, st, d), pf[st], dv[d], dvs[d]);
-                    mfmaN2<NP>(rd_tr<NP>(qimg, tl, qbk, st, d), df[st], dk[d], dks[d]);
+                    for (int d = 0; d < 2; ++d) {
+                        mfmaN2<NP>(rd_tr<NP>(oimg, tl, qbk, st, d), pf[st], dv[d], dvs[d]);
+                        mfmaN2<NP>(rd_tr<NP>(qimg, tl, qbk, st, d), df[st], dk[d], dks[d]);
+                    }
+            } else {
+                {
+                    const Frag<NP> pf[2] = {split_acc<NP, 0>(s), split_acc<NP, 1>(s)};
+#pragma unroll
+                    for (int st = 0; st < 2; ++st)
+#pragma unroll
+                        for (int d = 0; d < 2; ++d) dv[d] = mfmaN<NP>(rd_tr<NP>(oimg, tl, qbk, st, d), pf[st], dv[d]);
                 }
+                const Frag<NP> df[2] = {split_acc<NP, 0>(dp), split_acc<NP, 1>(dp)};
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+#pragma unroll
+                    for (int d = 0; d < 2; ++d) dk[d] = mfmaN<NP>(rd_tr<NP>(qimg, tl, qbk, st, d), df[st], dk[d]);
+            }
         }
         __syncthreads();
     }
+    if (OCC == 1) {
 #pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        dk[d] += dks[d];
-        dv[d] += dvs[d];
+        for (int d = 0; d < 2; ++d) {
+            dk[d] += dks[d];
+            dv[d] += dvs[d];
+        }
     }
     if (key < Nk) {
         store_tr(a.dk + (long long)b * a.sdk.b + (long long)key * a.sdk.n + (long long)h * a.sdk.h, dk, hh, a.scale, hd);
@@ -583,13 +605,18 @@ extern "C" int vfm_attention_f32_bwd(const void* q, const void* k, const void* v
         const char* e = getenv("VFM_ATTN32_DQ_OCC");
         return e && e[0] == '1' ? 1 : 2;
     }();
+    static const int dkdv_occ = [] {
+        const char* e = getenv("VFM_ATTN32_DKDV_OCC");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
     if (precision == VFM_F32) {
         if (dq_occ == 2) VFM_LAUNCH((attn32_dq<3, 2>), gq, dim3(64 * WAVES), 0, st, a);
         else VFM_LAUNCH((attn32_dq<3, 1>), gq, dim3(64 * WAVES), 0, st, a);
-        VFM_LAUNCH(attn32_dkdv<3>, gk, dim3(64 * WAVES), 0, st, a);
+        if (dkdv_occ == 2) VFM_LAUNCH((attn32_dkdv<3, 2>), gk, dim3(64 * WAVES), 0, st, a);
+        else VFM_LAUNCH((attn32_dkdv<3, 1>), gk, dim3(64 * WAVES), 0, st, a);
     } else {
         VFM_LAUNCH((attn32_dq<2, 2>), gq, dim3(64 * WAVES), 0, st, a);
-        VFM_LAUNCH(attn32_dkdv<2>, gk, dim3(64 * WAVES), 0, st, a);
+        VFM_LAUNCH((attn32_dkdv<2, 1>), gk, dim3(64 * WAVES), 0, st, a);
     }
     return launch_status();
 }
