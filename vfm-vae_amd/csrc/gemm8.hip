@@ -683,6 +683,25 @@ __global__ void split_f32_kernel(const float* __restrict__ src, __hip_bfloat16* 
     }
 }
 
+// The planar form (R = 1, kcont: dst = [NP][n] pieces of a contiguous n-element tensor, n % 8 == 0):
+// 8 elements per thread, two 16-B loads and one 16-B store per piece, no index division.
+template <int NP>
+__global__ __launch_bounds__(256) void split_planar_kernel(const float* __restrict__ src,
+                                                           __hip_bfloat16* __restrict__ dst, long long n) {
+    for (long long i8 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8; i8 < n; i8 += (long long)gridDim.x * 256 * 8) {
+        const float4 a = *reinterpret_cast<const float4*>(src + i8);
+        const float4 b = *reinterpret_cast<const float4*>(src + i8 + 4);
+        uint32_t q[4][NP];
+        split_pieces<NP>(a.x, a.y, q[0]);
+        split_pieces<NP>(a.z, a.w, q[1]);
+        split_pieces<NP>(b.x, b.y, q[2]);
+        split_pieces<NP>(b.z, b.w, q[3]);
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+            *reinterpret_cast<uint4*>(dst + (long long)p * n + i8) = make_uint4(q[0][p], q[1][p], q[2][p], q[3][p]);
+    }
+}
+
 }  // namespace
 
 extern "C" int vfm_split_f32(const float* src, void* dst, int R, int K, long long ld, long long sb, long long db,
@@ -691,6 +710,17 @@ extern "C" int vfm_split_f32(const float* src, void* dst, int R, int K, long lon
     if (precision != VFM_F32 && precision != VFM_F32X3) return VFM_ERR_ARGS;
     const int inner = kcont ? K : R;
     if (inner % 4 || ld % 4 || sb % 4 || ((uintptr_t)src % 16) || ((uintptr_t)dst % 8)) return VFM_NO_KERNEL;
+    if (R == 1 && kcont && batch == 1 && K % 8 == 0 && (uintptr_t)dst % 16 == 0) {
+        // planar pieces of one contiguous tensor (gemm_hip._planar)
+        const long long blocks = std::min<long long>(((long long)K / 8 + 255) / 256, 4096);
+        if (precision == VFM_F32)
+            VFM_LAUNCH(split_planar_kernel<3>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, src,
+                       (__hip_bfloat16*)dst, (long long)K);
+        else
+            VFM_LAUNCH(split_planar_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, src,
+                       (__hip_bfloat16*)dst, (long long)K);
+        return launch_status();
+    }
     const long long total4 = ((long long)R * K) / 4;
     dim3 grid((unsigned)((total4 + 255) / 256), batch);
     if (precision == VFM_F32)
