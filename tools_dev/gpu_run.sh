@@ -96,7 +96,7 @@ for s in "$@"; do
     r4tests9) timeout -k 10 900 python -u -m pytest tests/test_networks_gpu.py tests/test_decoder_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_configs_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests9.log 2>&1 ;;
     r4tests10) timeout -k 10 900 python -u -m pytest tests/test_attention_f32_gpu.py tests/test_networks_gpu.py tests/test_fullsize_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_patchgan_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests10.log 2>&1 ;;
     r4tests11) timeout -k 10 900 python -u -m pytest tests/test_decoder_attention_gpu.py tests/test_networks_gpu.py tests/test_fullsize_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_graphed_forward_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests11.log 2>&1 ;;
-    r4tests12) timeout -k 10 900 python -u -m pytest tests/test_specnorm_gpu.py tests/test_patchgan_gpu.py tests/test_networks_gpu.py tests/test_decoder_gpu.py tests/test_attention_f32_gpu.py tests/test_decoder_attention_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests12.log 2>&1 ;;
+    r4tests12) timeout -k 10 900 python -u -m pytest tests/test_specnorm_gpu.py tests/test_patchgan_gpu.py tests/test_networks_gpu.py tests/test_decoder_gpu.py tests/test_attention_f32_gpu.py tests/test_decoder_attention_gpu.py tests/test_gemm_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests12.log 2>&1 ;;
     r4tests13) timeout -k 10 900 python -u -m pytest tests/test_decoder_gpu.py tests/test_networks_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_fullsize_gpu.py tests/test_configs_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests13.log 2>&1 ;;
     abtimer) bash tools_dev/ab_args.sh $tag/abtimer "" "--no-kernel-timer" ;;
     abtimer3) bash tools_dev/ab3_args.sh $tag/abtimer3 "--timer-every 16" "--timer-every 256" "--no-kernel-timer" ;;
