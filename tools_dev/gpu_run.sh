@@ -100,6 +100,8 @@ for s in "$@"; do
     r4tests13) timeout -k 10 900 python -u -m pytest tests/test_decoder_gpu.py tests/test_networks_gpu.py tests/test_fullsize_bwd_gpu.py tests/test_fullsize_gpu.py tests/test_configs_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/r4tests13.log 2>&1 ;;
     abtimer) bash tools_dev/ab_args.sh $tag/abtimer "" "--no-kernel-timer" ;;
     abtimer3) bash tools_dev/ab3_args.sh $tag/abtimer3 "--timer-every 16" "--timer-every 256" "--no-kernel-timer" ;;
+    newpaths) VFM_IM2COL_ROWS=1 VFM_SPLIT_PLANAR8=1 timeout -k 10 900 python -u -m pytest tests/test_specnorm_gpu.py tests/test_patchgan_gpu.py tests/test_gemm_gpu.py tests/test_networks_gpu.py tests/test_fullsize_gpu.py -m gpu --maxfail=10 -v --timeout 240 --timeout-method thread > $out/newpaths.log 2>&1 ;;
+    abnew) bash tools_dev/ab_env2.sh $tag/abnew ;;
     dkdvtest) VFM_ATTN32_DKDV_OCC=2 timeout -k 10 600 python -u -m pytest tests/test_attention_f32_gpu.py tests/test_decoder_attention_gpu.py -m gpu -v --timeout 120 --timeout-method thread > $out/dkdvtest.log 2>&1 ;;
     dkdvab) for o in 1 2 1 2; do VFM_ATTN32_DKDV_OCC=$o timeout -k 10 300 python tools_dev/attn32bench.py > $out/attn32_dkdvocc${o}_$RANDOM.log 2>&1 || exit 1; done ;;
     dinobench) timeout -k 10 300 python tools_dev/dinobench.py > $out/dinobench.log 2>&1 ;;

@@ -409,10 +409,12 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void attn32_dq(Args a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// OCC = 1: Q / dO tile prefetch in registers, the small piece products of dK / dV in accumulators of
-// their own (420 registers, one wave per SIMD). OCC = 2 (VFM_ATTN32_DKDV_OCC=2, opt-in): no prefetch,
+// OCC = 1 (VFM_ATTN32_DKDV_OCC=1): Q / dO tile prefetch in registers, the small piece products of dK /
+// dV in accumulators of their own (420 registers, one wave per SIMD). OCC = 2 (default): no prefetch,
 // one accumulator per output block (all six piece products summed into it, as the S / dP products
-// are) and P's / dS's pieces live one after the other -- two workgroups per CU.
+// are) and P's / dS's pieces live one after the other -- 248 registers, two workgroups per CU:
+// attention backward -11 % on the adapter / decoder shapes, within the same error bounds (2x torch's
+// exact fp32 error, tests/test_attention_f32_gpu.py), profiles/r4_ah_attn32_dkdv_occ.txt.
 template <int NP, int OCC>
 __global__ __launch_bounds__(64 * WAVES, OCC) void attn32_dkdv(Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NP * IMG + 2 * TT * 4];
@@ -607,7 +609,7 @@ extern "C" int vfm_attention_f32_bwd(const void* q, const void* k, const void* v
     }();
     static const int dkdv_occ = [] {
         const char* e = getenv("VFM_ATTN32_DKDV_OCC");
-        return e && e[0] == '2' ? 2 : 1;
+        return e && e[0] == '1' ? 1 : 2;
     }();
     if (precision == VFM_F32) {
         if (dq_occ == 2) VFM_LAUNCH((attn32_dq<3, 2>), gq, dim3(64 * WAVES), 0, st, a);

@@ -36,6 +36,8 @@
 //     through LDS (8 KB per wave of the consumed buffer) with 16-B row stores;
 //   * operands read through buffer descriptors: the 8 per-lane DMA offsets of a tile are computed
 //     once, the K-tile advance is a scalar offset (no per-lane address arithmetic in the K-loop).
+#include <cstdlib>
+
 #include "vfm_common.h"
 
 namespace {
@@ -710,7 +712,11 @@ extern "C" int vfm_split_f32(const float* src, void* dst, int R, int K, long lon
     if (precision != VFM_F32 && precision != VFM_F32X3) return VFM_ERR_ARGS;
     const int inner = kcont ? K : R;
     if (inner % 4 || ld % 4 || sb % 4 || ((uintptr_t)src % 16) || ((uintptr_t)dst % 8)) return VFM_NO_KERNEL;
-    if (R == 1 && kcont && batch == 1 && K % 8 == 0 && (uintptr_t)dst % 16 == 0) {
+    static const bool planar8 = [] {                       // VFM_SPLIT_PLANAR8=0: the generic split kernel
+        const char* e = getenv("VFM_SPLIT_PLANAR8");
+        return !(e && e[0] == '0');
+    }();
+    if (planar8 && R == 1 && kcont && batch == 1 && K % 8 == 0 && (uintptr_t)dst % 16 == 0) {
         // planar pieces of one contiguous tensor (gemm_hip._planar)
         const long long blocks = std::min<long long>(((long long)K / 8 + 255) / 256, 4096);
         if (precision == VFM_F32)

@@ -7,6 +7,8 @@
 // CBL = 1: the batch folded into the columns, cols[c k + j, b, l] ([C k, B Lo]): the whole batch's
 // convolution is then one GEMM W [O, C k] x cols with K = C k, and its weight gradient one GEMM
 // dY [O, B Lo] x cols^T with the batch in the reduction (no per-sample [O, C k] products to sum).
+#include <cstdlib>
+
 #include "vfm_common.h"
 
 namespace {
@@ -16,7 +18,7 @@ using namespace vfm;
 // One wave per row: the row's (b, c, j) decomposition is wave-uniform (no per-element 64-bit
 // divisions), and the lanes walk the row's Lo (or L) elements with coalesced loads and stores.
 template <int CBL>
-__global__ __launch_bounds__(256) void im2col1d(const float* __restrict__ x, float* __restrict__ cols, int B, int C,
+__global__ __launch_bounds__(256) void im2col1d_rows(const float* __restrict__ x, float* __restrict__ cols, int B, int C,
                                                 int L, int k, int p, int Lo, int circ, long long rows) {
     const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);   // CBL ? (c k + j) B + b : (b C + c) k + j
     if (r >= rows) return;
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void im2col1d(const float* __restrict__ x, flo
 }
 
 template <int CBL>
-__global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols, float* __restrict__ dx, int B, int C,
+__global__ __launch_bounds__(256) void col2im1d_rows(const float* __restrict__ dcols, float* __restrict__ dx, int B, int C,
                                                 int L, int k, int p, int Lo, int circ, long long rows) {
     const long long bc = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);  // b C + c
     if (bc >= rows) return;
@@ -75,20 +77,95 @@ __global__ __launch_bounds__(256) void col2im1d(const float* __restrict__ dcols,
 }
 
 
+// One thread per element (VFM_IM2COL_ROWS=0; the one-wave-per-row form is the default).
+template <int CBL>
+__global__ __launch_bounds__(256) void im2col1d_el(const float* __restrict__ x, float* __restrict__ cols, int B, int C,
+                                                int L, int k, int p, int Lo, int circ, long long n) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int l = (int)(e % Lo);
+        const long long r = e / Lo;                  // CBL ? (c k + j) B + b : (b C + c) k + j
+        int j;
+        long long bc;
+        if (CBL) {
+            const int b = (int)(r % B);
+            const long long cj = r / B;
+            j = (int)(cj % k);
+            bc = (long long)b * C + cj / k;
+        } else {
+            j = (int)(r % k);
+            bc = r / k;
+        }
+        int s = l + j - p;
+        float v = 0.f;
+        if (circ) {
+            s %= L;
+            if (s < 0) s += L;
+            v = x[bc * L + s];
+        } else if (s >= 0 && s < L) {
+            v = x[bc * L + s];
+        }
+        cols[e] = v;
+    }
+}
+
+template <int CBL>
+__global__ __launch_bounds__(256) void col2im1d_el(const float* __restrict__ dcols, float* __restrict__ dx, int B, int C,
+                                                int L, int k, int p, int Lo, int circ, long long n) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int t = (int)(e % L);
+        const long long bc = e / L;
+        // row j of (b, c): CBL ? ((c k + j) B + b) Lo : ((b C + c) k + j) Lo
+        const long long jstride = CBL ? (long long)B * Lo : Lo;
+        const float* dr = CBL ? dcols + (((bc % C) * k) * B + bc / C) * Lo : dcols + bc * k * Lo;
+        float acc = 0.f;
+        for (int j = 0; j < k; ++j) {
+            int l = t - j + p;
+            if (circ) {                              // Lo == L: exactly one l per (t, j)
+                l %= L;
+                if (l < 0) l += L;
+            } else if (l < 0 || l >= Lo) {
+                continue;
+            }
+            acc += dr[(long long)j * jstride + l];
+        }
+        dx[e] = acc;
+    }
+}
+
+int grid_of(long long n) { return (int)std::min<long long>((n + 255) / 256, 16384); }
+
+bool rows_form() {
+    static const bool on = [] {
+        const char* e = getenv("VFM_IM2COL_ROWS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int im2col_launch(const float* x, float* cols, int B, int C, int L, int k, int p, int circular, int cbl,
                   void* stream) {
     if (!x || !cols || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
     const int Lo = L + 2 * p - k + 1;
     if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
+    if (!rows_form()) {
+        const long long n = (long long)B * C * k * Lo;
+        if (cbl)
+            VFM_LAUNCH(im2col1d_el<1>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo,
+                       circular ? 1 : 0, n);
+        else
+            VFM_LAUNCH(im2col1d_el<0>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo,
+                       circular ? 1 : 0, n);
+        return launch_status();
+    }
     const long long rows = (long long)B * C * k;
     if ((rows + 3) / 4 > 0x7fffffffLL) return VFM_ERR_ARGS;
     const dim3 grid((unsigned)((rows + 3) / 4));
     if (cbl)
-        VFM_LAUNCH(im2col1d<1>, grid, dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo, circular ? 1 : 0,
-                   rows);
+        VFM_LAUNCH(im2col1d_rows<1>, grid, dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo,
+                   circular ? 1 : 0, rows);
     else
-        VFM_LAUNCH(im2col1d<0>, grid, dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo, circular ? 1 : 0,
-                   rows);
+        VFM_LAUNCH(im2col1d_rows<0>, grid, dim3(256), 0, (hipStream_t)stream, x, cols, B, C, L, k, p, Lo,
+                   circular ? 1 : 0, rows);
     return launch_status();
 }
 
@@ -97,14 +174,24 @@ int col2im_launch(const float* dcols, float* dx, int B, int C, int L, int k, int
     if (!dcols || !dx || B <= 0 || C <= 0 || L <= 0 || k <= 0 || p < 0) return VFM_ERR_ARGS;
     const int Lo = L + 2 * p - k + 1;
     if (Lo <= 0 || (circular && (Lo != L || p > L))) return VFM_NO_KERNEL;
+    if (!rows_form()) {
+        const long long n = (long long)B * C * L;
+        if (cbl)
+            VFM_LAUNCH(col2im1d_el<1>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p,
+                       Lo, circular ? 1 : 0, n);
+        else
+            VFM_LAUNCH(col2im1d_el<0>, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p,
+                       Lo, circular ? 1 : 0, n);
+        return launch_status();
+    }
     const long long rows = (long long)B * C;
     if ((rows + 3) / 4 > 0x7fffffffLL) return VFM_ERR_ARGS;
     const dim3 grid((unsigned)((rows + 3) / 4));
     if (cbl)
-        VFM_LAUNCH(col2im1d<1>, grid, dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p, Lo,
+        VFM_LAUNCH(col2im1d_rows<1>, grid, dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p, Lo,
                    circular ? 1 : 0, rows);
     else
-        VFM_LAUNCH(col2im1d<0>, grid, dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p, Lo,
+        VFM_LAUNCH(col2im1d_rows<0>, grid, dim3(256), 0, (hipStream_t)stream, dcols, dx, B, C, L, k, p, Lo,
                    circular ? 1 : 0, rows);
     return launch_status();
 }

@@ -191,6 +191,10 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         tiles = -(-M // 128) * -(-N // 128) * z
         if tiles < 512 and K >= 2048:
             splits = max(1, min(-(-1024 // tiles), K // 512, 64))
+        elif z == 1 and tiles < 256 and K >= 1152 and A.dtype == torch.float32:
+            # the DINO tower's narrow-output products (6304 x 384 x 1536 / 1152: 150 128-tiles on 256 CUs):
+            # three K splits, 79 -> 67 us and 60 -> 56 us (tools_dev/dinobench.py, profiles/r4_ah_dinobench.txt)
+            splits = 3
     la = _layout(a3, True)                       # A rows = m, cols = k
     lb = _layout(b3.transpose(1, 2), True)       # B^T rows = n, cols = k
     if la is None or lb is None:

@@ -248,8 +248,11 @@ def rocprof_name(region):
         return f"conv3x3_kernel<{bm}, {args[1]}, {np_}>"
     if base in ("attention_fwd", "attention_bwd") and args and args[0] in ("f32x6", "f32x3"):
         np_ = _NP[args[0]]
-        occ = 2 if (np_ == 3 and os.environ.get("VFM_ATTN32_OCC", "2") != "1") else 1
-        return f"attn32_fwd<{np_}, {occ}>" if base == "attention_fwd" else f"attn32_dkdv<{np_}>"
+        if base == "attention_fwd":
+            occ = 2 if (np_ == 3 and os.environ.get("VFM_ATTN32_OCC", "2") != "1") else 1
+            return f"attn32_fwd<{np_}, {occ}>"
+        occ = 2 if (np_ == 3 and os.environ.get("VFM_ATTN32_DKDV_OCC", "2") != "1") else 1
+        return f"attn32_dkdv<{np_}, {occ}>"
     if base == "convnext_mlp_fwd" and len(args) == 3:          # mlp_fwd<C, SAVE>
         return f"mlp_fwd<{args[1]}, {args[2]}>"
     pat = _ROC.get(base)
