@@ -51,9 +51,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
-    ap.add_argument("--timer-every", type=int, default=16,
-                    help="per-launch HIP events on 1/n of each kernel region's launches (1 = all; on every "
-                         "launch they cost ~5 %% of the step in host time)")
+    ap.add_argument("--timer-steps", type=int, default=4,
+                    help="kernel timing on every launch of every n-th timed step (exact per-kernel averages for "
+                         "those steps; timing every launch costs ~5 %% of a step in host time, so 1/n of that overall)")
+    ap.add_argument("--timer-every", type=int, default=1,
+                    help="within the timed steps, per-launch HIP events on 1/n of each kernel region's launches")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", action="store_true",
                     help="experimental: replay the D-phase generator forward from HIP graphs (off: see DESIGN.md)")
@@ -239,8 +241,10 @@ def main(argv=None):
     every = max(1, args.timer_every)
     kernel_timer.enable(not args.no_kernel_timer, every)
     t0 = time.perf_counter()
+    tsteps = max(1, args.timer_steps)
     for i in range(args.steps):
         h0 = getattr(venc, "reuse_hits", 0)
+        kernel_timer.set_active(i % tsteps == 0)
         one(args.warmup + i, cur)
         hits.append(getattr(venc, "reuse_hits", 0) - h0)
         cur += args.batch * world
@@ -274,8 +278,10 @@ def main(argv=None):
     roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table)
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
-        roof["timer_sampling"] = (f"1/{every} of each kernel region's launches (pseudo-random by launch index) over all "
-                                  f"{args.steps} timed steps")
+        n_t = len(range(0, args.steps, tsteps))
+        roof["timer_sampling"] = ((f"1/{every} of each kernel region's launches (pseudo-random by launch index) in "
+                                   if every > 1 else "every launch in ") +
+                                  f"{n_t} of the {args.steps} timed steps (every {tsteps}th), all launches counted")
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -254,3 +254,18 @@ def test_fast_function_bypasses_apply_only_without_grad():
         z = Twice.apply(x, 3.0)
     assert z.grad_fn is None and not z.requires_grad and seen[-1] is False
     assert torch.equal(z, torch.arange(4.0) * 3)
+
+
+def test_kernel_timer_inactive_launches_are_counted_not_timed():
+    """set_active(False): a region's launches keep being counted (the totals extrapolate from the timed
+    launches to all of them) but none is timed; enable() re-activates."""
+    from torch_utils.ops import kernel_timer as kt
+    kt.enable(True, 1)
+    kt.set_active(False)
+    for _ in range(3):
+        assert kt.region("x<f32>", 4) is kt._NULL
+    assert kt._counts["x<f32>"] == 3
+    kt.enable(False)
+    kt.enable(True, 1)
+    assert kt._active
+    kt.enable(False)

@@ -32,13 +32,26 @@ _counts = {}       # name -> launches seen while enabled (timed or not)
 _every = 1         # time ~1/n of each region's launches (the events cost host time per launch)
 
 
+_active = True     # launches are timed only while active (bench.py: every launch of every n-th timed step)
+
+
 def enable(flag: bool, every: int = 1):
-    global _enabled, _every
+    global _enabled, _every, _active
     _enabled = bool(flag)
+    _active = True
     if flag:
         _records.clear()
         _counts.clear()
         _every = max(1, int(every))
+
+
+def set_active(flag: bool):
+    """While enabled: launches keep being counted, but only those issued while active are timed.
+    Timing every launch of whole steps (rather than a sample of each region's launches in every
+    step) makes a region's average exact for those steps: its launches differ in shape, so a
+    sampled average of them carries the shape mix's sampling error."""
+    global _active
+    _active = bool(flag)
 
 
 def is_enabled():
@@ -170,7 +183,7 @@ def region(name, nbytes=0, flops=0, bound="hbm", native=True):
         return _NULL
     c = _counts.get(name, 0)
     _counts[name] = c + 1
-    if _every > 1 and not _sampled(c):
+    if not _active or (_every > 1 and not _sampled(c)):
         return _NULL
     return _Timed(name, nbytes, flops, bound, native)
 
