@@ -57,8 +57,10 @@ def parse_args(argv=None):
     ap.add_argument("--timer-every", type=int, default=1,
                     help="within the timed steps, per-launch HIP events on 1/n of each kernel region's launches")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
-    ap.add_argument("--graphs", action="store_true",
-                    help="experimental: replay the D-phase generator forward from HIP graphs (off: see DESIGN.md)")
+    ap.add_argument("--graphs", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                    help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5): auto = on "
+                         "for a single process (same-box A/B: +1.1 %% over 7 pairs, profiles/r4_al_graphs_ab.txt), "
+                         "off under torch.distributed (capture next to RCCL's threads is not exercised here)")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
     ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="off",
                     help="GEMM solution table (torch TunableOp over hipBLASLt/rocBLAS): 'use' reads the "
@@ -169,14 +171,17 @@ def main(argv=None):
     torch.cuda.set_device(device)
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
+    use_graphs = args.graphs == "on" or (args.graphs == "auto" and world == 1)
     if args.tunableop == "tune":
-        args.graphs = False              # a GEMM cannot be tuned inside a HIP-graph capture
+        use_graphs = False               # a GEMM cannot be tuned inside a HIP-graph capture
+    if use_graphs:
+        os.environ.setdefault("VFM_EXPERIMENTAL_GRAPHS", "1")    # the bench opts in explicitly
     tunable = setup_tunableop(args.tunableop, args.tunableop_out)
     if tunable:
         _log(rank, f"tunableop: {tunable}")
 
     t_start = time.perf_counter()
-    c, step = build(args.config, args.batch, device, world, graphs=args.graphs)
+    c, step = build(args.config, args.batch, device, world, graphs=use_graphs)
     _log(rank, f"built in {time.perf_counter() - t_start:.1f}s")
     from training.data_synthetic import SyntheticDataset
     pool = SyntheticDataset(resolution=c.training_set_kwargs.resolution, seed=rank).make_pool(args.batch, device)
@@ -302,7 +307,8 @@ def main(argv=None):
                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "seq_len": 1024,
                        "resolution": 256, "parallelism": f"dp{world}",
                        "decoder_ops": "torch" if args.force_ref_ops else "hip",
-                       "d_phase_g_forward": "hip_graph" if args.graphs else "eager",
+                       "d_phase_g_forward": ("hip_graph" if (gr is not None and not gr.disabled and gr.graphs)
+                                             else "eager"),
                        "precision": ("bf16 where the reference autocasts (SigLIP2 tower, decoder blocks 3-5); the "
                                      "reference's fp32 legs (decoder blocks 0-2, adapter, fp32 attention, LPIPS VGG16, "
                                      "DINO D) with fp32-equivalent products: " + _fp32_mode()),
