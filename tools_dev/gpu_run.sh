@@ -78,7 +78,7 @@ for s in "$@"; do
     opsites) timeout -k 10 600 python tools_dev/opsites.py > $out/opsites.log 2>&1 ;;
     opsitest) OPSITES_TIME=1 timeout -k 10 600 python tools_dev/opsites.py > $out/opsites_timed.log 2>&1 ;;
     gapprof) timeout -k 10 600 python tools_dev/gapprof.py 1 > $out/gapprof.log 2>&1 ;;
-    benchg) VFM_EXPERIMENTAL_GRAPHS=1 timeout -k 10 600 python bench.py --graphs --no-cpu-baseline > $out/benchg.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_e.log 2>&1 ;;
+    benchg) timeout -k 10 600 python bench.py --graphs on --no-cpu-baseline > $out/benchg.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_e.log 2>&1 ;;
     benchst) VFM_STYLE_HIP=1 timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_st1.log 2>&1 && timeout -k 10 600 python bench.py --no-cpu-baseline > $out/bench_st0.log 2>&1 ;;
     styleprof) timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $out/styleprof -o run --output-format csv -- python3 tools_dev/stylebench.py > $out/styleprof.log 2>&1 ;;
     stylebench) timeout -k 10 300 python tools_dev/stylebench.py > $out/stylebench.log 2>&1 ;;
