@@ -51,11 +51,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
-    ap.add_argument("--timer-steps", type=int, default=4,
-                    help="kernel timing on every launch of every n-th timed step (exact per-kernel averages for "
-                         "those steps; timing every launch costs ~5 %% of a step in host time, so 1/n of that overall)")
-    ap.add_argument("--timer-every", type=int, default=1,
-                    help="within the timed steps, per-launch HIP events on 1/n of each kernel region's launches")
+    ap.add_argument("--timer-steps", type=int, default=1,
+                    help="kernel timing in every n-th timed step only (1 = all timed steps)")
+    ap.add_argument("--timer-every", type=int, default=4,
+                    help="per-launch HIP events on a pseudo-random 1/n of each kernel region's launches. Not every "
+                         "launch of whole steps: back-to-back event-bound launches run serialised, which timed the "
+                         "LPIPS conv 27 %% below its rocprof duration (profiles/r4_am_bench.json)")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
                     help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5): auto = on "
