@@ -285,9 +285,10 @@ def main(argv=None):
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
         n_t = len(range(0, args.steps, tsteps))
+        where = (f"all {args.steps} timed steps" if tsteps == 1 else
+                 f"{n_t} of the {args.steps} timed steps (every {tsteps}th)")
         roof["timer_sampling"] = ((f"1/{every} of each kernel region's launches (pseudo-random by launch index) in "
-                                   if every > 1 else "every launch in ") +
-                                  f"{n_t} of the {args.steps} timed steps (every {tsteps}th), all launches counted")
+                                   if every > 1 else "every launch in ") + where + ", all launches counted")
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
