@@ -58,10 +58,14 @@ def parse_args(argv=None):
                          "launch of whole steps: back-to-back event-bound launches run serialised, which timed the "
                          "LPIPS conv 27 %% below its rocprof duration (profiles/r4_am_bench.json)")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
-    ap.add_argument("--graphs", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
-                    help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5): auto = on "
-                         "for a single process (same-box A/B: +1.1 %% over 7 pairs, profiles/r4_al_graphs_ab.txt), "
-                         "off under torch.distributed (capture next to RCCL's threads is not exercised here)")
+    ap.add_argument("--graphs", nargs="?", const="on", default="off", choices=["auto", "on", "off"],
+                    help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5). Default off: "
+                         "the same eager path at N = 1 and N > 1 (the replay measured +1.1 %% over 7 same-box pairs, "
+                         "inside the bench noise, profiles/r4_al_graphs_ab.txt); on = opt in for one process; auto = "
+                         "on for a single process with the default config only")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: the same main() on the host (the 2-rank gloo test of the world > 1 branch, "
+                         "tests/test_distributed.py); the bench proper is cuda")
     ap.add_argument("--force-ref-ops", action="store_true", help="A/B: torch formulation of the decoder ops")
     ap.add_argument("--tunableop", choices=["off", "use", "tune"], default="off",
                     help="GEMM solution table (torch TunableOp over hipBLASLt/rocBLAS): 'use' reads the "
@@ -168,11 +172,19 @@ def main(argv=None):
         dist.init()
     rank, world = dist.get_rank(), dist.get_world_size()
     assert world == args.gpus or world_env == 1, f"--gpus {args.gpus} but WORLD_SIZE {world}"
-    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
-    torch.cuda.set_device(device)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device)
+    else:
+        device = torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
     if args.force_ref_ops:
         decoder_ops.set_force_ref(True)
-    use_graphs = args.graphs == "on" or (args.graphs == "auto" and world == 1)
+    use_graphs = on_gpu and (args.graphs == "on" or (args.graphs == "auto" and world == 1 and args.config == CONFIG))
     if args.tunableop == "tune":
         use_graphs = False               # a GEMM cannot be tuned inside a HIP-graph capture
     if use_graphs:
@@ -201,7 +213,7 @@ def main(argv=None):
         eqt.forced = v
         one(0, 0)
     eqt.forced = None
-    torch.cuda.synchronize()
+    sync()
     _log(rank, f"shape warm-up ({len(eqt.variants())} variants): {time.perf_counter() - t1:.1f}s")
     gr = getattr(step.loss, "graphed_nograd", None)
     if gr is not None:
@@ -224,7 +236,7 @@ def main(argv=None):
         t1 = time.perf_counter()
         one(i, cur)
         cur += args.batch * world
-        torch.cuda.synchronize()
+        sync()
         _log(rank, f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t1:.2f}s")
     if not args.trace:
         step.trace = None
@@ -234,18 +246,24 @@ def main(argv=None):
     gc.collect()
     if not args.no_gc_freeze:
         gc.freeze()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     # equivariance outcomes drawn inside the timed region (+ VFM feature reuse per step), to price
     # the timed steps from the FLOP table (profiles/r2_flops.json; host-side bookkeeping only)
     draws, hits = [], []
+    # the timed steps draw their equivariance outcomes (and noise) from a fixed seed, so runs with any
+    # --warmup time the same sequence of outcomes
+    seed = int(c.get("random_seed", 42)) + 7919 * (rank + 1)
+    random.seed(seed)
+    np.random.seed(seed % 2**32)
+    torch.manual_seed(seed)
     eq_fwd = eqt.forward
     eqt.forward = lambda *a, **k: draws.append(eq_fwd(*a, **k)) or draws[-1]
     venc = step.G.vfm_encoder
     every = max(1, args.timer_every)
-    kernel_timer.enable(not args.no_kernel_timer, every)
+    kernel_timer.enable(on_gpu and not args.no_kernel_timer, every)
     t0 = time.perf_counter()
     tsteps = max(1, args.timer_steps)
     for i in range(args.steps):
@@ -255,17 +273,17 @@ def main(argv=None):
         hits.append(getattr(venc, "reuse_hits", 0) - h0)
         cur += args.batch * world
         if args.trace:                      # diagnostics only: per-step wall time (synchronising)
-            torch.cuda.synchronize()
+            sync()
             _log(rank, f"step {i + 1}: {time.perf_counter() - t0:.3f}s cumulative")
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     kernel_timer.enable(False)
     eqt.forward = eq_fwd
     _log(rank, f"timed {args.steps} steps: {dt:.2f}s")
-    if args.trace:
+    if args.trace and on_gpu:
         ms = torch.cuda.memory_stats(device)
         _log(rank, "memory: peak alloc {:.1f} GB, reserved {:.1f} GB, alloc retries {}, device allocs {}, frees {}, "
              "gc counts {}".format(ms.get("allocated_bytes.all.peak", 0) / 2**30, ms.get("reserved_bytes.all.peak", 0) / 2**30,
@@ -281,7 +299,7 @@ def main(argv=None):
     traffic_table = None
     if os.path.exists(PMC_TRAFFIC):       # committed PMC passes of this workload (tools_dev/pmc_traffic.py)
         traffic_table = json.load(open(PMC_TRAFFIC)).get("kernels")
-    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table)
+    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table) if on_gpu else None
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
         n_t = len(range(0, args.steps, tsteps))
@@ -289,7 +307,7 @@ def main(argv=None):
                  f"{n_t} of the {args.steps} timed steps (every {tsteps}th)")
         roof["timer_sampling"] = ((f"1/{every} of each kernel region's launches (pseudo-random by launch index) in "
                                    if every > 1 else "every launch in ") + where + ", all launches counted")
-    step_mfma = step_flops(draws, hits, args.batch, args.steps, value)
+    step_mfma = step_flops(draws, hits, args.batch, args.steps, value) if args.config == CONFIG else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -292,3 +292,51 @@ def test_flat_grad_sync_two_microbatches(bucket_mb):
     expect1 = _accum_expect(1)
     for n, v in expect1.items():
         assert torch.allclose(out[n], v, rtol=1e-5, atol=1e-6), n
+
+
+def _bench_worker(rank, world, cfg_path):
+    """bench.main's world > 1 branch on a 2-rank gloo group (CPU): barrier-bracketed timed steps,
+    max-over-ranks time, one JSON line from rank 0."""
+    import contextlib
+    import io
+    import json
+    import bench
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--batch", "1", "--config", cfg_path,
+                    "--device", "cpu", "--no-cpu-baseline", "--no-kernel-timer"])
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("{")]
+    return {"lines": [json.loads(ln) for ln in lines]}
+
+
+def test_bench_main_two_ranks_gloo(tmp_path):
+    """The driver's N > 1 launch of bench.py (one process per device, WORLD_SIZE 2) on a tiny 64-px
+    stage-0 config: both ranks run the same iteration; only rank 0 prints, value = images of all ranks
+    / the max-over-ranks time, parallelism dp2."""
+    import json
+    import yaml
+    import net_cases
+    vfm = tmp_path / net_cases.VFM_DIRNAME
+    vfm.mkdir()
+    json.dump(dict(net_cases.SIGLIP_CFG, layer_norm_eps=1e-6), open(vfm / "config.json", "w"))
+    gk = net_cases.g_kwargs(str(vfm))
+    gk.pop("img_resolution")
+    gk.update(class_name="networks.generator.Generator")
+    lk = dict(net_cases.loss_kwargs(str(vfm)), class_name="training.loss.TotalLoss",
+              patchgan_discriminator_loss_weight=0.0,
+              feature_matching_loss_weight=0.0)
+    dk = dict(net_cases.D_KWARGS, class_name="networks.discriminator.ProjectedDiscriminator",
+              use_patchgan_discriminator=False, get_interm_feat=False)
+    opt = dict(class_name="torch.optim.Adam", lr=1e-4, betas=[0.0, 0.99], eps=1e-8)
+    cfg = dict(random_seed=42, training_set_kwargs=dict(class_name="training.data_synthetic.SyntheticDataset",
+                                                        resolution=64, conditional=False, label_type="cls2text"),
+               G_kwargs=gk, D_kwargs=dk, loss_kwargs=lk, G_opt_kwargs=opt, D_opt_kwargs=opt, batch_size=2,
+               ema_kimg=10.0, ema_rampup=None, cudnn_benchmark=False)
+    path = tmp_path / "tiny.yaml"
+    path.write_text(yaml.safe_dump(cfg))
+    res = _spawn("_bench_worker", 2, str(path))
+    assert res[1]["lines"] == []
+    (line,) = res[0]["lines"]
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2" and line["steps"] == 2
+    assert line["config"]["global_batch"] == 2 and line["value"] > 0
+    assert abs(line["value"] - 2 * 2 / (line["ms_per_step"] * 2 / 1e3)) / line["value"] < 1e-2

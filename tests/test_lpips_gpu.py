@@ -103,3 +103,19 @@ def test_lpips_module_hip_head_matches_torch_head():
     assert _rel(res["cuda"][0], ref) < 1e-4
     l2 = float((res["cuda"][1].double() - bc.grad.double()).norm() / bc.grad.double().norm())
     assert l2 < 1e-2, l2
+
+
+@pytest.mark.gpu
+def test_lpips_module_under_no_grad():
+    """LPIPS under torch.no_grad() (tools/reconstruct/evaluate.py): the paired VGG16 pass runs its
+    forward outside autograd (custom_ops.FastFunction's stand-in ctx) and gives the grad-mode value."""
+    from training.lpips import LPIPS
+    torch.manual_seed(0)
+    m = LPIPS().eval().to("cuda:0")
+    g = torch.Generator().manual_seed(3)
+    a = (torch.rand(2, 3, 64, 64, generator=g) * 2 - 1).to("cuda:0")
+    b = (a.cpu() + 0.2 * torch.randn(2, 3, 64, 64, generator=g)).clamp(-1, 1).to("cuda:0")
+    with torch.no_grad():
+        v0 = m(a, b)
+    v1 = m(a, b.clone().requires_grad_(True)).detach()
+    assert v0.shape == v1.shape and _rel(v0.cpu(), v1.cpu()) < 1e-6

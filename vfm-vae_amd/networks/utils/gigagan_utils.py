@@ -82,7 +82,7 @@ class SelfAttention(nn.Module):
         h, d = self.heads, self.dim_head
         x = self.norm(fmap).reshape(B, C, H * W)
         wqkv = torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], 0).reshape(3 * h * d, C)
-        if self.fused and self.to_out.bias is None:
+        if self.fused and self.to_out.bias is None and not decoder_ops.force_ref():
             from torch_utils.ops import gigaattn_hip
             if gigaattn_hip.supported(x, h, d):
                 y = gigaattn_hip.null_kv_self_attention(x, wqkv, self.null_kv,

@@ -161,15 +161,15 @@ def f32_precision():
     return (VFM_F32, 3, "f32x6") if F32_PRODUCTS == "f32x6" else (VFM_F32X3, 2, "f32x3")
 
 
-class _Never:
-    def __getitem__(self, i):
-        return False
-
-
 class _NoCtx:
     """The ctx a FastFunction's forward gets when it runs outside autograd: saving is a no-op and no
-    input needs a gradient; attributes may be set (and are dropped with the object)."""
-    needs_input_grad = _Never()
+    input needs a gradient (`needs_input_grad` is a tuple of False, one per forward argument, so
+    indexing and slicing behave as on autograd's ctx); attributes may be set (and are dropped with the
+    object)."""
+    __slots__ = ("needs_input_grad", "__dict__")
+
+    def __init__(self, nargs):
+        self.needs_input_grad = (False,) * nargs
 
     def save_for_backward(self, *tensors):
         pass
@@ -191,7 +191,7 @@ class FastFunction(torch.autograd.Function):
     def apply(cls, *args, **kwargs):
         if torch.is_grad_enabled():
             return super().apply(*args, **kwargs)
-        return cls.forward(_NoCtx(), *args, **kwargs)
+        return cls.forward(_NoCtx(len(args) + len(kwargs)), *args, **kwargs)
 
 
 class NativeError(RuntimeError):

@@ -1080,7 +1080,10 @@ class _StyleDemod(custom_ops.FastFunction):
         ds_in = _c(ds_in.float()) if ds_in is not None else torch.zeros([B, C], **f32)
         if d is not None:
             dd = _c(dd.float()) if dd is not None else torch.zeros([B, O], **f32)
-        ds_ws = torch.empty([max(1, _lib.vfm_style_demod_bwd_workspace_floats(B, C, WD, O))], **f32)
+        nws = _lib.vfm_style_demod_bwd_workspace_floats(B, C, WD, O)
+        if nws < 0:
+            raise custom_ops.NativeError(f"vfm_style_demod_bwd: workspace for B={B} C={C} WD={WD} O={O} exceeds 2^31 floats")
+        ds_ws = torch.empty([max(1, nws)], **f32)
         dW1 = torch.empty([O, C], **f32) if want_W1 else None
         dA = torch.empty([3 * C, WD], **f32) if want_A else None
         dab = torch.empty([3 * C], **f32) if want_ab else None

@@ -35,6 +35,12 @@ def set_force_ref(flag: bool):
     _FORCE_REF = bool(flag)
 
 
+def force_ref() -> bool:
+    """True while set_force_ref(True) holds: every decoder op (and the fused ones built on them, e.g.
+    the GigaGAN null-KV attention Function) takes its torch formulation."""
+    return _FORCE_REF
+
+
 # ---------------------------------------------------------------------------
 # GroupNorm (fp32 statistics), optionally fused with a per-sample channel scale.
 

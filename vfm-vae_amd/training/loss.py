@@ -243,11 +243,12 @@ class TotalLoss:
     def enable_graphed_nograd_forward(self, flag=True):
         """Replay the D phase's no-grad generator forward from HIP graphs
         (training/graphed_forward.py); numerics and RNG draws as the eager pass.
-        Opt-in (VFM_EXPERIMENTAL_GRAPHS=1): torch's reduction kernels on their global-reduce path do not
-        replay correctly from HIP graphs on this stack (the attention blocks' channel norm
-        was the instance in the shipped configs' D-phase forward and is a HIP kernel now; the C1-size
-        regression test passes), and the replay measured no faster than the eager pass (the D-phase
-        forward is GPU-bound), so a configuration not covered by that test should not take it silently."""
+        Opt-in everywhere (VFM_EXPERIMENTAL_GRAPHS=1; `bench.py --graphs on`): torch's reduction kernels on
+        their global-reduce path do not replay correctly from HIP graphs on this stack (the
+        attention blocks' channel norm was the instance in the shipped configs and is a HIP kernel now; the
+        C1-size replay==eager regression test passes), and the replay measured +1.1 % over 7 same-box
+        pairs, inside the bench noise, so neither the bench (same eager path at N = 1 and N > 1) nor a
+        training config takes it by default."""
         if flag and os.environ.get("VFM_EXPERIMENTAL_GRAPHS", "0") != "1":
             raise RuntimeError("graphed no-grad generator forward is experimental (torch reductions replay wrongly "
                                "from HIP graphs, DESIGN.md §5); set VFM_EXPERIMENTAL_GRAPHS=1 to use it")
