@@ -407,6 +407,16 @@ int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, in
 int vfm_gemm4(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
               int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
               long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
+/* bf16 form of the same contract on the LDS-DMA one-wave-per-SIMD kernel (csrc/gemm9.hip: 256 x 256 tiles,
+ * 4 waves of 128 x 128, both operand tiles moved global -> LDS by LDS-DMA two K-tiles ahead, two barriers
+ * per K-tile, accumulators pinned to AGPRs, C stored from the accumulators): the frozen SigLIP2 tower's
+ * linears (reference networks/utils/vfms/siglip2_utils.py:120-121, HF SiglipMLP / SiglipAttention
+ * projections under bf16 autocast) and the decoder's bf16 1x1 convolutions (reference
+ * networks/utils/convnext_utils.py:135-138 pwconv1 / pwconv2, :241-249 the upsample's pointwise conv,
+ * under autocast). bf16 A / B only; K % 64 == 0, N % 8 == 0, 16-B aligned A / B / C (else VFM_NO_KERNEL). */
+int vfm_gemm9(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+              int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 /* K-tile staging schedule of vfm_gemm8 / vfm_gemm8_gelu (process-wide A/B switch for microbenchmarks):
  * 1 = half-tile slots restaged two K-tiles ahead, 0 = one K-tile ahead (default). Returns the previous
  * setting. */

@@ -1,0 +1,108 @@
+"""The LDS-DMA one-wave-per-SIMD bf16 GEMM (csrc/gemm9.hip, `vfm_gemm9`) against an fp32 product of the
+same bf16 operands: every operand layout (K- or M/N-contiguous A and B), bf16 and fp32 outputs, the
+bias / GELU / alpha-beta epilogues, ragged M / N edges, one and two K-tiles, batched and shared (stride-0)
+operands. Tolerances: fp32 output 2e-5 of max |ref| (fp32 accumulation order); bf16 output one bf16
+rounding of the result, 8e-3 of max |ref|."""
+import pytest
+import torch
+
+from torch_utils.ops import gemm_hip
+
+DEV = "cuda:0"
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-30))
+
+
+def _rnd(*shape, g):
+    return (torch.rand(*shape, generator=g) * 2 - 1).to(torch.bfloat16).to(DEV)
+
+
+def _operand(t, kcont_inner):
+    """The same values with the other memory layout when kcont_inner is False (transposed storage)."""
+    return t if kcont_inner else t.transpose(-1, -2).contiguous().transpose(-1, -2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("a_kc", [True, False])
+@pytest.mark.parametrize("b_kc", [True, False])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (304, 264, 64), (264, 520, 128), (1024, 768, 1024), (257, 136, 192)])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_gemm9_layouts(a_kc, b_kc, M, N, K, out_f32):
+    if M % 8 and not a_kc:
+        pytest.skip("M-contiguous A needs M % 8 == 0 (16-B DMA chunks)")
+    g = torch.Generator().manual_seed(M + N + K)
+    A = _rnd(M, K, g=g)
+    Bt = _rnd(N, K, g=g)                       # B = Bt^T: [K, N]
+    a = A if a_kc else _operand(A, False)
+    b = Bt.t() if b_kc else Bt.t().contiguous()
+    ref = A.float() @ Bt.float().t()
+    out = gemm_hip.try_gemm(a, b, route=("g9", 0), out_dtype=torch.float32 if out_f32 else None)
+    assert out is not None and out.shape == (M, N)
+    assert _rel(out, ref) < (2e-5 if out_f32 else 8e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", [None, "gelu_tanh", "gelu"])
+@pytest.mark.parametrize("bias_dim", [None, 0, 1])
+def test_gemm9_epilogues(act, bias_dim):
+    g = torch.Generator().manual_seed(7)
+    M, N, K = 384, 520, 192
+    A, Bt = _rnd(M, K, g=g), _rnd(N, K, g=g)
+    bias = None
+    ref = A.float() @ Bt.float().t()
+    if bias_dim is not None:
+        bias = torch.randn(M if bias_dim == 0 else N, generator=g).to(DEV)
+        ref = ref + (bias[:, None] if bias_dim == 0 else bias[None, :])
+    if act == "gelu_tanh":
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    elif act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    out = gemm_hip.try_gemm(A, Bt.t(), bias=bias, bias_dim=bias_dim, act=act, route=("g9", 0),
+                            out_dtype=torch.float32)
+    assert _rel(out, ref) < 2e-5
+    # alpha / beta on an fp32 output
+    c0 = torch.randn(M, N, generator=g).to(DEV)
+    out2 = c0.clone()
+    gemm_hip.try_gemm(A, Bt.t(), out=out2, alpha=0.5, beta=-2.0, route=("g9", 0), out_dtype=torch.float32)
+    assert _rel(out2, 0.5 * (A.float() @ Bt.float().t()) - 2.0 * c0) < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shared", ["A", "B", None])
+def test_gemm9_batched(shared):
+    """Batched products as the decoder's 1x1 convs run them: W [O, I] shared (stride 0) against per-sample
+    planes x[b] [I, P] (N-contiguous), and the data gradient's W^T (M-contiguous A)."""
+    g = torch.Generator().manual_seed(11)
+    z, O, I, P = 3, 256, 512, 1024
+    W = _rnd(O, I, g=g)
+    x = _rnd(z, I, P, g=g)
+    if shared == "A":
+        out = gemm_hip.try_gemm(W, x, route=("g9", 0))
+        ref = torch.matmul(W.float(), x.float())
+    elif shared == "B":
+        dy = _rnd(z, O, P, g=g)
+        out = gemm_hip.try_gemm(W.t(), dy, route=("g9", 0))
+        ref = torch.matmul(W.t().float(), dy.float())
+    else:
+        Ws = _rnd(z, O, I, g=g)
+        out = gemm_hip.try_gemm(Ws, x, route=("g9", 0))
+        ref = torch.matmul(Ws.float(), x.float())
+    assert out is not None and out.shape == ref.shape
+    assert _rel(out, ref) < 8e-3
+
+
+@pytest.mark.gpu
+def test_gemm9_siglip_shape_bitwise_stable():
+    """A full SigLIP2-L shape (32 x 1024 tokens, fc1 with the tanh-GELU epilogue): against fp32, and two
+    launches bit-identical (no data race between the DMA ring and the fragment reads)."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 32768, 4096, 1024
+    A, W = _rnd(M, K, g=g), _rnd(N, K, g=g)
+    b = torch.randn(N, generator=g).to(DEV)
+    outs = [gemm_hip.try_gemm(A, W.t(), bias=b, bias_dim=1, act="gelu_tanh", route=("g9", 0)) for _ in range(2)]
+    assert torch.equal(outs[0], outs[1])
+    rows = torch.randint(0, M, (512,), generator=g).to(DEV)
+    ref = torch.nn.functional.gelu(A[rows].float() @ W.float().t() + b, approximate="tanh")
+    assert _rel(outs[0][rows], ref) < 8e-3

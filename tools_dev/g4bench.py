@@ -31,7 +31,10 @@ def timeit(fn, iters=10):
     return s.elapsed_time(e) / iters * 1e3
 
 
-def case(name, A, B, ref_fn, torch_fn, flops, kinds=("g4", "g8")):
+KINDS = tuple(os.environ.get("G4_KINDS", "g9,g8").split(","))
+
+
+def case(name, A, B, ref_fn, torch_fn, flops, kinds=KINDS):
     if ONLY and ONLY not in name:
         return
     ref = ref_fn()
@@ -83,6 +86,6 @@ for tag, O, I, P in [("b3 W1 512->2048 @64^2", 2048, 512, 4096), ("b3 W2 2048->5
 for M, N, K in [(300, 200, 64), (257, 520, 128), (1000, 136, 192)]:
     A, W = rnd(M, K), rnd(N, K)
     ref = A.float() @ W.float().t()
-    out = gemm_hip.try_gemm(A, W.t(), route=("g4", 0))
+    out = gemm_hip.try_gemm(A, W.t(), route=(KINDS[0], 0))
     err = float((out.float() - ref).abs().max() / ref.abs().max())
     print(f"ragged {M}x{N}x{K}: err {err:.1e}", flush=True)

@@ -1,0 +1,373 @@
+// 256 x 256 bf16 GEMM, one wave per SIMD, both operands staged by LDS-DMA: the hot path's bf16
+// products (the frozen SigLIP2 tower's QKV / O / fc1 / fc2 linears, the decoder's bf16 1x1
+// convolutions): C[z] = epi(alpha A[z] B[z] + beta C[z]).
+//
+// Why this structure (the third 256-tile kernel of the tree): hipBLASLt's fastest gfx950 kernel for
+// these shapes is a 256-thread workgroup whose 4 waves each own a 128 x 128 block, with both operand
+// tiles moved global -> LDS by LDS-DMA, two K-tiles in flight and two barriers per 64-deep K-tile
+// (its code object's name and instruction mix: DirectToLds A/B, prefetch depth 2, wave tile 8 x 8 of
+// v_mfma_f32_16x16x32_bf16). gemm4 (register staging) lost its K-loop to the compiler serialising the
+// staged loads behind the MFMA chain; gemm8 (8 waves of 128 x 64) spends twice the fragment reads per
+// MFMA and 8 barriers per K-tile. Here, per K-tile and wave: 128 MFMAs, 32 fragment reads (one per
+// MFMA in the two read phases), 16 LDS-DMA issues (one per ~5 MFMAs), 2 barriers:
+//
+//   phase 1: MFMAs on k-half 0 of K-tile t (fragments in VGPRs since the previous iteration) beside the
+//            fragment reads of k-half 1 of t;
+//   barrier B1 (after lgkmcnt(0)): every wave has read all of buffer t & 1;
+//   phase 2: the rest of k-half 0 and most of k-half 1 beside the 16 LDS-DMA of K-tile t + 2 into
+//            buffer t & 1;
+//   vmcnt(16) + barrier B2: K-tile t + 1 (issued one iteration earlier) has landed for every wave;
+//   phase 3: the last MFMAs of k-half 1 beside the fragment reads of k-half 0 of K-tile t + 1.
+//
+// The order of every MFMA, fragment read and DMA issue is pinned with sched_barrier(0) (the compiler
+// inserts the counted lgkmcnt waits of the fragment reads itself); the DMAs are inline asm so that the
+// waitcnt pass does not drain them before every ds_read, and only the counted waits above retire them.
+// LDS images (two 64 KB stages, A then B): K-contiguous operands [256 rows][64 k] with 128-B rows and
+// chunk ^= (row >> 1) & 7 (ds_read_b128 fragments); M/N-contiguous ones two [64 k][128] halves with
+// 256-B rows and the 4 x 4 chunk swizzle of the transposed reads (ds_read_b64_tr_b16) -- the images of
+// gemm8.hip, swizzled on the DMA source address (the destination is lane-linear).
+// The MFMA takes the B fragment first, so a lane's accumulator holds 4 consecutive columns of one C
+// row; the epilogue pairs column blocks with v_permlane16_swap and stores 16 B per lane straight from
+// the accumulators (no LDS round trip).
+#include <type_traits>
+
+#include "vfm_common.h"
+
+namespace {
+
+using namespace vfm;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 256;
+constexpr int OPB = 256 * BK * 2;          // one operand image (32 KB)
+constexpr int STAGE = 2 * OPB;             // A + B of one K-tile (64 KB)
+
+struct G9Args {
+    const __hip_bfloat16* A;
+    const __hip_bfloat16* B;
+    void* C;
+    const float* bias;
+    long long lda, ldb, ldc, sA, sB, sC;
+    int M, N, K;
+    float alpha, beta;
+    int bias_mode, act;
+    unsigned spanA, spanB;     // buffer-descriptor ranges in bytes (< 2^31, checked on the host)
+};
+
+__device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
+__device__ __forceinline__ int mc_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int mc_off(int row, int ch) { return row * 256 + 16 * (ch ^ mc_swz(row)); }
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+    const float u = 0.7978845608028654f * fmaf(0.044715f * x, x * x, x);
+    const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * u);
+    return 0.5f * x * (2.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f));
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    const f2 x = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, b2));
+}
+
+// One LDS-DMA instruction (buffer_load_dwordx4 ... offen lds): lane l's 16 B from rsrc + voff + soff land
+// at M0 + 16 l. M0 and soff are SALU values (no VALU -> SGPR hand-off before the load).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned m0) {
+    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
+                 "s"(soff), "s"(m0)
+                 : "memory");
+}
+
+// Per-lane byte offset (from the operand's K-tile origin) of DMA slot u (0..7) of a 256-wide operand tile
+// starting at outer0; destination byte u * 4096 + 16 tid of the operand image. Rows / columns past
+// outer_n read a valid element whose product is never stored.
+template <bool KCONT>
+__device__ __forceinline__ unsigned dma_voff(long long ld, int outer0, int outer_n, int u, int tid) {
+    if (KCONT) {
+        const int row = 32 * u + (tid >> 3), chs = (tid & 7) ^ ((row >> 1) & 7);
+        const int o = min(outer0 + row, outer_n - 1);
+        return (unsigned)(((long long)o * ld + 8 * chs) * 2);
+    } else {
+        const int h = u >> 2, row = 16 * (u & 3) + (tid >> 4), chs = (tid & 15) ^ mc_swz(row);
+        int o = outer0 + 128 * h + 8 * chs;
+        if (o >= outer_n) o = 0;                       // (outer_n % 8 == 0): a valid chunk, result unused
+        return (unsigned)(((long long)row * ld + o) * 2);
+    }
+}
+
+// 16x16x32 fragment of 16-row block blk (0..15) of an operand image, k32 step t: lane l carries row
+// (column) l & 15, k = 32 t + 8 (l >> 4) .. + 7.
+template <bool KCONT>
+__device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int t, int lane) {
+    if (KCONT) {
+        return *reinterpret_cast<const bf16x8*>(img + kc_off(16 * blk + (lane & 15), 4 * t + (lane >> 4)));
+    } else {
+        const unsigned char* h = img + (blk >> 3) * (OPB / 2);
+        const int b = blk & 7;
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int ch = 2 * b + (p >> 1);
+        const int row = 32 * t + 8 * g + q;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(h + mc_off(row, ch) + 8 * (p & 1)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(h + mc_off(row + 4, ch) + 8 * (p & 1)));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+}
+
+// acc += x y on the matrix core with the accumulator pinned to AGPRs: the builtin's form lets the register
+// allocator split the 256 accumulator registers between the two files and shuffle them every K-tile
+// (hundreds of v_accvgpr moves per K-tile, which is also what held gemm4's loop back)
+__device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8& x, const bf16x8& y) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
+}
+
+#define SB() __builtin_amdgcn_sched_barrier(0)
+#define VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+template <bool AK, bool BKC, bool OUTF32>
+__global__ __launch_bounds__(THREADS, 1) void gemm9_kernel(G9Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    int m0, n0;
+    {
+        // XCD-aware bijective remap, then grouped order (GROUP tile-rows per column sweep), as gemm8
+        const int bid = blockIdx.x;
+        const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+        const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        constexpr int GROUP = 4;
+        const int gsz = GROUP * tiles_n, grp = tile / gsz, rem = tile - grp * gsz;
+        const int rows_g = min(GROUP, tiles_m - grp * GROUP);
+        m0 = (grp * GROUP + rem % rows_g) * BM;
+        n0 = (rem / rows_g) * BN;
+    }
+    const int z = blockIdx.y;
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.spanA, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.spanB, 0x00020000);
+    unsigned voA[8], voB[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        voA[u] = dma_voff<AK>(a.lda, m0, a.M, u, tid);
+        voB[u] = dma_voff<BKC>(a.ldb, n0, a.N, u, tid);
+    }
+    const unsigned m0A = (unsigned)(size_t)(lds_void*)lds + (unsigned)wave * 1024u;
+    const unsigned zA = (unsigned)(z * a.sA * 2), zB = (unsigned)(z * a.sB * 2);
+    const unsigned dkA = (unsigned)(AK ? BK * 2 : BK * a.lda * 2), dkB = (unsigned)(BKC ? BK * 2 : BK * a.ldb * 2);
+    const int KT = a.K / BK;
+
+    // DMA slot g (0..7 A, 8..15 B) of K-tile kt into buffer buf; past the last K-tile the descriptors have no
+    // records (the DMA writes zeros into a buffer nobody reads any more and moves no memory), so every K-tile
+    // runs the same body
+    const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, 0, 0x00020000);
+    auto dma = [&](int g, int buf, int kt) __attribute__((always_inline)) {
+        const bool live = kt < KT;
+        if (g < 8) dma16(live ? rA : nA, voA[g], zA + (unsigned)kt * dkA, m0A + buf * STAGE + g * 4096);
+        else dma16(live ? rB : nB, voB[g - 8], zB + (unsigned)kt * dkB, m0A + buf * STAGE + OPB + (g - 8) * 4096);
+    };
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+    // fragment read r (0..15) of k-half h from buffer buf, in the order A0 B0 A1..A7 B1..B7: the MFMAs of a
+    // k-half walk j (B block) outer, i (A block) inner, so the first MFMA needs reads 0 and 1 only
+    auto rd = [&](int h, int r, int buf) __attribute__((always_inline)) {
+        const unsigned char* base = lds + buf * STAGE;
+        const bool isb = (r == 1) || r >= 9;
+        const int idx = r == 0 ? 0 : r == 1 ? 0 : r <= 8 ? r - 1 : r - 8;
+        if (!isb) {
+            const bf16x8 v = frag<AK>(base, 8 * wm + idx, h, lane);
+            if (h == 0) fa0[idx] = v; else fa1[idx] = v;
+        } else {
+            const bf16x8 v = frag<BKC>(base + OPB, 8 * wn + idx, h, lane);
+            if (h == 0) fb0[idx] = v; else fb1[idx] = v;
+        }
+    };
+    // MFMA q (0..63) of k-half h: B block j = q / 8, A block i = q % 8
+    auto mf = [&](int h, int q) __attribute__((always_inline)) {
+        const int j = q >> 3, i = q & 7;
+        mfma_acc(acc[i][j], h ? fb1[j] : fb0[j], h ? fa1[i] : fa0[i]);
+    };
+
+    // prologue: K-tiles 0 and 1 in flight (1 as a null DMA when K has one tile), K-tile 0 landed, k-half 0
+    // fragments of K-tile 0 read
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dma(g, 0, 0);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dma(g, 1, 1);
+    VMCNT(16);
+    __builtin_amdgcn_s_barrier();
+    SB();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rd(0, r, 0);
+    SB();
+
+    // one K-tile per iteration (the last one's phase 3 reads a buffer that holds no K-tile: unused)
+    for (int t = 0; t < KT; ++t) {
+        const int cur = t & 1;
+        // phase 1: 26 MFMAs of k-half 0 beside the 16 reads of k-half 1
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            mf(0, q);
+            SB();
+            rd(1, q, cur);
+            SB();
+        }
+#pragma unroll
+        for (int q = 16; q < 26; ++q) mf(0, q);
+        SB();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        SB();
+        // phase 2: 38 MFMAs of k-half 0 + 43 of k-half 1 beside the 16 DMA of K-tile t + 2 (every 5th)
+#pragma unroll
+        for (int s = 0; s < 81; ++s) {
+            if (s < 38) mf(0, 26 + s);
+            else mf(1, s - 38);
+            SB();
+            if ((s % 5) == 4 && s / 5 < 16) {
+                dma(s / 5, cur, t + 2);
+                SB();
+            }
+        }
+        VMCNT(16);
+        __builtin_amdgcn_s_barrier();
+        SB();
+        // phase 3: 21 MFMAs of k-half 1 beside the 16 reads of k-half 0 of K-tile t + 1
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            mf(1, 43 + q);
+            SB();
+            rd(0, q, cur ^ 1);
+            SB();
+        }
+#pragma unroll
+        for (int q = 59; q < 64; ++q) mf(1, q);
+        SB();
+    }
+    VMCNT(0);                                  // the null DMAs of the last two iterations
+    // the asm MFMAs are opaque to the hazard recognizer: wait out the last results (XDL write -> VALU read)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+    // epilogue straight from the accumulators: acc[i][j][r] = C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r]
+    const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
+    const int l15 = lane & 15, row4 = lane >> 4;
+    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
+    TC* Cz = reinterpret_cast<TC*>(a.C) + (long long)z * a.sC;
+    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
+    // epilogue value of column n of row m (the generic form; plain products skip it)
+    auto epi = [&](float x, int m, bool mok, int n, const TC* crow) __attribute__((always_inline)) {
+        const bool in = mok && n < a.N;
+        x *= a.alpha;
+        if (a.beta != 0.f && in) x = fmaf(a.beta, ld(crow + n), x);
+        x += a.bias_mode == 1 ? (n < a.N ? a.bias[n] : 0.f) : (a.bias_mode == 2 && mok ? a.bias[m] : 0.f);
+        if (a.act == 1) x = gelu_tanh(x);
+        else if (a.act == 2) x = x * gelu_parts(x).cdf;
+        return x;
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = mw + 16 * i + l15;
+        const bool mok = m < a.M;
+        TC* crow = Cz + (long long)(mok ? m : 0) * a.ldc;
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+            const int j0 = 2 * jp, j1 = j0 + 1;
+            f32x4 v0 = acc[i][j0], v1 = acc[i][j1];
+            if (!plain) {
+                const int n0c = nw + 16 * j0 + 4 * row4, n1c = n0c + 16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v0[r] = epi(v0[r], m, mok, n0c + r, crow);
+                    v1[r] = epi(v1[r], m, mok, n1c + r, crow);
+                }
+            }
+            if (OUTF32) {
+                const int n0c = nw + 16 * j0 + 4 * row4;
+                float* cf = reinterpret_cast<float*>(crow);
+                if (mok && n0c < a.N) *reinterpret_cast<f32x4*>(cf + n0c) = v0;
+                if (mok && n0c + 16 < a.N) *reinterpret_cast<f32x4*>(cf + n0c + 16) = v1;
+            } else {
+                const uint32_t a0 = pack_bf16x2(v0[0], v0[1]), a1 = pack_bf16x2(v0[2], v0[3]);
+                const uint32_t b0 = pack_bf16x2(v1[0], v1[1]), b1 = pack_bf16x2(v1[2], v1[3]);
+                // rows (16-lane groups) 1 and 3 of (a0, a1) <-> rows 0 and 2 of (b0, b1): each lane then holds 8
+                // consecutive columns (a0 a1 b0 b1) of block j0 (rows 0, 2) or j1 (rows 1, 3)
+                const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+                const int n = nw + 16 * (j0 + (row4 & 1)) + 8 * (row4 >> 1);
+                if (mok && n < a.N)
+                    *reinterpret_cast<uint4*>(reinterpret_cast<__hip_bfloat16*>(crow) + n) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            }
+        }
+    }
+}
+
+template <bool AK, bool BKC, bool OUTF32>
+void launch9(const G9Args& a, int batch, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm9_kernel<AK, BKC, OUTF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * STAGE);
+        attr = true;
+    }
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    VFM_LAUNCH((gemm9_kernel<AK, BKC, OUTF32>), dim3(nwg, batch), dim3(THREADS), 2 * STAGE, st, a);
+}
+
+long long span9(int kcont, long long outer, long long kdim, long long ld, long long sb, int batch) {
+    const long long rows = kcont ? outer : kdim;
+    const long long cols = kcont ? kdim : outer;
+    const long long e = (rows - 1) * ld + cols + (long long)(batch - 1) * sb;
+    const long long bytes = e * 2;
+    return bytes >= (1LL << 31) ? -1 : bytes;
+}
+
+}  // namespace
+
+// bf16 operands: C[z] (M x N, ldc, batch stride sC) = epi(alpha A[z] B[z] + beta C[z]) with A [M, K]
+// (a_kcont: K-contiguous rows of stride lda, else M-contiguous rows of K) and B [K, N] (b_kcont: B is
+// given as N rows of K, stride ldb; else K rows of N). bias_mode 0 none / 1 per column / 2 per row;
+// act 0 none / 1 tanh-GELU / 2 erf-GELU; out_dtype VFM_BF16 or VFM_F32. Returns VFM_NO_KERNEL for shapes
+// it does not take (K % 64, N % 8, unaligned operands, > 2 GiB spans).
+extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+                         int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream) {
+    if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
+    if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
+    if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
+    if (K % BK || N % 8) return VFM_NO_KERNEL;
+    const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
+    if (a_c % 8 || b_c % 8 || lda % 8 || ldb % 8 || sA % 8 || sB % 8 || ldc % 8 || sC % 8) return VFM_NO_KERNEL;
+    if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16) return VFM_NO_KERNEL;
+    if (lda < (a_kcont ? (long long)K : M) || ldb < (b_kcont ? (long long)K : N) || ldc < N) return VFM_ERR_ARGS;
+    const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
+    const long long spA = span9(a_kcont, M, K, lda, sA, batch);
+    const long long spB = span9(b_kcont, N, K, ldb, sB, batch);
+    if (spA < 0 || spB < 0) return VFM_NO_KERNEL;
+    G9Args a{};
+    a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
+    a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
+    a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
+    a.spanA = (unsigned)spA; a.spanB = (unsigned)spB;
+    hipStream_t st = (hipStream_t)stream;
+    const bool of32 = out_dtype == VFM_F32;
+#define VFM_G9(AK, BK_) of32 ? launch9<AK, BK_, true>(a, batch, st) : launch9<AK, BK_, false>(a, batch, st)
+    if (a_kcont && b_kcont) VFM_G9(true, true);
+    else if (a_kcont && !b_kcont) VFM_G9(true, false);
+    else if (!a_kcont && b_kcont) VFM_G9(false, true);
+    else VFM_G9(false, false);
+#undef VFM_G9
+    return launch_status();
+}

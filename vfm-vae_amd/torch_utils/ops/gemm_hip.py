@@ -225,6 +225,19 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     stream = custom_ops.stream_ptr(A.device)
     kern, arg = route or _plan(A.dtype, M, N, K, z, reduce_batch, splits, auto)
     tb = lambda v: "true" if v else "false"
+    if kern == "g9" and A.dtype == torch.bfloat16 and not reduce_batch:
+        # one wave per SIMD, 128 x 128 per wave, LDS-DMA staging two K-tiles ahead (csrc/gemm9.hip)
+        region = f"gemm9<bf16,{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
+        if kernel_timer.SHAPES:
+            region += f"[{M}x{N}x{K}x{z}]"
+        with kernel_timer.region(region, nbytes, flops, "mfma"):
+            rc = _lib.vfm_gemm9(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype],
+                                M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, sC, float(alpha), float(beta),
+                                bias_mode, ACTS[act], stream)
+        if rc != custom_ops.VFM_NO_KERNEL:
+            custom_ops.check(rc, "vfm_gemm9")
+            return out
+        kern, arg = "g8", 0
     if kern == "g4" and A.dtype == torch.bfloat16 and not reduce_batch:
         # one wave per SIMD, 128 x 128 per wave (csrc/gemm4.hip)
         region = f"gemm4<bf16,{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
