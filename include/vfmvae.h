@@ -417,6 +417,10 @@ int vfm_gemm4(const void* A, const void* B, void* C, const float* bias, int out_
 int vfm_gemm9(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
               int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
               long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
+/* Kernel form of vfm_gemm9 (process-wide A/B switch for microbenchmarks): 1 = persistent (one workgroup per CU
+ * walking the output tiles as one K-tile stream; default), 0 = one workgroup per output tile. Returns the
+ * previous setting. */
+int vfm_gemm9_set_mode(int persistent);
 /* K-tile staging schedule of vfm_gemm8 / vfm_gemm8_gelu (process-wide A/B switch for microbenchmarks):
  * 1 = half-tile slots restaged two K-tiles ahead, 0 = one K-tile ahead (default). Returns the previous
  * setting. */

@@ -29,7 +29,8 @@ def _operand(t, kcont_inner):
 @pytest.mark.parametrize("b_kc", [True, False])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 256), (304, 264, 64), (264, 520, 128), (1024, 768, 1024), (257, 136, 192)])
 @pytest.mark.parametrize("out_f32", [False, True])
-def test_gemm9_layouts(a_kc, b_kc, M, N, K, out_f32):
+@pytest.mark.parametrize("persistent", [1, 0])
+def test_gemm9_layouts(a_kc, b_kc, M, N, K, out_f32, persistent):
     if M % 8 and not a_kc:
         pytest.skip("M-contiguous A needs M % 8 == 0 (16-B DMA chunks)")
     g = torch.Generator().manual_seed(M + N + K)
@@ -38,7 +39,11 @@ def test_gemm9_layouts(a_kc, b_kc, M, N, K, out_f32):
     a = A if a_kc else _operand(A, False)
     b = Bt.t() if b_kc else Bt.t().contiguous()
     ref = A.float() @ Bt.float().t()
-    out = gemm_hip.try_gemm(a, b, route=("g9", 0), out_dtype=torch.float32 if out_f32 else None)
+    prev = gemm_hip._lib.vfm_gemm9_set_mode(persistent)
+    try:
+        out = gemm_hip.try_gemm(a, b, route=("g9", 0), out_dtype=torch.float32 if out_f32 else None)
+    finally:
+        gemm_hip._lib.vfm_gemm9_set_mode(prev)
     assert out is not None and out.shape == (M, N)
     assert _rel(out, ref) < (2e-5 if out_f32 else 8e-3)
 
@@ -106,3 +111,18 @@ def test_gemm9_siglip_shape_bitwise_stable():
     rows = torch.randint(0, M, (512,), generator=g).to(DEV)
     ref = torch.nn.functional.gelu(A[rows].float() @ W.float().t() + b, approximate="tanh")
     assert _rel(outs[0][rows], ref) < 8e-3
+
+
+@pytest.mark.gpu
+def test_gemm9_persistent_many_items_bitwise_stable():
+    """The persistent form walks several output tiles per workgroup (a K-tile stream across tile boundaries,
+    the stores of one tile in flight beside the next tile's first K-tile): a 4096-tile batched product twice,
+    bit-identical, and against fp32 on sampled planes."""
+    g = torch.Generator().manual_seed(5)
+    z, O, I, P = 32, 512, 2048, 4096            # the decoder's b3 pwconv2 at batch 32: 8 K-tiles per tile
+    W = _rnd(O, I, g=g)
+    x = _rnd(z, I, P, g=g)
+    outs = [gemm_hip.try_gemm(W, x, route=("g9", 0)) for _ in range(2)]
+    assert torch.equal(outs[0], outs[1])
+    for b in (0, 13, 31):
+        assert _rel(outs[0][b], W.float() @ x[b].float()) < 8e-3

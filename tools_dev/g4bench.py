@@ -38,7 +38,15 @@ def case(name, A, B, ref_fn, torch_fn, flops, kinds=KINDS):
     if ONLY and ONLY not in name:
         return
     ref = ref_fn()
-    fns = {k: (lambda k=k: gemm_hip.try_gemm(A, B, route=(k, 0))) for k in kinds}
+    def run(k):
+        if k == "g9np":                     # gemm9, one workgroup per tile
+            prev = gemm_hip._lib.vfm_gemm9_set_mode(0)
+            try:
+                return gemm_hip.try_gemm(A, B, route=("g9", 0))
+            finally:
+                gemm_hip._lib.vfm_gemm9_set_mode(prev)
+        return gemm_hip.try_gemm(A, B, route=(k, 0))
+    fns = {k: (lambda k=k: run(k)) for k in kinds}
     fns["blas"] = torch_fn
     errs = {}
     for k in kinds:

@@ -40,6 +40,7 @@ using namespace vfm;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -56,7 +57,7 @@ struct G9Args {
     int M, N, K;
     float alpha, beta;
     int bias_mode, act;
-    unsigned spanA, spanB;     // buffer-descriptor ranges in bytes (< 2^31, checked on the host)
+    unsigned spanA, spanB, spanC;     // buffer-descriptor ranges in bytes (< 2^31, checked on the host)
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -124,6 +125,12 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int blk, int t,
 // (hundreds of v_accvgpr moves per K-tile, which is also what held gemm4's loop back)
 __device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8& x, const bf16x8& y) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
+}
+
+// acc = x y (the first K-tile of an output tile: the accumulator is defined by the MFMA, no zeroing pass and no
+// loop-carried zeros for the register allocator to juggle)
+__device__ __forceinline__ void mfma_acc0(f32x4& c, const bf16x8& x, const bf16x8& y) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(x), "v"(y));
 }
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
@@ -313,6 +320,241 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9_kernel(G9Args a) {
     }
 }
 
+// Persistent form: one workgroup per CU walks items (z, tile) = blockIdx.x, + gridDim.x, ...; the K-tiles of
+// consecutive items form one stream, so the DMA of the next item's first two K-tiles is issued during the
+// current item's last two (no prologue per item) and the epilogue's stores leave while the next item's first
+// K-tile computes. The stores are buffer stores with an out-of-range offset for the lanes outside C (the
+// hardware drops them), so every wave issues exactly NST of them and the counted vmcnt waits stay exact:
+// at B2 of an item's first K-tile the stores are younger than the DMA waited for.
+__device__ __forceinline__ void item_tile(int item, int nwg, int total, int tiles_m, int tiles_n, int& z, int& m0,
+                                          int& n0) {
+    // XCD-aware bijective remap over all items (blocks b and b + 8 share an XCD; with gridDim.x % 8 == 0 the
+    // items a workgroup walks stay on its XCD), then grouped order inside the output batch
+    const int xcd = item & 7, q8 = total >> 3, r8 = total & 7;
+    const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (item >> 3);
+    z = g / nwg;
+    const int tile = g - z * nwg;
+    constexpr int GROUP = 4;
+    const int gsz = GROUP * tiles_n, grp = tile / gsz, rem = tile - grp * gsz;
+    const int rows_g = min(GROUP, tiles_m - grp * GROUP);
+    m0 = (grp * GROUP + rem % rows_g) * BM;
+    n0 = (rem / rows_g) * BN;
+}
+
+template <bool AK, bool BKC, bool OUTF32>
+__global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int G = gridDim.x;
+    const int KT = a.K / BK;
+    const unsigned m0A = (unsigned)(size_t)(lds_void*)lds + (unsigned)wave * 1024u;
+    const unsigned dkA = (unsigned)(AK ? BK * 2 : BK * a.lda * 2), dkB = (unsigned)(BKC ? BK * 2 : BK * a.ldb * 2);
+
+    // DMA cursor: the item and K-tile of the next stream position to issue. Per-lane offsets are relative to the
+    // operand tile's K-tile origin and the same for every item and K-tile; the origin itself moves the buffer
+    // descriptor's base (SALU), whose record count is the operand's remaining span, so rows / columns past the
+    // operand read in-bounds garbage or zeros that no stored output depends on, and nothing past its end.
+    unsigned voA[8], voB[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        voA[u] = dma_voff<AK>(a.lda, 0, 0x7fffffff, u, tid);
+        voB[u] = dma_voff<BKC>(a.ldb, 0, 0x7fffffff, u, tid);
+    }
+    int d_item = blockIdx.x, d_kt = 0;
+    long long offA = 0, offB = 0;                 // byte offsets of the cursor's K-tile origin in A / B
+    auto setup_dma = [&](int item) __attribute__((always_inline)) {
+        int z, m0, n0;
+        item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
+        offA = (z * a.sA + (AK ? (long long)m0 * a.lda : (long long)m0)) * 2;
+        offB = (z * a.sB + (BKC ? (long long)n0 * a.ldb : (long long)n0)) * 2;
+    };
+    auto rsrc = [&](const void* base, long long off, long long span) __attribute__((always_inline)) {
+        const long long left = span - off;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, (int)(left > 0 ? left : 0),
+                                                 0x00020000);
+    };
+    __amdgpu_buffer_rsrc_t rA = rsrc(a.A, 0, a.spanA), rB = rsrc(a.B, 0, a.spanB);
+    auto dma = [&](int g, int buf) __attribute__((always_inline)) {
+        if (g < 8) dma16(rA, voA[g], 0u, m0A + buf * STAGE + g * 4096);
+        else dma16(rB, voB[g - 8], 0u, m0A + buf * STAGE + OPB + (g - 8) * 4096);
+    };
+    // descriptors of the cursor's position (after setup_dma / a K-tile step)
+    // (past the workgroup's last item: no records, the DMA writes zeros into a buffer nobody reads again)
+    auto point = [&]() __attribute__((always_inline)) {
+        const bool live = d_item < total;
+        rA = rsrc(a.A, offA + (long long)d_kt * dkA, live ? (long long)a.spanA : 0);
+        rB = rsrc(a.B, offB + (long long)d_kt * dkB, live ? (long long)a.spanB : 0);
+    };
+    auto advance = [&]() __attribute__((always_inline)) {
+        if (++d_kt == KT) {
+            d_kt = 0;
+            d_item += G;
+            if (d_item < total) setup_dma(d_item);
+        }
+        point();
+    };
+
+    f32x4 acc[8][8];
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+    auto rd = [&](int h, int r, int buf) __attribute__((always_inline)) {
+        const unsigned char* base = lds + buf * STAGE;
+        const bool isb = (r == 1) || r >= 9;
+        const int idx = r == 0 ? 0 : r == 1 ? 0 : r <= 8 ? r - 1 : r - 8;
+        if (!isb) {
+            const bf16x8 v = frag<AK>(base, 8 * wm + idx, h, lane);
+            if (h == 0) fa0[idx] = v; else fa1[idx] = v;
+        } else {
+            const bf16x8 v = frag<BKC>(base + OPB, 8 * wn + idx, h, lane);
+            if (h == 0) fb0[idx] = v; else fb1[idx] = v;
+        }
+    };
+    auto mf = [&](int h, int q, bool first) __attribute__((always_inline)) {
+        const int j = q >> 3, i = q & 7;
+        if (first && h == 0) mfma_acc0(acc[i][j], fb0[j], fa0[i]);
+        else mfma_acc(acc[i][j], h ? fb1[j] : fb0[j], h ? fa1[i] : fa0[i]);
+    };
+
+    // C through a buffer descriptor: out-of-range lanes store to an offset past its records (dropped)
+    typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
+    constexpr int ES = sizeof(TC);
+    const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, (int)a.spanC, 0x00020000);
+    constexpr int NST = OUTF32 ? 64 : 32;       // store instructions per wave and item
+    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
+    const int l15 = lane & 15, row4 = lane >> 4;
+
+    // prologue: stream positions 0 and 1 in flight, 0 landed, k-half 0 fragments of position 0 read
+    setup_dma(d_item);
+    point();
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dma(g, 0);
+    advance();
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dma(g, 1);
+    advance();
+    VMCNT(16);
+    __builtin_amdgcn_s_barrier();
+    SB();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rd(0, r, 0);
+    SB();
+
+    int p = 0;                                  // stream position (buffer p & 1)
+    for (int item = blockIdx.x; item < total; item += G) {
+        const bool stores_young = item != (int)blockIdx.x && !OUTF32;
+        // one K-tile (first: the item's first, whose k-half-0 MFMAs define the accumulators)
+        auto ktile = [&](int t, auto first_c) __attribute__((always_inline)) {
+            constexpr bool first = decltype(first_c)::value;
+            const int cur = p & 1;
+            // phase 1: 26 MFMAs of k-half 0 beside the 16 reads of k-half 1
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                mf(0, q, first);
+                SB();
+                rd(1, q, cur);
+                SB();
+            }
+#pragma unroll
+            for (int q = 16; q < 26; ++q) mf(0, q, first);
+            SB();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            SB();
+            // phase 2: 38 MFMAs of k-half 0 + 43 of k-half 1 beside the 16 DMA of position p + 2 (every 5th)
+#pragma unroll
+            for (int s = 0; s < 81; ++s) {
+                if (s < 38) mf(0, 26 + s, first);
+                else mf(1, s - 38, false);
+                SB();
+                if ((s % 5) == 4 && s / 5 < 16) {
+                    dma(s / 5, cur);
+                    SB();
+                }
+            }
+            advance();
+            SB();
+            // position p + 1 landed; younger than it: this iteration's DMA and, in an item's first K-tile, the
+            // previous item's stores
+            if (t == 0 && stores_young) VMCNT(48);
+            else VMCNT(16);
+            __builtin_amdgcn_s_barrier();
+            SB();
+            // phase 3: 21 MFMAs of k-half 1 beside the 16 reads of k-half 0 of position p + 1 (past the stream's
+            // end: reads of a buffer that holds nothing, unused)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                mf(1, 43 + q, false);
+                SB();
+                rd(0, q, cur ^ 1);
+                SB();
+            }
+#pragma unroll
+            for (int q = 59; q < 64; ++q) mf(1, q, false);
+            SB();
+            ++p;
+        };
+        ktile(0, std::true_type{});
+        for (int t = 1; t < KT; ++t) ktile(t, std::false_type{});
+        // epilogue of this item; acc[i][j][r] = C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r]
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");     // XDL write -> VALU read of the asm MFMAs
+        int z, m0, n0;
+        item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
+        const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
+        const unsigned zc = (unsigned)(z * a.sC * ES);
+        auto epi = [&](float x, int m, bool mok, int n) __attribute__((always_inline)) {
+            const bool in = mok && n < a.N;
+            x *= a.alpha;
+            if (a.beta != 0.f && in) x = fmaf(a.beta, ld(reinterpret_cast<const TC*>(a.C) + (long long)z * a.sC + (long long)m * a.ldc + n), x);
+            x += a.bias_mode == 1 ? (n < a.N ? a.bias[n] : 0.f) : (a.bias_mode == 2 && mok ? a.bias[m] : 0.f);
+            if (a.act == 1) x = gelu_tanh(x);
+            else if (a.act == 2) x = x * gelu_parts(x).cdf;
+            return x;
+        };
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = mw + 16 * i + l15;
+            const bool mok = m < a.M;
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+                const int j0 = 2 * jp, j1 = j0 + 1;
+                f32x4 v0 = acc[i][j0], v1 = acc[i][j1];
+                if (!plain) {
+                    const int n0c = nw + 16 * j0 + 4 * row4, n1c = n0c + 16;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v0[r] = epi(v0[r], m, mok, n0c + r);
+                        v1[r] = epi(v1[r], m, mok, n1c + r);
+                    }
+                }
+                if (OUTF32) {
+                    const int n0c = nw + 16 * j0 + 4 * row4;
+                    const unsigned o0 = (mok && n0c < a.N) ? (unsigned)(((long long)m * a.ldc + n0c) * ES) : 0x80000000u;
+                    const unsigned o1 = (mok && n0c + 16 < a.N) ? (unsigned)(((long long)m * a.ldc + n0c + 16) * ES) : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v0), rC, o0, zc, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v1), rC, o1, zc, 0);
+                } else {
+                    const uint32_t a0 = pack_bf16x2(v0[0], v0[1]), a1 = pack_bf16x2(v0[2], v0[3]);
+                    const uint32_t b0 = pack_bf16x2(v1[0], v1[1]), b1 = pack_bf16x2(v1[2], v1[3]);
+                    const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+                    const int n = nw + 16 * (j0 + (row4 & 1)) + 8 * (row4 >> 1);
+                    const unsigned o = (mok && n < a.N) ? (unsigned)(((long long)m * a.ldc + n) * ES) : 0x80000000u;
+                    const v4u32 d = {s0[0], s1[0], s0[1], s1[1]};
+                    __builtin_amdgcn_raw_buffer_store_b128(d, rC, o, zc, 0);
+                }
+                SB();                           // one column pair at a time (no hoisting of all 256 AGPR reads)
+            }
+        }
+        SB();
+    }
+    VMCNT(0);                                   // the null DMAs past the stream's end land before the LDS is freed
+}
+
+int g_persistent = 1;            // vfm_gemm9_set_mode: 1 persistent (default), 0 one workgroup per tile
+
 template <bool AK, bool BKC, bool OUTF32>
 void launch9(const G9Args& a, int batch, hipStream_t st) {
     static bool attr = false;
@@ -322,6 +564,26 @@ void launch9(const G9Args& a, int batch, hipStream_t st) {
         attr = true;
     }
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
+    if (g_persistent && plain) {
+        static bool attrp = false;
+        if (!attrp) {
+            (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE);
+            attrp = true;
+        }
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (cus <= 0) cus = 256;
+        }
+        const long long total = (long long)nwg * batch;
+        const int grid = (int)std::min<long long>(total, cus);
+        VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32>), dim3(grid), dim3(THREADS), 2 * STAGE, st, a, (int)total);
+        return;
+    }
     VFM_LAUNCH((gemm9_kernel<AK, BKC, OUTF32>), dim3(nwg, batch), dim3(THREADS), 2 * STAGE, st, a);
 }
 
@@ -361,6 +623,12 @@ extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bia
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
     a.spanA = (unsigned)spA; a.spanB = (unsigned)spB;
+    {
+        const int es = out_dtype == VFM_F32 ? 4 : 2;
+        const long long spC = ((long long)(M - 1) * ldc + N + (long long)(batch - 1) * sC) * es;
+        if (spC >= (1LL << 31) || nwg * (long long)batch > 0x7fffffffLL) return VFM_NO_KERNEL;
+        a.spanC = (unsigned)spC;
+    }
     hipStream_t st = (hipStream_t)stream;
     const bool of32 = out_dtype == VFM_F32;
 #define VFM_G9(AK, BK_) of32 ? launch9<AK, BK_, true>(a, batch, st) : launch9<AK, BK_, false>(a, batch, st)
@@ -370,4 +638,12 @@ extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bia
     else VFM_G9(false, false);
 #undef VFM_G9
     return launch_status();
+}
+
+// Kernel form of vfm_gemm9 (A/B switch for microbenchmarks): 1 = persistent (one workgroup per CU walking the
+// output tiles, default), 0 = one workgroup per output tile. Returns the previous setting.
+extern "C" int vfm_gemm9_set_mode(int persistent) {
+    const int prev = g_persistent;
+    g_persistent = persistent ? 1 : 0;
+    return prev;
 }

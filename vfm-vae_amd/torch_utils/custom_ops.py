@@ -132,6 +132,7 @@ SIGNATURES = {
                               c_llp, c_float, c_int, c_vp],
     "vfm_gemm4": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
+    "vfm_gemm9_set_mode": [c_int],
     "vfm_gemm9": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,
