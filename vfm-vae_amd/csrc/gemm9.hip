@@ -47,6 +47,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int BM = 256, BN = 256, BK = 64, THREADS = 256;
 constexpr int OPB = 256 * BK * 2;          // one operand image (32 KB)
 constexpr int STAGE = 2 * OPB;             // A + B of one K-tile (64 KB)
+constexpr int LDS9P = 2 * STAGE + 4096;    // persistent form: + 4 bias slots of 1 KB
 
 struct G9Args {
     const __hip_bfloat16* A;
@@ -82,6 +83,22 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned m0) {
     asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
                  "s"(soff), "s"(m0)
+                 : "memory");
+}
+
+// The same with the per-lane offset voff0 + su formed inside the statement (su: the slot's wave-uniform step):
+// the compiler cannot hoist the 8 slot offsets of an operand out of the K-loop into 8 live VGPRs.
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, unsigned voff0, unsigned su, unsigned m0) {
+    unsigned t;
+    asm volatile("v_add_u32 %0, %1, %2\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %3, 0 offen lds"
+                 : "=&v"(t)
+                 : "v"(voff0), "s"(su), "s"(rsrc), "s"(m0)
+                 : "memory");
+}
+
+// The dword form (4 B per lane: 256 B per wave), for the epilogue's bias values.
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned m0) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(m0)
                  : "memory");
 }
 
@@ -341,7 +358,11 @@ __device__ __forceinline__ void item_tile(int item, int nwg, int total, int tile
     n0 = (rem / rows_g) * BN;
 }
 
-template <bool AK, bool BKC, bool OUTF32>
+// EPI 0: plain C = A B; EPI 1 / 2 / 3: C = act(alpha A B + bias), act = none / tanh-GELU / erf-GELU, with the
+// item's 256 bias values (per column or per
+// row) moved into one of 4 LDS slots by a dword LDS-DMA that rides with every K-tile's 16 operand DMAs (the
+// slot of the cursor's item, so the counted waits cover it and it has landed before the item's epilogue)
+template <bool AK, bool BKC, bool OUTF32, int EPI>
 __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -358,29 +379,34 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     // operand tile's K-tile origin and the same for every item and K-tile; the origin itself moves the buffer
     // descriptor's base (SALU), whose record count is the operand's remaining span, so rows / columns past the
     // operand read in-bounds garbage or zeros that no stored output depends on, and nothing past its end.
-    unsigned voA[8], voB[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        voA[u] = dma_voff<AK>(a.lda, 0, 0x7fffffff, u, tid);
-        voB[u] = dma_voff<BKC>(a.ldb, 0, 0x7fffffff, u, tid);
-    }
-    int d_item = blockIdx.x, d_kt = 0;
+    // slot u of an operand: voff(u) = voff(0) + a wave-uniform step (the swizzle chunk does not depend on u)
+    const unsigned voA0 = dma_voff<AK>(a.lda, 0, 0x7fffffff, 0, tid), voB0 = dma_voff<BKC>(a.ldb, 0, 0x7fffffff, 0, tid);
+    auto ustep = [&](bool kc, long long ld, int u) __attribute__((always_inline)) {
+        return (unsigned)((kc ? 32LL * u * ld : 16LL * (u & 3) * ld + 128 * (u >> 2)) * 2);
+    };
+    int d_item = blockIdx.x, d_kt = 0, d_k = 0;   // d_k: the cursor item's index among this workgroup's items
     long long offA = 0, offB = 0;                 // byte offsets of the cursor's K-tile origin in A / B
+    long long offS = 0;                           // byte offset of the cursor item's bias values
     auto setup_dma = [&](int item) __attribute__((always_inline)) {
         int z, m0, n0;
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
         offA = (z * a.sA + (AK ? (long long)m0 * a.lda : (long long)m0)) * 2;
         offB = (z * a.sB + (BKC ? (long long)n0 * a.ldb : (long long)n0)) * 2;
+        offS = (long long)(a.bias_mode == 2 ? m0 : n0) * 4;
     };
     auto rsrc = [&](const void* base, long long off, long long span) __attribute__((always_inline)) {
         const long long left = span - off;
         return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, (int)(left > 0 ? left : 0),
                                                  0x00020000);
     };
-    __amdgpu_buffer_rsrc_t rA = rsrc(a.A, 0, a.spanA), rB = rsrc(a.B, 0, a.spanB);
+    __amdgpu_buffer_rsrc_t rA = rsrc(a.A, 0, a.spanA), rB = rsrc(a.B, 0, a.spanB), rS = rA;
+    const long long spanS = EPI && a.bias_mode ? (long long)(a.bias_mode == 2 ? a.M : a.N) * 4 : 0;
+    const unsigned sl0 = (unsigned)(size_t)(lds_void*)lds + 2 * STAGE + (unsigned)wave * 256u;
+    const unsigned voS = (unsigned)lane * 4u;
     auto dma = [&](int g, int buf) __attribute__((always_inline)) {
-        if (g < 8) dma16(rA, voA[g], 0u, m0A + buf * STAGE + g * 4096);
-        else dma16(rB, voB[g - 8], 0u, m0A + buf * STAGE + OPB + (g - 8) * 4096);
+        if (g < 8) dma16s(rA, voA0, ustep(AK, a.lda, g), m0A + buf * STAGE + g * 4096);
+        else if (g < 16) dma16s(rB, voB0, ustep(BKC, a.ldb, g - 8), m0A + buf * STAGE + OPB + (g - 8) * 4096);
+        else dma4(rS, voS, sl0 + (unsigned)(d_k & 3) * 1024u);     // the cursor item's bias (EPI 1)
     };
     // descriptors of the cursor's position (after setup_dma / a K-tile step)
     // (past the workgroup's last item: no records, the DMA writes zeros into a buffer nobody reads again)
@@ -388,11 +414,13 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         const bool live = d_item < total;
         rA = rsrc(a.A, offA + (long long)d_kt * dkA, live ? (long long)a.spanA : 0);
         rB = rsrc(a.B, offB + (long long)d_kt * dkB, live ? (long long)a.spanB : 0);
+        if (EPI) rS = rsrc(a.bias, offS, live ? spanS : 0);
     };
     auto advance = [&]() __attribute__((always_inline)) {
         if (++d_kt == KT) {
             d_kt = 0;
             d_item += G;
+            ++d_k;
             if (d_item < total) setup_dma(d_item);
         }
         point();
@@ -400,15 +428,19 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
 
     f32x4 acc[8][8];
     bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+    // lane index as the fragment addresses see it: re-made opaque in every K-tile, so the M/N-contiguous
+    // images' per-block addresses (lane-dependent XOR swizzle) are formed next to their reads instead of
+    // being hoisted out of the K-loop into dozens of live VGPRs
+    int flane = lane;
     auto rd = [&](int h, int r, int buf) __attribute__((always_inline)) {
         const unsigned char* base = lds + buf * STAGE;
         const bool isb = (r == 1) || r >= 9;
         const int idx = r == 0 ? 0 : r == 1 ? 0 : r <= 8 ? r - 1 : r - 8;
         if (!isb) {
-            const bf16x8 v = frag<AK>(base, 8 * wm + idx, h, lane);
+            const bf16x8 v = frag<AK>(base, 8 * wm + idx, h, AK ? lane : flane);
             if (h == 0) fa0[idx] = v; else fa1[idx] = v;
         } else {
-            const bf16x8 v = frag<BKC>(base + OPB, 8 * wn + idx, h, lane);
+            const bf16x8 v = frag<BKC>(base + OPB, 8 * wn + idx, h, BKC ? lane : flane);
             if (h == 0) fb0[idx] = v; else fb1[idx] = v;
         }
     };
@@ -423,19 +455,20 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     constexpr int ES = sizeof(TC);
     const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, (int)a.spanC, 0x00020000);
     constexpr int NST = OUTF32 ? 64 : 32;       // store instructions per wave and item
-    const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
     const int l15 = lane & 15, row4 = lane >> 4;
 
     // prologue: stream positions 0 and 1 in flight, 0 landed, k-half 0 fragments of position 0 read
     setup_dma(d_item);
     point();
+    constexpr int NG = EPI ? 17 : 16;          // DMA instructions per K-tile and wave
 #pragma unroll
-    for (int g = 0; g < 16; ++g) dma(g, 0);
+    for (int g = 0; g < NG; ++g) dma(g, 0);
     advance();
 #pragma unroll
-    for (int g = 0; g < 16; ++g) dma(g, 1);
+    for (int g = 0; g < NG; ++g) dma(g, 1);
     advance();
-    VMCNT(16);
+    if (EPI) VMCNT(17);
+    else VMCNT(16);
     __builtin_amdgcn_s_barrier();
     SB();
 #pragma unroll
@@ -443,12 +476,14 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     SB();
 
     int p = 0;                                  // stream position (buffer p & 1)
+    int item_k = 0;                             // index of the item among this workgroup's items (bias slot)
     for (int item = blockIdx.x; item < total; item += G) {
         const bool stores_young = item != (int)blockIdx.x && !OUTF32;
         // one K-tile (first: the item's first, whose k-half-0 MFMAs define the accumulators)
         auto ktile = [&](int t, auto first_c) __attribute__((always_inline)) {
             constexpr bool first = decltype(first_c)::value;
             const int cur = p & 1;
+            if (!AK || !BKC) asm volatile("" : "+v"(flane));
             // phase 1: 26 MFMAs of k-half 0 beside the 16 reads of k-half 1
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
@@ -469,7 +504,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                 if (s < 38) mf(0, 26 + s, first);
                 else mf(1, s - 38, false);
                 SB();
-                if ((s % 5) == 4 && s / 5 < 16) {
+                if ((s % 5) == 4 && s / 5 < NG) {
                     dma(s / 5, cur);
                     SB();
                 }
@@ -478,8 +513,13 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             SB();
             // position p + 1 landed; younger than it: this iteration's DMA and, in an item's first K-tile, the
             // previous item's stores
-            if (t == 0 && stores_young) VMCNT(48);
-            else VMCNT(16);
+            if (EPI) {
+                if (t == 0 && stores_young) VMCNT(49);
+                else VMCNT(17);
+            } else {
+                if (t == 0 && stores_young) VMCNT(48);
+                else VMCNT(16);
+            }
             __builtin_amdgcn_s_barrier();
             SB();
             // phase 3: 21 MFMAs of k-half 1 beside the 16 reads of k-half 0 of position p + 1 (past the stream's
@@ -504,29 +544,35 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
         const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
         const unsigned zc = (unsigned)(z * a.sC * ES);
-        auto epi = [&](float x, int m, bool mok, int n) __attribute__((always_inline)) {
-            const bool in = mok && n < a.N;
-            x *= a.alpha;
-            if (a.beta != 0.f && in) x = fmaf(a.beta, ld(reinterpret_cast<const TC*>(a.C) + (long long)z * a.sC + (long long)m * a.ldc + n), x);
-            x += a.bias_mode == 1 ? (n < a.N ? a.bias[n] : 0.f) : (a.bias_mode == 2 && mok ? a.bias[m] : 0.f);
-            if (a.act == 1) x = gelu_tanh(x);
-            else if (a.act == 2) x = x * gelu_parts(x).cdf;
+        const float* bsl = reinterpret_cast<const float*>(lds + 2 * STAGE + (item_k & 3) * 1024);
+        auto act = [&](float x) __attribute__((always_inline)) {
+            if (EPI == 2) x = gelu_tanh(x);
+            else if (EPI == 3) x = x * gelu_parts(x).cdf;
             return x;
         };
+        // the slot holds the item's 256 bias values (zeros without a bias): per column or per row, selected
+        // by scalar factors (no per-element branches)
+        const float fcol = a.bias_mode == 1 ? 1.f : 0.f, frow = a.bias_mode == 2 ? 1.f : 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = mw + 16 * i + l15;
-            const bool mok = m < a.M;
+        for (int jp = 0; jp < 4; ++jp) {
+            const int j0 = 2 * jp, j1 = j0 + 1;
+            const int c0 = 128 * wn + 16 * j0 + 4 * row4;          // tile-local column of v0[0] (v1: + 16)
+            f32x4 bc0 = {}, bc1 = {};
+            if (EPI) {
+                bc0 = *reinterpret_cast<const f32x4*>(bsl + c0) * fcol;
+                bc1 = *reinterpret_cast<const f32x4*>(bsl + c0 + 16) * fcol;
+            }
 #pragma unroll
-            for (int jp = 0; jp < 4; ++jp) {
-                const int j0 = 2 * jp, j1 = j0 + 1;
+            for (int i = 0; i < 8; ++i) {
+                const int m = mw + 16 * i + l15;
+                const bool mok = m < a.M;
                 f32x4 v0 = acc[i][j0], v1 = acc[i][j1];
-                if (!plain) {
-                    const int n0c = nw + 16 * j0 + 4 * row4, n1c = n0c + 16;
+                if (EPI) {
+                    const float br = bsl[128 * wm + 16 * i + l15] * frow;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        v0[r] = epi(v0[r], m, mok, n0c + r);
-                        v1[r] = epi(v1[r], m, mok, n1c + r);
+                        v0[r] = act(fmaf(a.alpha, v0[r], bc0[r] + br));
+                        v1[r] = act(fmaf(a.alpha, v1[r], bc1[r] + br));
                     }
                 }
                 if (OUTF32) {
@@ -538,6 +584,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                 } else {
                     const uint32_t a0 = pack_bf16x2(v0[0], v0[1]), a1 = pack_bf16x2(v0[2], v0[3]);
                     const uint32_t b0 = pack_bf16x2(v1[0], v1[1]), b1 = pack_bf16x2(v1[2], v1[3]);
+                    // rows (16-lane groups) 1 and 3 of (a0, a1) <-> rows 0 and 2 of (b0, b1): each lane then holds 8
+                    // consecutive columns (a0 a1 b0 b1) of block j0 (rows 0, 2) or j1 (rows 1, 3)
                     const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
                     const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
                     const int n = nw + 16 * (j0 + (row4 & 1)) + 8 * (row4 >> 1);
@@ -545,9 +593,10 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                     const v4u32 d = {s0[0], s1[0], s0[1], s1[1]};
                     __builtin_amdgcn_raw_buffer_store_b128(d, rC, o, zc, 0);
                 }
-                SB();                           // one column pair at a time (no hoisting of all 256 AGPR reads)
+                SB();                           // one block pair at a time (no hoisting of all 256 AGPR reads)
             }
         }
+        ++item_k;
         SB();
     }
     VMCNT(0);                                   // the null DMAs past the stream's end land before the LDS is freed
@@ -565,11 +614,13 @@ void launch9(const G9Args& a, int batch, hipStream_t st) {
     }
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
-    if (g_persistent && plain) {
+    if (g_persistent && a.beta == 0.f) {
         static bool attrp = false;
         if (!attrp) {
-            (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE);
+            (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+            (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+            (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+            (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
             attrp = true;
         }
         static int cus = 0;
@@ -581,7 +632,14 @@ void launch9(const G9Args& a, int batch, hipStream_t st) {
         }
         const long long total = (long long)nwg * batch;
         const int grid = (int)std::min<long long>(total, cus);
-        VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32>), dim3(grid), dim3(THREADS), 2 * STAGE, st, a, (int)total);
+        if (plain)
+            VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32, 0>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+        else if (a.act == 0)
+            VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32, 1>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+        else if (a.act == 1)
+            VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32, 2>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+        else
+            VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32, 3>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
         return;
     }
     VFM_LAUNCH((gemm9_kernel<AK, BKC, OUTF32>), dim3(nwg, batch), dim3(THREADS), 2 * STAGE, st, a);
