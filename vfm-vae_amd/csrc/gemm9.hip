@@ -504,8 +504,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                 if (s < 38) mf(0, 26 + s, first);
                 else mf(1, s - 38, false);
                 SB();
-                if ((s % 5) == 4 && s / 5 < NG) {
+                if ((s % 5) == 4 && s / 5 < 16) {
                     dma(s / 5, cur);
+                    SB();
+                }
+                if (NG > 16 && s == 80) {        // the bias DMA (EPI > 0) after the operands'
+                    dma(16, cur);
                     SB();
                 }
             }
