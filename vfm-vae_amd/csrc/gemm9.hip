@@ -402,7 +402,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     __amdgpu_buffer_rsrc_t rA = rsrc(a.A, 0, a.spanA), rB = rsrc(a.B, 0, a.spanB), rS = rA;
     const long long spanS = EPI && a.bias_mode ? (long long)(a.bias_mode == 2 ? a.M : a.N) * 4 : 0;
     const unsigned sl0 = (unsigned)(size_t)(lds_void*)lds + 2 * STAGE + (unsigned)wave * 256u;
-    const unsigned voS = (unsigned)lane * 4u;
+    const unsigned voS = (unsigned)tid * 4u;          // wave w: values 64 w .. 64 w + 63 of the slot
     auto dma = [&](int g, int buf) __attribute__((always_inline)) {
         if (g < 8) dma16s(rA, voA0, ustep(AK, a.lda, g), m0A + buf * STAGE + g * 4096);
         else if (g < 16) dma16s(rB, voB0, ustep(BKC, a.ldb, g - 8), m0A + buf * STAGE + OPB + (g - 8) * 4096);
