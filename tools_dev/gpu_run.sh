@@ -72,6 +72,10 @@ for s in "$@"; do
     g8sched) timeout -k 10 300 python tools_dev/g8sched.py > $out/g8sched.log 2>&1 ;;
     g8k) timeout -k 10 300 python tools_dev/g8ksweep.py > $out/g8k.log 2>&1 && G8_DEEP=0 timeout -k 10 300 python tools_dev/g8ksweep.py > $out/g8k0.log 2>&1 ;;
     g8pmc1) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS --kernel-include-regex gemm8_kernel -d $out/p1 -o run --output-format csv -- python3 tools_dev/g8one.py > $out/p1.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum --kernel-include-regex gemm8_kernel -d $out/p2 -o run --output-format csv -- python3 tools_dev/g8one.py > $out/p2.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex gemm8_kernel -d $out/p3 -o run --output-format csv -- python3 tools_dev/g8one.py > $out/p3.log 2>&1 ;;
+    g9pmc) for kd in g9 blas; do
+             G8_KIND=$kd G8_K=8192 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS -d $out/p1_$kd -o run --output-format csv -- python3 tools_dev/g8one.py > $out/p1_$kd.log 2>&1 || exit 1
+             G8_KIND=$kd G8_K=8192 timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT -d $out/p2_$kd -o run --output-format csv -- python3 tools_dev/g8one.py > $out/p2_$kd.log 2>&1 || exit 1
+           done ;;
     g8st) timeout -k 10 300 python tools_dev/g8stamps.py > $out/g8st.log 2>&1 ;;
     mlpbench) timeout -k 10 300 python tools_dev/mlpbench.py > $out/mlpbench.log 2>&1 ;;
     gc1) timeout -k 10 400 python tools_dev/graph_c1.py > $out/gc1.log 2>&1 && GC1_NORM=mm timeout -k 10 400 python tools_dev/graph_c1.py > $out/gc1_mm.log 2>&1 ;;

@@ -112,10 +112,16 @@ def _planar(t3, stream):
     return dst, off, n
 
 
+BF16_OWN = __import__("os").environ.get("VFM_BF16_GEMM", "hip") == "hip"
+
+
 def preferred(A, M, N, reduce_batch=False):
-    """Where this kernel family is routed (tools_dev/gemmbench.py, MI355X): fp32 operands (the
-    fp32-equivalent split at >= 128-wide tiles, and the batch-reduced weight gradients at any
-    width). bf16 operands stay on hipBLASLt (0.69-0.88 PF/s here vs 1.2-1.45 PF/s)."""
+    """Where this kernel family is routed (tools_dev/gemmbench.py, tools_dev/g4bench.py, MI355X): fp32
+    operands (the fp32-equivalent split at >= 128-wide tiles, and the batch-reduced weight gradients at
+    any width); bf16 operands on the LDS-DMA one-wave-per-SIMD kernel (csrc/gemm9.hip) at >= 128-wide
+    outputs (VFM_BF16_GEMM=torch: hipBLASLt, for A/B)."""
+    if A.dtype == torch.bfloat16:
+        return BF16_OWN and not reduce_batch and M >= 128 and N >= 128
     if A.dtype != torch.float32:
         return False
     return reduce_batch or (M >= 128 and N >= 128)
@@ -132,6 +138,8 @@ def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
         registers and fills the chip with 4x the tiles (6304x384x1536: 95 us vs 101 us for the best
         256-tile split-K);
       * otherwise the 256-tile kernel."""
+    if dtype == torch.bfloat16 and not reduce_batch and splits <= 1 and K % 64 == 0:
+        return "g9", 0
     if not FAST or K % 64:
         return "g128", splits
     nterm = 1 if dtype == torch.bfloat16 else (6 if custom_ops.f32_precision()[1] == 3 else 3)

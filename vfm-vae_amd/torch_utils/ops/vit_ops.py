@@ -6,8 +6,8 @@ under bf16 autocast: GEMMs in the compute dtype with fp32 accumulation,
 LayerNorm and residual stream in fp32.
 
 bf16 GEMMs (the SigLIP2 tower under autocast) run on our 256-tile MFMA GEMM on ROCm tensors outside
-autograd (csrc/gemm8.hip), with the bias and fc1's tanh-GELU (the form SigLIP uses) in the epilogue;
-elsewhere (and with VFM_VIT_GEMM=torch) they are hipBLASLt GEMMs through torch.matmul / addmm.
+autograd (csrc/gemm9.hip), with the bias and fc1's tanh-GELU (the form SigLIP uses) in the epilogue;
+with VFM_VIT_GEMM=torch they are hipBLASLt GEMMs through torch.matmul / addmm (A/B).
 fp32 linears (the DINO ViT-S tower of the projected discriminator, whose input gradient
 the G phase takes) run on our GEMM with fp32-equivalent f32x6 products and autograd
 (torch_utils/ops/linear.py). LayerNorm -> compute dtype (optionally fused with the
@@ -20,10 +20,9 @@ import torch.nn.functional as F
 
 from . import kernel_timer
 
-# bf16 linears of the frozen towers on our 256-tile GEMM (csrc/gemm8.hip, bias / bias + tanh-GELU in
-# the epilogue) with VFM_VIT_GEMM=hip; off by default while gemm8 measures 0.72-0.82x hipBLASLt on the
-# SigLIP2 shapes (profiles/r3_j_gemm8_shapes.txt)
-OWN_GEMM = os.environ.get("VFM_VIT_GEMM", "torch") == "hip"
+# bf16 linears of the frozen towers on our 256-tile GEMM (csrc/gemm9.hip, bias / bias + tanh-GELU in the
+# epilogue); VFM_VIT_GEMM=torch: hipBLASLt (A/B)
+OWN_GEMM = os.environ.get("VFM_VIT_GEMM", "hip") == "hip"
 
 
 def frozen_weight(w, dtype):
@@ -47,7 +46,7 @@ def _own_linear(x, w, b, act=None):
     from .decoder_hip import _cast_cached
     bias = None if b is None else _cast_cached(_cast_cached(b, x.dtype), torch.float32)
     x2 = x.reshape(-1, x.shape[-1])
-    y = gemm_hip.try_gemm(x2, w.t(), bias=bias, bias_dim=1, act=act, route=("g8", 0))
+    y = gemm_hip.try_gemm(x2, w.t(), bias=bias, bias_dim=1, act=act, route=("g9", 0))
     return None if y is None else y.reshape(*x.shape[:-1], w.shape[0])
 
 
