@@ -417,6 +417,16 @@ int vfm_gemm4(const void* A, const void* B, void* C, const float* bias, int out_
 int vfm_gemm9(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
               int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
               long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
+/* vfm_gemm9 with K splits and / or the batch reduction C = alpha sum_z A[z] B[z] (reduce_batch; C [M, N], row
+ * stride ldc): the decoder's bf16 1x1 weight gradients dW = sum_b dY[b] X[b]^T (reference
+ * networks/utils/convnext_utils.py:135-138, :241-249 under autocast; torch computes them as per-sample
+ * fp32 products summed over the batch). S = min(splits, batch K / 64) chunks of the batch-concatenated
+ * reduction write fp32 partials into `workspace` (vfm_gemm9_workspace_floats), combined in a fixed order
+ * (deterministic). Plain products (no bias / activation); VFM_NO_KERNEL when not covered. */
+int vfm_gemm9_ex(const void* A, const void* B, void* C, int out_dtype, int M, int N, int K, int batch, int a_kcont,
+                 long long lda, long long sA, int b_kcont, long long ldb, long long sB, long long ldc, float alpha,
+                 float* workspace, int splits, int reduce_batch, void* stream);
+long long vfm_gemm9_workspace_floats(int M, int N, int K, int batch, int splits, int reduce_batch);
 /* Kernel form of vfm_gemm9 (process-wide A/B switch for microbenchmarks): 1 = persistent (one workgroup per CU
  * walking the output tiles as one K-tile stream; default), 0 = one workgroup per output tile. Returns the
  * previous setting. */

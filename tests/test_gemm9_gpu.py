@@ -126,3 +126,19 @@ def test_gemm9_persistent_many_items_bitwise_stable():
     assert torch.equal(outs[0], outs[1])
     for b in (0, 13, 31):
         assert _rel(outs[0][b], W.float() @ x[b].float()) < 8e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("O,I,P,z", [(2048, 512, 4096, 32), (256, 1024, 16384, 4), (512, 256, 1024, 3)])
+@pytest.mark.parametrize("out_f32", [True, False])
+def test_gemm9_batch_reduced_weight_grad(O, I, P, z, out_f32):
+    """dW = sum_b dY[b] X[b]^T (the decoder's bf16 1x1 weight gradient) on gemm9's batch-reduced split-K
+    (fp32 partials, fixed-order combine): against fp32 (2e-5 of max for fp32 C), deterministic."""
+    g = torch.Generator().manual_seed(O + P + z)
+    dy, x = _rnd(z, O, P, g=g), _rnd(z, I, P, g=g)
+    od = torch.float32 if out_f32 else torch.bfloat16
+    outs = [gemm_hip.try_gemm(dy, x.transpose(1, 2), reduce_batch=True, out_dtype=od, auto=True) for _ in range(2)]
+    assert outs[0] is not None and outs[0].shape == (O, I)
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.einsum("bop,bip->oi", dy.float(), x.float())
+    assert _rel(outs[0], ref) < (2e-5 if out_f32 else 8e-3)

@@ -59,6 +59,10 @@ struct G9Args {
     float alpha, beta;
     int bias_mode, act;
     unsigned spanA, spanB, spanC;     // buffer-descriptor ranges in bytes (< 2^31, checked on the host)
+    // batch-reduced split-K (persistent form): the K-tiles of all Z batches form one reduction of V = Z KTz
+    // K-tiles cut into S chunks of kchunk; item (tile, chunk s) writes its fp32 partial to C[s] (the
+    // workspace, sC = M N), gemm9_reduce sums the S partials in a fixed order
+    int reduce, S, kchunk, KTz;
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -362,6 +366,18 @@ __device__ __forceinline__ void item_tile(int item, int nwg, int total, int tile
 // item's 256 bias values (per column or per
 // row) moved into one of 4 LDS slots by a dword LDS-DMA that rides with every K-tile's 16 operand DMAs (the
 // slot of the cursor's item, so the counted waits cover it and it has landed before the item's epilogue)
+// K range of an item: its batch's KT K-tiles, or (reduce) chunk s = z of the batch-concatenated reduction
+__device__ __forceinline__ void item_k_range(const G9Args& a, int z, int KT, int& v0, int& n) {
+    if (a.reduce) {
+        const int V = a.KTz * a.reduce;
+        v0 = z * a.kchunk;
+        n = min(V, v0 + a.kchunk) - v0;
+    } else {
+        v0 = 0;
+        n = KT;
+    }
+}
+
 template <bool AK, bool BKC, bool OUTF32, int EPI>
 __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -385,13 +401,16 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         return (unsigned)((kc ? 32LL * u * ld : 16LL * (u & 3) * ld + 128 * (u >> 2)) * 2);
     };
     int d_item = blockIdx.x, d_kt = 0, d_k = 0;   // d_k: the cursor item's index among this workgroup's items
-    long long offA = 0, offB = 0;                 // byte offsets of the cursor's K-tile origin in A / B
+    int d_KT = KT, d_v0 = 0, d_z = 0;             // the cursor item's K-tiles, first reduction K-tile, batch
+    long long offA = 0, offB = 0;                 // byte offsets of the cursor item's tile origin in A / B
     long long offS = 0;                           // byte offset of the cursor item's bias values
     auto setup_dma = [&](int item) __attribute__((always_inline)) {
         int z, m0, n0;
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
-        offA = (z * a.sA + (AK ? (long long)m0 * a.lda : (long long)m0)) * 2;
-        offB = (z * a.sB + (BKC ? (long long)n0 * a.ldb : (long long)n0)) * 2;
+        offA = (AK ? (long long)m0 * a.lda : (long long)m0) * 2;
+        offB = (BKC ? (long long)n0 * a.ldb : (long long)n0) * 2;
+        d_z = z;
+        item_k_range(a, z, KT, d_v0, d_KT);
         offS = (long long)(a.bias_mode == 2 ? m0 : n0) * 4;
     };
     auto rsrc = [&](const void* base, long long off, long long span) __attribute__((always_inline)) {
@@ -412,12 +431,18 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     // (past the workgroup's last item: no records, the DMA writes zeros into a buffer nobody reads again)
     auto point = [&]() __attribute__((always_inline)) {
         const bool live = d_item < total;
-        rA = rsrc(a.A, offA + (long long)d_kt * dkA, live ? (long long)a.spanA : 0);
-        rB = rsrc(a.B, offB + (long long)d_kt * dkB, live ? (long long)a.spanB : 0);
+        int zt = d_z, kk = d_kt;
+        if (a.reduce) {                         // reduction K-tile v -> (batch, K-tile of that batch)
+            const int v = d_v0 + d_kt;
+            zt = v / a.KTz;
+            kk = v - zt * a.KTz;
+        }
+        rA = rsrc(a.A, offA + (zt * a.sA + (long long)kk * (dkA / 2)) * 2, live ? (long long)a.spanA : 0);
+        rB = rsrc(a.B, offB + (zt * a.sB + (long long)kk * (dkB / 2)) * 2, live ? (long long)a.spanB : 0);
         if (EPI) rS = rsrc(a.bias, offS, live ? spanS : 0);
     };
     auto advance = [&]() __attribute__((always_inline)) {
-        if (++d_kt == KT) {
+        if (++d_kt == d_KT) {
             d_kt = 0;
             d_item += G;
             ++d_k;
@@ -478,7 +503,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     int p = 0;                                  // stream position (buffer p & 1)
     int item_k = 0;                             // index of the item among this workgroup's items (bias slot)
     for (int item = blockIdx.x; item < total; item += G) {
-        const bool stores_young = item != (int)blockIdx.x && !OUTF32;
+        const bool stores_young = item != (int)blockIdx.x;
         // one K-tile (first: the item's first, whose k-half-0 MFMAs define the accumulators)
         auto ktile = [&](int t, auto first_c) __attribute__((always_inline)) {
             constexpr bool first = decltype(first_c)::value;
@@ -517,12 +542,22 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             SB();
             // position p + 1 landed; younger than it: this iteration's DMA and, in an item's first K-tile, the
             // previous item's stores
+            // (fp32 C: 64 stores + 16 DMA younger than the awaited ones exceed vmcnt's 63; waiting for 63 still
+            // retires every older operation)
             if (EPI) {
-                if (t == 0 && stores_young) VMCNT(49);
-                else VMCNT(17);
+                if (t == 0 && stores_young) {
+                    if (OUTF32) VMCNT(63);
+                    else VMCNT(49);
+                } else {
+                    VMCNT(17);
+                }
             } else {
-                if (t == 0 && stores_young) VMCNT(48);
-                else VMCNT(16);
+                if (t == 0 && stores_young) {
+                    if (OUTF32) VMCNT(63);
+                    else VMCNT(48);
+                } else {
+                    VMCNT(16);
+                }
             }
             __builtin_amdgcn_s_barrier();
             SB();
@@ -541,7 +576,13 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             ++p;
         };
         ktile(0, std::true_type{});
-        for (int t = 1; t < KT; ++t) ktile(t, std::false_type{});
+        int iKT, iv0;
+        {
+            int z_, m0_, n0_;
+            item_tile(item, nwg, total, tiles_m, tiles_n, z_, m0_, n0_);
+            item_k_range(a, z_, KT, iv0, iKT);
+        }
+        for (int t = 1; t < iKT; ++t) ktile(t, std::false_type{});
         // epilogue of this item; acc[i][j][r] = C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r]
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");     // XDL write -> VALU read of the asm MFMAs
         int z, m0, n0;
@@ -606,6 +647,25 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     VMCNT(0);                                   // the null DMAs past the stream's end land before the LDS is freed
 }
 
+// C = alpha sum_s ws[s] (fixed order), fp32 or bf16 C (row stride ldc): the batch-reduced split-K's combine
+template <bool OUTF32>
+__global__ __launch_bounds__(256) void gemm9_reduce(const float* __restrict__ ws, void* C, int M, int N, long long ldc,
+                                                    int S, float alpha) {
+    const long long MN = (long long)M * N;
+    for (long long i4 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i4 < MN; i4 += (long long)gridDim.x * 1024) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(ws + i4);
+        for (int k = 1; k < S; ++k) v += *reinterpret_cast<const f32x4*>(ws + k * MN + i4);
+        v *= alpha;
+        const int m = (int)(i4 / N), n = (int)(i4 - (long long)m * N);
+        if (OUTF32) {
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + m * ldc + n) = v;
+        } else {
+            const uint2 b = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+            *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(C) + m * ldc + n) = b;
+        }
+    }
+}
+
 int g_persistent = 1;            // vfm_gemm9_set_mode: 1 persistent (default), 0 one workgroup per tile
 
 template <bool AK, bool BKC, bool OUTF32>
@@ -634,7 +694,7 @@ void launch9(const G9Args& a, int batch, hipStream_t st) {
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (cus <= 0) cus = 256;
         }
-        const long long total = (long long)nwg * batch;
+        const long long total = (long long)nwg * (a.reduce ? a.S : batch);
         const int grid = (int)std::min<long long>(total, cus);
         if (plain)
             VFM_LAUNCH((gemm9p_kernel<AK, BKC, OUTF32, 0>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
@@ -664,9 +724,10 @@ long long span9(int kcont, long long outer, long long kdim, long long ld, long l
 // given as N rows of K, stride ldb; else K rows of N). bias_mode 0 none / 1 per column / 2 per row;
 // act 0 none / 1 tanh-GELU / 2 erf-GELU; out_dtype VFM_BF16 or VFM_F32. Returns VFM_NO_KERNEL for shapes
 // it does not take (K % 64, N % 8, unaligned operands, > 2 GiB spans).
-extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
-                         int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream) {
+static int gemm9_impl(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+                      int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+                      long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, float* workspace,
+                      int splits, int reduce_batch, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
     if (out_dtype != VFM_BF16 && out_dtype != VFM_F32) return VFM_NO_KERNEL;
     if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || act < 0 || act > 2) return VFM_ERR_ARGS;
@@ -685,14 +746,42 @@ extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bia
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
     a.spanA = (unsigned)spA; a.spanB = (unsigned)spB;
+    hipStream_t st = (hipStream_t)stream;
+    const bool of32 = out_dtype == VFM_F32;
+    if (reduce_batch || splits > 1) {
+        // batch-reduced (and / or K-split) product: fp32 partials of S chunks into the workspace, then the
+        // fixed-order combine into C (plain epilogue, alpha only)
+        if (!workspace || beta != 0.f || bias_mode || act || !g_persistent) return VFM_NO_KERNEL;
+        if (!reduce_batch && batch != 1) return VFM_NO_KERNEL;
+        const int KTz = K / BK, V = KTz * batch;
+        const int S = std::max(1, std::min(splits, V));
+        a.reduce = batch;
+        a.KTz = KTz;
+        a.kchunk = (V + S - 1) / S;
+        a.S = (V + a.kchunk - 1) / a.kchunk;
+        const long long MN = (long long)M * N;
+        if (MN * a.S * 4 >= (1LL << 31) || MN % 4) return VFM_NO_KERNEL;
+        G9Args p = a;
+        p.C = workspace; p.ldc = N; p.sC = MN; p.alpha = 1.f;
+        p.spanC = (unsigned)(MN * a.S * 4);
+        p.bias = nullptr; p.bias_mode = 0; p.act = 0;
+#define VFM_G9R(AK, BK_) launch9<AK, BK_, true>(p, 1, st)
+        if (a_kcont && b_kcont) VFM_G9R(true, true);
+        else if (a_kcont && !b_kcont) VFM_G9R(true, false);
+        else if (!a_kcont && b_kcont) VFM_G9R(false, true);
+        else VFM_G9R(false, false);
+#undef VFM_G9R
+        const int blocks = (int)std::min<long long>((MN / 4 + 255) / 256, 4096);
+        if (of32) VFM_LAUNCH(gemm9_reduce<true>, dim3(blocks), dim3(256), 0, st, workspace, C, M, N, ldc, a.S, alpha);
+        else VFM_LAUNCH(gemm9_reduce<false>, dim3(blocks), dim3(256), 0, st, workspace, C, M, N, ldc, a.S, alpha);
+        return launch_status();
+    }
     {
-        const int es = out_dtype == VFM_F32 ? 4 : 2;
+        const int es = of32 ? 4 : 2;
         const long long spC = ((long long)(M - 1) * ldc + N + (long long)(batch - 1) * sC) * es;
         if (spC >= (1LL << 31) || nwg * (long long)batch > 0x7fffffffLL) return VFM_NO_KERNEL;
         a.spanC = (unsigned)spC;
     }
-    hipStream_t st = (hipStream_t)stream;
-    const bool of32 = out_dtype == VFM_F32;
 #define VFM_G9(AK, BK_) of32 ? launch9<AK, BK_, true>(a, batch, st) : launch9<AK, BK_, false>(a, batch, st)
     if (a_kcont && b_kcont) VFM_G9(true, true);
     else if (a_kcont && !b_kcont) VFM_G9(true, false);
@@ -700,6 +789,38 @@ extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bia
     else VFM_G9(false, false);
 #undef VFM_G9
     return launch_status();
+}
+
+// bf16 operands: C[z] (M x N, ldc, batch stride sC) = epi(alpha A[z] B[z] + beta C[z]) with A [M, K]
+// (a_kcont: K-contiguous rows of stride lda, else M-contiguous rows of K) and B [K, N] (b_kcont: B is
+// given as N rows of K, stride ldb; else K rows of N). bias_mode 0 none / 1 per column / 2 per row;
+// act 0 none / 1 tanh-GELU / 2 erf-GELU; out_dtype VFM_BF16 or VFM_F32. Returns VFM_NO_KERNEL for shapes
+// it does not take (K % 64, N % 8, unaligned operands, > 2 GiB spans).
+extern "C" int vfm_gemm9(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
+                         int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+                         long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream) {
+    return gemm9_impl(A, B, C, bias, out_dtype, M, N, K, batch, a_kcont, lda, sA, b_kcont, ldb, sB, ldc, sC, alpha,
+                      beta, bias_mode, act, nullptr, 1, 0, stream);
+}
+
+// vfm_gemm9 with K splits and / or the batch reduction C = alpha sum_z A[z] B[z] (reduce_batch; C is [M, N]):
+// S = min(splits, Z K/64) chunks of the batch-concatenated reduction, fp32 partials in `workspace`
+// (vfm_gemm9_workspace_floats), combined in a fixed order. Plain products only (beta 0, no bias / act).
+extern "C" int vfm_gemm9_ex(const void* A, const void* B, void* C, int out_dtype, int M, int N, int K, int batch,
+                            int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
+                            long long ldc, float alpha, float* workspace, int splits, int reduce_batch, void* stream) {
+    return gemm9_impl(A, B, C, nullptr, out_dtype, M, N, K, batch, a_kcont, lda, sA, b_kcont, ldb, sB, ldc, 0, alpha,
+                      0.f, 0, 0, workspace, splits, reduce_batch, stream);
+}
+
+// fp32 workspace floats vfm_gemm9_ex needs (M N S); -1 when the shapes are not covered
+extern "C" long long vfm_gemm9_workspace_floats(int M, int N, int K, int batch, int splits, int reduce_batch) {
+    if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || K % BK) return -1;
+    const int V = (K / BK) * (reduce_batch ? batch : 1);
+    const int S0 = std::max(1, std::min(splits, V));
+    const int kc = (V + S0 - 1) / S0;
+    const int S = (V + kc - 1) / kc;
+    return (long long)M * N * S;
 }
 
 // Kernel form of vfm_gemm9 (A/B switch for microbenchmarks): 1 = persistent (one workgroup per CU walking the

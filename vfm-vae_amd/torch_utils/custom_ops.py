@@ -133,6 +133,9 @@ SIGNATURES = {
     "vfm_gemm4": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm9_set_mode": [c_int],
+    "vfm_gemm9_ex": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll, c_ll,
+                     c_float, c_vp, c_int, c_int, c_vp],
+    "vfm_gemm9_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm9": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,
@@ -223,6 +226,7 @@ def get_native():
                 fn.restype = c_int
             lib.vfm_version.restype = ctypes.c_char_p
             lib.vfm_bnl_workspace_floats.restype = c_ll
+            lib.vfm_gemm9_workspace_floats.restype = c_ll
             lib.vfm_channel_rms_norm_rows.restype = c_ll
             lib.vfm_specnorm_workspace_floats.restype = c_ll
             lib.vfm_dwconv2d_fwd_mfma_units.restype = c_ll

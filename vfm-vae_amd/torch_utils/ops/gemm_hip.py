@@ -115,13 +115,29 @@ def _planar(t3, stream):
 BF16_OWN = __import__("os").environ.get("VFM_BF16_GEMM", "hip") == "hip"
 
 
+_WS = {}
+
+
+def _workspace(n, dev):
+    """fp32 scratch of at least n floats per (device, stream), reused by that stream's split-K products,
+    which it orders (grown on demand; a HIP-graph capture gets a buffer of its own, kept alive by the
+    graph's allocation)."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    w = _WS.get(key)
+    if w is None or w.numel() < n or torch.cuda.is_current_stream_capturing():
+        w = torch.empty(n, dtype=torch.float32, device=dev)
+        if not torch.cuda.is_current_stream_capturing():
+            _WS[key] = w
+    return w
+
+
 def preferred(A, M, N, reduce_batch=False):
     """Where this kernel family is routed (tools_dev/gemmbench.py, tools_dev/g4bench.py, MI355X): fp32
     operands (the fp32-equivalent split at >= 128-wide tiles, and the batch-reduced weight gradients at
     any width); bf16 operands on the LDS-DMA one-wave-per-SIMD kernel (csrc/gemm9.hip) at >= 128-wide
     outputs (VFM_BF16_GEMM=torch: hipBLASLt, for A/B)."""
     if A.dtype == torch.bfloat16:
-        return BF16_OWN and not reduce_batch and M >= 128 and N >= 128
+        return BF16_OWN and M >= 128 and N >= 128
     if A.dtype != torch.float32:
         return False
     return reduce_batch or (M >= 128 and N >= 128)
@@ -138,8 +154,13 @@ def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
         registers and fills the chip with 4x the tiles (6304x384x1536: 95 us vs 101 us for the best
         256-tile split-K);
       * otherwise the 256-tile kernel."""
-    if dtype == torch.bfloat16 and not reduce_batch and splits <= 1 and K % 64 == 0:
-        return "g9", 0
+    if dtype == torch.bfloat16 and K % 64 == 0:
+        if reduce_batch:
+            # batch-reduced weight gradients (few output tiles over a deep reduction): ~2 items per CU
+            tiles = -(-M // 256) * -(-N // 256)
+            return "g9r", max(1, min(-(-512 // tiles), z * (K // 64) // 4))
+        if splits <= 1:
+            return "g9", 0
     if not FAST or K % 64:
         return "g128", splits
     nterm = 1 if dtype == torch.bfloat16 else (6 if custom_ops.f32_precision()[1] == 3 else 3)
@@ -193,7 +214,7 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             return out
     if auto and not preferred(A, M, N, reduce_batch):
         return None
-    if auto and splits == 1:
+    if auto and splits == 1 and A.dtype != torch.bfloat16:
         # few output tiles over a deep reduction (weight gradients of token-major linears):
         # split K so the grid covers the 256 CUs several times (128-tile kernel)
         tiles = -(-M // 128) * -(-N // 128) * z
@@ -233,6 +254,23 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     stream = custom_ops.stream_ptr(A.device)
     kern, arg = route or _plan(A.dtype, M, N, K, z, reduce_batch, splits, auto)
     tb = lambda v: "true" if v else "false"
+    if kern == "g9r" and A.dtype == torch.bfloat16:
+        # batch-reduced / K-split product on gemm9 (fp32 partials of arg chunks + fixed-order combine)
+        S = max(1, int(arg))
+        n = _lib.vfm_gemm9_workspace_floats(M, N, K, z, S, int(reduce_batch))
+        if n > 0 and (reduce_batch or z == 1) and beta == 0.0 and bias is None and act is None:
+            ws = _workspace(n, A.device)
+            region = f"gemm9<bf16,{tb(a_kc)},{tb(b_kc)},true>r"
+            if kernel_timer.SHAPES:
+                region += f"[{M}x{N}x{K}x{z}s{S}]"
+            with kernel_timer.region(region, nbytes, flops, "mfma"):
+                rc = _lib.vfm_gemm9_ex(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), _CODES[out_dtype], M, N, K, z,
+                                       int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, float(alpha), ws.data_ptr(), S,
+                                       int(reduce_batch), stream)
+            if rc != custom_ops.VFM_NO_KERNEL:
+                custom_ops.check(rc, "vfm_gemm9_ex")
+                return out
+        kern, arg = "g8", 0
     if kern == "g9" and A.dtype == torch.bfloat16 and not reduce_batch:
         # one wave per SIMD, 128 x 128 per wave, LDS-DMA staging two K-tiles ahead (csrc/gemm9.hip)
         region = f"gemm9<bf16,{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
