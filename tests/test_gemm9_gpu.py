@@ -142,3 +142,25 @@ def test_gemm9_batch_reduced_weight_grad(O, I, P, z, out_f32):
     assert torch.equal(outs[0], outs[1])
     ref = torch.einsum("bop,bip->oi", dy.float(), x.float())
     assert _rel(outs[0], ref) < (2e-5 if out_f32 else 8e-3)
+
+
+@pytest.mark.gpu
+def test_gemm9_operands_past_2gib():
+    """The b5 ConvNeXt layer's data gradient dm = W1^T dh at batch 32: dh is [32, 512, 65536] bf16 = 2 GiB, past
+    a buffer descriptor's 31-bit record count. The persistent form moves 64-bit descriptor bases per K-tile and
+    output slice; checked against fp32 on the first, a middle and the last sample (where a 32-bit offset would
+    wrap), and the batch-reduced weight gradient over the same planes."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    z, C, O, P = 32, 128, 512, 65536
+    W1 = (torch.rand(O, C, generator=g, device=DEV) * 2 - 1).to(torch.bfloat16)
+    dh = (torch.rand(z, O, P, generator=g, device=DEV) * 2 - 1).to(torch.bfloat16)
+    dm = gemm_hip.try_gemm(W1.t(), dh, route=("g9", 0))
+    assert dm is not None and dm.shape == (z, C, P)
+    for b in (0, 17, z - 1):
+        assert _rel(dm[b], W1.t().float() @ dh[b].float()) < 8e-3
+    m = (torch.rand(z, C, P, generator=g, device=DEV) * 2 - 1).to(torch.bfloat16)
+    dw = gemm_hip.try_gemm(dh, m.transpose(1, 2), reduce_batch=True, out_dtype=torch.float32, auto=True)
+    ref = torch.zeros(O, C, device=DEV)
+    for b in range(z):
+        ref += dh[b].float() @ m[b].float().t()
+    assert dw is not None and _rel(dw, ref) < 2e-5

@@ -1,5 +1,5 @@
 """Frozen-tower bf16 linears on our 256-tile GEMM (torch_utils/ops/vit_ops.py `_own_linear`,
-csrc/gemm8.hip) against the plain PyTorch fp32 reference of the same op (reference
+csrc/gemm9.hip) against the plain PyTorch fp32 reference of the same op (reference
 networks/utils/vfms/siglip2_utils.py:114-137: q/k/v/out projections, fc1 + tanh-GELU, fc2 under bf16
 autocast). Tolerance: one bf16 output rounding of an fp32-accumulated product plus the bias rounded to
 bf16 first (hipBLASLt's bias epilogue): 8e-3 of max |ref|."""
@@ -23,7 +23,7 @@ def test_own_linear_matches_fp32(M, N, K, act, monkeypatch):
     with torch.no_grad():
         y = vit_ops.linear_gelu_tanh(x, w, b) if act else vit_ops.linear(x, w, b)
     torch.cuda.synchronize()
-    assert any(k.startswith("gemm8<") for k in kernel_timer.summary())
+    assert any(k.startswith("gemm9<") for k in kernel_timer.summary())
     kernel_timer.enable(False)
     ref = x.float() @ w.float().t() + b.to(torch.bfloat16).float()
     if act:

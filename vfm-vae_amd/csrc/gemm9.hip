@@ -58,7 +58,7 @@ struct G9Args {
     int M, N, K;
     float alpha, beta;
     int bias_mode, act;
-    unsigned spanA, spanB, spanC;     // buffer-descriptor ranges in bytes (< 2^31, checked on the host)
+    long long spanA, spanB, spanC;    // operand / output spans in bytes (the one-tile-per-workgroup form: < 2^31)
     // batch-reduced split-K (persistent form): the K-tiles of all Z batches form one reduction of V = Z KTz
     // K-tiles cut into S chunks of kchunk; item (tile, chunk s) writes its fp32 partial to C[s] (the
     // workspace, sC = M N), gemm9_reduce sums the S partials in a fixed order
@@ -414,8 +414,10 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         offS = (long long)(a.bias_mode == 2 ? m0 : n0) * 4;
     };
     auto rsrc = [&](const void* base, long long off, long long span) __attribute__((always_inline)) {
+        // 64-bit base, record count clamped to 31 bits: a tile's accesses from its origin stay far below that
         const long long left = span - off;
-        return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, (int)(left > 0 ? left : 0),
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0,
+                                                 (int)(left > 0 ? (left < 0x7fffffffLL ? left : 0x7fffffffLL) : 0),
                                                  0x00020000);
     };
     __amdgpu_buffer_rsrc_t rA = rsrc(a.A, 0, a.spanA), rB = rsrc(a.B, 0, a.spanB), rS = rA;
@@ -478,9 +480,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     // C through a buffer descriptor: out-of-range lanes store to an offset past its records (dropped)
     typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
     constexpr int ES = sizeof(TC);
-    const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, (int)a.spanC, 0x00020000);
+
     constexpr int NST = OUTF32 ? 64 : 32;       // store instructions per wave and item
-    const int l15 = lane & 15, row4 = lane >> 4;
 
     // prologue: stream positions 0 and 1 in flight, 0 landed, k-half 0 fragments of position 0 read
     setup_dma(d_item);
@@ -585,10 +586,17 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         for (int t = 1; t < iKT; ++t) ktile(t, std::false_type{});
         // epilogue of this item; acc[i][j][r] = C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r]
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");     // XDL write -> VALU read of the asm MFMAs
+        // lane-derived epilogue values from an opaque lane index: formed here, not hoisted into registers that
+        // stay live through the K-loop
+        int elane = lane;
+        asm volatile("" : "+v"(elane));
+        const int l15 = elane & 15, row4 = elane >> 4;
         int z, m0, n0;
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
         const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
-        const unsigned zc = (unsigned)(z * a.sC * ES);
+        // the output batch's slice through its own descriptor (64-bit base): tile offsets stay 32-bit
+        const __amdgpu_buffer_rsrc_t rC = rsrc(a.C, z * a.sC * ES, a.spanC);
+        const unsigned zc = 0u;
         const float* bsl = reinterpret_cast<const float*>(lds + 2 * STAGE + (item_k & 3) * 1024);
         auto act = [&](float x) __attribute__((always_inline)) {
             if (EPI == 2) x = gelu_tanh(x);
@@ -713,8 +721,7 @@ long long span9(int kcont, long long outer, long long kdim, long long ld, long l
     const long long rows = kcont ? outer : kdim;
     const long long cols = kcont ? kdim : outer;
     const long long e = (rows - 1) * ld + cols + (long long)(batch - 1) * sb;
-    const long long bytes = e * 2;
-    return bytes >= (1LL << 31) ? -1 : bytes;
+    return e * 2;
 }
 
 }  // namespace
@@ -738,14 +745,17 @@ static int gemm9_impl(const void* A, const void* B, void* C, const float* bias, 
     if (lda < (a_kcont ? (long long)K : M) || ldb < (b_kcont ? (long long)K : N) || ldc < N) return VFM_ERR_ARGS;
     const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (nwg > 0x7fffffffLL) return VFM_ERR_ARGS;
-    const long long spA = span9(a_kcont, M, K, lda, sA, batch);
-    const long long spB = span9(b_kcont, N, K, ldb, sB, batch);
-    if (spA < 0 || spB < 0) return VFM_NO_KERNEL;
+    // spans in bytes; the persistent form moves 64-bit descriptor bases and needs only one batch element's
+    // tile offsets below 2^31, the one-workgroup-per-tile form the whole operand
+    const long long spA = span9(a_kcont, M, K, lda, sA, batch), spB = span9(b_kcont, N, K, ldb, sB, batch);
+    const long long spA1 = span9(a_kcont, M, K, lda, 0, 1), spB1 = span9(b_kcont, N, K, ldb, 0, 1);
+    if (spA1 >= (1LL << 31) || spB1 >= (1LL << 31)) return VFM_NO_KERNEL;
+    if (!g_persistent && (spA >= (1LL << 31) || spB >= (1LL << 31))) return VFM_NO_KERNEL;
     G9Args a{};
     a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
-    a.spanA = (unsigned)spA; a.spanB = (unsigned)spB;
+    a.spanA = spA; a.spanB = spB;
     hipStream_t st = (hipStream_t)stream;
     const bool of32 = out_dtype == VFM_F32;
     if (reduce_batch || splits > 1) {
@@ -760,10 +770,10 @@ static int gemm9_impl(const void* A, const void* B, void* C, const float* bias, 
         a.kchunk = (V + S - 1) / S;
         a.S = (V + a.kchunk - 1) / a.kchunk;
         const long long MN = (long long)M * N;
-        if (MN * a.S * 4 >= (1LL << 31) || MN % 4) return VFM_NO_KERNEL;
+        if (MN * 4 >= (1LL << 31) || MN % 4) return VFM_NO_KERNEL;
         G9Args p = a;
         p.C = workspace; p.ldc = N; p.sC = MN; p.alpha = 1.f;
-        p.spanC = (unsigned)(MN * a.S * 4);
+        p.spanC = MN * a.S * 4;
         p.bias = nullptr; p.bias_mode = 0; p.act = 0;
 #define VFM_G9R(AK, BK_) launch9<AK, BK_, true>(p, 1, st)
         if (a_kcont && b_kcont) VFM_G9R(true, true);
@@ -778,9 +788,11 @@ static int gemm9_impl(const void* A, const void* B, void* C, const float* bias, 
     }
     {
         const int es = of32 ? 4 : 2;
-        const long long spC = ((long long)(M - 1) * ldc + N + (long long)(batch - 1) * sC) * es;
-        if (spC >= (1LL << 31) || nwg * (long long)batch > 0x7fffffffLL) return VFM_NO_KERNEL;
-        a.spanC = (unsigned)spC;
+        const long long spC1 = ((long long)(M - 1) * ldc + N) * es;
+        const long long spC = spC1 + (long long)(batch - 1) * sC * es;
+        if (spC1 >= (1LL << 31) || nwg * (long long)batch > 0x7fffffffLL) return VFM_NO_KERNEL;
+        if (!g_persistent && spC >= (1LL << 31)) return VFM_NO_KERNEL;
+        a.spanC = spC;
     }
 #define VFM_G9(AK, BK_) of32 ? launch9<AK, BK_, true>(a, batch, st) : launch9<AK, BK_, false>(a, batch, st)
     if (a_kcont && b_kcont) VFM_G9(true, true);
