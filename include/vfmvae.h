@@ -427,6 +427,17 @@ int vfm_gemm9_ex(const void* A, const void* B, void* C, int out_dtype, int M, in
                  long long lda, long long sA, int b_kcont, long long ldb, long long sB, long long ldc, float alpha,
                  float* workspace, int splits, int reduce_batch, void* stream);
 long long vfm_gemm9_workspace_floats(int M, int N, int K, int batch, int splits, int reduce_batch);
+/* The ConvNeXt MLP's bf16 1x1 GEMMs on the persistent gemm9 kernel with the GELU in the epilogue (replaces
+ * pwconv1 -> nn.GELU and the GELU backward of reference networks/utils/convnext_utils.py:135-142 under
+ * autocast): C[z] = W[M, K] X[z][K, N] (W K-contiguous, lda; X N-contiguous, ldb, batch stride sB);
+ * mode 1: C = h (may be null), C2 = g = bf16(GELU(bf16(h) s + b1)); mode 2: dg = bf16(acc),
+ * dz = dg GELU'(h s + b1) with h read from H, C = dh = bf16(dz s), per-row partial sums of dz h (rsum0,
+ * may be null) and dz (rsum1) at [batch][vfm_gemm9_gelu_parts(N)][M]. rscale [batch][M] (null: 1),
+ * bias [M] (null: 0); C, C2, H share (ldc, sC). */
+int vfm_gemm9_gelu(const void* W, const void* X, void* C, void* C2, const void* H, const float* rscale,
+                   const float* bias, float* rsum0, float* rsum1, int mode, int M, int N, int K, int batch,
+                   long long lda, long long ldb, long long sB, long long ldc, long long sC, void* stream);
+int vfm_gemm9_gelu_parts(int N);
 /* Kernel form of vfm_gemm9 (process-wide A/B switch for microbenchmarks): 1 = persistent (one workgroup per CU
  * walking the output tiles as one K-tile stream; default), 0 = one workgroup per output tile. Returns the
  * previous setting. */

@@ -1,4 +1,4 @@
-"""ConvNeXt-MLP GEMMs with the GELU in the epilogue (csrc/gemm8.hip vfm_gemm8_gelu) against the plain
+"""ConvNeXt-MLP GEMMs with the GELU in the epilogue (csrc/gemm9.hip vfm_gemm9_gelu) against the plain
 PyTorch fp32 reference of the same ops (reference networks/utils/convnext_utils.py:135-142:
 pwconv1 -> GELU(h * s + b1) -> ..., and its backward).
 
@@ -8,7 +8,7 @@ against GELU of OUR h (the epilogue's own arithmetic, exact-erf GELU to ~1e-7): 
 rounding). dh / the row sums are compared against an fp32 chain fed with a bf16-rounded dg:
 8e-3 / 2e-3 (sums over hundreds of columns of terms that carry one bf16 rounding each).
 The layer test runs the fused autograd Function against the unfused chain of HIP ops
-(hipBLASLt 1x1s + scale_bias_gelu + layer_scale_residual) at the two widths it serves (C = 256, 512)."""
+(gemm9 1x1s + scale_bias_gelu + layer_scale_residual) at the two widths it serves (C = 256, 512)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -70,7 +70,7 @@ def test_gemm_gelu_backward(O, C, P, B, with_s):
 
 @pytest.mark.parametrize("C,H", [(256, 32), (512, 16)])
 def test_convnext_mlp_gemm_layer_matches_unfused(C, H):
-    """Fused (gemm8 + GELU epilogues) vs unfused HIP chain, forward output and every gradient."""
+    """Fused (gemm9 + GELU epilogues) vs unfused HIP chain, forward output and every gradient."""
     from torch_utils.ops import decoder_hip
     assert C in decoder_hip.GEMM_MLP_TESTED
     g0 = torch.Generator().manual_seed(C)

@@ -128,6 +128,8 @@ def test_kernel_timer_rocprof_names():
     assert kt.rocprof_name("gemm<bf16,false,true,false>[4x8x16x1]") == "gemm_kernel<false, true, 1, false, 4>"
     assert kt.rocprof_name("gemm8<f32x6,true,true,true>") == "gemm8_kernel<true, true, true, false, 0>"
     assert kt.rocprof_name("gemm8_gelu<2>") == "gemm8_kernel<true, false, false, false, 2>"
+    assert kt.rocprof_name("gemm9_gelu<2>") == "gemm9p_kernel<true, false, false, 5>"
+    assert kt.rocprof_name("gemm9<bf16,true,false,false>[64x64x64x1]").startswith("gemm9p_kernel<true, false, false, ")
     assert kt.rocprof_name("conv3x3_nhwc<f32x6,128>") == "conv3x3_kernel<256, 128, 3>"
     assert kt.rocprof_name("conv3x3_nhwc<f32x3,64>") == "conv3x3_kernel<128, 64, 2>"
     assert kt.rocprof_name("conv3x3_nhwc<f32x6,64>") == "conv3x3_kernel<128, 64, 3>"

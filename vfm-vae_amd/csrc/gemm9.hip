@@ -47,7 +47,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int BM = 256, BN = 256, BK = 64, THREADS = 256;
 constexpr int OPB = 256 * BK * 2;          // one operand image (32 KB)
 constexpr int STAGE = 2 * OPB;             // A + B of one K-tile (64 KB)
-constexpr int LDS9P = 2 * STAGE + 4096;    // persistent form: + 4 bias slots of 1 KB
+constexpr int LDS9P = 2 * STAGE + 8192;    // persistent form: + 4 epilogue slots of 2 KB
 
 struct G9Args {
     const __hip_bfloat16* A;
@@ -63,6 +63,14 @@ struct G9Args {
     // K-tiles cut into S chunks of kchunk; item (tile, chunk s) writes its fp32 partial to C[s] (the
     // workspace, sC = M N), gemm9_reduce sums the S partials in a fixed order
     int reduce, S, kchunk, KTz;
+    // ConvNeXt-MLP GELU epilogues (EPI 4 / 5, bf16 C; see the epilogue): second output C2 (g), aux input H
+    // (h, C's layout), per-(batch, row) scale rscale [Z][M] (null: 1), bias per row, and per-row partial sums
+    // rs0 / rs1 [Z][2 tiles_n][M] of the backward (rs0 may be null)
+    void* C2;
+    const __hip_bfloat16* H;
+    const float* rscale;
+    float* rs0;
+    float* rs1;
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -366,6 +374,140 @@ __device__ __forceinline__ void item_tile(int item, int nwg, int total, int tile
 // item's 256 bias values (per column or per
 // row) moved into one of 4 LDS slots by a dword LDS-DMA that rides with every K-tile's 16 operand DMAs (the
 // slot of the cursor's item, so the counted waits cover it and it has landed before the item's epilogue)
+// ConvNeXt-MLP GELU epilogues (reference networks/utils/convnext_utils.py:135-142: pwconv1 -> GELU ->
+// pwconv2 with the modulation scale s[b, o] and bias b1[o] of channel o = GEMM row; the roundings of the
+// separate scale_bias_gelu kernels, csrc/decoder.hip gelu_fwd / gelu_bwd):
+//   EPI 4 (forward):  h = bf16(acc) -> C (when non-null); g = bf16(GELU(h s + b1)) -> C2;
+//   EPI 5 (backward): dg = bf16(acc); dz = dg GELU'(h s + b1) with h read from H; dh = bf16(dz s) -> C; per-row
+//                     sums of dz h and dz over the wave's 128 columns -> rs0 / rs1 at [z][2 tn + wn][m].
+// Row values (b1, s) come from the item's LDS slot; every wave issues a fixed number of buffer stores
+// (out-of-range lanes and a null output: offsets past the descriptor's records, dropped), which the
+// counted waits of the next item's first K-tile rely on.
+template <int EPI>
+__device__ __forceinline__ void gelu_epilogue9(const G9Args& a, const f32x4 (&acc)[8][8], const float* bsl,
+                                               __amdgpu_buffer_rsrc_t rC, int z, int m0, int n0, int wm, int wn,
+                                               int l15, int row4, int tiles_n) {
+    auto rsrc2 = [&](const void* base, long long off, long long span) __attribute__((always_inline)) {
+        const long long left = base ? span - off : 0;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (base ? off : 0)), 0,
+                                                 (int)(left > 0 ? (left < 0x7fffffffLL ? left : 0x7fffffffLL) : 0),
+                                                 0x00020000);
+    };
+    const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
+    const bool hasS = a.rscale != nullptr;
+    const long long zoff = (long long)z * a.sC * 2;
+    const __amdgpu_buffer_rsrc_t rC2 = rsrc2(a.C2, zoff, a.spanC);
+    const __amdgpu_buffer_rsrc_t rH = rsrc2(a.H, zoff, a.spanC);
+    const long long nparts = 2LL * tiles_n;
+    const long long pbase = ((long long)z * nparts + 2 * (n0 / BN) + wn) * a.M;
+    const __amdgpu_buffer_rsrc_t rP0 = rsrc2(a.rs0, pbase * 4, (long long)a.M * 4 * nparts * (z + 1));
+    const __amdgpu_buffer_rsrc_t rP1 = rsrc2(a.rs1, pbase * 4, (long long)a.M * 4 * nparts * (z + 1));
+    // H prefetch one row block ahead (EPI 5): the lane's 4 + 4 columns of blocks j0, j1 for each column pair
+    uint2 hn[4][2];
+    // (unconditional loads: rows / columns past C read garbage of the same slice or zeros past its end -- the
+    // masked dz ignores them -- and no select in the address lets the compiler sink a load into a branch)
+    auto load_h = [&](int i, uint2 (&hv)[4][2]) __attribute__((always_inline)) {
+        const unsigned ob = (unsigned)((mw + 16 * i + l15) * a.ldc + nw + 4 * row4) * 2u;
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+            hv[jp][0] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rH, ob + 64u * jp, 0, 0));
+            hv[jp][1] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rH, ob + 64u * jp + 32u, 0, 0));
+        }
+    };
+    if (EPI == 5) load_h(0, hn);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int ml = 128 * wm + 16 * i + l15;
+        const int m = m0 + ml;
+        const bool mok = m < a.M;
+        const float b1v = bsl[ml], scv = hasS ? bsl[256 + ml] : 1.f;
+        uint2 hc[4][2];
+        if (EPI == 5) {
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+                hc[jp][0] = hn[jp][0];
+                hc[jp][1] = hn[jp][1];
+            }
+            if (i < 7) load_h(i + 1, hn);
+        }
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+            const int j0 = 2 * jp, j1 = j0 + 1;
+            const int n0c = nw + 16 * j0 + 4 * row4;
+            const f32x4 v0 = acc[i][j0], v1 = acc[i][j1];
+            uint32_t pa[2], pb[2], qa[2], qb[2];        // bf16 pairs of blocks j0 (a) / j1 (b): C, C2 outputs
+            if (EPI == 4) {
+                float h0[4], h1[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    h0[r] = __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(unsigned short, __float2bfloat16(v0[r])) << 16);
+                    h1[r] = __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(unsigned short, __float2bfloat16(v1[r])) << 16);
+                }
+                float g0[4], g1[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float z0 = fmaf(h0[r], scv, b1v), z1 = fmaf(h1[r], scv, b1v);
+                    g0[r] = z0 * gelu_parts(z0).cdf;
+                    g1[r] = z1 * gelu_parts(z1).cdf;
+                }
+                pa[0] = pack_bf16x2(h0[0], h0[1]); pa[1] = pack_bf16x2(h0[2], h0[3]);
+                pb[0] = pack_bf16x2(h1[0], h1[1]); pb[1] = pack_bf16x2(h1[2], h1[3]);
+                qa[0] = pack_bf16x2(g0[0], g0[1]); qa[1] = pack_bf16x2(g0[2], g0[3]);
+                qb[0] = pack_bf16x2(g1[0], g1[1]); qb[1] = pack_bf16x2(g1[2], g1[3]);
+            } else {
+                float d0[4], d1[4];
+                const uint32_t hw[4] = {hc[jp][0].x, hc[jp][0].y, hc[jp][1].x, hc[jp][1].y};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float dg0 = __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(unsigned short, __float2bfloat16(v0[r])) << 16);
+                    const float dg1 = __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(unsigned short, __float2bfloat16(v1[r])) << 16);
+                    const uint32_t w0 = hw[r >> 1], w1 = hw[2 + (r >> 1)];
+                    const float hv0 = __builtin_bit_cast(float, (r & 1) ? (w0 & 0xffff0000u) : (w0 << 16));
+                    const float hv1 = __builtin_bit_cast(float, (r & 1) ? (w1 & 0xffff0000u) : (w1 << 16));
+                    const GeluParts gp0 = gelu_parts(fmaf(hv0, scv, b1v)), gp1 = gelu_parts(fmaf(hv1, scv, b1v));
+                    float dz0 = dg0 * (gp0.cdf + gp0.zpdf), dz1 = dg1 * (gp1.cdf + gp1.zpdf);
+                    if (!mok || n0c + r >= a.N) dz0 = 0.f;
+                    if (!mok || n0c + 16 + r >= a.N) dz1 = 0.f;
+                    s0 = fmaf(dz0, hv0, s0);
+                    s1 += dz0;
+                    s0 = fmaf(dz1, hv1, s0);
+                    s1 += dz1;
+                    d0[r] = dz0 * scv;
+                    d1[r] = dz1 * scv;
+                }
+                pa[0] = pack_bf16x2(d0[0], d0[1]); pa[1] = pack_bf16x2(d0[2], d0[3]);
+                pb[0] = pack_bf16x2(d1[0], d1[1]); pb[1] = pack_bf16x2(d1[2], d1[3]);
+            }
+            const int n = nw + 16 * (j0 + (row4 & 1)) + 8 * (row4 >> 1);
+            const unsigned o = (mok && n < a.N) ? (unsigned)(((long long)m * a.ldc + n) * 2) : 0x80000000u;
+            {
+                const auto x0 = __builtin_amdgcn_permlane16_swap(pa[0], pb[0], false, false);
+                const auto x1 = __builtin_amdgcn_permlane16_swap(pa[1], pb[1], false, false);
+                const v4u32 d = {x0[0], x1[0], x0[1], x1[1]};
+                __builtin_amdgcn_raw_buffer_store_b128(d, rC, o, 0, 0);
+            }
+            if (EPI == 4) {
+                const auto x0 = __builtin_amdgcn_permlane16_swap(qa[0], qb[0], false, false);
+                const auto x1 = __builtin_amdgcn_permlane16_swap(qa[1], qb[1], false, false);
+                const v4u32 d = {x0[0], x1[0], x0[1], x1[1]};
+                __builtin_amdgcn_raw_buffer_store_b128(d, rC2, o, 0, 0);
+            }
+        }
+        if (EPI == 5) {
+            // the 4 lanes of a row (l >> 4 = 0..3): xor 16, 32 (fixed order, identical on every lane)
+            s0 += __shfl_xor(s0, 16);
+            s1 += __shfl_xor(s1, 16);
+            s0 += __shfl_xor(s0, 32);
+            s1 += __shfl_xor(s1, 32);
+            const unsigned po = (row4 == 0 && mok) ? (unsigned)((long long)m * 4) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s0), rP0, po, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s1), rP1, po, 0, 0);
+        }
+        SB();
+    }
+}
+
 // K range of an item: its batch's KT K-tiles, or (reduce) chunk s = z of the batch-concatenated reduction
 __device__ __forceinline__ void item_k_range(const G9Args& a, int z, int KT, int& v0, int& n) {
     if (a.reduce) {
@@ -403,7 +545,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     int d_item = blockIdx.x, d_kt = 0, d_k = 0;   // d_k: the cursor item's index among this workgroup's items
     int d_KT = KT, d_v0 = 0, d_z = 0;             // the cursor item's K-tiles, first reduction K-tile, batch
     long long offA = 0, offB = 0;                 // byte offsets of the cursor item's tile origin in A / B
-    long long offS = 0;                           // byte offset of the cursor item's bias values
+    long long offS = 0, offR = 0;                 // byte offsets of the cursor item's bias values / row scales
     auto setup_dma = [&](int item) __attribute__((always_inline)) {
         int z, m0, n0;
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
@@ -411,7 +553,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         offB = (BKC ? (long long)n0 * a.ldb : (long long)n0) * 2;
         d_z = z;
         item_k_range(a, z, KT, d_v0, d_KT);
-        offS = (long long)(a.bias_mode == 2 ? m0 : n0) * 4;
+        offS = (long long)(a.bias_mode == 1 ? n0 : m0) * 4;
+        offR = ((long long)z * a.M + m0) * 4;
     };
     auto rsrc = [&](const void* base, long long off, long long span) __attribute__((always_inline)) {
         // 64-bit base, record count clamped to 31 bits: a tile's accesses from its origin stay far below that
@@ -421,13 +564,18 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                                                  0x00020000);
     };
     __amdgpu_buffer_rsrc_t rA = rsrc(a.A, 0, a.spanA), rB = rsrc(a.B, 0, a.spanB), rS = rA;
-    const long long spanS = EPI && a.bias_mode ? (long long)(a.bias_mode == 2 ? a.M : a.N) * 4 : 0;
+    // epilogue slot of an item (2 KB): [0, 1 KB) its 256 bias values (per column or per row, zeros without a
+    // bias), [1 KB, 2 KB) its 256 row scales (EPI 4 / 5, rscale of the item's batch)
+    const long long spanS = EPI && a.bias ? (long long)(a.bias_mode == 1 ? a.N : a.M) * 4 : 0;
+    const long long spanR = EPI >= 4 && a.rscale ? (long long)a.M * 4 * (a.reduce ? 1 : 1) : 0;
+    __amdgpu_buffer_rsrc_t rR = rA;
     const unsigned sl0 = (unsigned)(size_t)(lds_void*)lds + 2 * STAGE + (unsigned)wave * 256u;
     const unsigned voS = (unsigned)tid * 4u;          // wave w: values 64 w .. 64 w + 63 of the slot
     auto dma = [&](int g, int buf) __attribute__((always_inline)) {
         if (g < 8) dma16s(rA, voA0, ustep(AK, a.lda, g), m0A + buf * STAGE + g * 4096);
         else if (g < 16) dma16s(rB, voB0, ustep(BKC, a.ldb, g - 8), m0A + buf * STAGE + OPB + (g - 8) * 4096);
-        else dma4(rS, voS, sl0 + (unsigned)(d_k & 3) * 1024u);     // the cursor item's bias (EPI 1)
+        else if (g == 16) dma4(rS, voS, sl0 + (unsigned)(d_k & 3) * 2048u);          // the cursor item's bias
+        else dma4(rR, voS, sl0 + (unsigned)(d_k & 3) * 2048u + 1024u);               // and row scales (EPI 4 / 5)
     };
     // descriptors of the cursor's position (after setup_dma / a K-tile step)
     // (past the workgroup's last item: no records, the DMA writes zeros into a buffer nobody reads again)
@@ -442,6 +590,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         rA = rsrc(a.A, offA + (zt * a.sA + (long long)kk * (dkA / 2)) * 2, live ? (long long)a.spanA : 0);
         rB = rsrc(a.B, offB + (zt * a.sB + (long long)kk * (dkB / 2)) * 2, live ? (long long)a.spanB : 0);
         if (EPI) rS = rsrc(a.bias, offS, live ? spanS : 0);
+        if (EPI >= 4) rR = rsrc(a.rscale, offR, live ? (long long)d_z * a.M * 4 + spanR : 0);
     };
     auto advance = [&]() __attribute__((always_inline)) {
         if (++d_kt == d_KT) {
@@ -486,14 +635,15 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     // prologue: stream positions 0 and 1 in flight, 0 landed, k-half 0 fragments of position 0 read
     setup_dma(d_item);
     point();
-    constexpr int NG = EPI ? 17 : 16;          // DMA instructions per K-tile and wave
+    constexpr int NG = EPI >= 4 ? 18 : EPI ? 17 : 16;    // DMA instructions per K-tile and wave
 #pragma unroll
     for (int g = 0; g < NG; ++g) dma(g, 0);
     advance();
 #pragma unroll
     for (int g = 0; g < NG; ++g) dma(g, 1);
     advance();
-    if (EPI) VMCNT(17);
+    if (EPI >= 4) VMCNT(18);
+    else if (EPI) VMCNT(17);
     else VMCNT(16);
     __builtin_amdgcn_s_barrier();
     SB();
@@ -534,8 +684,9 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                     dma(s / 5, cur);
                     SB();
                 }
-                if (NG > 16 && s == 80) {        // the bias DMA (EPI > 0) after the operands'
+                if (NG > 16 && s == 80) {        // the slot DMAs (EPI > 0) after the operands'
                     dma(16, cur);
+                    if (NG > 17) dma(17, cur);
                     SB();
                 }
             }
@@ -545,7 +696,10 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             // previous item's stores
             // (fp32 C: 64 stores + 16 DMA younger than the awaited ones exceed vmcnt's 63; waiting for 63 still
             // retires every older operation)
-            if (EPI) {
+            if (EPI >= 4) {                     // 64 (h, g) / 48 (dh, row sums) stores: past 63 with the DMA
+                if (t == 0 && stores_young) VMCNT(63);
+                else VMCNT(18);
+            } else if (EPI) {
                 if (t == 0 && stores_young) {
                     if (OUTF32) VMCNT(63);
                     else VMCNT(49);
@@ -597,7 +751,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         // the output batch's slice through its own descriptor (64-bit base): tile offsets stay 32-bit
         const __amdgpu_buffer_rsrc_t rC = rsrc(a.C, z * a.sC * ES, a.spanC);
         const unsigned zc = 0u;
-        const float* bsl = reinterpret_cast<const float*>(lds + 2 * STAGE + (item_k & 3) * 1024);
+        const float* bsl = reinterpret_cast<const float*>(lds + 2 * STAGE + (item_k & 3) * 2048);
         auto act = [&](float x) __attribute__((always_inline)) {
             if (EPI == 2) x = gelu_tanh(x);
             else if (EPI == 3) x = x * gelu_parts(x).cdf;
@@ -606,6 +760,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         // the slot holds the item's 256 bias values (zeros without a bias): per column or per row, selected
         // by scalar factors (no per-element branches)
         const float fcol = a.bias_mode == 1 ? 1.f : 0.f, frow = a.bias_mode == 2 ? 1.f : 0.f;
+        if (EPI >= 4) {
+            gelu_epilogue9<EPI>(a, acc, bsl, rC, z, m0, n0, wm, wn, l15, row4, tiles_n);
+            ++item_k;
+            SB();
+            continue;
+        }
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
             const int j0 = 2 * jp, j1 = j0 + 1;
@@ -834,6 +994,58 @@ extern "C" long long vfm_gemm9_workspace_floats(int M, int N, int K, int batch, 
     const int S = (V + kc - 1) / kc;
     return (long long)M * N * S;
 }
+
+// ConvNeXt-MLP 1x1 GEMMs with the GELU epilogues (gelu_epilogue9), bf16 operands and outputs, on the persistent
+// kernel: C[z] = W[M, K] X[z][K, N] with W K-contiguous (lda), X N-contiguous (ldb, batch stride sB);
+// mode 1: C = h (may be null), C2 = g = GELU(h s + b1); mode 2: C = dh from acc = dg and H = h,
+// rsum0 (may be null) / rsum1 = [batch][vfm_gemm9_gelu_parts(N)][M] partial sums.
+// rscale [batch][M] (null: 1), bias [M] (null: 0). C, C2, H share (ldc, sC).
+extern "C" int vfm_gemm9_gelu(const void* W, const void* X, void* C, void* C2, const void* H, const float* rscale,
+                              const float* bias, float* rsum0, float* rsum1, int mode, int M, int N, int K, int batch,
+                              long long lda, long long ldb, long long sB, long long ldc, long long sC, void* stream) {
+    if (!W || !X || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
+    if (mode == 1 ? !C2 : (mode == 2 ? (!C || !H || !rsum1) : true)) return VFM_ERR_ARGS;
+    if (K % BK || K % 8 || N % 8 || M % 8 || lda % 8 || ldb % 8 || sB % 8 || ldc % 8 || sC % 8) return VFM_NO_KERNEL;
+    if (((uintptr_t)W | (uintptr_t)X | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)H) % 16) return VFM_NO_KERNEL;
+    if (lda < K || ldb < N || ldc < N) return VFM_ERR_ARGS;
+    if (span9(1, M, K, lda, 0, 1) >= (1LL << 31) || span9(0, N, K, ldb, 0, 1) >= (1LL << 31) ||
+        ((long long)(M - 1) * ldc + N) * 2 >= (1LL << 31))
+        return VFM_NO_KERNEL;
+    const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (nwg * batch > 0x7fffffffLL) return VFM_ERR_ARGS;
+    G9Args a{};
+    a.A = (const __hip_bfloat16*)W; a.B = (const __hip_bfloat16*)X; a.C = C; a.C2 = C2;
+    a.H = (const __hip_bfloat16*)H; a.rscale = rscale; a.bias = bias; a.rs0 = rsum0; a.rs1 = rsum1;
+    a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = 0; a.sB = sB; a.sC = sC;
+    a.M = M; a.N = N; a.K = K; a.alpha = 1.f; a.beta = 0.f; a.bias_mode = 0; a.act = 0;
+    a.spanA = span9(1, M, K, lda, 0, 1);
+    a.spanB = span9(0, N, K, ldb, sB, batch);
+    a.spanC = ((long long)(M - 1) * ldc + N + (long long)(batch - 1) * sC) * 2;
+    hipStream_t st = (hipStream_t)stream;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm9p_kernel<true, false, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+        (void)hipFuncSetAttribute((const void*)gemm9p_kernel<true, false, false, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+        attr = true;
+    }
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    const long long total = nwg * batch;
+    const int grid = (int)std::min<long long>(total, cus);
+    if (mode == 1)
+        VFM_LAUNCH((gemm9p_kernel<true, false, false, 4>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+    else
+        VFM_LAUNCH((gemm9p_kernel<true, false, false, 5>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+    return launch_status();
+}
+
+// Partial-sum slots per (batch, row) of vfm_gemm9_gelu mode 2 for N columns.
+extern "C" int vfm_gemm9_gelu_parts(int N) { return N <= 0 ? -1 : 2 * ((N + BN - 1) / BN); }
 
 // Kernel form of vfm_gemm9 (A/B switch for microbenchmarks): 1 = persistent (one workgroup per CU walking the
 // output tiles, default), 0 = one workgroup per output tile. Returns the previous setting.

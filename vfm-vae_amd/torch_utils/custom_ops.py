@@ -133,6 +133,9 @@ SIGNATURES = {
     "vfm_gemm4": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm9_set_mode": [c_int],
+    "vfm_gemm9_gelu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_ll,
+                       c_ll, c_ll, c_ll, c_ll, c_vp],
+    "vfm_gemm9_gelu_parts": [c_int],
     "vfm_gemm9_ex": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll, c_ll,
                      c_float, c_vp, c_int, c_int, c_vp],
     "vfm_gemm9_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int],

@@ -620,11 +620,11 @@ def layer_scale_residual(y, bias, gamma, x_in, slot=None):
 
 # measured faster than the unfused chain only at C = 128 (b5 256^2); VFM_NO_FUSED_MLP=1 for A/B
 MLP_CHANNELS = () if os.environ.get("VFM_NO_FUSED_MLP") else (128,)
-# wider layers (b3: C = 512 at 64^2, b4: C = 256 at 128^2): the two 1x1s on the 256-tile GEMM with
-# the GELU fused into pwconv1's epilogue (forward) and into the 4C-wide data gradient's (backward)
-# (csrc/gemm8.hip vfm_gemm8_gelu) with VFM_GEMM_MLP=1; off by default while the layer measures 1.09-1.12x
-# the unfused chain on hipBLASLt (profiles/r3_j_mlpbench.txt)
-GEMM_MLP_CHANNELS = (256, 512) if os.environ.get("VFM_GEMM_MLP") == "1" else ()
+# wider layers (b3: C = 512 at 64^2, b4: C = 256 at 128^2): the two 1x1s on the persistent 256-tile GEMM
+# (csrc/gemm9.hip) with the GELU fused into pwconv1's epilogue (forward: h and g, or g alone without
+# autograd) and into the 4C-wide data gradient's (backward: dh and the d_s / d_b1 row sums), no separate
+# scale_bias_gelu passes; VFM_GEMM_MLP=0: the unfused chain (pointwise GEMMs + GELU row kernels, A/B)
+GEMM_MLP_CHANNELS = () if os.environ.get("VFM_GEMM_MLP") == "0" else (256, 512)
 GEMM_MLP_TESTED = (256, 512)
 
 
@@ -637,43 +637,44 @@ def convnext_mlp_supported(m, C, P):
 
 
 def _g8(A, B, **kw):
-    """bf16 product on the 256-tile kernel (gemm_hip route ("g8", 0)); raises if not covered."""
+    """bf16 product on the persistent 256-tile kernel (gemm_hip route ("g9", 0), csrc/gemm9.hip); raises if not
+    covered."""
     from . import gemm_hip
-    out = gemm_hip.try_gemm(A, B, route=("g8", 0), **kw)
+    out = gemm_hip.try_gemm(A, B, route=("g9", 0), **kw)
     if out is None:
-        raise custom_ops.NativeError(f"vfm_gemm8 does not cover {tuple(A.shape)} x {tuple(B.shape)}")
+        raise custom_ops.NativeError(f"vfm_gemm9 does not cover {tuple(A.shape)} x {tuple(B.shape)}")
     return out
 
 
 def gemm_gelu_fwd(w1c, m, s, b1, want_h=True):
     """(h, g): h = W1 m[b] (bf16 [B, O, P], None unless want_h) and g = GELU(h s[b] + b1) in one
-    GEMM (vfm_gemm8_gelu mode 1). w1c bf16 [O, I] contiguous, m bf16 [B, I, P], s fp32 [B, O] or
+    GEMM (vfm_gemm9_gelu mode 1). w1c bf16 [O, I] contiguous, m bf16 [B, I, P], s fp32 [B, O] or
     None, b1 fp32 [O] or None."""
     B, I, P = m.shape
     O = w1c.shape[0]
     g = torch.empty([B, O, P], dtype=torch.bfloat16, device=m.device)
     h = torch.empty_like(g) if want_h else None
-    with kernel_timer.region('gemm8_gelu<1>', _nb(m, g, h) + w1c.numel() * 2, flops=2.0 * B * O * I * P, bound="mfma"):
-        _check(_lib.vfm_gemm8_gelu(w1c.data_ptr(), m.data_ptr(), _p(h), g.data_ptr(), None, _p(s), _p(b1), None, None,
+    with kernel_timer.region('gemm9_gelu<1>', _nb(m, g, h) + w1c.numel() * 2, flops=2.0 * B * O * I * P, bound="mfma"):
+        _check(_lib.vfm_gemm9_gelu(w1c.data_ptr(), m.data_ptr(), _p(h), g.data_ptr(), None, _p(s), _p(b1), None, None,
                                    1, O, P, I, B, w1c.stride(0), m.stride(1), m.stride(0), P, O * P, _stream()),
-               'vfm_gemm8_gelu')
+               'vfm_gemm9_gelu')
     return h, g
 
 
 def gemm_gelu_bwd(w2t, dy, h, s, b1):
     """dh = (W2^T dy[b]) GELU'(h s + b1) s with the per-(b, o) sums for d_s ([B, O], None when s is
-    None) and d_b1 ([O]) (vfm_gemm8_gelu mode 2). w2t bf16 [O, C] contiguous, dy bf16 [B, C, P]."""
+    None) and d_b1 ([O]) (vfm_gemm9_gelu mode 2). w2t bf16 [O, C] contiguous, dy bf16 [B, C, P]."""
     B, C, P = dy.shape
     O = w2t.shape[0]
-    parts = _lib.vfm_gemm8_gelu_parts(P)
+    parts = _lib.vfm_gemm9_gelu_parts(P)
     dh = torch.empty_like(h)
     p1 = torch.empty([B, parts, O], dtype=torch.float32, device=dy.device)
     p0 = torch.empty_like(p1) if s is not None else None
-    with kernel_timer.region('gemm8_gelu<2>', _nb(dy, h, dh) + w2t.numel() * 2, flops=2.0 * B * O * C * P,
+    with kernel_timer.region('gemm9_gelu<2>', _nb(dy, h, dh) + w2t.numel() * 2, flops=2.0 * B * O * C * P,
                              bound="mfma"):
-        _check(_lib.vfm_gemm8_gelu(w2t.data_ptr(), dy.data_ptr(), dh.data_ptr(), None, h.data_ptr(), _p(s), _p(b1),
+        _check(_lib.vfm_gemm9_gelu(w2t.data_ptr(), dy.data_ptr(), dh.data_ptr(), None, h.data_ptr(), _p(s), _p(b1),
                                    _p(p0), p1.data_ptr(), 2, O, P, C, B, w2t.stride(0), dy.stride(1), dy.stride(0), P,
-                                   O * P, _stream()), 'vfm_gemm8_gelu')
+                                   O * P, _stream()), 'vfm_gemm9_gelu')
     return dh, (p0.sum(1) if p0 is not None else None), p1.sum((0, 1))
 
 

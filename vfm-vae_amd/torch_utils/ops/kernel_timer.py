@@ -242,6 +242,10 @@ def rocprof_name(region):
     args = args.rstrip(">").split(",") if args else []
     if base == "gemm8" and len(args) == 4:                     # <tag, AK, BK, OUTF32> (default schedule, EPI 0)
         return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}, false, 0>"
+    if base == "gemm9" and len(args) == 4:                     # persistent gemm9p_kernel<AK, BK, OUTF32, EPI>
+        return f"gemm9p_kernel<{args[1]}, {args[2]}, {args[3]}, "
+    if base == "gemm9_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2: EPI 4 / 5)
+        return f"gemm9p_kernel<true, false, false, {3 + int(args[0])}>"
     if base == "gemm8_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2)
         return f"gemm8_kernel<true, false, false, false, {args[0]}>"
     if base == "gemm_fold" and len(args) == 3:                 # batch-folded: gemm_kernel<AK, false, NP, OUTF32, NW>
