@@ -590,7 +590,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         rA = rsrc(a.A, offA + (zt * a.sA + (long long)kk * (dkA / 2)) * 2, live ? (long long)a.spanA : 0);
         rB = rsrc(a.B, offB + (zt * a.sB + (long long)kk * (dkB / 2)) * 2, live ? (long long)a.spanB : 0);
         if (EPI) rS = rsrc(a.bias, offS, live ? spanS : 0);
-        if (EPI >= 4) rR = rsrc(a.rscale, offR, live ? (long long)d_z * a.M * 4 + spanR : 0);
+        if (EPI >= 4) rR = rsrc(a.rscale, offR, (live && spanR) ? (long long)d_z * a.M * 4 + spanR : 0);
     };
     auto advance = [&]() __attribute__((always_inline)) {
         if (++d_kt == d_KT) {
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
         const int mw = m0 + 128 * wm, nw = n0 + 128 * wn;
         // the output batch's slice through its own descriptor (64-bit base): tile offsets stay 32-bit
-        const __amdgpu_buffer_rsrc_t rC = rsrc(a.C, z * a.sC * ES, a.spanC);
+        const __amdgpu_buffer_rsrc_t rC = rsrc(a.C, z * a.sC * ES, a.C ? a.spanC : 0);   // (null C: no records)
         const unsigned zc = 0u;
         const float* bsl = reinterpret_cast<const float*>(lds + 2 * STAGE + (item_k & 3) * 2048);
         auto act = [&](float x) __attribute__((always_inline)) {
