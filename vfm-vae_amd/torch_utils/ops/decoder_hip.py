@@ -625,6 +625,9 @@ MLP_CHANNELS = () if os.environ.get("VFM_NO_FUSED_MLP") else (128,)
 # autograd) and into the 4C-wide data gradient's (backward: dh and the d_s / d_b1 row sums), no separate
 # scale_bias_gelu passes; VFM_GEMM_MLP=0: the unfused chain (pointwise GEMMs + GELU row kernels, A/B)
 GEMM_MLP_CHANNELS = () if os.environ.get("VFM_GEMM_MLP") == "0" else (256, 512)
+# the backward's GELU' in the 4C-wide data gradient's epilogue (vfm_gemm9_gelu mode 2) instead of a plain
+# GEMM + the GELU' row kernel: opt-in (VFM_GEMM_MLP_BWD=1), slower at one wave per SIMD (see backward)
+GEMM_MLP_BWD_EPI = os.environ.get("VFM_GEMM_MLP_BWD") == "1"
 GEMM_MLP_TESTED = (256, 512)
 
 
@@ -729,7 +732,23 @@ class _ConvNeXtMLPGemm(custom_ops.FastFunction):
             dgm = r0.view(B, C).sum(0).to(gdt)
         if _wanted(ctx, 4):
             dw2 = weight_grad_1x1(dy, g, w2dt)
-        dh, sum_s, sum_b = gemm_gelu_bwd(w2c.t().contiguous(), dy, h, s, fb1)
+        if GEMM_MLP_BWD_EPI:
+            dh, sum_s, sum_b = gemm_gelu_bwd(w2c.t().contiguous(), dy, h, s, fb1)
+        else:
+            # dg = W2^T dy on the plain GEMM, then the HBM-bound GELU' row kernel: the GELU' epilogue's VALU
+            # work (erf GELU + derivative per element) does not overlap the MFMAs at one wave per SIMD and
+            # measured slower than this pass (profiles/r5_j_benchshape.txt: 17.6 ms/step vs ~3 + 7 ms/step)
+            dg = _g8(w2c.t(), dy)
+            dh = torch.empty_like(h)
+            O = h.shape[1]
+            ds_rows = torch.empty([B * O], dtype=torch.float32, device=h.device) if s is not None else None
+            db_rows = torch.empty([B * O], dtype=torch.float32, device=h.device)
+            with kernel_timer.region(_rn('scale_bias_gelu_bwd', h), _nb(h, dg, dh)):
+                _check(_lib.vfm_scale_bias_gelu_bwd(h.data_ptr(), dg.data_ptr(), _p(s), _p(fb1), dh.data_ptr(),
+                                                    _p(ds_rows), db_rows.data_ptr(), _code(h), B, O, P, _stream()),
+                       'vfm_scale_bias_gelu_bwd')
+            sum_s = ds_rows.view(B, O) if s is not None else None
+            sum_b = db_rows.view(B, O).sum(0)
         if s is not None and _wanted(ctx, 2):
             ds = sum_s.to(sdt)
         if fb1 is not None and _wanted(ctx, 3):
