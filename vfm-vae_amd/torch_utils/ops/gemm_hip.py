@@ -113,6 +113,9 @@ def _planar(t3, stream):
 
 
 BF16_OWN = __import__("os").environ.get("VFM_BF16_GEMM", "hip") == "hip"
+# fp32 products narrower than 128 (the 8^2 / 16^2 decoder blocks' 1x1s): the f32x6 128-tile kernel
+# (VFM_F32_SMALL=torch: hipBLASLt's exact-fp32 GEMM, A/B)
+F32_SMALL_OWN = __import__("os").environ.get("VFM_F32_SMALL", "hip") == "hip"
 
 
 _WS = {}
@@ -137,10 +140,10 @@ def preferred(A, M, N, reduce_batch=False):
     any width); bf16 operands on the LDS-DMA one-wave-per-SIMD kernel (csrc/gemm9.hip) at >= 128-wide
     outputs (VFM_BF16_GEMM=torch: hipBLASLt, for A/B)."""
     if A.dtype == torch.bfloat16:
-        return BF16_OWN and M >= 128 and N >= 128
+        return BF16_OWN
     if A.dtype != torch.float32:
         return False
-    return reduce_batch or (M >= 128 and N >= 128)
+    return reduce_batch or (M >= 128 and N >= 128) or F32_SMALL_OWN
 
 
 def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):

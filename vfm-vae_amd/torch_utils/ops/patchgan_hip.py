@@ -11,6 +11,8 @@ is the HIP bias_act kernel.
 
 Only reached for ROCm fp32 tensors (`supported`); a missing kernel library raises.
 """
+import os
+
 import torch
 
 from .. import custom_ops
@@ -312,8 +314,11 @@ def im2col1d(x, k, p, circular):
 #   forward   y [O, B Lo] = W [O, C k] cols (+ bias), one [B, O, Lo] transpose copy of the small output;
 #   backward  dW = dY [O, B Lo] cols^T  (the batch inside the reduction: no per-sample [O, C k] products
 #             and no batch sum), dcols = W^T dY, dx = the folded col2im; db = row sums of dY.
-# Exact fp32 products on the vendor GEMM (TF32 off), as the reference runs them: the heads' BatchNormLocal
-# over virtual batches of 8 samples amplifies GEMM rounding into the input gradient.
+# fp32-equivalent products on our GEMMs (f32x6: three exact bf16 pieces per operand, the six piece products
+# of order >= 2^-16, fp32 accumulation -- the precision class of the reference's exact fp32 with TF32 off,
+# which matters here: the heads' BatchNormLocal over virtual batches of 8 samples amplifies GEMM rounding
+# into the input gradient); VFM_DHEAD_GEMM=torch keeps hipBLASLt's exact fp32 products (A/B).
+_DHEAD_OWN = os.environ.get("VFM_DHEAD_GEMM", "hip") == "hip"
 
 
 class _Conv1dFolded(custom_ops.FastFunction):
@@ -328,7 +333,9 @@ class _Conv1dFolded(custom_ops.FastFunction):
             _check(_lib.vfm_im2col1d_cbl_f32(x.data_ptr(), cols.data_ptr(), B, C, L, k, p, int(circular), _stream()),
                    'vfm_im2col1d_cbl_f32')
         w = w2.detach().float()
-        if bias is not None:
+        if _DHEAD_OWN:
+            y2 = _gemm(w, cols, bias=None if bias is None else bias.detach().float(), bias_dim=0)
+        elif bias is not None:
             y2 = torch.addmm(bias.detach().float()[:, None], w, cols)
         else:
             y2 = torch.mm(w, cols)
@@ -345,13 +352,16 @@ class _Conv1dFolded(custom_ops.FastFunction):
         gy2 = dy.float().transpose(0, 1).reshape(O, -1)                       # [O, B Lo]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dcols = _c16(torch.mm(w.t(), gy2))
+            dcols = _c16(_gemm(w.t(), gy2) if _DHEAD_OWN else torch.mm(w.t(), gy2))
             dx = torch.empty([B, C, L], dtype=torch.float32, device=dy.device)
             with kernel_timer.region('col2im1d_cbl<f32>', 4 * (dx.numel() + dcols.numel())):
                 _check(_lib.vfm_col2im1d_cbl_f32(dcols.data_ptr(), dx.data_ptr(), B, C, L, k, p, int(circular),
                                                  _stream()), 'vfm_col2im1d_cbl_f32')
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(gy2, cols.t()).to(wdt)
+            if _DHEAD_OWN:     # deep reduction over the batch-folded columns: K splits fill the chip
+                dw = _gemm(gy2, cols.t(), splits=_splits(O, cols.shape[0], gy2.shape[1])).to(wdt)
+            else:
+                dw = torch.mm(gy2, cols.t()).to(wdt)
         if ctx.needs_input_grad[2]:
             db = gy2.sum(1).to(bdt)
         return dx, dw, db, None, None, None

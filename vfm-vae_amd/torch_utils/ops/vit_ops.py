@@ -71,8 +71,15 @@ def patch_embed(pixels, weight, bias, patch, compute_dtype):
     x = pixels[:, :, :gh * patch, :gw * patch].to(compute_dtype)
     x = x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * patch * patch)
     w = frozen_weight(weight, compute_dtype).reshape(weight.shape[0], -1)
-    with _vg(x, w, "vit_patch"):
-        y = torch.matmul(x, w.t())
+    y = None
+    if x.is_cuda and OWN_GEMM and _frozen(x, w):
+        # the patch projection on our GEMMs (bf16: gemm9, fp32: f32x6)
+        from . import gemm_hip
+        y = gemm_hip.try_gemm(x.reshape(-1, x.shape[-1]), w.t(), auto=True)
+        y = None if y is None else y.reshape(B, gh * gw, w.shape[0])
+    if y is None:
+        with _vg(x, w, "vit_patch"):
+            y = torch.matmul(x, w.t())
     if bias is not None:
         y = y + frozen_weight(bias, compute_dtype)
     return y
