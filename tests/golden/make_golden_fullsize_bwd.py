@@ -14,8 +14,10 @@ validation) with the posterior noise drawn from the CPU generator seeded 123. Th
 tests/golden/make_golden_networks.py's 64-px case, with a KL weight that keeps the three terms of similar size) is back-propagated into the trainable groups the
 reference's G phase updates -- synthesis, mapping, ldm_adapter (the VFM tower is frozen; reference
 training/loss.py:721-1001 accumulate_gradients and networks/generator.py set_train_mode). Stored:
-the loss terms, the per-parameter gradient norms and sums, per-group gradient norms, and per-image
-sums / norms of the outputs. The decoder runs in fp32 here (num_fp16_res 0: the CPU reference has no
+the loss terms, the per-parameter gradient norms, sums and NPROJ projections <g, P_k> on seeded
+random P_k (tests/fullsize_case.py grad_probe: sensitive to a transposed or permuted gradient, which keeps norm
+and sum), whole (or row-subsampled) gradients of the weights in fullsize_case.FULL_GRADS, per-group
+gradient norms, and per-image sums / norms of the outputs. The decoder runs in fp32 here (num_fp16_res 0: the CPU reference has no
 fp16 path); the GPU test compares both its fp32 product path and the bench's precision (bf16 blocks
 3-5, bf16 tower) against these fp32 numbers with stated tolerances.
 
@@ -87,7 +89,7 @@ meta["ms_sums"] = [float(m.double().sum()) for m in out.gen_multiscale_imgs]
 meta["ms_norms"] = [float(m.double().norm()) for m in out.gen_multiscale_imgs]
 arrays["gen_img"] = out.gen_img.detach().float().numpy()
 loss.backward()
-names, norms, sums = [], [], []
+names, norms, sums, projs = [], [], [], []
 group_sq = {g: 0.0 for g in fc.TRAIN_GROUPS}
 for n, p in G.named_parameters():
     if p.grad is None:
@@ -96,11 +98,18 @@ for n, p in G.named_parameters():
     names.append(n)
     norms.append(float(gd.norm()))
     sums.append(float(gd.sum()))
+    projs.append(fc.projections(n, gd).numpy())
     group_sq[n.split(".")[0]] += float(gd.square().sum())
 meta["grad_names"] = names
 meta["group_norms"] = {g: v ** 0.5 for g, v in group_sq.items()}
 arrays["grad_norm"] = np.asarray(norms, np.float64)
 arrays["grad_sum"] = np.asarray(sums, np.float64)
+arrays["grad_proj"] = np.stack(projs).astype(np.float64)          # [n_params, NPROJ]
+params = dict(G.named_parameters())
+meta["full_grads"] = []
+for i, (n, step) in enumerate(fc.FULL_GRADS):
+    arrays[f"full_grad{i}"] = params[n].grad.detach()[::step].float().numpy()
+    meta["full_grads"].append([n, step])
 meta["g_kwargs"] = {k: v for k, v in g_kwargs.items() if k != "vfm_name"}
 arrays["meta"] = np.array(json.dumps(meta))
 np.savez_compressed(OUT, **arrays)

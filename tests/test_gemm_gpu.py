@@ -166,9 +166,12 @@ def test_gemm_unsupported_shape_returns_none():
 
 
 @pytest.fixture(params=[1, 0], ids=["deep", "one_ahead"])
-def g8_schedule(request):
-    """Both K-tile staging schedules of gemm8 (two / one K-tiles ahead)."""
+def g8_schedule(request, monkeypatch):
+    """Both K-tile staging schedules of gemm8 (two / one K-tiles ahead); bf16 products routed to gemm8
+    rather than gemm9 (the default bf16 kernel, tests/test_gemm9_gpu.py)."""
     from torch_utils import custom_ops
+    from torch_utils.ops import gemm_hip
+    monkeypatch.setattr(gemm_hip, "G9", False)
     lib = custom_ops.get_native()
     prev = lib.vfm_gemm8_set_schedule(request.param)
     yield request.param

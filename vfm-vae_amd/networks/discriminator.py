@@ -137,7 +137,8 @@ class BatchNormLocal2d(nn.Module):
 class HeadBlock(nn.Sequential):
     """SpectralConv1d -> BatchNormLocal -> LeakyReLU(0.2) (same modules / state-dict keys as the
     reference's nn.Sequential). On ROCm fp32 inputs the BatchNormLocal + LeakyReLU pair runs as one
-    fused HIP kernel per direction (patchgan_hip.bn_local1d_lrelu); the conv stays exact fp32."""
+    fused HIP kernel per direction (patchgan_hip.bn_local1d_lrelu); the conv is the batch-folded
+    im2col + exact-fp32 product of patchgan_hip._Conv1dFolded."""
 
     def forward(self, x):
         conv, bn, act = self[0], self[1], self[2]

@@ -113,9 +113,12 @@ def _planar(t3, stream):
 
 
 BF16_OWN = __import__("os").environ.get("VFM_BF16_GEMM", "hip") == "hip"
-# fp32 products narrower than 128 (the 8^2 / 16^2 decoder blocks' 1x1s): the f32x6 128-tile kernel
-# (VFM_F32_SMALL=torch: hipBLASLt's exact-fp32 GEMM, A/B)
-F32_SMALL_OWN = __import__("os").environ.get("VFM_F32_SMALL", "hip") == "hip"
+# fp32 products narrower than 128 (the 8^2 / 16^2 decoder blocks' 1x1s): hipBLASLt's exact-fp32 GEMM by
+# default; VFM_F32_SMALL=hip routes them to the f32x6 128-tile kernel, which measured slower at these
+# shapes (r5o bench, profiles/r5_o_f32small_ab.txt)
+F32_SMALL_OWN = __import__("os").environ.get("VFM_F32_SMALL", "torch") == "hip"
+# bf16 products on gemm9 (csrc/gemm9.hip); False: gemm8's 256-tile pipeline (tests, A/B)
+G9 = __import__("os").environ.get("VFM_GEMM9", "1") == "1"
 
 
 _WS = {}
@@ -157,7 +160,7 @@ def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
         registers and fills the chip with 4x the tiles (6304x384x1536: 95 us vs 101 us for the best
         256-tile split-K);
       * otherwise the 256-tile kernel."""
-    if dtype == torch.bfloat16 and K % 64 == 0:
+    if dtype == torch.bfloat16 and K % 64 == 0 and G9:
         if reduce_batch:
             # batch-reduced weight gradients (few output tiles over a deep reduction): ~2 items per CU
             tiles = -(-M // 256) * -(-N // 256)

@@ -39,6 +39,19 @@ def _gemm(A, B, **kw):
     return gemm_hip.gemm(A, B, out_dtype=torch.float32, **kw)
 
 
+def _gemm_or_mm(A, B, bias=None, **kw):
+    """fp32 A @ B (+ bias[:, None]): our f32x6 GEMM under VFM_DHEAD_GEMM=hip (falling back to the library
+    product for a K or N that is not a multiple of 4 fp32 elements: 1-channel logits, ragged token counts),
+    else hipBLASLt's exact-fp32 product (the default), timed as a vendor region."""
+    if _DHEAD_OWN:
+        from . import gemm_hip
+        out = gemm_hip.try_gemm(A, B, out_dtype=torch.float32, bias=bias, bias_dim=None if bias is None else 0, **kw)
+        if out is not None:
+            return out
+    with kernel_timer.vendor_gemm("f32,dhead", A.shape[0], B.shape[1], A.shape[1], esize=4):
+        return torch.mm(A, B) if bias is None else torch.addmm(bias[:, None], A, B)
+
+
 def _splits(M, N, K):
     tiles = -(-M // 128) * -(-N // 128)
     return max(1, min(-(-1024 // tiles), K // 512, 64))
@@ -314,11 +327,12 @@ def im2col1d(x, k, p, circular):
 #   forward   y [O, B Lo] = W [O, C k] cols (+ bias), one [B, O, Lo] transpose copy of the small output;
 #   backward  dW = dY [O, B Lo] cols^T  (the batch inside the reduction: no per-sample [O, C k] products
 #             and no batch sum), dcols = W^T dY, dx = the folded col2im; db = row sums of dY.
-# fp32-equivalent products on our GEMMs (f32x6: three exact bf16 pieces per operand, the six piece products
-# of order >= 2^-16, fp32 accumulation -- the precision class of the reference's exact fp32 with TF32 off,
-# which matters here: the heads' BatchNormLocal over virtual batches of 8 samples amplifies GEMM rounding
-# into the input gradient); VFM_DHEAD_GEMM=torch keeps hipBLASLt's exact fp32 products (A/B).
-_DHEAD_OWN = os.environ.get("VFM_DHEAD_GEMM", "hip") == "hip"
+# The products: hipBLASLt's exact fp32 by default -- the reference's precision with TF32 off, which matters
+# here: the heads' BatchNormLocal over virtual batches of 8 samples amplifies GEMM rounding into the input
+# gradient. VFM_DHEAD_GEMM=hip puts them on our f32x6 GEMM (three exact bf16 pieces per operand, six piece
+# products; parity-green, tests/test_patchgan_gpu.py), which measured 13.7 ms/step SLOWER in the bench
+# (r5o: 91.0 vs 94.7 img/s with the narrow decoder 1x1s, profiles/r5_o_f32small_ab.txt).
+_DHEAD_OWN = os.environ.get("VFM_DHEAD_GEMM", "torch") == "hip"
 
 
 class _Conv1dFolded(custom_ops.FastFunction):
@@ -333,12 +347,7 @@ class _Conv1dFolded(custom_ops.FastFunction):
             _check(_lib.vfm_im2col1d_cbl_f32(x.data_ptr(), cols.data_ptr(), B, C, L, k, p, int(circular), _stream()),
                    'vfm_im2col1d_cbl_f32')
         w = w2.detach().float()
-        if _DHEAD_OWN:
-            y2 = _gemm(w, cols, bias=None if bias is None else bias.detach().float(), bias_dim=0)
-        elif bias is not None:
-            y2 = torch.addmm(bias.detach().float()[:, None], w, cols)
-        else:
-            y2 = torch.mm(w, cols)
+        y2 = _gemm_or_mm(w, cols, bias=None if bias is None else bias.detach().float())
         ctx.save_for_backward(cols, w)
         ctx.meta = (B, C, L, k, p, circular, w2.dtype, None if bias is None else bias.dtype)
         return y2.view(O, B, Lo).transpose(0, 1).contiguous()
@@ -352,16 +361,14 @@ class _Conv1dFolded(custom_ops.FastFunction):
         gy2 = dy.float().transpose(0, 1).reshape(O, -1)                       # [O, B Lo]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dcols = _c16(_gemm(w.t(), gy2) if _DHEAD_OWN else torch.mm(w.t(), gy2))
+            dcols = _c16(_gemm_or_mm(w.t(), gy2))
             dx = torch.empty([B, C, L], dtype=torch.float32, device=dy.device)
             with kernel_timer.region('col2im1d_cbl<f32>', 4 * (dx.numel() + dcols.numel())):
                 _check(_lib.vfm_col2im1d_cbl_f32(dcols.data_ptr(), dx.data_ptr(), B, C, L, k, p, int(circular),
                                                  _stream()), 'vfm_col2im1d_cbl_f32')
         if ctx.needs_input_grad[1]:
-            if _DHEAD_OWN:     # deep reduction over the batch-folded columns: K splits fill the chip
-                dw = _gemm(gy2, cols.t(), splits=_splits(O, cols.shape[0], gy2.shape[1])).to(wdt)
-            else:
-                dw = torch.mm(gy2, cols.t()).to(wdt)
+            # deep reduction over the batch-folded columns (own GEMM: K splits fill the chip)
+            dw = _gemm_or_mm(gy2, cols.t(), splits=_splits(O, cols.shape[0], gy2.shape[1])).to(wdt)
         if ctx.needs_input_grad[2]:
             db = gy2.sum(1).to(bdt)
         return dx, dw, db, None, None, None
