@@ -52,8 +52,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
-    ap.add_argument("--timer-steps", type=int, default=1,
-                    help="kernel timing in every n-th timed step only (1 = all timed steps)")
+    ap.add_argument("--timer-steps", type=int, default=4,
+                    help="kernel timing in every n-th timed step only (1 = all timed steps). Default 4: steps "
+                         "0, 4, 8, 12, 16 of the fixed-seed sequence; timing 1/4 of the launches of every step "
+                         "cost 2.2 %% of the step rate (r5p: 93.4 vs 95.5 img/s with the timer off)")
     ap.add_argument("--timer-every", type=int, default=4,
                     help="per-launch HIP events on a pseudo-random 1/n of each kernel region's launches. Not every "
                          "launch of whole steps: back-to-back event-bound launches run serialised, which timed the "

@@ -14,8 +14,9 @@ proves it on CPU with a deliberately transposed gradient).
 Stated tolerances:
   fp32 -- the product path at reference precision (decoder num_fp16_res 0, fp32 tower; our kernels
   with fp32-equivalent f32x6 products): loss terms 1e-5 relative; every parameter's gradient norm and
-  projection within 1e-3 (relative to the gradient's norm, floor 1e-4 of the largest norm for gradients
-  that are ~0 in exact math), sum within 1e-3 scaled; stored gradients within 1e-3; group norms 1e-3;
+  projection within FP32_TOL = 2e-4 (relative to the gradient's norm, floor 1e-4 of the largest norm for
+  gradients that are ~0 in exact math), sum within 1e-3 scaled; stored gradients within 2e-4; group
+  norms 1e-3;
   bf16 -- the bench's precision (decoder blocks 3-5 and the SigLIP2 tower in bf16, BASELINE config 1)
   against the same fp32 numbers: loss within 3e-2, group gradient norms within 5e-2, every parameter's
   gradient norm within BF16_NORM_TOL and projection within BF16_PROJ_TOL of its own size (floor 1e-3 of
@@ -75,10 +76,13 @@ def _run(vfm_dir, meta, precision):
     return G, out, loss
 
 
-# bf16 bounds: 1.5x the measured worst case (MEASURED_BF16, r5 on MI355X)
-MEASURED_BF16 = dict(norm=None, proj=None, full=None)
-BF16_NORM_TOL = 1.2e-1
-BF16_PROJ_TOL = 2.5e-1
+# measured worst cases on MI355X (r5p): fp32 norm 4.8e-5, projection 4.6e-5, stored tensors 6.3e-6; bf16
+# norm 8.9e-2 (synthesis.blocks.5.convs1.0.noise_strength), projection 1.05e-1
+# (ldm_adapter.post_quant.blocks.0.norm3.weight), stored tensors 5.8e-2. Bounds: fp32 2e-4 (4x), bf16 1.5x.
+MEASURED_BF16 = dict(norm=8.91e-2, proj=1.05e-1, full=5.79e-2)
+FP32_TOL = 2e-4
+BF16_NORM_TOL = 1.35e-1
+BF16_PROJ_TOL = 1.6e-1
 
 
 def _rel(a, b):
@@ -100,8 +104,8 @@ def test_generator_training_backward_full_size(vfm_dir, golden, precision):
     got = {n for n, p in params.items() if p.grad is not None}
     assert got == set(names), got ^ set(names)
     floor = (1e-4 if precision == "fp32" else 1e-3) * float(np.max(norms))
-    tol_norm = 1e-3 if precision == "fp32" else BF16_NORM_TOL
-    tol_proj = 1e-3 if precision == "fp32" else BF16_PROJ_TOL
+    tol_norm = FP32_TOL if precision == "fp32" else BF16_NORM_TOL
+    tol_proj = FP32_TOL if precision == "fp32" else BF16_PROJ_TOL
     worst = {"norm": (0.0, None), "proj": (0.0, None), "full": (0.0, None)}
     bad = []
     group_sq = {g: 0.0 for g in fc.TRAIN_GROUPS}

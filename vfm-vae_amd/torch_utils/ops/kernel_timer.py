@@ -29,6 +29,7 @@ SHAPES = os.environ.get("VFM_TIMER_SHAPES", "0") == "1"
 _enabled = False
 _records = {}      # name -> list of (start_event, end_event, bytes, flops, bound)
 _counts = {}       # name -> launches seen while enabled (timed or not)
+_flops_all = {}    # name -> algorithmic flops of every launch seen while enabled (host arithmetic)
 _every = 1         # time ~1/n of each region's launches (the events cost host time per launch)
 
 
@@ -42,6 +43,7 @@ def enable(flag: bool, every: int = 1):
     if flag:
         _records.clear()
         _counts.clear()
+        _flops_all.clear()
         _every = max(1, int(every))
 
 
@@ -183,6 +185,8 @@ def region(name, nbytes=0, flops=0, bound="hbm", native=True):
         return _NULL
     c = _counts.get(name, 0)
     _counts[name] = c + 1
+    if flops:
+        _flops_all[name] = _flops_all.get(name, 0.0) + flops
     if not _active or (_every > 1 and not _sampled(c)):
         return _NULL
     return _Timed(name, nbytes, flops, bound, native)
@@ -211,7 +215,7 @@ def summary():
         scale = n / len(timed)              # every n-th launch timed: totals extrapolated to all launches
         out[name] = dict(launches=n, timed_launches=len(timed), total_ms=ms * scale,
                          bytes=sum(t[1] for t in timed) * scale, flops=sum(t[2] for t in timed) * scale,
-                         bound=timed[0][3])
+                         flops_all=_flops_all.get(name, 0.0), bound=timed[0][3])
     return out
 
 
@@ -333,6 +337,9 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None, steps=
                 "ms_total": round(r["total_ms"], 3),
                 "bytes_per_launch": bpl,
                 "flops_per_launch": int(r["flops"] / r["launches"]),
+                # every launch's flops (host arithmetic over all launches, timed or not): the timed
+                # launches' mean above should agree with it
+                "flops_per_launch_all": int(r["flops_all"] / r["launches"]) if r["flops_all"] else None,
                 "traffic_over_algorithmic": round(traffic / bpl, 3) if traffic and bpl else None}
 
     out = entry(*ranked[0])
