@@ -108,6 +108,16 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, unsigned vof
                  : "memory");
 }
 
+// dma16s with the LDS destination formed in M0 itself: m0 = mb + mo (two SGPR operands, no separate add)
+__device__ __forceinline__ void dma16m(__amdgpu_buffer_rsrc_t rsrc, unsigned voff0, unsigned su, unsigned mb,
+                                       unsigned mo) {
+    unsigned t;
+    asm volatile("v_add_u32 %0, %1, %2\n\ts_add_u32 m0, %4, %5\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %3, 0 offen lds"
+                 : "=&v"(t)
+                 : "v"(voff0), "s"(su), "s"(rsrc), "s"(mb), "s"(mo)
+                 : "memory", "scc");
+}
+
 // The dword form (4 B per lane: 256 B per wave), for the epilogue's bias values.
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned m0) {
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(m0)
@@ -572,13 +582,25 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     const unsigned sl0 = (unsigned)(size_t)(lds_void*)lds + 2 * STAGE + (unsigned)wave * 256u;
     const unsigned voS = (unsigned)tid * 4u;          // wave w: values 64 w .. 64 w + 63 of the slot
     auto dma = [&](int g, int buf) __attribute__((always_inline)) {
-        if (g < 8) dma16s(rA, voA0, ustep(AK, a.lda, g), m0A + buf * STAGE + g * 4096);
-        else if (g < 16) dma16s(rB, voB0, ustep(BKC, a.ldb, g - 8), m0A + buf * STAGE + OPB + (g - 8) * 4096);
+        const unsigned mb = m0A + (unsigned)buf * STAGE;
+        if (g < 8) dma16m(rA, voA0, ustep(AK, a.lda, g), mb, (unsigned)(g * 4096));
+        else if (g < 16) dma16m(rB, voB0, ustep(BKC, a.ldb, g - 8), mb, (unsigned)(OPB + (g - 8) * 4096));
         else if (g == 16) dma4(rS, voS, sl0 + (unsigned)(d_k & 3) * 2048u);          // the cursor item's bias
         else dma4(rR, voS, sl0 + (unsigned)(d_k & 3) * 2048u + 1024u);               // and row scales (EPI 4 / 5)
     };
     // descriptors of the cursor's position (after setup_dma / a K-tile step)
     // (past the workgroup's last item: no records, the DMA writes zeros into a buffer nobody reads again)
+    // The operand descriptors of the cursor as (64-bit address, record count) in SGPRs: rebuilt in full at an
+    // item's first K-tile (and per K-tile of a batch-reduced product, whose K-tiles cross batches), else
+    // advanced by one K-tile's step in SALU asm (a 64-bit add and a saturating subtract per operand instead of
+    // the multiplies, compares and selects of a full rebuild in every K-tile)
+    unsigned aLo = 0, aHi = 0, aN = 0, bLo = 0, bHi = 0, bN = 0;
+    auto clamp31 = [](long long left) __attribute__((always_inline)) {
+        return (unsigned)(left > 0 ? (left < 0x7fffffffLL ? left : 0x7fffffffLL) : 0);
+    };
+    auto mk = [](unsigned lo, unsigned hi, unsigned n) __attribute__((always_inline)) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, (int)n, 0x00020000);
+    };
     auto point = [&]() __attribute__((always_inline)) {
         const bool live = d_item < total;
         int zt = d_z, kk = d_kt;
@@ -587,10 +609,29 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             zt = v / a.KTz;
             kk = v - zt * a.KTz;
         }
-        rA = rsrc(a.A, offA + (zt * a.sA + (long long)kk * (dkA / 2)) * 2, live ? (long long)a.spanA : 0);
-        rB = rsrc(a.B, offB + (zt * a.sB + (long long)kk * (dkB / 2)) * 2, live ? (long long)a.spanB : 0);
+        const long long cA = offA + (zt * a.sA + (long long)kk * (dkA / 2)) * 2;
+        const long long cB = offB + (zt * a.sB + (long long)kk * (dkB / 2)) * 2;
+        const unsigned long long pA = (unsigned long long)((const char*)a.A + cA);
+        const unsigned long long pB = (unsigned long long)((const char*)a.B + cB);
+        aLo = __builtin_amdgcn_readfirstlane((unsigned)pA);
+        aHi = __builtin_amdgcn_readfirstlane((unsigned)(pA >> 32));
+        aN = __builtin_amdgcn_readfirstlane(live ? clamp31(a.spanA - cA) : 0u);
+        bLo = __builtin_amdgcn_readfirstlane((unsigned)pB);
+        bHi = __builtin_amdgcn_readfirstlane((unsigned)(pB >> 32));
+        bN = __builtin_amdgcn_readfirstlane(live ? clamp31(a.spanB - cB) : 0u);
+        rA = mk(aLo, aHi, aN);
+        rB = mk(bLo, bHi, bN);
         if (EPI) rS = rsrc(a.bias, offS, live ? spanS : 0);
         if (EPI >= 4) rR = rsrc(a.rscale, offR, (live && spanR) ? (long long)d_z * a.M * 4 + spanR : 0);
+    };
+    auto step = [&]() __attribute__((always_inline)) {
+        asm volatile("s_add_u32 %0, %0, %6\n\ts_addc_u32 %1, %1, 0\n\ts_sub_u32 %2, %2, %6\n\ts_cselect_b32 %2, 0, %2\n\t"
+                     "s_add_u32 %3, %3, %7\n\ts_addc_u32 %4, %4, 0\n\ts_sub_u32 %5, %5, %7\n\ts_cselect_b32 %5, 0, %5"
+                     : "+s"(aLo), "+s"(aHi), "+s"(aN), "+s"(bLo), "+s"(bHi), "+s"(bN)
+                     : "s"(dkA), "s"(dkB)
+                     : "scc");
+        rA = mk(aLo, aHi, aN);
+        rB = mk(bLo, bHi, bN);
     };
     auto advance = [&]() __attribute__((always_inline)) {
         if (++d_kt == d_KT) {
@@ -598,8 +639,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             d_item += G;
             ++d_k;
             if (d_item < total) setup_dma(d_item);
+            point();
+        } else if (a.reduce) {
+            point();
+        } else {
+            step();
         }
-        point();
     };
 
     f32x4 acc[8][8];

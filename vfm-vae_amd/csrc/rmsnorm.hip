@@ -33,9 +33,16 @@ __global__ __launch_bounds__(THREADS) void crms_fwd(const float* __restrict__ x,
     const float* xb = x + (long long)b * C * P + p;
     float ss = 0.f;
     if (ok)
-        for (int c = g; c < C; c += GROUPS) {
-            const float v = xb[(long long)c * P];
-            ss = fmaf(v, v, ss);
+        // 8 channels per round, their loads issued before the FMAs (one round trip per 8 channels)
+        for (int c0 = g; c0 < C; c0 += 8 * GROUPS) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int c = c0 + k * GROUPS;
+                v[k] = c < C ? xb[(long long)c * P] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ss = fmaf(v[k], v[k], ss);
         }
     red[g][col] = ss;
     __syncthreads();
@@ -46,6 +53,7 @@ __global__ __launch_bounds__(THREADS) void crms_fwd(const float* __restrict__ x,
     if (!ok) return;
     if (g == 0 && rinv) rinv[(long long)b * P + p] = r;
     float* yb = y + (long long)b * C * P + p;
+#pragma unroll 8
     for (int c = g; c < C; c += GROUPS) yb[(long long)c * P] = xb[(long long)c * P] * r * (scale * gamma[c]);
 }
 
@@ -61,9 +69,18 @@ __global__ __launch_bounds__(THREADS) void crms_bwd(const float* __restrict__ x,
     const long long base = (long long)b * C * P + p;
     float dot = 0.f;
     if (ok)
-        for (int c = g; c < C; c += GROUPS) {
-            const long long o = base + (long long)c * P;
-            dot = fmaf(scale * gamma[c] * dy[o], x[o], dot);
+        for (int c0 = g; c0 < C; c0 += 8 * GROUPS) {
+            float dv[8], xv[8], gv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int c = c0 + k * GROUPS;
+                const long long o = base + (long long)c * P;
+                dv[k] = c < C ? dy[o] : 0.f;
+                xv[k] = c < C ? x[o] : 0.f;
+                gv[k] = c < C ? gamma[c] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dot = fmaf(scale * gv[k] * dv[k], xv[k], dot);
         }
     red[g][col] = dot;
     __syncthreads();
@@ -73,6 +90,7 @@ __global__ __launch_bounds__(THREADS) void crms_bwd(const float* __restrict__ x,
     const float r = ok ? rinv[(long long)b * P + p] : 0.f;
     // r == 1 / 1e-12 exactly when the norm was clamped: no gradient through the norm then
     const float corr = (r < 1.f / NORM_EPS) ? tot * r * r * r : 0.f;
+#pragma unroll 4
     for (int c = g; c < C; c += GROUPS) {
         float gx = 0.f;
         if (ok) {

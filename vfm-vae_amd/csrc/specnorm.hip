@@ -9,8 +9,8 @@
 // backward (u, v constants, as torch detaches them):
 //   dW = g / sigma - (sum_ij g_ij W_ij) / sigma^2 * u v^T
 // Launches (fwd): K1 t = W^T u (16 columns x 16 row groups per block) + per-block ||t||^2 partials;
-// K2 r = W v (one row per wave, v = t / max(||t||, eps) formed from the K1 partials on the fly; block 0
-// stores v) + per-block ||r||^2 partials; K3 W_sn = W / sigma (grid-stride; block 0 stores u and sigma).
+// K2 r = W v (one row per block, v = t / max(||t||, eps) formed from the K1 partials on the fly; block 0
+// stores v) + per-row ||r||^2 partials; K3 W_sn = W / sigma (grid-stride; block 0 stores u and sigma).
 // (bwd): K4 per-block partials of sum g W; K5 dW. Partial sums are added in a fixed order.
 #include "vfm_common.h"
 
@@ -48,8 +48,18 @@ __global__ __launch_bounds__(THREADS) void sn_wtu(const float* __restrict__ W, c
     const int i = blockIdx.x * TU_COLS + col;
     float s = 0.f;
     if (i < I)
-#pragma unroll 4
-        for (int o = rg; o < O; o += TU_RG) s = fmaf(W[(long long)o * I + i], u[o], s);
+        // 8 rows per round, their loads issued before the FMAs (one round trip per 8 rows)
+        for (int o0 = rg; o0 < O; o0 += 8 * TU_RG) {
+            float w[8], uv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int o = o0 + k * TU_RG;
+                w[k] = o < O ? W[(long long)o * I + i] : 0.f;
+                uv[k] = o < O ? u[o] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s = fmaf(w[k], uv[k], s);
+        }
     red[rg][col] = s;
     __syncthreads();
     float tv = 0.f;
@@ -62,6 +72,8 @@ __global__ __launch_bounds__(THREADS) void sn_wtu(const float* __restrict__ W, c
     if (threadIdx.x == 0) part[blockIdx.x] = ss;
 }
 
+// one row of W per block (the 256 threads striding over the row, their loads issued in rounds of 8 before
+// the FMAs: a 3456-wide row is two round trips; one row per wave took fourteen)
 __global__ __launch_bounds__(THREADS) void sn_wv(const float* __restrict__ W, const float* __restrict__ t,
                                                  const float* __restrict__ tpart, int ntp, float* __restrict__ v,
                                                  float* __restrict__ v_copy, float* __restrict__ r,
@@ -74,18 +86,25 @@ __global__ __launch_bounds__(THREADS) void sn_wv(const float* __restrict__ W, co
             v[i] = x;
             if (v_copy) v_copy[i] = x;
         }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int o = blockIdx.x * 4 + wave;
+    const int o = blockIdx.x;
+    const float* wr = W + (long long)o * I;
     float s = 0.f;
-    if (o < O) {
-        const float* wr = W + (long long)o * I;
-#pragma unroll 4
-        for (int i = lane; i < I; i += 64) s = fmaf(wr[i], t[i] * inv, s);
+    for (int i0 = threadIdx.x; i0 < I; i0 += 8 * THREADS) {
+        float w[8], tv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * THREADS;
+            w[k] = i < I ? wr[i] : 0.f;
+            tv[k] = i < I ? t[i] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s = fmaf(w[k], tv[k] * inv, s);
     }
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    if (o < O && lane == 0) r[o] = s;
-    const float ss = block_reduce(lane == 0 && o < O ? s * s : 0.f, sh);
-    if (threadIdx.x == 0) rpart[blockIdx.x] = ss;
+    s = block_reduce(s, sh);
+    if (threadIdx.x == 0) {
+        r[o] = s;
+        rpart[o] = s * s;
+    }
 }
 
 __global__ __launch_bounds__(THREADS) void sn_scale(const float* __restrict__ W, const float* __restrict__ r,
@@ -105,6 +124,15 @@ __global__ __launch_bounds__(THREADS) void sn_scale(const float* __restrict__ W,
         if (threadIdx.x == 0) sigma[0] = sg;
     }
     const float is = 1.f / sg;
+    if ((n & 3) == 0) {                              // float4 per thread (the grid covers n / 4 in one pass)
+        const long long n4 = n >> 2;
+        for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n4; e += (long long)gridDim.x * THREADS) {
+            float4 w = reinterpret_cast<const float4*>(W)[e];
+            w.x *= is; w.y *= is; w.z *= is; w.w *= is;
+            reinterpret_cast<float4*>(Wsn)[e] = w;
+        }
+        return;
+    }
     for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS)
         Wsn[e] = W[e] * is;
 }
@@ -113,8 +141,16 @@ __global__ __launch_bounds__(THREADS) void sn_gw(const float* __restrict__ g, co
                                                  float* __restrict__ part, long long n) {
     __shared__ float sh[4];
     float s = 0.f;
-    for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS)
-        s = fmaf(g[e], W[e], s);
+    if ((n & 3) == 0) {
+        const long long n4 = n >> 2;
+        for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n4; e += (long long)gridDim.x * THREADS) {
+            const float4 a = reinterpret_cast<const float4*>(g)[e], b = reinterpret_cast<const float4*>(W)[e];
+            s = fmaf(a.x, b.x, s); s = fmaf(a.y, b.y, s); s = fmaf(a.z, b.z, s); s = fmaf(a.w, b.w, s);
+        }
+    } else {
+        for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS)
+            s = fmaf(g[e], W[e], s);
+    }
     s = block_reduce(s, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
@@ -127,6 +163,19 @@ __global__ __launch_bounds__(THREADS) void sn_dw(const float* __restrict__ g, co
     const float S = sum_parts(part, np, sh);
     const float sg = sigma[0];
     const float is = 1.f / sg, c = S / (sg * sg);
+    if ((I & 3) == 0) {                              // float4 per thread: the 4 elements share a row
+        const long long n4 = n >> 2;
+        const int I4 = I >> 2;
+        for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n4; e += (long long)gridDim.x * THREADS) {
+            const long long o = e / I4;
+            const float4 gv = reinterpret_cast<const float4*>(g)[e];
+            const float4 vv = reinterpret_cast<const float4*>(v)[e - o * I4];
+            const float cu = c * u[o];
+            reinterpret_cast<float4*>(dW)[e] =
+                make_float4(gv.x * is - cu * vv.x, gv.y * is - cu * vv.y, gv.z * is - cu * vv.z, gv.w * is - cu * vv.w);
+        }
+        return;
+    }
     for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n; e += (long long)gridDim.x * THREADS) {
         const long long o = e / I;
         dW[e] = g[e] * is - c * u[o] * v[e - o * I];
@@ -140,7 +189,7 @@ constexpr int SCALE_BLOCKS = 512;
 // floats of workspace vfm_specnorm_fwd / _bwd need for an [O, I] weight
 extern "C" long long vfm_specnorm_workspace_floats(int O, int I) {
     if (O <= 0 || I <= 0) return VFM_ERR_ARGS;
-    const long long tb = (I + TU_COLS - 1) / TU_COLS, rb = (O + 3) / 4;
+    const long long tb = (I + TU_COLS - 1) / TU_COLS, rb = O;
     return (long long)I + O + tb + rb + SCALE_BLOCKS;
 }
 
@@ -150,7 +199,7 @@ extern "C" long long vfm_specnorm_workspace_floats(int O, int I) {
 extern "C" int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_copy, float* v_copy, float* sigma,
                                 float* Wsn, float* ws, int O, int I, float eps, void* stream) {
     if (!W || !u || !v || !sigma || !Wsn || !ws || O <= 0 || I <= 0) return VFM_ERR_ARGS;
-    const int tb = (I + TU_COLS - 1) / TU_COLS, rb = (O + 3) / 4;
+    const int tb = (I + TU_COLS - 1) / TU_COLS, rb = O;
     float* t = ws;
     float* r = t + I;
     float* tpart = r + O;
@@ -159,7 +208,8 @@ extern "C" int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_cop
     VFM_LAUNCH(sn_wtu, dim3(tb), dim3(THREADS), 0, st, W, u, t, tpart, O, I);
     VFM_LAUNCH(sn_wv, dim3(rb), dim3(THREADS), 0, st, W, t, tpart, tb, v, v_copy, r, rpart, O, I, eps);
     const long long n = (long long)O * I;
-    const int sb = (int)std::min<long long>(SCALE_BLOCKS, (n + THREADS - 1) / THREADS);
+    const long long work = (n & 3) ? n : n / 4;       // threads' items (float4 when n % 4 == 0)
+    const int sb = (int)std::min<long long>(4096, (work + THREADS - 1) / THREADS);
     VFM_LAUNCH(sn_scale, dim3(sb), dim3(THREADS), 0, st, W, r, rpart, rb, u, u_copy, sigma, Wsn, O, n, eps);
     return launch_status();
 }
