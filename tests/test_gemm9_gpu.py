@@ -164,3 +164,60 @@ def test_gemm9_operands_past_2gib():
     for b in range(z):
         ref += dh[b].float() @ m[b].float().t()
     assert dw is not None and _rel(dw, ref) < 2e-5
+
+
+def _f32(*shape, g):
+    return (torch.rand(*shape, generator=g) * 2 - 1).to(DEV)
+
+
+def _route_f32(a, b, g9, **kw):
+    """fp32 product on the 256-tile f32x6 route: gemm9's persistent kernel (vfm_gemm9_pieces) or gemm8's."""
+    prev = gemm_hip.G9_F32
+    gemm_hip.G9_F32 = g9
+    try:
+        return gemm_hip.try_gemm(a, b, route=("g8", 0), **kw)
+    finally:
+        gemm_hip.G9_F32 = prev
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("a_kc", [True, False])
+@pytest.mark.parametrize("b_kc", [True, False])
+@pytest.mark.parametrize("M,N,K,z", [(512, 512, 256, 1), (304, 264, 64, 1), (264, 520, 128, 2), (1024, 768, 1024, 1)])
+def test_gemm9_f32x6_pieces(a_kc, b_kc, M, N, K, z):
+    """f32x6 on gemm9 (six piece products of a real K-tile as consecutive virtual K-tiles, planar pieces of
+    the whole fp32 tensors) against fp64: within twice hipBLASLt's exact-fp32 error, and equal to gemm8's f32x6
+    route (same piece products, same K order, same MFMA)."""
+    if M % 8 and not a_kc:
+        pytest.skip("M-contiguous A needs M % 8 == 0 (16-B DMA chunks)")
+    g = torch.Generator().manual_seed(M + N + K + z)
+    A = _f32(z, M, K, g=g)
+    Bt = _f32(z, N, K, g=g)
+    a = A if a_kc else A.transpose(1, 2).contiguous().transpose(1, 2)
+    b = Bt.transpose(1, 2) if b_kc else Bt.transpose(1, 2).contiguous()
+    if z == 1:
+        a, b = a[0], b[0]
+    ref = (A.double() @ Bt.double().transpose(1, 2))
+    vend = (A @ Bt.transpose(1, 2))
+    out = _route_f32(a, b, True)
+    out8 = _route_f32(a, b, False)
+    assert out is not None and out.shape == out8.shape
+    out = out.reshape(ref.shape)
+    err, err_v = _rel(out, ref), _rel(vend, ref)
+    assert err <= 2 * err_v + 1e-7, (err, err_v)
+    assert _rel(out, out8.reshape(ref.shape)) < 1e-6
+
+
+@pytest.mark.gpu
+def test_gemm9_f32x6_bias_alpha_stacked():
+    """The bias / alpha epilogue of the f32x6 form and the stacked piece layout (a view that does not cover its
+    tensor: per-product split along K)."""
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 520, 384, 320
+    big = _f32(M, 2 * K, g=g)
+    A = big[:, :K]                              # a column slice: stacked pieces, not planar
+    Bt = _f32(N, K, g=g)
+    bias = _f32(N, g=g)
+    ref = 0.5 * (A.double() @ Bt.double().t()) + bias.double()
+    out = _route_f32(A, Bt.t(), True, bias=bias, bias_dim=1, alpha=0.5)
+    assert _rel(out, ref) < 2e-6

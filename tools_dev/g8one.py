@@ -11,7 +11,9 @@ from torch_utils.ops import gemm_hip
 
 M, N, K = (int(os.environ.get(k, d)) for k, d in (("G8_M", 8192), ("G8_N", 8192), ("G8_K", 4096)))
 Z = int(os.environ.get("G8_Z", 1))
-KIND = os.environ.get("G8_KIND", "g8")          # g8 / g9 / blas (hipBLASLt through torch)
+KIND = os.environ.get("G8_KIND", "g8")          # g8 / g9 / g9f (f32x6 on gemm9) / blas (hipBLASLt through torch)
+if KIND == "g9f":
+    gemm_hip.G9_F32, KIND = True, "g8"
 dt = torch.float32 if os.environ.get("G8_DT", "bf16") == "f32" else torch.bfloat16   # f32: the f32x6 products
 if Z > 1:   # the decoder's 1x1 conv form: shared weight [M, K] times per-sample planes [Z, K, N]
     A = (torch.rand(M, K, device="cuda") * 2 - 1).to(dt)

@@ -71,6 +71,11 @@ struct G9Args {
     const float* rscale;
     float* rs0;
     float* rs1;
+    // fp32-equivalent products (NP = 3, csrc/gemm8.hip's f32x6): fp32 operands as three exact bf16 pieces, T = 6
+    // product terms per real K-tile run back to back as "virtual" K-tiles (term-fastest), term t reading piece
+    // (pa >> 2t) & 3 of A at psA elements per piece and (pb >> 2t) & 3 of B at psB; T = 1 for bf16 operands
+    int T, pa, pb;
+    long long psA, psB;
 };
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -526,11 +531,11 @@ __device__ __forceinline__ void item_k_range(const G9Args& a, int z, int KT, int
         n = min(V, v0 + a.kchunk) - v0;
     } else {
         v0 = 0;
-        n = KT;
+        n = KT * a.T;
     }
 }
 
-template <bool AK, bool BKC, bool OUTF32, int EPI>
+template <bool AK, bool BKC, bool OUTF32, int EPI, int NP = 1>
 __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -554,6 +559,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     };
     int d_item = blockIdx.x, d_kt = 0, d_k = 0;   // d_k: the cursor item's index among this workgroup's items
     int d_KT = KT, d_v0 = 0, d_z = 0;             // the cursor item's K-tiles, first reduction K-tile, batch
+    int d_term = 0, d_kk = 0;                     // (NP = 3) the cursor's product term and real K-tile
     long long offA = 0, offB = 0;                 // byte offsets of the cursor item's tile origin in A / B
     long long offS = 0, offR = 0;                 // byte offsets of the cursor item's bias values / row scales
     auto setup_dma = [&](int item) __attribute__((always_inline)) {
@@ -603,14 +609,19 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     };
     auto point = [&]() __attribute__((always_inline)) {
         const bool live = d_item < total;
-        int zt = d_z, kk = d_kt;
-        if (a.reduce) {                         // reduction K-tile v -> (batch, K-tile of that batch)
+        int zt = d_z, kk = NP > 1 ? d_kk : d_kt;
+        if (NP == 1 && a.reduce) {              // reduction K-tile v -> (batch, K-tile of that batch)
             const int v = d_v0 + d_kt;
             zt = v / a.KTz;
             kk = v - zt * a.KTz;
         }
-        const long long cA = offA + (zt * a.sA + (long long)kk * (dkA / 2)) * 2;
-        const long long cB = offB + (zt * a.sB + (long long)kk * (dkB / 2)) * 2;
+        long long pofa = 0, pofb = 0;           // the term's piece planes
+        if (NP > 1) {
+            pofa = ((a.pa >> (2 * d_term)) & 3) * a.psA;
+            pofb = ((a.pb >> (2 * d_term)) & 3) * a.psB;
+        }
+        const long long cA = offA + (zt * a.sA + (long long)kk * (dkA / 2) + pofa) * 2;
+        const long long cB = offB + (zt * a.sB + (long long)kk * (dkB / 2) + pofb) * 2;
         const unsigned long long pA = (unsigned long long)((const char*)a.A + cA);
         const unsigned long long pB = (unsigned long long)((const char*)a.B + cB);
         aLo = __builtin_amdgcn_readfirstlane((unsigned)pA);
@@ -636,9 +647,17 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     auto advance = [&]() __attribute__((always_inline)) {
         if (++d_kt == d_KT) {
             d_kt = 0;
+            d_term = 0;
+            d_kk = 0;
             d_item += G;
             ++d_k;
             if (d_item < total) setup_dma(d_item);
+            point();
+        } else if (NP > 1) {                    // next term of the real K-tile, or the next real K-tile
+            if (++d_term == a.T) {
+                d_term = 0;
+                ++d_kk;
+            }
             point();
         } else if (a.reduce) {
             point();
@@ -881,6 +900,32 @@ __global__ __launch_bounds__(256) void gemm9_reduce(const float* __restrict__ ws
 
 int g_persistent = 1;            // vfm_gemm9_set_mode: 1 persistent (default), 0 one workgroup per tile
 
+// fp32-equivalent (NP = 3) products: fp32 C, plain or bias epilogue, persistent form
+template <bool AK, bool BKC>
+void launch9_pieces(const G9Args& a, int batch, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, true, 0, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+        (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, true, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
+        attr = true;
+    }
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    const long long total = (long long)nwg * batch;
+    const int grid = (int)std::min<long long>(total, cus);
+    const bool plain = a.bias_mode == 0 && a.alpha == 1.f;
+    if (plain)
+        VFM_LAUNCH((gemm9p_kernel<AK, BKC, true, 0, 3>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+    else
+        VFM_LAUNCH((gemm9p_kernel<AK, BKC, true, 1, 3>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+}
+
 template <bool AK, bool BKC, bool OUTF32>
 void launch9(const G9Args& a, int batch, hipStream_t st) {
     static bool attr = false;
@@ -957,6 +1002,7 @@ static int gemm9_impl(const void* A, const void* B, void* C, const float* bias, 
     if (spA1 >= (1LL << 31) || spB1 >= (1LL << 31)) return VFM_NO_KERNEL;
     if (!g_persistent && (spA >= (1LL << 31) || spB >= (1LL << 31))) return VFM_NO_KERNEL;
     G9Args a{};
+    a.T = 1;
     a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
@@ -1059,6 +1105,7 @@ extern "C" int vfm_gemm9_gelu(const void* W, const void* X, void* C, void* C2, c
     const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if (nwg * batch > 0x7fffffffLL) return VFM_ERR_ARGS;
     G9Args a{};
+    a.T = 1;
     a.A = (const __hip_bfloat16*)W; a.B = (const __hip_bfloat16*)X; a.C = C; a.C2 = C2;
     a.H = (const __hip_bfloat16*)H; a.rscale = rscale; a.bias = bias; a.rs0 = rsum0; a.rs1 = rsum1;
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = 0; a.sB = sB; a.sC = sC;
@@ -1086,6 +1133,55 @@ extern "C" int vfm_gemm9_gelu(const void* W, const void* X, void* C, void* C2, c
         VFM_LAUNCH((gemm9p_kernel<true, false, false, 4>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
     else
         VFM_LAUNCH((gemm9p_kernel<true, false, false, 5>), dim3(grid), dim3(THREADS), LDS9P, st, a, (int)total);
+    return launch_status();
+}
+
+// fp32 operands given as their three exact bf16 pieces (vfm_split_f32; csrc/gemm8.hip's f32x6 contract): C[z]
+// (fp32, M x N) = alpha sum_t A_pa(t)[z] B_pb(t)[z] + bias over the six product terms of order >= 2^-16, on the
+// persistent gemm9 kernel (the terms of a real K-tile as consecutive virtual K-tiles). psA / psB: elements
+// between an operand's pieces (0: the stacked layouts, pieces along K). Plain or bias epilogues only (no split,
+// beta 0, no activation); VFM_NO_KERNEL for what it does not take.
+extern "C" int vfm_gemm9_pieces(const void* A, const void* B, float* C, const float* bias, int M, int N, int K,
+                                int batch, int a_kcont, long long lda, long long sA, long long psA, int b_kcont,
+                                long long ldb, long long sB, long long psB, long long ldc, long long sC, float alpha,
+                                int bias_mode, void* stream) {
+    if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
+    if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || psA < 0 || psB < 0) return VFM_ERR_ARGS;
+    if (K % BK || N % 8) return VFM_NO_KERNEL;
+    const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : N;
+    if (a_c % 8 || b_c % 8 || lda % 8 || ldb % 8 || sA % 8 || sB % 8 || ldc % 8 || sC % 8 || psA % 8 || psB % 8)
+        return VFM_NO_KERNEL;
+    if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16) return VFM_NO_KERNEL;
+    const int kra = (a_kcont && !psA) ? 3 * K : K, krb = (b_kcont && !psB) ? 3 * K : K;
+    if (lda < (a_kcont ? (long long)kra : M) || ldb < (b_kcont ? (long long)krb : N) || ldc < N) return VFM_ERR_ARGS;
+    const long long nwg = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (nwg * batch > 0x7fffffffLL || !g_persistent) return VFM_NO_KERNEL;
+    G9Args a{};
+    a.T = 6;
+    for (int t = 0; t < 6; ++t) {
+        a.pa |= Terms<3>::a(t) << (2 * t);
+        a.pb |= Terms<3>::b(t) << (2 * t);
+    }
+    a.psA = psA ? psA : (a_kcont ? (long long)K : (long long)K * lda);
+    a.psB = psB ? psB : (b_kcont ? (long long)K : (long long)K * ldb);
+    // spans: one batch element's piece-0 extent plus the two further planes (the tile offsets of one batch
+    // element below 2^31: the descriptor bases move per tile, as in vfm_gemm9)
+    const long long spA1 = span9(a_kcont, M, K, lda, 0, 1) + 2 * a.psA * 2;
+    const long long spB1 = span9(b_kcont, N, K, ldb, 0, 1) + 2 * a.psB * 2;
+    if (spA1 >= (1LL << 31) || spB1 >= (1LL << 31)) return VFM_NO_KERNEL;
+    a.spanA = span9(a_kcont, M, K, lda, sA, batch) + 2 * a.psA * 2;
+    a.spanB = span9(b_kcont, N, K, ldb, sB, batch) + 2 * a.psB * 2;
+    const long long spC1 = ((long long)(M - 1) * ldc + N) * 4;
+    if (spC1 >= (1LL << 31)) return VFM_NO_KERNEL;
+    a.spanC = spC1 + (long long)(batch - 1) * sC * 4;
+    a.A = (const __hip_bfloat16*)A; a.B = (const __hip_bfloat16*)B; a.C = C; a.bias = bias;
+    a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
+    a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = 0.f; a.bias_mode = bias_mode; a.act = 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (a_kcont && b_kcont) launch9_pieces<true, true>(a, batch, st);
+    else if (a_kcont) launch9_pieces<true, false>(a, batch, st);
+    else if (b_kcont) launch9_pieces<false, true>(a, batch, st);
+    else launch9_pieces<false, false>(a, batch, st);
     return launch_status();
 }
 

@@ -119,6 +119,9 @@ BF16_OWN = __import__("os").environ.get("VFM_BF16_GEMM", "hip") == "hip"
 F32_SMALL_OWN = __import__("os").environ.get("VFM_F32_SMALL", "torch") == "hip"
 # bf16 products on gemm9 (csrc/gemm9.hip); False: gemm8's 256-tile pipeline (tests, A/B)
 G9 = __import__("os").environ.get("VFM_GEMM9", "1") == "1"
+# fp32 (f32x6) products of the 256-tile route on gemm9's persistent kernel (vfm_gemm9_pieces) instead of gemm8:
+# same-box bench A/B +1.8 %, f32x6 GEMM time 70.6 -> 65.2 ms/step (profiles/r5_x_g9f32_ab.txt); VFM_GEMM9_F32=0: gemm8
+G9_F32 = __import__("os").environ.get("VFM_GEMM9_F32", "1") == "1"
 
 
 _WS = {}
@@ -325,6 +328,21 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             prec, tag = custom_ops.VFM_BF16, "bf16"
             Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB = a3, a_kc, lda, sA, b3, b_kc, ldb, sB
             a_off = b_off = 0
+        if (Ak is not None and Bk is not None and A.dtype == torch.float32 and G9_F32 and int(arg) == 0
+                and not reduce_batch and beta == 0.0 and act is None and out_dtype == torch.float32
+                and prec == custom_ops.VFM_F32):
+            # f32x6 on the persistent one-wave-per-SIMD kernel: the six piece products of a real K-tile as
+            # consecutive virtual K-tiles (csrc/gemm9.hip vfm_gemm9_pieces)
+            region = f"gemm9<f32x6,{tb(fa_kc)},{tb(fb_kc)},true>"
+            if kernel_timer.SHAPES:
+                region += f"[{M}x{N}x{K}x{z}]"
+            with kernel_timer.region(region, nbytes, flops, "mfma"):
+                rc = _lib.vfm_gemm9_pieces(Ak.data_ptr() + 2 * a_off, Bk.data_ptr() + 2 * b_off, out.data_ptr(),
+                                           custom_ops.ptr(bias), M, N, K, z, int(fa_kc), flda, fsA, psA, int(fb_kc),
+                                           fldb, fsB, psB, ldc, sC, float(alpha), bias_mode, stream)
+            if rc != custom_ops.VFM_NO_KERNEL:
+                custom_ops.check(rc, "vfm_gemm9_pieces")
+                return out
         if Ak is not None and Bk is not None:
             kchunk = int(arg)
             ws = None
