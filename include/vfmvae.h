@@ -433,10 +433,14 @@ long long vfm_gemm9_workspace_floats(int M, int N, int K, int batch, int splits,
  * consecutive virtual K-tiles into fp32 accumulators: C[z] (fp32) = alpha A[z] B[z] + bias. The decoder's
  * fp32 1x1 convolutions, the GigaGAN attention / FFN projections and the adapter linears (reference
  * networks/utils/convnext_utils.py:135-138, gigagan_utils.py:53-185, ldm_utils.py:55-166, fp32 with TF32 off:
- * training/training_loop.py:504-505). No split, beta 0, no activation; VFM_NO_KERNEL when not covered. */
+ * training/training_loop.py:504-505). splits > 1 and / or reduce_batch (C = alpha sum_z A[z] B[z], [M, N]): whole real
+ * K-tiles of the batch-concatenated reduction in S chunks of fp32 partials in `workspace`
+ * (vfm_gemm9_workspace_floats), combined in a fixed order (no bias then). Beta 0, no activation;
+ * VFM_NO_KERNEL when not covered. */
 int vfm_gemm9_pieces(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int batch,
                      int a_kcont, long long lda, long long sA, long long psA, int b_kcont, long long ldb, long long sB,
-                     long long psB, long long ldc, long long sC, float alpha, int bias_mode, void* stream);
+                     long long psB, long long ldc, long long sC, float alpha, int bias_mode, float* workspace,
+                     int splits, int reduce_batch, void* stream);
 /* The ConvNeXt MLP's bf16 1x1 GEMMs on the persistent gemm9 kernel with the GELU in the epilogue (replaces
  * pwconv1 -> nn.GELU and the GELU backward of reference networks/utils/convnext_utils.py:135-142 under
  * autocast): C[z] = W[M, K] X[z][K, N] (W K-contiguous, lda; X N-contiguous, ldb, batch stride sB);

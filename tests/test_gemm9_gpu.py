@@ -172,12 +172,12 @@ def _f32(*shape, g):
 
 def _route_f32(a, b, g9, **kw):
     """fp32 product on the 256-tile f32x6 route: gemm9's persistent kernel (vfm_gemm9_pieces) or gemm8's."""
-    prev = gemm_hip.G9_F32
-    gemm_hip.G9_F32 = g9
+    prev = gemm_hip.G9_F32, gemm_hip.G9F_BIAS
+    gemm_hip.G9_F32 = gemm_hip.G9F_BIAS = g9
     try:
         return gemm_hip.try_gemm(a, b, route=("g8", 0), **kw)
     finally:
-        gemm_hip.G9_F32 = prev
+        gemm_hip.G9_F32, gemm_hip.G9F_BIAS = prev
 
 
 @pytest.mark.gpu
@@ -221,3 +221,80 @@ def test_gemm9_f32x6_bias_alpha_stacked():
     ref = 0.5 * (A.double() @ Bt.double().t()) + bias.double()
     out = _route_f32(A, Bt.t(), True, bias=bias, bias_dim=1, alpha=0.5)
     assert _rel(out, ref) < 2e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("a_kc,b_kc", [(True, False), (False, True), (True, True), (False, False)])
+@pytest.mark.parametrize("O,I,P,Bn", [(512, 256, 1024, 6), (304, 264, 320, 3), (2048, 512, 256, 32)])
+def test_gemm9_f32x6_batch_reduced(a_kc, b_kc, O, I, P, Bn):
+    """sum_b dy[b] x[b]^T (the decoder's fp32 1x1 weight gradients) on gemm9's f32x6 form through the auto
+    route: chunks of whole real K-tiles of the batch-concatenated reduction, fp32 partials, fixed-order combine;
+    against fp64 and deterministic."""
+    from torch_utils.ops import kernel_timer
+    g = torch.Generator().manual_seed(O + I + P + Bn)
+    dy = _f32(Bn, O, P, g=g)
+    x = _f32(Bn, I, P, g=g)
+    A = dy if a_kc else dy.transpose(1, 2).contiguous().transpose(1, 2)
+    Bm = x.transpose(1, 2) if b_kc else x.transpose(1, 2).contiguous()
+    kernel_timer.enable(True)
+    prev = gemm_hip.G9F_PLAN
+    gemm_hip.G9F_PLAN = True
+    try:
+        dW = gemm_hip.try_gemm(A, Bm, out_dtype=torch.float32, reduce_batch=True, auto=True)
+        torch.cuda.synchronize()
+        names = list(kernel_timer.summary())
+        again = gemm_hip.try_gemm(A, Bm, out_dtype=torch.float32, reduce_batch=True, auto=True)
+    finally:
+        kernel_timer.enable(False)
+        gemm_hip.G9F_PLAN = prev
+    assert any(n.startswith("gemm9<f32x6") for n in names), names
+    ref = (dy.double() @ x.double().transpose(1, 2)).sum(0)
+    vend = (dy @ x.transpose(1, 2)).sum(0)
+    assert _rel(dW, ref) <= 2 * _rel(vend, ref) + 1e-7
+    assert torch.equal(dW, again)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(512, 384, 4096), (6304, 384, 1536), (3072, 1024, 8192)])
+def test_gemm9_f32x6_split_k(M, N, K):
+    """Single products with fewer 256-tiles than CUs (the DINO tower's narrow outputs, the token-major linears'
+    weight gradients): K split into chunks of real K-tiles, fp32 partials, fixed-order combine."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = _f32(M, K, g=g)
+    Bt = _f32(N, K, g=g)
+    assert gemm_hip._splits9f(M, N, K, 1, False) > 1
+    prev = gemm_hip.G9F_PLAN
+    gemm_hip.G9F_PLAN = True
+    try:
+        out = gemm_hip.try_gemm(A, Bt.t(), out_dtype=torch.float32, auto=True)
+        again = gemm_hip.try_gemm(A, Bt.t(), out_dtype=torch.float32, auto=True)
+    finally:
+        gemm_hip.G9F_PLAN = prev
+    ref = A.double() @ Bt.double().t()
+    vend = A @ Bt.t()
+    assert _rel(out, ref) <= 2 * _rel(vend, ref) + 1e-7
+    assert torch.equal(out, again)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("a_kc,b_kc", [(True, False), (False, True), (True, True), (False, False)])
+@pytest.mark.parametrize("bias_dim", [0, 1, None])
+@pytest.mark.parametrize("M,N,K,z,alpha", [(512, 256, 512, 1, 1.0), (1024, 512, 192, 1, 0.5), (384, 1024, 1024, 2, 1.0)])
+def test_gemm9_f32x6_epilogue_layouts(a_kc, b_kc, bias_dim, M, N, K, z, alpha):
+    """f32x6 on gemm9 through the pinned 256-tile route with a per-row / per-column bias and alpha, every layout,
+    few output tiles (one workgroup per item)."""
+    g = torch.Generator().manual_seed(M * 7 + N + K + z)
+    A = _f32(z, M, K, g=g)
+    Bt = _f32(z, N, K, g=g)
+    a = A if a_kc else A.transpose(1, 2).contiguous().transpose(1, 2)
+    b = Bt.transpose(1, 2) if b_kc else Bt.transpose(1, 2).contiguous()
+    if z == 1:
+        a, b = a[0], b[0]
+    bias = None if bias_dim is None else _f32(M if bias_dim == 0 else N, g=g)
+    ref = alpha * (A.double() @ Bt.double().transpose(1, 2))
+    if bias_dim == 0:
+        ref = ref + bias.double()[:, None]
+    elif bias_dim == 1:
+        ref = ref + bias.double()
+    out = _route_f32(a, b, True, bias=bias, bias_dim=bias_dim, alpha=alpha)
+    assert _rel(out.reshape(ref.shape), ref) < 2e-6

@@ -172,6 +172,7 @@ def g8_schedule(request, monkeypatch):
     from torch_utils import custom_ops
     from torch_utils.ops import gemm_hip
     monkeypatch.setattr(gemm_hip, "G9", False)
+    monkeypatch.setattr(gemm_hip, "G9_F32", False)
     lib = custom_ops.get_native()
     prev = lib.vfm_gemm8_set_schedule(request.param)
     yield request.param

@@ -526,7 +526,7 @@ __device__ __forceinline__ void gelu_epilogue9(const G9Args& a, const f32x4 (&ac
 // K range of an item: its batch's KT K-tiles, or (reduce) chunk s = z of the batch-concatenated reduction
 __device__ __forceinline__ void item_k_range(const G9Args& a, int z, int KT, int& v0, int& n) {
     if (a.reduce) {
-        const int V = a.KTz * a.reduce;
+        const int V = a.KTz * a.reduce * a.T;            // virtual K-tiles (kchunk: a multiple of T)
         v0 = z * a.kchunk;
         n = min(V, v0 + a.kchunk) - v0;
     } else {
@@ -537,6 +537,7 @@ __device__ __forceinline__ void item_k_range(const G9Args& a, int z, int KT, int
 
 template <bool AK, bool BKC, bool OUTF32, int EPI, int NP = 1>
 __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total) {
+    constexpr int NP_T = NP == 3 ? 6 : NP == 2 ? 3 : 1;     // product terms per real K-tile (a.T)
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -610,8 +611,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     auto point = [&]() __attribute__((always_inline)) {
         const bool live = d_item < total;
         int zt = d_z, kk = NP > 1 ? d_kk : d_kt;
-        if (NP == 1 && a.reduce) {              // reduction K-tile v -> (batch, K-tile of that batch)
-            const int v = d_v0 + d_kt;
+        if (a.reduce) {                         // reduction K-tile v -> (batch, K-tile of that batch)
+            const int v = NP > 1 ? d_v0 / NP_T + d_kk : d_v0 + d_kt;
             zt = v / a.KTz;
             kk = v - zt * a.KTz;
         }
@@ -1144,7 +1145,7 @@ extern "C" int vfm_gemm9_gelu(const void* W, const void* X, void* C, void* C2, c
 extern "C" int vfm_gemm9_pieces(const void* A, const void* B, float* C, const float* bias, int M, int N, int K,
                                 int batch, int a_kcont, long long lda, long long sA, long long psA, int b_kcont,
                                 long long ldb, long long sB, long long psB, long long ldc, long long sC, float alpha,
-                                int bias_mode, void* stream) {
+                                int bias_mode, float* workspace, int splits, int reduce_batch, void* stream) {
     if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return VFM_ERR_ARGS;
     if (bias_mode < 0 || bias_mode > 2 || (bias_mode && !bias) || psA < 0 || psB < 0) return VFM_ERR_ARGS;
     if (K % BK || N % 8) return VFM_NO_KERNEL;
@@ -1178,10 +1179,37 @@ extern "C" int vfm_gemm9_pieces(const void* A, const void* B, float* C, const fl
     a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
     a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = 0.f; a.bias_mode = bias_mode; a.act = 0;
     hipStream_t st = (hipStream_t)stream;
-    if (a_kcont && b_kcont) launch9_pieces<true, true>(a, batch, st);
-    else if (a_kcont) launch9_pieces<true, false>(a, batch, st);
-    else if (b_kcont) launch9_pieces<false, true>(a, batch, st);
-    else launch9_pieces<false, false>(a, batch, st);
+    auto go = [&](const G9Args& g, int items_batch) {
+        if (a_kcont && b_kcont) launch9_pieces<true, true>(g, items_batch, st);
+        else if (a_kcont) launch9_pieces<true, false>(g, items_batch, st);
+        else if (b_kcont) launch9_pieces<false, true>(g, items_batch, st);
+        else launch9_pieces<false, false>(g, items_batch, st);
+    };
+    if (reduce_batch || splits > 1) {
+        // K-split and / or batch-reduced product (vfm_gemm9_ex's scheme): S chunks of whole real K-tiles of the
+        // batch-concatenated reduction (each chunk its six terms per real K-tile) into fp32 partials, then the
+        // fixed-order combine
+        if (!workspace || bias_mode) return VFM_NO_KERNEL;
+        if (!reduce_batch && batch != 1) return VFM_NO_KERNEL;
+        const int KTz = K / BK, V = KTz * batch;
+        const int S0 = std::max(1, std::min(splits, V));
+        const int kcr = (V + S0 - 1) / S0;
+        a.reduce = batch;
+        a.KTz = KTz;
+        a.kchunk = kcr * a.T;
+        a.S = (V + kcr - 1) / kcr;
+        const long long MN = (long long)M * N;
+        if (MN * 4 >= (1LL << 31) || MN % 4) return VFM_NO_KERNEL;
+        G9Args p = a;
+        p.C = workspace; p.ldc = N; p.sC = MN; p.alpha = 1.f;
+        p.spanC = MN * a.S * 4;
+        p.bias = nullptr; p.bias_mode = 0;
+        go(p, a.S);
+        const int blocks = (int)std::min<long long>((MN / 4 + 255) / 256, 4096);
+        VFM_LAUNCH(gemm9_reduce<true>, dim3(blocks), dim3(256), 0, st, workspace, C, M, N, ldc, a.S, alpha);
+        return launch_status();
+    }
+    go(a, batch);
     return launch_status();
 }
 

@@ -140,7 +140,7 @@ SIGNATURES = {
                      c_float, c_vp, c_int, c_int, c_vp],
     "vfm_gemm9_workspace_floats": [c_int, c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm9_pieces": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_ll, c_ll,
-                         c_ll, c_ll, c_ll, c_float, c_int, c_vp],
+                         c_ll, c_ll, c_ll, c_float, c_int, c_vp, c_int, c_int, c_vp],
     "vfm_gemm9": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,

@@ -193,6 +193,50 @@ def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
 
 
 SPLIT_TILES = 128           # fewer 256-tiles than this: the 128-tile kernel (auto routing)
+
+
+# f32x6 routing by _splits9f (batch-reduced weight gradients and few-tile products split on gemm9) instead of
+# _plan's choice with gemm9 standing in for gemm8 only: opt-in (VFM_G9F_PLAN=1). Measured slower in the step
+# (r5ai: 87.9 img/s, f32x6 GEMM time 65.4 -> 76.7 ms/step): the batched products with few tiles per sample ran
+# unsplit at a fraction of the CUs, where the 128-tile kernel's K splits fill the chip
+G9F_PLAN = __import__("os").environ.get("VFM_G9F_PLAN", "0") == "1"
+SPLIT9F = __import__("os").environ.get("VFM_G9F_SPLIT", "1") == "1"     # 0: f32x6 single products unsplit (A/B)
+# biased f32x6 products on gemm9 (VFM_G9F_BIAS=0: on gemm8 / the 128-tile kernel). Through the opt-in planner
+# (G9F_PLAN) the few-tile biased linears of the adapter at batch 1 ran unsplit on gemm9 instead of split-K on the
+# 128-tile kernel: each product within fp32 rounding of fp64 (3e-6, tools_dev/g9f_bias_probe.py; no stray writes,
+# tools_dev/g9f_guard_probe.py) but the K-long fp32 sums are ~8x less accurate than the split ones, which the
+# adapter's attention amplifies past the full-size backward pin's 2e-4 (projection errors up to 3e-3); on the
+# default route gemm9 only stands in for gemm8, whose K order and rounding it shares
+G9F_BIAS = __import__("os").environ.get("VFM_G9F_BIAS", "1") == "1"
+
+
+_G9F_CHECK = __import__("os").environ.get("VFM_G9F_CHECK") == "1"
+
+
+def _check9f(a3, b3, out, bias, bias_dim, alpha, reduce_batch, region, *info):
+    """Debug (VFM_G9F_CHECK=1): an f32x6 gemm9 product against fp64 torch; prints the ones off by > 1e-5."""
+    ref = alpha * torch.matmul(a3.double(), b3.double())
+    if reduce_batch:
+        ref = ref.sum(0)
+    if bias is not None:
+        ref = ref + (bias.double()[:, None] if bias_dim == 0 else bias.double())
+    o = out.double().reshape(ref.shape) if out.numel() == ref.numel() else out.double()
+    e = float((o - ref).abs().max() / (ref.abs().max() + 1e-30))
+    if e > 1e-5:
+        print(f"[g9f check] {region} A{tuple(a3.shape)}{a3.stride()} B{tuple(b3.shape)}{b3.stride()} bias_dim={bias_dim} "
+              f"alpha={alpha} err {e:.2e} info {info}", flush=True)
+
+
+def _splits9f(M, N, K, z, reduce_batch):
+    """K splits of an f32x6 product on gemm9's persistent kernel (one workgroup per CU walking the items): the
+    batch-reduced weight gradients and the single products with fewer output tiles than CUs (the DINO tower's
+    6304 x 384 products, the token-major linears' weight gradients) cut their reduction into chunks of at least
+    4 real K-tiles until about 256 items fill the chip; batched products run unsplit."""
+    tiles = -(-M // 256) * -(-N // 256) * (1 if reduce_batch else z)
+    if not reduce_batch and (z > 1 or tiles >= 256 or not SPLIT9F):
+        return 1
+    vr = (K // 64) * (z if reduce_batch else 1)
+    return max(1, min(-(-256 // tiles), vr // 4))
 REDUCE_SPLITS = 16          # splits of a batch-reduced weight gradient on the 256-tile kernel
 
 
@@ -223,6 +267,13 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             return out
     if auto and not preferred(A, M, N, reduce_batch):
         return None
+    g9f = None                                  # f32x6 on gemm9: K splits of the product (see _splits9f)
+    if (auto and route is None and G9_F32 and G9F_PLAN and A.dtype == torch.float32 and beta == 0.0 and act is None
+            and (out_dtype or A.dtype) == torch.float32 and K % 64 == 0 and min(M, N) >= 128
+            and custom_ops.f32_precision()[0] == custom_ops.VFM_F32):
+        g9f = _splits9f(M, N, K, z, reduce_batch)
+        if bias is not None and (g9f > 1 or reduce_batch or not G9F_BIAS):
+            g9f = None
     if auto and splits == 1 and A.dtype != torch.bfloat16:
         # few output tiles over a deep reduction (weight gradients of token-major linears):
         # split K so the grid covers the 256 CUs several times (128-tile kernel)
@@ -261,7 +312,7 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     flops = 2.0 * z * M * N * K
     nbytes = gemm_bytes(a3, b3, M, N, K, z, out_dtype, reduce_batch)
     stream = custom_ops.stream_ptr(A.device)
-    kern, arg = route or _plan(A.dtype, M, N, K, z, reduce_batch, splits, auto)
+    kern, arg = route or (("g8", 0) if g9f is not None else _plan(A.dtype, M, N, K, z, reduce_batch, splits, auto))
     tb = lambda v: "true" if v else "false"
     if kern == "g9r" and A.dtype == torch.bfloat16:
         # batch-reduced / K-split product on gemm9 (fp32 partials of arg chunks + fixed-order combine)
@@ -328,20 +379,30 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
             prec, tag = custom_ops.VFM_BF16, "bf16"
             Ak, fa_kc, flda, fsA, Bk, fb_kc, fldb, fsB = a3, a_kc, lda, sA, b3, b_kc, ldb, sB
             a_off = b_off = 0
+        S9 = g9f if g9f is not None else 1
         if (Ak is not None and Bk is not None and A.dtype == torch.float32 and G9_F32 and int(arg) == 0
-                and not reduce_batch and beta == 0.0 and act is None and out_dtype == torch.float32
-                and prec == custom_ops.VFM_F32):
+                and (bias is None or G9F_BIAS)
+                and S9 is not None and (g9f is not None or not reduce_batch) and beta == 0.0 and act is None
+                and out_dtype == torch.float32 and prec == custom_ops.VFM_F32):
             # f32x6 on the persistent one-wave-per-SIMD kernel: the six piece products of a real K-tile as
-            # consecutive virtual K-tiles (csrc/gemm9.hip vfm_gemm9_pieces)
-            region = f"gemm9<f32x6,{tb(fa_kc)},{tb(fb_kc)},true>"
+            # consecutive virtual K-tiles (csrc/gemm9.hip vfm_gemm9_pieces); K splits / the batch reduction
+            # through fp32 partials and the fixed-order combine
+            ws9 = None
+            if S9 > 1 or reduce_batch:
+                n9 = _lib.vfm_gemm9_workspace_floats(M, N, K, z, S9, int(reduce_batch))
+                ws9 = _workspace(max(n9, 1), A.device)
+            region = f"gemm9<f32x6,{tb(fa_kc)},{tb(fb_kc)},true>{'r' if ws9 is not None else ''}"
             if kernel_timer.SHAPES:
-                region += f"[{M}x{N}x{K}x{z}]"
+                region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % S9 if S9 > 1 else ''}]"
             with kernel_timer.region(region, nbytes, flops, "mfma"):
                 rc = _lib.vfm_gemm9_pieces(Ak.data_ptr() + 2 * a_off, Bk.data_ptr() + 2 * b_off, out.data_ptr(),
                                            custom_ops.ptr(bias), M, N, K, z, int(fa_kc), flda, fsA, psA, int(fb_kc),
-                                           fldb, fsB, psB, ldc, sC, float(alpha), bias_mode, stream)
+                                           fldb, fsB, psB, ldc, sC, float(alpha), bias_mode, custom_ops.ptr(ws9),
+                                           int(S9), int(reduce_batch), stream)
             if rc != custom_ops.VFM_NO_KERNEL:
                 custom_ops.check(rc, "vfm_gemm9_pieces")
+                if _G9F_CHECK:
+                    _check9f(a3, b3, out, bias, bias_dim, alpha, reduce_batch, region, fa_kc, fb_kc, a_off, b_off, psA, psB)
                 return out
         if Ak is not None and Bk is not None:
             kchunk = int(arg)
