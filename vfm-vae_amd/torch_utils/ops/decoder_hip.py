@@ -163,6 +163,34 @@ would be baked into the graph and go stale after the next optimizer step)."""
     return wc
 
 
+# The data gradients W^T dY of the fp32 1x1 convolutions read W^T as the GEMM's A operand: as a view it is
+# M-contiguous, which gemm9 stages with transposed LDS reads (two ds_read_b64_tr_b16 per fragment); a row-major
+# copy of W^T (K-contiguous A, its f32x6 pieces split once) runs the kernel's direct-read form: f32x6 data-gradient
+# GEMM time 24.1 -> 19.9 ms/step (same-box A/B, profiles/r5_am_wt_copy_ab.txt). Not for bf16 weights (their (t, f)
+# form measured 0.6 ms/step slower than the transposed reads). Weights change once per optimizer step, so the copy
+# is cached on the weight until its version moves (not while a HIP graph is captured). VFM_WT_COPY=0: the view.
+_WT_COPY = os.environ.get("VFM_WT_COPY", "1") == "1"
+
+
+def _wt(w):
+    """W^T of a [O, I] fp32 weight as a contiguous [I, O] tensor (cached per weight version), else the view."""
+    if not _WT_COPY or not w.is_cuda or w.dim() != 2 or w.dtype != torch.float32:
+        return w.t()
+    if torch.cuda.is_current_stream_capturing():
+        return w.t().contiguous()
+    base = w._base if w._base is not None else w
+    key = (w.data_ptr(), tuple(w.shape), w.stride(), w.dtype, base._version)
+    hit = getattr(base, "_vfm_wt", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    wt = w.detach().t().contiguous()
+    try:
+        base._vfm_wt = (key, wt)
+    except AttributeError:
+        pass
+    return wt
+
+
 # Dense products of the decoder on the MFMA GEMM (csrc/gemm.hip: bf16, or fp32 operands with
 # fp32-equivalent f32x6 products); VFM_GEMM=torch keeps hipBLASLt (A/B switch). Shapes the kernel does not
 # cover fall back to torch.bmm explicitly.
@@ -265,7 +293,7 @@ class _Pointwise(custom_ops.FastFunction):
             return weight_grad_1x1(dy, x, ctx.wdt)
 
         def dgrad():
-            dx = _gemm(wc.t(), dy, cache_a=True)
+            dx = _gemm(_wt(wc), dy, cache_a=True)
             if dx is None:
                 with kernel_timer.vendor_gemm(f"{_tn(dy)},1x1_dx", I, P, O, B, dy.element_size()):
                     dx = torch.bmm(wc.t().expand(B, I, O), dy)
@@ -738,7 +766,7 @@ class _ConvNeXtMLPGemm(custom_ops.FastFunction):
             # dg = W2^T dy on the plain GEMM, then the HBM-bound GELU' row kernel: the GELU' epilogue's VALU
             # work (erf GELU + derivative per element) does not overlap the MFMAs at one wave per SIMD and
             # measured slower than this pass (profiles/r5_j_benchshape.txt: 17.6 ms/step vs ~3 + 7 ms/step)
-            dg = _g8(w2c.t(), dy)
+            dg = _g8(_wt(w2c), dy)
             dh = torch.empty_like(h)
             O = h.shape[1]
             ds_rows = torch.empty([B * O], dtype=torch.float32, device=h.device) if s is not None else None
@@ -756,7 +784,7 @@ class _ConvNeXtMLPGemm(custom_ops.FastFunction):
         if _wanted(ctx, 1):
             dw1 = weight_grad_1x1(dh, m, w1dt)
         if ctx.needs_input_grad[0]:
-            dm = _g8(w1c.t(), dh)
+            dm = _g8(_wt(w1c), dh)
         dx = dout if ctx.needs_input_grad[7] and not _stash_residual(ctx.slot, dout) else None
         return dm, dw1, ds, db1, dw2, db2, dgm, dx, None
 
@@ -831,7 +859,7 @@ class _ConvNeXtMLP(custom_ops.FastFunction):
         # dh = (W2^T dy) * GELU'(h*s+b1) * s, with the per-(b, o) sums for d_s and d_b1 (next to dW2 on
         # the side stream, _overlapped)
         tiles = _lib.vfm_pw_gemm_gelu_tiles(P)
-        w2t = w2c.t().contiguous()
+        w2t = _wt(w2c)
 
         def dh_kernel():
             dh = torch.empty_like(h)
@@ -852,7 +880,7 @@ class _ConvNeXtMLP(custom_ops.FastFunction):
             db1 = p1.sum((0, 1)).to(b1dt)
 
         def dm_gemm():
-            dm = _gemm(w1c.t(), dh)
+            dm = _gemm(_wt(w1c), dh)
             if dm is None:
                 with kernel_timer.vendor_gemm(f"{_tn(dh)},1x1_dx", C, dh.shape[2], O, B, dh.element_size()):
                     dm = torch.bmm(w1c.t().expand(B, C, O), dh)
