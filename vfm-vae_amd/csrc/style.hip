@@ -39,7 +39,7 @@ namespace {
 using namespace vfm;
 
 constexpr int THREADS = 256, WAVES = THREADS / 64, RB = 4;
-constexpr int KCH = 64;                  // K range of one column-sum block
+constexpr int KCH = 32;                  // K range of one column-sum block (32: four load round trips per column at unroll 8; 64 took eight)
 constexpr int SPASS = 32;                // samples per pass of the column sums
 
 struct StyleArgs {

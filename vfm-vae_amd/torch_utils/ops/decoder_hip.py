@@ -172,9 +172,10 @@ would be baked into the graph and go stale after the next optimizer step)."""
 _WT_COPY = os.environ.get("VFM_WT_COPY", "1") == "1"
 
 
-def _wt(w):
-    """W^T of a [O, I] fp32 weight as a contiguous [I, O] tensor (cached per weight version), else the view."""
-    if not _WT_COPY or not w.is_cuda or w.dim() != 2 or w.dtype != torch.float32:
+def _wt(w, contiguous=False):
+    """W^T of a [O, I] fp32 weight as a contiguous [I, O] tensor (cached per weight version), else the view;
+    contiguous=True: the cached contiguous copy for any dtype (kernels that take W^T as a plain row-major array)."""
+    if not contiguous and (not _WT_COPY or not w.is_cuda or w.dim() != 2 or w.dtype != torch.float32):
         return w.t()
     if torch.cuda.is_current_stream_capturing():
         return w.t().contiguous()
@@ -859,7 +860,7 @@ class _ConvNeXtMLP(custom_ops.FastFunction):
         # dh = (W2^T dy) * GELU'(h*s+b1) * s, with the per-(b, o) sums for d_s and d_b1 (next to dW2 on
         # the side stream, _overlapped)
         tiles = _lib.vfm_pw_gemm_gelu_tiles(P)
-        w2t = _wt(w2c)
+        w2t = _wt(w2c, contiguous=True)         # vfm_pw_gemm_gelu reads W2^T as a row-major [C][O] array
 
         def dh_kernel():
             dh = torch.empty_like(h)

@@ -227,6 +227,25 @@ def _check9f(a3, b3, out, bias, bias_dim, alpha, reduce_batch, region, *info):
               f"alpha={alpha} err {e:.2e} info {info}", flush=True)
 
 
+DEEP9F = __import__("os").environ.get("VFM_G9F_DEEP", "1") == "1"
+
+
+def _deep9f(M, N, K, z, reduce_batch):
+    """The default f32x6 K-split on gemm9: single products with fewer 256-tiles than CUs over a deep reduction
+    (the adapter's token-major weight gradients, K = 32 x 1024 tokens), cut into S chunks of at least 16 real
+    K-tiles with tiles x S <= 256 (one round of items). tools_dev/g9f_routebench.py (r5aq): 4096x1024x32768
+    1905 -> 1479 us, 1024x4096x32768 1828 -> 1451, 1024x1024x32768 557 -> 447 against the 128-tile kernel's
+    split-K; at S = 6 for 48 tiles (288 items, a second round of 32) it lost (1578 -> 1980), and the DINO tower's
+    K <= 1536 products lose on gemm9 at any split. None: the product keeps _plan's route."""
+    if reduce_batch or z > 1 or K < 8192 or not DEEP9F:
+        return None
+    tiles = -(-M // 256) * -(-N // 256)
+    if tiles >= 256:
+        return None
+    S = min(256 // tiles, (K // 64) // 16)
+    return S if S >= 2 else None
+
+
 def _splits9f(M, N, K, z, reduce_batch):
     """K splits of an f32x6 product on gemm9's persistent kernel (one workgroup per CU walking the items): the
     batch-reduced weight gradients and the single products with fewer output tiles than CUs (the DINO tower's
@@ -268,11 +287,11 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     if auto and not preferred(A, M, N, reduce_batch):
         return None
     g9f = None                                  # f32x6 on gemm9: K splits of the product (see _splits9f)
-    if (auto and route is None and G9_F32 and G9F_PLAN and A.dtype == torch.float32 and beta == 0.0 and act is None
+    if (auto and route is None and G9_F32 and A.dtype == torch.float32 and beta == 0.0 and act is None
             and (out_dtype or A.dtype) == torch.float32 and K % 64 == 0 and min(M, N) >= 128
             and custom_ops.f32_precision()[0] == custom_ops.VFM_F32):
-        g9f = _splits9f(M, N, K, z, reduce_batch)
-        if bias is not None and (g9f > 1 or reduce_batch or not G9F_BIAS):
+        g9f = _splits9f(M, N, K, z, reduce_batch) if G9F_PLAN else _deep9f(M, N, K, z, reduce_batch)
+        if g9f is not None and bias is not None and (g9f > 1 or reduce_batch or not G9F_BIAS):
             g9f = None
     if auto and splits == 1 and A.dtype != torch.bfloat16:
         # few output tiles over a deep reduction (weight gradients of token-major linears):
