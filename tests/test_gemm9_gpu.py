@@ -298,3 +298,32 @@ def test_gemm9_f32x6_epilogue_layouts(a_kc, b_kc, bias_dim, M, N, K, z, alpha):
         ref = ref + bias.double()
     out = _route_f32(a, b, True, bias=bias, bias_dim=bias_dim, alpha=alpha)
     assert _rel(out.reshape(ref.shape), ref) < 2e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,z,b_kc", [(512, 256, 2048, 32, False), (512, 256, 1088, 8, True), (304, 264, 1024, 3, False)])
+def test_gemm9_f32x6_batched_split(M, N, K, z, b_kc):
+    """Batched products with few tiles per sample (the 16^2 decoder block's 1x1s) on gemm9's batched K-split: chunks
+    of real K-tiles per sample into [z][S] fp32 partials, combined per sample in a fixed order; against fp64,
+    deterministic."""
+    g = torch.Generator().manual_seed(M + N + K + z)
+    A = _f32(M, K, g=g)
+    Bt = _f32(z, N, K, g=g)
+    b = Bt.transpose(1, 2) if b_kc else Bt.transpose(1, 2).contiguous()
+    S = max(2, min(256 // (-(-M // 256) * -(-N // 256) * z), (K // 64) // 4))
+    ws = torch.empty(gemm_hip._lib.vfm_gemm9_workspace_floats(M, N, K, z, S, 0), dtype=torch.float32, device=DEV)
+    pieces = lambda t: gemm_hip._planar(t.unsqueeze(0) if t.dim() == 2 else t, gemm_hip.custom_ops.stream_ptr(t.device))
+    pa, pb = pieces(A), pieces(b)
+    out = torch.empty(z, M, N, dtype=torch.float32, device=DEV)
+    st = gemm_hip.custom_ops.stream_ptr(A.device)
+    b_ld = K if b_kc else N
+    rc = gemm_hip._lib.vfm_gemm9_pieces(pa[0].data_ptr(), pb[0].data_ptr(), out.data_ptr(), None, M, N, K, z, 1, K, 0,
+                                       pa[2], int(b_kc), b_ld, K * N, pb[2], N, M * N, 1.0, 0, ws.data_ptr(), S, 0, st)
+    assert rc == 0
+    again = out.clone()
+    rc = gemm_hip._lib.vfm_gemm9_pieces(pa[0].data_ptr(), pb[0].data_ptr(), again.data_ptr(), None, M, N, K, z, 1, K, 0,
+                                       pa[2], int(b_kc), b_ld, K * N, pb[2], N, M * N, 1.0, 0, ws.data_ptr(), S, 0, st)
+    ref = torch.matmul(A.double(), Bt.double().transpose(1, 2))
+    vend = torch.matmul(A, Bt.transpose(1, 2))
+    assert _rel(out, ref) <= 2 * _rel(vend, ref) + 1e-7
+    assert torch.equal(out, again)

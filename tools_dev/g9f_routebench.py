@@ -30,6 +30,8 @@ cases = [("adapter dW qkv", 3072, 1024, 32768, "ff"), ("adapter dW w0/w1", 4096,
          ("adapter dW w2", 1024, 4096, 32768, "ff"), ("adapter dW proj", 1024, 1024, 32768, "ff"),
          ("dino fc2/proj", 6304, 384, 1536, "tt"), ("dino fc2 dx", 6304, 384, 1536, "tf"),
          ("dino qkv", 6304, 1152, 384, "tt"), ("dino proj", 6304, 384, 384, "tt")]
+ZB = 32
+bcases = [("b1 pwconv2", 512, 256, 2048, "tf"), ("b1 pwconv1 dx", 512, 256, 2048, "tf"), ("b2 small", 512, 1024, 2048, "tf")]
 for name, M, N, K, lay in cases:
     A = (torch.rand(K, M, generator=g) * 2 - 1).cuda().t() if lay[0] == "f" else (torch.rand(M, K, generator=g) * 2 - 1).cuda()
     B = (torch.rand(K, N, generator=g) * 2 - 1).cuda() if lay[1] == "f" else (torch.rand(N, K, generator=g) * 2 - 1).cuda().t()
@@ -39,3 +41,15 @@ for name, M, N, K, lay in cases:
         t = bench(lambda: gemm_hip.try_gemm(A, B, out_dtype=torch.float32, auto=True))
         res.append(f"{'g9 split' if plan else 'default '} {t:8.1f}us {2.0 * M * N * K / t / 1e6:6.1f} TF/s")
     print(f"{name:18s} {M}x{N}x{K} {lay} S={gemm_hip._splits9f(M, N, K, 1, False)} | " + " | ".join(res), flush=True)
+for name, M, N, K, lay in bcases:
+    A = (torch.rand(M, K, generator=g) * 2 - 1).cuda()
+    B = (torch.rand(ZB, K, N, generator=g) * 2 - 1).cuda()
+    res = []
+    for deep in (False, True):
+        gemm_hip.G9F_PLAN, gemm_hip.DEEP9F = False, deep
+        t = bench(lambda: gemm_hip.try_gemm(A, B, out_dtype=torch.float32, auto=True))
+        res.append(f"{'g9 bsplit' if deep else 'default  '} {t:8.1f}us {2.0 * M * N * K * ZB / t / 1e6:6.1f} TF/s")
+    ref = torch.matmul(A.double(), B.double())
+    out = gemm_hip.try_gemm(A, B, out_dtype=torch.float32, auto=True)
+    e = float((out.double() - ref).abs().max() / ref.abs().max())
+    print(f"{name:18s} {M}x{N}x{K}x{ZB} {lay} S={gemm_hip._deep9f(M, N, K, ZB, False)} err {e:.1e} | " + " | ".join(res), flush=True)

@@ -63,6 +63,9 @@ struct G9Args {
     // K-tiles cut into S chunks of kchunk; item (tile, chunk s) writes its fp32 partial to C[s] (the
     // workspace, sC = M N), gemm9_reduce sums the S partials in a fixed order
     int reduce, S, kchunk, KTz;
+    // batched K-split (f32x6 pieces form): item batch index zz = z bs + s, chunk s of batch z's K-tiles; the
+    // partial of (z, s) goes to C[zz] (the workspace), gemm9_reduce_batched sums each batch's bs partials
+    int bs;
     // ConvNeXt-MLP GELU epilogues (EPI 4 / 5, bf16 C; see the epilogue): second output C2 (g), aux input H
     // (h, C's layout), per-(batch, row) scale rscale [Z][M] (null: 1), bias per row, and per-row partial sums
     // rs0 / rs1 [Z][2 tiles_n][M] of the backward (rs0 may be null)
@@ -179,6 +182,24 @@ __device__ __forceinline__ void mfma_acc0(f32x4& c, const bf16x8& x, const bf16x
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
 #define VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+template <int N>
+__device__ __forceinline__ void vmcnt_const() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// operand DMAs of a K-tile moved from phase 2 into phase 3 of the persistent kernel (A/B builds; 0: none)
+#ifndef G9_P3
+#define G9_P3 0
+#endif
+// MFMAs in phase 1 (k-half 0, beside the k-half-1 fragment reads) and phase 3 (k-half 1, beside the next K-tile's
+// k-half-0 reads) of the persistent kernel; phase 2 (the DMA window between the barriers) takes the rest
+#ifndef G9_PH1
+#define G9_PH1 26
+#endif
+#ifndef G9_PH3
+#define G9_PH3 21
+#endif
 
 template <bool AK, bool BKC, bool OUTF32>
 __global__ __launch_bounds__(THREADS, 1) void gemm9_kernel(G9Args a) {
@@ -529,6 +550,10 @@ __device__ __forceinline__ void item_k_range(const G9Args& a, int z, int KT, int
         const int V = a.KTz * a.reduce * a.T;            // virtual K-tiles (kchunk: a multiple of T)
         v0 = z * a.kchunk;
         n = min(V, v0 + a.kchunk) - v0;
+    } else if (a.bs > 1) {                             // batched split: chunk z % bs of the batch's K-tiles
+        const int V = KT * a.T;
+        v0 = (z % a.bs) * a.kchunk;
+        n = min(V, v0 + a.kchunk) - v0;
     } else {
         v0 = 0;
         n = KT * a.T;
@@ -568,7 +593,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
         item_tile(item, nwg, total, tiles_m, tiles_n, z, m0, n0);
         offA = (AK ? (long long)m0 * a.lda : (long long)m0) * 2;
         offB = (BKC ? (long long)n0 * a.ldb : (long long)n0) * 2;
-        d_z = z;
+        d_z = a.bs > 1 ? z / a.bs : z;
         item_k_range(a, z, KT, d_v0, d_KT);
         offS = (long long)(a.bias_mode == 1 ? n0 : m0) * 4;
         offR = ((long long)z * a.M + m0) * 4;
@@ -610,7 +635,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     };
     auto point = [&]() __attribute__((always_inline)) {
         const bool live = d_item < total;
-        int zt = d_z, kk = NP > 1 ? d_kk : d_kt;
+        int zt = d_z, kk = NP > 1 ? d_kk + (a.bs > 1 ? d_v0 / NP_T : 0) : d_kt;
         if (a.reduce) {                         // reduction K-tile v -> (batch, K-tile of that batch)
             const int v = NP > 1 ? d_v0 / NP_T + d_kk : d_v0 + d_kt;
             zt = v / a.KTz;
@@ -701,6 +726,11 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     setup_dma(d_item);
     point();
     constexpr int NG = EPI >= 4 ? 18 : EPI ? 17 : 16;    // DMA instructions per K-tile and wave
+    constexpr int D2 = 16 - G9_P3;                        // operand DMAs in phase 2 (the rest in phase 3)
+    constexpr int PH2 = 128 - G9_PH1 - G9_PH3;            // MFMAs between the two barriers
+    constexpr int PH1 = G9_PH1, PH3 = G9_PH3;
+    constexpr int SP = PH2 / D2;                          // MFMAs per phase-2 DMA
+    static_assert(PH1 >= 16 && PH3 >= 16 && PH1 <= 64 && PH3 <= 64 && SP >= 1, "gemm9 phase split");
 #pragma unroll
     for (int g = 0; g < NG; ++g) dma(g, 0);
     advance();
@@ -725,7 +755,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             constexpr bool first = decltype(first_c)::value;
             const int cur = p & 1;
             if (!AK || !BKC) asm volatile("" : "+v"(flane));
-            // phase 1: 26 MFMAs of k-half 0 beside the 16 reads of k-half 1
+            // phase 1: PH1 MFMAs of k-half 0 beside the 16 reads of k-half 1
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 mf(0, q, first);
@@ -734,49 +764,53 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
                 SB();
             }
 #pragma unroll
-            for (int q = 16; q < 26; ++q) mf(0, q, first);
+            for (int q = 16; q < PH1; ++q) mf(0, q, first);
             SB();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             SB();
-            // phase 2: 38 MFMAs of k-half 0 + 43 of k-half 1 beside the 16 DMA of position p + 2 (every 5th)
+            // phase 2: 64 - PH1 MFMAs of k-half 0 + 64 - PH3 of k-half 1 beside D2 of the 16 operand DMAs of position
+            // p + 2 (every SP-th MFMA); the other P3 ride in phase 3 (G9_P3, default 0: all 16 here)
 #pragma unroll
-            for (int s = 0; s < 81; ++s) {
-                if (s < 38) mf(0, 26 + s, first);
-                else mf(1, s - 38, false);
+            for (int s = 0; s < PH2; ++s) {
+                if (s < 64 - PH1) mf(0, PH1 + s, first);
+                else mf(1, s - (64 - PH1), false);
                 SB();
-                if ((s % 5) == 4 && s / 5 < 16) {
-                    dma(s / 5, cur);
+                if ((s % SP) == SP - 1 && s / SP < D2) {
+                    dma(s / SP, cur);
                     SB();
                 }
-                if (NG > 16 && s == 80) {        // the slot DMAs (EPI > 0) after the operands'
+                if (NG > 16 && s == PH2 - 1) {   // the slot DMAs (EPI > 0) after the operands'
                     dma(16, cur);
                     if (NG > 17) dma(17, cur);
                     SB();
                 }
             }
-            advance();
-            SB();
+            if (G9_P3 == 0) {
+                advance();
+                SB();
+            }
             // position p + 1 landed; younger than it: this iteration's DMA and, in an item's first K-tile, the
             // previous item's stores
             // (fp32 C: 64 stores + 16 DMA younger than the awaited ones exceed vmcnt's 63; waiting for 63 still
             // retires every older operation)
+            // (with G9_P3 > 0 only D2 of this iteration's operand DMAs are younger than position p + 1's)
             if (EPI >= 4) {                     // 64 (h, g) / 48 (dh, row sums) stores: past 63 with the DMA
                 if (t == 0 && stores_young) VMCNT(63);
-                else VMCNT(18);
+                else vmcnt_const<D2 + 2>();
             } else if (EPI) {
                 if (t == 0 && stores_young) {
                     if (OUTF32) VMCNT(63);
-                    else VMCNT(49);
+                    else vmcnt_const<D2 + 33>();
                 } else {
-                    VMCNT(17);
+                    vmcnt_const<D2 + 1>();
                 }
             } else {
                 if (t == 0 && stores_young) {
                     if (OUTF32) VMCNT(63);
-                    else VMCNT(48);
+                    else vmcnt_const<D2 + 32>();
                 } else {
-                    VMCNT(16);
+                    vmcnt_const<D2>();
                 }
             }
             __builtin_amdgcn_s_barrier();
@@ -785,14 +819,22 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
             // end: reads of a buffer that holds nothing, unused)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                mf(1, 43 + q, false);
+                mf(1, 64 - PH3 + q, false);
                 SB();
                 rd(0, q, cur ^ 1);
                 SB();
+                if (G9_P3 > 0 && (q % (16 / (G9_P3 > 0 ? G9_P3 : 1))) == 1 && q / (16 / (G9_P3 > 0 ? G9_P3 : 1)) < G9_P3) {
+                    dma(D2 + q / (16 / (G9_P3 > 0 ? G9_P3 : 1)), cur);
+                    SB();
+                }
             }
 #pragma unroll
-            for (int q = 59; q < 64; ++q) mf(1, q, false);
+            for (int q = 64 - PH3 + 16; q < 64; ++q) mf(1, q, false);
             SB();
+            if (G9_P3 > 0) {
+                advance();
+                SB();
+            }
             ++p;
         };
         ktile(0, std::true_type{});
@@ -896,6 +938,22 @@ __global__ __launch_bounds__(256) void gemm9_reduce(const float* __restrict__ ws
             const uint2 b = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
             *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(C) + m * ldc + n) = b;
         }
+    }
+}
+
+// C[z] = alpha sum_s ws[z S + s] (fixed order) for each batch z: the batched K-split's combine (fp32 C, row
+// stride ldc, batch stride sC)
+__global__ __launch_bounds__(256) void gemm9_reduce_batched(const float* __restrict__ ws, float* C, int M, int N,
+                                                            long long ldc, long long sC, int S, float alpha) {
+    const long long MN = (long long)M * N;
+    const int z = blockIdx.y;
+    const float* w = ws + (long long)z * S * MN;
+    for (long long i4 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i4 < MN; i4 += (long long)gridDim.x * 1024) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(w + i4);
+        for (int k = 1; k < S; ++k) v += *reinterpret_cast<const f32x4*>(w + k * MN + i4);
+        v *= alpha;
+        const int m = (int)(i4 / N), n = (int)(i4 - (long long)m * N);
+        *reinterpret_cast<f32x4*>(C + z * sC + m * ldc + n) = v;
     }
 }
 
@@ -1080,6 +1138,12 @@ extern "C" int vfm_gemm9_ex(const void* A, const void* B, void* C, int out_dtype
 // fp32 workspace floats vfm_gemm9_ex needs (M N S); -1 when the shapes are not covered
 extern "C" long long vfm_gemm9_workspace_floats(int M, int N, int K, int batch, int splits, int reduce_batch) {
     if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || K % BK) return -1;
+    if (!reduce_batch && batch > 1) {                  // the batched K-split of vfm_gemm9_pieces: [batch][S][M][N]
+        const int KTz = K / BK;
+        const int S0 = std::max(1, std::min(splits, KTz));
+        const int kc = (KTz + S0 - 1) / S0;
+        return (long long)M * N * batch * ((KTz + kc - 1) / kc);
+    }
     const int V = (K / BK) * (reduce_batch ? batch : 1);
     const int S0 = std::max(1, std::min(splits, V));
     const int kc = (V + S0 - 1) / S0;
@@ -1190,7 +1254,25 @@ extern "C" int vfm_gemm9_pieces(const void* A, const void* B, float* C, const fl
         // batch-concatenated reduction (each chunk its six terms per real K-tile) into fp32 partials, then the
         // fixed-order combine
         if (!workspace || bias_mode) return VFM_NO_KERNEL;
-        if (!reduce_batch && batch != 1) return VFM_NO_KERNEL;
+        if (!reduce_batch && batch != 1) {
+            // batched K-split: bs chunks of each batch's real K-tiles, partials [batch][bs][M][N] in the workspace
+            const int KTz = K / BK;
+            const int S0 = std::max(1, std::min(splits, KTz));
+            const int kcr = (KTz + S0 - 1) / S0;
+            a.bs = (KTz + kcr - 1) / kcr;
+            a.kchunk = kcr * a.T;
+            const long long MN = (long long)M * N;
+            if (MN * 4 >= (1LL << 31) || MN % 4 || (long long)batch * a.bs > 65535) return VFM_NO_KERNEL;
+            G9Args p = a;
+            p.C = workspace; p.ldc = N; p.sC = MN; p.alpha = 1.f;
+            p.spanC = MN * (long long)batch * a.bs * 4;
+            p.bias = nullptr; p.bias_mode = 0;
+            go(p, batch * a.bs);
+            const int blocks = (int)std::min<long long>((MN / 4 + 255) / 256, 1024);
+            VFM_LAUNCH(gemm9_reduce_batched, dim3(blocks, batch), dim3(256), 0, st, workspace, C, M, N, ldc, sC, a.bs,
+                       alpha);
+            return launch_status();
+        }
         const int KTz = K / BK, V = KTz * batch;
         const int S0 = std::max(1, std::min(splits, V));
         const int kcr = (V + S0 - 1) / S0;

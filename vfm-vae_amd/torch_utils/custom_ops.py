@@ -14,6 +14,9 @@ import threading
 import torch
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libvfmvae_hip.so")
+# A/B builds of the same library (tools_dev experiments): VFM_HIP_LIB names another in-tree build in lib/
+if os.environ.get("VFM_HIP_LIB"):
+    _LIB_PATH = os.path.join(os.path.dirname(_LIB_PATH), os.path.basename(os.environ["VFM_HIP_LIB"]))
 # TORCH_LIBRARY(vfmvae) registration of the reference's plugin ops (csrc/torch_ops.cpp)
 _TORCH_LIB_PATH = os.path.join(os.path.dirname(_LIB_PATH), "libvfmvae_torch.so")
 _torch_ops = None

@@ -237,10 +237,19 @@ def _deep9f(M, N, K, z, reduce_batch):
     1905 -> 1479 us, 1024x4096x32768 1828 -> 1451, 1024x1024x32768 557 -> 447 against the 128-tile kernel's
     split-K; at S = 6 for 48 tiles (288 items, a second round of 32) it lost (1578 -> 1980), and the DINO tower's
     K <= 1536 products lose on gemm9 at any split. None: the product keeps _plan's route."""
-    if reduce_batch or z > 1 or K < 8192 or not DEEP9F:
+    if reduce_batch or not DEEP9F:
         return None
-    tiles = -(-M // 256) * -(-N // 256)
+    tiles = -(-M // 256) * -(-N // 256) * z
     if tiles >= 256:
+        return None
+    if z > 1:
+        # batched products with few tiles per sample (the 16^2 decoder block's 1x1s, 512 x 256 per sample over
+        # K = 2048): chunks of at least 4 real K-tiles of each sample, partials combined per sample
+        if K < 1024:
+            return None
+        S = min(256 // tiles, (K // 64) // 4)
+        return S if S >= 2 else None
+    if K < 8192:
         return None
     S = min(256 // tiles, (K // 64) // 16)
     return S if S >= 2 else None
