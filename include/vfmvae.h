@@ -226,6 +226,12 @@ int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int d
 int vfm_group_norm_fwd(const void* x, const float* w, const float* b, const float* s, void* y,
                        float* mean, float* rstd, int dtype_in, int dtype_out,
                        int B, int C, int G, int HW, float eps, void* stream);
+/* vfm_group_norm_fwd (bf16 x) with each group's statistics merged, in double and a fixed order,
+ * from the producer's per-wave partials stats [B C upc][4] (vfm_dwconv2d_fwd_mfma_gs; upc = units
+ * per (sample, channel) plane) instead of a pass over x: x is read once. */
+int vfm_group_norm_fwd_stats(const void* x, const float* w, const float* b, const float* s, void* y,
+                             float* mean, float* rstd, const float* stats, int upc, int dtype_in, int dtype_out,
+                             int B, int C, int G, int HW, float eps, void* stream);
 
 /* GroupNorm backward: dx (dtype_x); dw_part/db_part [B, C] per-sample
  * contributions to d_weight / d_bias; ds [B, C] (when s != NULL). */
@@ -568,6 +574,13 @@ int vfm_dwconv2d_fwd_mfma_nz(const void* x, const float* w, const float* bias, c
                              void* y, const float* nplane, float* npart, int B, int C, int H, int W, int K, int pad,
                              int flip, void* stream);
 long long vfm_dwconv2d_fwd_mfma_units(int B, int C, int H, int W, int K, int pad);
+/* vfm_dwconv2d_fwd_mfma (no residual, no flip) that also writes the GroupNorm statistics of the
+ * bf16-rounded y: gstat [units][4] (16-B aligned, units = vfm_dwconv2d_fwd_mfma_units(...)) =
+ * {count, shift, sum (y - shift), sum (y - shift)^2} per wave, the units of one (sample, channel)
+ * plane consecutive. Replaces the statistics pass of the GroupNorm that follows the ConvNeXt
+ * block's dwconv (reference convnext_utils.py:117-127 dwconv -> norm), see vfm_group_norm_fwd_stats. */
+int vfm_dwconv2d_fwd_mfma_gs(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                             float* gstat, int B, int C, int H, int W, int K, int pad, void* stream);
 /* dw[c, t] = sum_r partial[r, c, t] (t < KK), db[c] = sum_r partial[r, c, KK] over the [rows, C, KK + 1]
  * partials of the depthwise weight-gradient kernels (either output may be null). */
 int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float* db, int rows, int C, int KK, void* stream);

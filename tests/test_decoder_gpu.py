@@ -208,6 +208,89 @@ def test_group_norm_large_mean_is_stable():
     assert _rel(y.cpu(), r) < 5e-3
 
 
+# (B, C, H, W, K, G): both MFMA tile widths, partial row bands, one-band planes, many units per group
+GS_CASES = [(2, 64, 16, 16, 7, 32), (2, 32, 37, 48, 7, 8), (3, 16, 64, 64, 5, 4), (1, 128, 128, 128, 7, 32),
+            (4, 8, 8, 16, 3, 2), (2, 256, 32, 32, 7, 32), (1, 12, 100, 64, 3, 3)]
+
+
+@pytest.mark.parametrize("case", GS_CASES)
+@pytest.mark.parametrize("offset", [0.0, 40.0])
+def test_group_norm_stats_from_dwconv(case, offset):
+    """GroupNorm statistics from the dwconv's per-wave partials (vfm_dwconv2d_fwd_mfma_gs ->
+    vfm_group_norm_fwd_stats, the ConvNeXt block's dwconv -> norm): an fp32-output GroupNorm of the
+    bf16 conv output against an fp64 GroupNorm of the same bf16 values within 2e-5 (also with a large
+    common offset: the shifted partial sums), the bf16-output form and both gradients against the
+    unfused path, and the fused kernels asserted to have run."""
+    from torch_utils.ops import decoder_hip
+    ops, kt = _ops()
+    B, C, H, W, K, G = case
+    torch.manual_seed(5)
+    x = torch.randn(B, C, H, W, device=DEV).to(torch.bfloat16)
+    w = torch.randn(C, 1, K, K, device=DEV) * 0.2
+    b = torch.randn(C, device=DEV) * 0.1 + offset
+    plane = torch.randn(H, W, device=DEV)
+    gw = 1 + 0.1 * torch.randn(C, device=DEV)
+    gb = 0.1 * torch.randn(C, device=DEV)
+    st = 1 + 0.3 * torch.randn(B, C, device=DEV)
+    kt.enable(True)
+    d = ops.dwconv2d(x, w, b, K // 2, noise=plane)
+    y32 = ops.group_norm(d, G, gw, gb, 1e-5, out_dtype=torch.float32, style=st)
+    torch.cuda.synchronize()
+    names = set(kt.summary())
+    kt.enable(False)
+    assert any(n.startswith("dwconv2d_mfma_fwd") for n in names), names
+    assert any(n.startswith("group_norm_fwd_stats") for n in names), names
+    ref = torch.nn.functional.group_norm(d.double(), G, gw.double(), gb.double(), 1e-5) * st.double()[:, :, None, None]
+    assert _rel(y32, ref) < 2e-5, _rel(y32, ref)
+
+    def fwd_bwd(fused):
+        decoder_hip.GN_STATS = fused
+        try:
+            leaves = [t.clone().requires_grad_(True) for t in (x, w, b, gw, gb, st)]
+            kt.enable(True)
+            out = ops.group_norm(ops.dwconv2d(leaves[0], leaves[1], leaves[2], K // 2, noise=plane), G, leaves[3],
+                                 leaves[4], 1e-5, out_dtype=torch.bfloat16, style=leaves[5])
+            torch.manual_seed(6)
+            out.backward(torch.randn(out.shape, device=DEV).to(out.dtype))
+            torch.cuda.synchronize()
+            used = any(n.startswith("group_norm_fwd_stats") for n in kt.summary())
+            kt.enable(False)
+            assert used == fused
+            return out, [t.grad for t in leaves]
+        finally:
+            decoder_hip.GN_STATS = True
+
+    yf, gf = fwd_bwd(True)
+    yu, gu = fwd_bwd(False)
+    assert _rel(yf.float(), yu.float()) < 1.5e-2
+    for a, r in zip(gf, gu):
+        assert _rel(a.float(), r.float()) < 3e-2, _rel(a.float(), r.float())
+
+
+def test_group_norm_stats_need_the_unchanged_output():
+    """The partials are used only by a GroupNorm of the dwconv's own, unmodified output."""
+    from torch_utils.ops import decoder_hip
+    ops, kt = _ops()
+    torch.manual_seed(7)
+    x = torch.randn(2, 32, 32, 64, device=DEV).to(torch.bfloat16)
+    w = torch.randn(32, 1, 7, 7, device=DEV) * 0.2
+    kt.enable(True)
+    d = ops.dwconv2d(x, w, None, 3)
+    d.mul_(2.0)                                    # in-place change after the conv: version differs
+    y = ops.group_norm(d, 8, None, None, 1e-5, out_dtype=torch.float32)
+    d2 = ops.dwconv2d(x, w, None, 3)
+    other = d2.clone()                             # a different tensor of the same shape
+    y2 = ops.group_norm(other, 8, None, None, 1e-5, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    names = set(kt.summary())
+    kt.enable(False)
+    assert not any(n.startswith("group_norm_fwd_stats") for n in names), names
+    for inp, out in ((d, y), (other, y2)):
+        ref = torch.nn.functional.group_norm(inp.double(), 8, None, None, 1e-5)
+        assert _rel(out, ref) < 2e-5
+    assert decoder_hip._gn_stats is None or decoder_hip._gn_stats[0]() is d2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(2, 32, 64), (4, 256, 256), (1, 8, 8), (3, 40, 1000)])
 @pytest.mark.parametrize("with_scale", [True, False])

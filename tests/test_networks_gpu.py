@@ -41,8 +41,8 @@ def vfm_dir(tmp_path_factory):
 
 def _native_ran(kt, *names):
     got = {k.split("<")[0] for k in kt.summary()}
-    for n in names:
-        assert n in got, (n, sorted(got))
+    for n in names:      # group_norm_fwd: also its form with the dwconv's statistics (bf16 ConvNeXt blocks)
+        assert n in got or f"{n}_stats" in got, (n, sorted(got))
 
 
 def _gen(vfm_dir, precision):

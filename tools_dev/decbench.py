@@ -2,7 +2,9 @@
 
 Prints per kernel: average microseconds, algorithmic GB/s (unique inputs + outputs), and
 for the depthwise convs the fp32 VALU TFLOP/s (2*K*K flop per output).
-  python tools_dev/decbench.py [--only dw,gn,gelu,lsr,blur]"""
+  python tools_dev/decbench.py [--only dw,gn,dwgn,gelu,lsr,blur]
+dwgn: the ConvNeXt dwconv -> GroupNorm pair (bf16 blocks), with the GroupNorm statistics from the
+dwconv's partials (decoder_hip.GN_STATS) and without."""
 import argparse
 import os
 import sys
@@ -77,6 +79,21 @@ def main():
             gy = torch.randn_like(y)
             us = timeit(lambda: torch.autograd.grad(y, xr, gy, retain_graph=True))
             report(f"{bname} group_norm bwd", us, 3 * n * es)
+        if "dwgn" in only and dt == torch.bfloat16:
+            w = torch.randn(C, K, K, device=dev) * 0.1
+            b = torch.randn(C, device=dev)
+            G = min(32, C // 4)
+            gw, gb = torch.randn(C, device=dev), torch.randn(C, device=dev)
+            st = torch.rand(B, C, device=dev)
+            for fused in (False, True):
+                decoder_hip.GN_STATS = fused
+
+                def pair():
+                    d = decoder_hip._dw_fwd(x, w, b, None, K // 2, "dwconv2d_fwd", gstat=True)
+                    decoder_hip.group_norm(d, G, gw, gb, 1e-5, dt, st)
+                us = timeit(pair)
+                report(f"{bname} dwconv{K}+group_norm {'fused' if fused else 'plain'}", us, 4 * n * es)
+            decoder_hip.GN_STATS = True
         if "gelu" in only:
             h = torch.randn(B, 4 * C, R * R, device=dev, dtype=dt)
             sc, bi = torch.rand(B, 4 * C, device=dev), torch.randn(4 * C, device=dev)

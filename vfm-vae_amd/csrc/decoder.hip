@@ -632,7 +632,44 @@ struct GnArgs {
     float* rstd;         // [B*G]
     int B, C, G, HW;
     float eps;
+    // precomputed statistics (vfm_dwconv2d_fwd_mfma_gs): [B C upc][4] {count, shift, sum (x - shift),
+    // sum (x - shift)^2} per producer wave, upc per (sample, channel) plane; null: computed here
+    const float* stats;
+    int upc;
 };
+
+// (count, sum, sum of squares) of a (sample, group) about the shift of its first partial, merged from the
+// producer's per-wave partials in double precision, in a fixed order (thread-strided then a fixed tree)
+__device__ __forceinline__ void gn_merge_stats(const GnArgs& a, int bg, float& mean_out, float& rstd_out) {
+    __shared__ double red[3][NT];
+    const int cpg = a.C / a.G;
+    const long long n_units = (long long)cpg * a.upc;
+    const float* st = a.stats + (long long)bg * n_units * 4;    // (b, g) units are consecutive: (b C + g cpg) upc
+    const double S = st[1];
+    double n = 0.0, s1 = 0.0, s2 = 0.0;
+    for (long long u = threadIdx.x; u < n_units; u += NT) {
+        const float4 v = *reinterpret_cast<const float4*>(st + 4 * u);
+        const double c = v.x, d = (double)v.y - S;
+        n += c;
+        s1 += (double)v.z + c * d;
+        s2 += (double)v.w + 2.0 * d * (double)v.z + c * d * d;
+    }
+    red[0][threadIdx.x] = n;
+    red[1][threadIdx.x] = s1;
+    red[2][threadIdx.x] = s2;
+    __syncthreads();
+    for (int w = NT / 2; w >= 1; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    const double m1 = red[1][0] / red[0][0];
+    const double var = fmax(red[2][0] / red[0][0] - m1 * m1, 0.0);
+    mean_out = (float)(S + m1);
+    rstd_out = rsqrtf((float)var + a.eps);
+}
 
 // Flat forms (8 | HW, HW / 8 a power of two, at most GN_FLAT_MAX channels per group): the
 // group is walked as one run of 8-element chunks by all threads instead of channel by channel
@@ -648,10 +685,14 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
     const long long n = (long long)cpg * a.HW;
     const bool vec = (a.HW % 8) == 0;
     const TI* xp = reinterpret_cast<const TI*>(a.x) + (long long)bg * n;
+    const long long nv = vec ? n / 8 : 0;
+    float mean, rstd;
+    if (a.stats) {
+        gn_merge_stats(a, bg, mean, rstd);
+    } else {
     // Shifted sums (shift = first element of the group) keep the one-pass variance accurate.
     const float shift = ld(xp);
     float s1 = 0.f, s2 = 0.f;
-    const long long nv = vec ? n / 8 : 0;
     // unrolled so that several 16-B loads per thread are in flight (the loop is latency-bound otherwise)
 #pragma unroll 4
     for (long long i = threadIdx.x; i < nv; i += NT) {
@@ -673,8 +714,9 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
     s2 = block_sum(s2, scratch + 4);
     const float m1 = s1 / (float)n;
     const float var = fmaxf(s2 / (float)n - m1 * m1, 0.f);
-    const float mean = shift + m1;
-    const float rstd = rsqrtf(var + a.eps);
+    mean = shift + m1;
+    rstd = rsqrtf(var + a.eps);
+    }
     if (threadIdx.x == 0) {
         a.mean[bg] = mean;
         a.rstd[bg] = rstd;
@@ -1497,7 +1539,7 @@ extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b,
                                   float* mean, float* rstd, int dtype_in, int dtype_out, int B, int C, int G, int HW,
                                   float eps, void* stream) {
     if (!x || !y || !mean || !rstd || B <= 0 || C <= 0 || G <= 0 || C % G || HW <= 0) return VFM_ERR_ARGS;
-    GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps};
+    GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps, nullptr, 0};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define GN_CASE(DI, TI)                                                        \
     if (dtype_in == DI) {                                                      \
@@ -1510,6 +1552,21 @@ extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b,
     GN_CASE(VFM_F16, __half)
 #undef GN_CASE
     return VFM_ERR_ARGS;
+}
+
+// vfm_group_norm_fwd with the statistics merged from a producer's per-wave partials (vfm_dwconv2d_fwd_mfma_gs:
+// stats [B C upc][4]) instead of a first pass over x: x is read once.
+extern "C" int vfm_group_norm_fwd_stats(const void* x, const float* w, const float* b, const float* s, void* y,
+                                        float* mean, float* rstd, const float* stats, int upc, int dtype_in,
+                                        int dtype_out, int B, int C, int G, int HW, float eps, void* stream) {
+    if (!x || !y || !mean || !rstd || !stats || upc <= 0 || B <= 0 || C <= 0 || G <= 0 || C % G || HW <= 0)
+        return VFM_ERR_ARGS;
+    if ((uintptr_t)stats % 16) return VFM_ERR_ARGS;
+    GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps, stats, upc};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (dtype_in == VFM_BF16 && dtype_out == VFM_BF16) return gn_fwd_launch<__hip_bfloat16, __hip_bfloat16>(a, st);
+    if (dtype_in == VFM_BF16 && dtype_out == VFM_F32) return gn_fwd_launch<__hip_bfloat16, float>(a, st);
+    return VFM_NO_KERNEL;
 }
 
 template <class TX, class TY>

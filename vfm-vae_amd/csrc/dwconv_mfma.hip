@@ -43,6 +43,9 @@ struct DwmArgs {
     const __hip_bfloat16* res;            // [B, C, H, W] bf16 added before the output rounding, or null
     const float* nplane;                  // [H, W] fp32: with npart, sum x * nplane per wave (see below)
     float* npart;                         // [units] or null
+    // [units][4] or null: the wave's GroupNorm statistics of its stored (bf16-rounded) outputs, {count, shift,
+    // sum (y - shift), sum (y - shift)^2} with shift = the wave's first output (group_norm_fwd_stats merges them)
+    float* gstat;
     __hip_bfloat16* y;
     int B, C, H, W, XW, nyb, nxs, rb;     // rb: 16-row blocks per wave
     int flip;                             // taps read rotated by 180 degrees (the data gradient)
@@ -55,7 +58,7 @@ __device__ __forceinline__ uint32_t pk_bf16(float a0, float a1) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(vfm_f2{a0, a1}, vfm_bf16x2));
 }
 
-template <int K, int XW>
+template <int K, int XW, bool GS>
 __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     constexpr int P = (K - 1) / 2;
     constexpr int NQ = XW / 8 + 2;                          // 16-B chunks per staged row
@@ -134,6 +137,7 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     const float bias = a.bias ? a.bias[c] : 0.f;
     const int n = lane & 15;                                // output row of this lane (B / C column)
     float ndot = 0.f;
+    float g_sh = 0.f, g_s1 = 0.f, g_s2 = 0.f, g_n = 0.f;    // GroupNorm statistics (GS: a.gstat)
 
     for (int kb = 0; kb < nblk; ++kb) {
         const int y0 = 16 * (yb0 + kb);
@@ -161,8 +165,24 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
                 acc[0] += __uint_as_float(rv.x << 16); acc[1] += __uint_as_float(rv.x & 0xffff0000u);
                 acc[2] += __uint_as_float(rv.y << 16); acc[3] += __uint_as_float(rv.y & 0xffff0000u);
             }
+            const uint2 o = make_uint2(pk_bf16(acc[0], acc[1]), pk_bf16(acc[2], acc[3]));   // 2 v_cvt_pk_bf16_f32
+            if constexpr (GS) {
+                // statistics of the rounded outputs; the shift is lane 0's first value (row y0 >= 0 is in the plane)
+                const float v[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                                    __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+                if (kb == 0 && s == 0) g_sh = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                  __builtin_bit_cast(int, v[0])));
+                if (oy < a.H) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float d = v[r] - g_sh;
+                        g_s1 += d;
+                        g_s2 = fmaf(d, d, g_s2);
+                    }
+                    g_n += 4.f;
+                }
+            }
             if (oy < a.H) {
-                const uint2 o = make_uint2(pk_bf16(acc[0], acc[1]), pk_bf16(acc[2], acc[3]));   // 2 v_cvt_pk_bf16_f32
                 *reinterpret_cast<uint2*>(yp + 16 * s) = o;
                 if (a.npart) {     // input at the output position: staged row n + P, column 8 + 16 s + 4 g
                     const uint2 xv = *reinterpret_cast<const uint2*>(img + (n + P) * RS + 16 + 32 * s + 8 * g);
@@ -181,14 +201,28 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
         for (int m = 32; m >= 1; m >>= 1) ndot += __shfl_xor(ndot, m);
         if (lane == 0) a.npart[unit] = ndot;
     }
+    if constexpr (GS) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            g_s1 += __shfl_xor(g_s1, m);
+            g_s2 += __shfl_xor(g_s2, m);
+            g_n += __shfl_xor(g_n, m);
+        }
+        if (lane == 0) *reinterpret_cast<float4*>(a.gstat + 4 * unit) = make_float4(g_n, g_sh, g_s1, g_s2);
+    }
 }
 
 template <int K>
 int dwm_launch(DwmArgs& a, hipStream_t st) {
     const long long blocks = (a.units + WAVES - 1) / WAVES;
     if (blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
-    if (a.XW == 64) VFM_LAUNCH((dwm_fwd<K, 64>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
-    else VFM_LAUNCH((dwm_fwd<K, 16>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+    if (a.gstat) {
+        if (a.XW == 64) VFM_LAUNCH((dwm_fwd<K, 64, true>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+        else VFM_LAUNCH((dwm_fwd<K, 16, true>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+    } else {
+        if (a.XW == 64) VFM_LAUNCH((dwm_fwd<K, 64, false>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+        else VFM_LAUNCH((dwm_fwd<K, 16, false>), dim3((unsigned)blocks), dim3(64 * WAVES), 0, st, a);
+    }
     return launch_status();
 }
 
@@ -388,7 +422,26 @@ extern "C" int vfm_dwconv2d_fwd_mfma_nz(const void* x, const float* w, const flo
     a.x = (const __hip_bfloat16*)x; a.w = w; a.bias = bias; a.noise = noise; a.y = (__hip_bfloat16*)y;
     a.res = (const __hip_bfloat16*)res;
     a.nplane = nplane; a.npart = npart;
+    a.gstat = nullptr;
     a.flip = flip != 0;
+    hipStream_t st = (hipStream_t)stream;
+    switch (K) {
+    case 3: return dwm_launch<3>(a, st);
+    case 5: return dwm_launch<5>(a, st);
+    default: return dwm_launch<7>(a, st);
+    }
+}
+
+// vfm_dwconv2d_fwd_mfma with the GroupNorm statistics of y: gstat [units][4] (vfm_dwconv2d_fwd_mfma_units; the
+// units of a (sample, channel) plane are consecutive), consumed by vfm_group_norm_fwd_stats.
+extern "C" int vfm_dwconv2d_fwd_mfma_gs(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                                        float* gstat, int B, int C, int H, int W, int K, int pad, void* stream) {
+    if (!x || !w || !y || !gstat || B <= 0 || C <= 0 || H <= 0 || W <= 0) return VFM_ERR_ARGS;
+    DwmArgs a;
+    if (!dwm_plan(a, B, C, H, W, K, pad)) return VFM_NO_KERNEL;
+    if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)noise | (uintptr_t)gstat) % 16) return VFM_NO_KERNEL;
+    a.x = (const __hip_bfloat16*)x; a.w = w; a.bias = bias; a.noise = noise; a.y = (__hip_bfloat16*)y;
+    a.res = nullptr; a.nplane = nullptr; a.npart = nullptr; a.gstat = gstat; a.flip = 0;
     hipStream_t st = (hipStream_t)stream;
     switch (K) {
     case 3: return dwm_launch<3>(a, st);

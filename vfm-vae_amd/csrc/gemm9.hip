@@ -720,8 +720,6 @@ __global__ __launch_bounds__(THREADS, 1) void gemm9p_kernel(G9Args a, int total)
     typedef typename std::conditional<OUTF32, float, __hip_bfloat16>::type TC;
     constexpr int ES = sizeof(TC);
 
-    constexpr int NST = OUTF32 ? 64 : 32;       // store instructions per wave and item
-
     // prologue: stream positions 0 and 1 in flight, 0 landed, k-half 0 fragments of position 0 read
     setup_dma(d_item);
     point();

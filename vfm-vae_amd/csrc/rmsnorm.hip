@@ -90,7 +90,6 @@ __global__ __launch_bounds__(THREADS) void crms_bwd(const float* __restrict__ x,
     const float r = ok ? rinv[(long long)b * P + p] : 0.f;
     // r == 1 / 1e-12 exactly when the norm was clamped: no gradient through the norm then
     const float corr = (r < 1.f / NORM_EPS) ? tot * r * r * r : 0.f;
-#pragma unroll 4
     for (int c = g; c < C; c += GROUPS) {
         float gx = 0.f;
         if (ok) {

@@ -43,6 +43,8 @@ SIGNATURES = {
     "vfm_dwconv2d_bwd_weight": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_group_norm_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_float, c_vp],
+    "vfm_group_norm_fwd_stats": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_int, c_float, c_vp],
     "vfm_group_norm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                            c_int, c_int, c_int, c_vp],
     "vfm_scale_bias_gelu_fwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
@@ -89,6 +91,8 @@ SIGNATURES = {
     "vfm_dwconv2d_fwd_mfma_nz": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, c_vp],
     "vfm_dwconv2d_fwd_mfma_units": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "vfm_dwconv2d_fwd_mfma_gs": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 c_vp],
     "vfm_dwconv2d_wgrad_reduce": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
     "vfm_specnorm_workspace_floats": [c_int, c_int],
     "vfm_specnorm_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp],

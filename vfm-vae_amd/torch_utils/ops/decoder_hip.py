@@ -12,6 +12,7 @@ report the dominant kernel's roofline.
 """
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -320,12 +321,31 @@ def pointwise(w, x):
 DW_MFMA = os.environ.get("VFM_DW_MFMA", "1") == "1"      # A/B switch for the banded-MFMA dwconv
 
 
-def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None):
+GN_STATS = os.environ.get("VFM_GN_STATS", "1") == "1"      # A/B switch: GroupNorm statistics from the dwconv
+_gn_stats = None        # (weakref of y, data_ptr, version, shape, partials, units per plane) of the last dwconv
+
+
+def _gn_stats_for(x):
+    """The dwconv's GroupNorm partials when x is that dwconv's unchanged output (one consumer)."""
+    global _gn_stats
+    e, _gn_stats = _gn_stats, None
+    if e is None:
+        return None
+    yref, ptr, ver, shape, part, upc = e
+    y = yref()
+    if y is None or x.data_ptr() != ptr or x.shape != shape or x._version != ver or y._version != ver:
+        return None
+    return part, upc
+
+
+def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None, gstat=False):
     """y = dwconv(x) (+ bias, + noise plane) (+ res, a tensor of y's shape: the residual-branch
     gradient added in the MFMA kernel's epilogue, else by a torch add); flip: taps rotated by 180
     degrees in the kernel (the data gradient). nplane ([H, W] fp32): also return sum x * nplane over
     (b, c, y, x) as a 0-d fp32 tensor -- from per-wave partials of the MFMA kernel when it runs, else
-    by torch -- i.e. (y, dot)."""
+    by torch -- i.e. (y, dot). gstat: the MFMA kernel also writes y's GroupNorm partials, which the
+    GroupNorm that consumes y picks up (_gn_stats_for) instead of its own statistics pass."""
+    global _gn_stats
     B, C, H, W = x.shape
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -336,6 +356,17 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None):
         # bf16 planes: the banded-MFMA kernel (csrc/dwconv_mfma.hip); taps rounded to bf16 as
         # the reference's autocast conv does
         r = None if res is None else _c(res.to(torch.bfloat16))
+        if gstat and GN_STATS and r is None and not flip and nplane is None and Ho == H and Wo == W:
+            units = _lib.vfm_dwconv2d_fwd_mfma_units(B, C, H, W, K, pad)
+            if units > 0:
+                gs = torch.empty([units, 4], dtype=torch.float32, device=x.device)
+                with kernel_timer.region(_rn(name.replace('dwconv2d', 'dwconv2d_mfma'), x, K), _nb(x, y)):
+                    rc = _lib.vfm_dwconv2d_fwd_mfma_gs(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise),
+                                                       y.data_ptr(), gs.data_ptr(), B, C, H, W, K, pad, _stream())
+                if rc != custom_ops.VFM_NO_KERNEL:
+                    _check(rc, name)
+                    _gn_stats = (weakref.ref(y), y.data_ptr(), y._version, y.shape, gs, units // (B * C))
+                    return y
         part = None
         if nplane is not None and Ho == H and Wo == W:
             units = _lib.vfm_dwconv2d_fwd_mfma_units(B, C, H, W, K, pad)
@@ -419,7 +450,7 @@ class _DwConv2d(custom_ops.FastFunction):
             plane = n
             ctx.strength = strength.detach().float()
             n = (n * ctx.strength).contiguous()
-        y = _dw_fwd(x, w3, b, n, pad, 'dwconv2d_fwd')
+        y = _dw_fwd(x, w3, b, n, pad, 'dwconv2d_fwd', gstat=True)
         ctx.save_for_backward(x, w3, plane)
         ctx.pad = pad
         ctx.meta = (weight.dtype, weight.shape, None if bias is None else bias.dtype,
@@ -508,10 +539,18 @@ class _GroupNorm(custom_ops.FastFunction):
         y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
         mean = torch.empty([B * groups], dtype=torch.float32, device=x.device)
         rstd = torch.empty_like(mean)
-        with kernel_timer.region(_rn('group_norm_fwd', x), _nb(x, y)):
-            _check(_lib.vfm_group_norm_fwd(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), mean.data_ptr(),
-                                           rstd.data_ptr(), _code(x), _code(y), B, C, groups, HW, float(eps),
-                                           _stream()), 'vfm_group_norm_fwd')
+        st = _gn_stats_for(x) if x.dtype == torch.bfloat16 and y.dtype in (torch.bfloat16, torch.float32) else None
+        if st is not None:
+            # statistics merged from the producing dwconv's partials: x is read once
+            with kernel_timer.region(_rn('group_norm_fwd_stats', x), _nb(x, y)):
+                _check(_lib.vfm_group_norm_fwd_stats(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), mean.data_ptr(),
+                                                     rstd.data_ptr(), st[0].data_ptr(), st[1], _code(x), _code(y), B,
+                                                     C, groups, HW, float(eps), _stream()), 'vfm_group_norm_fwd_stats')
+        else:
+            with kernel_timer.region(_rn('group_norm_fwd', x), _nb(x, y)):
+                _check(_lib.vfm_group_norm_fwd(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), mean.data_ptr(),
+                                               rstd.data_ptr(), _code(x), _code(y), B, C, groups, HW, float(eps),
+                                               _stream()), 'vfm_group_norm_fwd')
         ctx.save_for_backward(x, w, b, s, mean, rstd)
         ctx.groups = groups
         ctx.meta = tuple(None if t is None else t.dtype for t in (weight, bias, style))
