@@ -210,7 +210,9 @@ def test_group_norm_large_mean_is_stable():
 
 # (B, C, H, W, K, G): both MFMA tile widths, partial row bands, one-band planes, many units per group
 GS_CASES = [(2, 64, 16, 16, 7, 32), (2, 32, 37, 48, 7, 8), (3, 16, 64, 64, 5, 4), (1, 128, 128, 128, 7, 32),
-            (4, 8, 8, 16, 3, 2), (2, 256, 32, 32, 7, 32), (1, 12, 100, 64, 3, 3)]
+            (4, 8, 8, 16, 3, 2), (2, 256, 32, 32, 7, 32), (1, 12, 100, 64, 3, 3),
+            # more than GN_FLAT_MAX channels per group: the one-block-per-group form of the stats mode
+            (1, 256, 16, 16, 3, 1)]
 
 
 @pytest.mark.parametrize("case", GS_CASES)

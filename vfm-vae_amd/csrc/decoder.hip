@@ -778,6 +778,55 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
     }
 }
 
+// Statistics-mode apply (vfm_group_norm_fwd_stats): with the statistics already merged from the producer's
+// partials the pass is one read + one write of the group, so the group is split over gridDim.y blocks of
+// GN_APPLY_VEC 8-element chunks each (the one-block-per-group form leaves ~4 waves per SIMD in flight at
+// 1024 groups). Every block merges the (few) partials itself; block y == 0 writes mean/rstd.
+constexpr int GN_APPLY_VEC = 2048;
+
+template <class TI, class TO>
+__global__ __launch_bounds__(NT) void gn_apply(GnArgs a) {
+    __shared__ float s_sc[GN_FLAT_MAX], s_sh[GN_FLAT_MAX];
+    const int bg = blockIdx.x;
+    const int bidx = bg / a.G, g = bg - bidx * a.G;
+    const int cpg = a.C / a.G;
+    const long long n = (long long)cpg * a.HW;
+    float mean, rstd;
+    gn_merge_stats(a, bg, mean, rstd);
+    if (threadIdx.x == 0 && blockIdx.y == 0) {
+        a.mean[bg] = mean;
+        a.rstd[bg] = rstd;
+    }
+    for (int cl = threadIdx.x; cl < cpg; cl += NT) {
+        const int c = g * cpg + cl;
+        float sc = rstd * (a.w ? a.w[c] : 1.f);
+        float sh = (a.b ? a.b[c] : 0.f) - mean * sc;
+        if (a.s) {
+            const float m = a.s[bidx * a.C + c];
+            sc *= m;
+            sh *= m;
+        }
+        s_sc[cl] = sc;
+        s_sh[cl] = sh;
+    }
+    __syncthreads();
+    const TI* xp = reinterpret_cast<const TI*>(a.x) + (long long)bg * n;
+    TO* yp = reinterpret_cast<TO*>(a.y) + (long long)bg * n;
+    const int cpc = a.HW >> 3;
+    const long long v0 = (long long)blockIdx.y * GN_APPLY_VEC;
+    const long long v1 = min((long long)(n >> 3), v0 + GN_APPLY_VEC);
+#pragma unroll 8
+    for (long long i = v0 + threadIdx.x; i < v1; i += NT) {
+        const int cl = (int)(i / cpc);
+        const float sc = s_sc[cl], sh = s_sh[cl];
+        float v[8];
+        load8(xp + i * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sc, sh);
+        store8(yp + i * 8, v);
+    }
+}
+
 struct GnBwdArgs {
     const void* x;
     const void* dy;
@@ -1564,6 +1613,17 @@ extern "C" int vfm_group_norm_fwd_stats(const void* x, const float* w, const flo
     if ((uintptr_t)stats % 16) return VFM_ERR_ARGS;
     GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps, stats, upc};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (HW % 8 == 0 && C / G <= GN_FLAT_MAX) {
+        const long long nv = (long long)(C / G) * HW / 8;
+        const dim3 grid(B * G, (unsigned)((nv + GN_APPLY_VEC - 1) / GN_APPLY_VEC));
+        if (dtype_in == VFM_BF16 && dtype_out == VFM_BF16)
+            VFM_LAUNCH((gn_apply<__hip_bfloat16, __hip_bfloat16>), grid, dim3(NT), 0, st, a);
+        else if (dtype_in == VFM_BF16 && dtype_out == VFM_F32)
+            VFM_LAUNCH((gn_apply<__hip_bfloat16, float>), grid, dim3(NT), 0, st, a);
+        else
+            return VFM_NO_KERNEL;
+        return launch_status();
+    }
     if (dtype_in == VFM_BF16 && dtype_out == VFM_BF16) return gn_fwd_launch<__hip_bfloat16, __hip_bfloat16>(a, st);
     if (dtype_in == VFM_BF16 && dtype_out == VFM_F32) return gn_fwd_launch<__hip_bfloat16, float>(a, st);
     return VFM_NO_KERNEL;

@@ -225,7 +225,7 @@ def summary():
 _ROC = {
     "scale_bias_gelu_fwd": "gelu_fwd<{T}>", "scale_bias_gelu_bwd": "gelu_bwd<{T}>",
     "layer_scale_residual_fwd": "lsr_fwd<{T}, ", "layer_scale_residual_bwd": "lsr_bwd<{T}, ",
-    "group_norm_fwd": "gn_fwd<{T}, ", "group_norm_bwd": "gn_bwd<{T}, ", "group_norm_fwd_stats": "gn_fwd<{T}, ",
+    "group_norm_fwd": "gn_fwd<{T}, ", "group_norm_bwd": "gn_bwd<{T}, ", "group_norm_fwd_stats": "gn_apply<{T}, ",
     "dwconv2d_fwd": "dwr_fwd<{T}, {K}>", "dwconv2d_bwd_data": "dwr_fwd<{T}, {K}>",
     "dwconv2d_bwd_weight": "dwr_bwd_w<{T}, {K}>",
     "dwconv2d_mfma_fwd": "dwm_fwd<{K}, ", "dwconv2d_mfma_bwd_data": "dwm_fwd<{K}, ",
