@@ -330,7 +330,9 @@ def test_layer_scale_residual(shape, dt_y, dt_x):
 @pytest.mark.parametrize("shape,r", [((2, 16, 8, 8), 2), ((1, 12, 5, 7), 2), ((2, 4, 9, 6), 1), ((1, 4, 1, 1), 2),
                                      ((1, 2, 16, 32), 1), ((1, 8, 40, 70), 2), ((1, 3, 70, 130), 1),
                                      # 16-B vector forms (W % 8 == 0) with partial edge tiles
-                                     ((2, 8, 40, 48), 2), ((1, 3, 72, 136), 1), ((1, 4, 3, 8), 2)])
+                                     ((2, 8, 40, 48), 2), ((1, 3, 72, 136), 1), ((1, 4, 3, 8), 2),
+                                     # forward strips of BSTRIP tiles: several strips, a partial last one
+                                     ((1, 4, 136, 16), 2), ((1, 2, 300, 64), 1), ((2, 12, 64, 64), 2)])
 def test_shuffle_blur(shape, r, taps, dt):
     ops, _ = _ops()
     torch.manual_seed(7)
