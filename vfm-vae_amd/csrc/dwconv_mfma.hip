@@ -25,6 +25,8 @@
 // rows: the noise strength's gradient sum_{b,c,y,x} dY * noise_plane without another pass over dY.
 #include "vfm_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace vfm;
@@ -397,7 +399,15 @@ bool dwm_plan(DwmArgs& a, int B, int C, int H, int W, int K, int pad) {
     a.B = B; a.C = C; a.H = H; a.W = W;
     a.XW = W % 64 == 0 ? 64 : 16;
     const int rows16 = (H + 15) / 16;
-    a.rb = rows16 < 4 ? rows16 : 4;                        // up to 64 output rows per wave
+    // up to 4 row blocks (64 output rows) per wave. VFM_DWM_RB overrides the cap (A/B, profiles/r5_bi_dwm_rb.txt:
+    // 8 or 16 blocks amortise the wave's prologue better but leave fewer waves: the plain form 6-19 % slower at
+    // 256^2, the GS form 2 % faster at 8)
+    static const int rb_cap = [] {
+        const char* e = getenv("VFM_DWM_RB");
+        const int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : v;
+    }();
+    a.rb = rows16 < rb_cap ? rows16 : rb_cap;
     a.nyb = (rows16 + a.rb - 1) / a.rb;
     a.nxs = W / a.XW;
     a.units = (long long)B * C * a.nyb * a.nxs;
