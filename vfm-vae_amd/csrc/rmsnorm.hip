@@ -9,8 +9,8 @@
 //   dx         = k dy / n - x (sum_c k dy x) / n^3   where the norm is not clamped,   k dy / n  where it is
 //   dgamma[c]  = scale * sum_{b, p} dy x / n
 //
-// Block = 16 columns (consecutive p) x 16 channel groups; a thread sums every 16th channel of its
-// column, the 16 partial sums meet in LDS, then the same threads write their channels. The gamma
+// Block = 16 columns (consecutive p) x 64 channel groups; a thread sums every 64th channel of its
+// column (1024 threads: the 8^2-32^2 planes give only 128-2048 blocks), the 64 partial sums meet in LDS, then the same threads write their channels. The gamma
 // gradient: each block reduces dy x / n over its 16 columns per channel into one partial (channel-major
 // [C][blocks]), and a second kernel sums every channel's partials in a fixed order (deterministic).
 #include "vfm_common.h"
@@ -19,7 +19,10 @@ namespace {
 
 using namespace vfm;
 
-constexpr int COLS = 16, GROUPS = 16, THREADS = COLS * GROUPS;
+#ifndef CRMS_GROUPS
+#define CRMS_GROUPS 64
+#endif
+constexpr int COLS = 16, GROUPS = CRMS_GROUPS, THREADS = COLS * GROUPS;
 constexpr float NORM_EPS = 1e-12f;
 
 __global__ __launch_bounds__(THREADS) void crms_fwd(const float* __restrict__ x, const float* __restrict__ gamma,
