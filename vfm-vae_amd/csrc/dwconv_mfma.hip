@@ -54,7 +54,6 @@ struct DwmArgs {
     long long units;
 };
 
-__device__ __forceinline__ uint16_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, __float2bfloat16(v)); }
 // two floats -> packed bf16 pair (RNE, element 0 low), one v_cvt_pk_bf16_f32
 __device__ __forceinline__ uint32_t pk_bf16(float a0, float a1) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(vfm_f2{a0, a1}, vfm_bf16x2));
@@ -73,7 +72,8 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     constexpr int NR = 16 + K - 1;
     constexpr int NL = (NR * NQ + 63) / 64;                 // staging loads per lane per row block
     __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES][ROWS * RS];
-    __shared__ float taps[WAVES][64];
+    constexpr int TOFF = 23, TROW = 48;                     // padded tap row: kx + TOFF - P in [0, 47)
+    __shared__ float taps[WAVES][K * TROW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long unit = (long long)blockIdx.x * WAVES + wave;
     if (unit >= a.units) return;                            // wave-uniform; no block-level barrier below
@@ -114,26 +114,28 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     const int nblk = min(a.rb, (a.H + 15) / 16 - yb0);
     fetch(16 * yb0);
 
-    // the channel's taps, one per lane, through LDS (one global load per lane instead of 8 K)
-    if (lane < K * K) taps[wave][lane] = a.w[(long long)c * K * K + (a.flip ? K * K - 1 - lane : lane)];
+    // the channel's taps through LDS as zero-padded rows: tp[ky][kx + TOFF] (one global load per lane
+    // instead of 8 K), so a lane's 8 band values of a kernel row are 8 consecutive entries, read without
+    // range tests (the band's kx = 8 g + e - i - 8 + P spans -23 + P .. 23 + P over the wave)
+    float* tp = taps[wave];
+#pragma unroll
+    for (int t = lane; t < K * TROW; t += 64) tp[t] = 0.f;
     __builtin_amdgcn_wave_barrier();
-    // A fragments: lane l holds A_ky[i = l & 15][j = 8 (l >> 4) + e], e < 8
+    if (lane < K * K) {
+        const int ky = lane / K, kx = lane - ky * K;
+        tp[ky * TROW + kx + TOFF - P] = a.w[(long long)c * K * K + (a.flip ? K * K - 1 - lane : lane)];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // A fragments: lane l holds A_ky[i = l & 15][j = 8 (l >> 4) + e], e < 8 (taps rounded to bf16, RNE)
     const int i = lane & 15, g = lane >> 4;
+    const int tb = 8 * g - i - 8 + TOFF;                    // row entry of e = 0
     bf16x8 af[K];
 #pragma unroll
     for (int ky = 0; ky < K; ++ky) {
+        const float* row = tp + ky * TROW + tb;
         uint32_t u[4];
 #pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-            uint32_t h2 = 0;
-#pragma unroll
-            for (int hlf = 0; hlf < 2; ++hlf) {
-                const int kx = 8 * g + 2 * e2 + hlf - i - 8 + P;
-                const float wv = (kx >= 0 && kx < K) ? taps[wave][ky * K + kx] : 0.f;
-                h2 |= (uint32_t)bf16_bits(wv) << (16 * hlf);
-            }
-            u[e2] = h2;
-        }
+        for (int e2 = 0; e2 < 4; ++e2) u[e2] = pk_bf16(row[2 * e2], row[2 * e2 + 1]);
         af[ky] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
     }
     const float bias = a.bias ? a.bias[c] : 0.f;
