@@ -90,25 +90,33 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     // staging of row block y0: rows y0 - P .. y0 + 15 + K - 1 - P, columns x0 - 8 .. x0 + XW + 7,
     // zero outside the plane; loads go to registers first so the next block's are in flight while
     // the current block computes
+    // per staging slot u (loop-invariant): its row r - P relative to y0 (or a large negative value when
+    // the slot is unused or its columns lie outside the plane), its 16-B chunk and its LDS offset
+    // (srow packed with the chunk index: srow * 16 + ch, two registers per slot with slds)
     uint4 st[NL];
+    int srow[NL], slds[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+        const int q = lane + 64 * u;
+        const int r = q / NQ, ch = q - r * NQ;
+        const int xx = x0 - 8 + 8 * ch;
+        const bool ok = q < NR * NQ && xx >= 0 && xx < a.W;
+        srow[u] = (ok ? r - P : -(1 << 24)) * 16 + ch;
+        slds[u] = q < NR * NQ ? r * RS + 16 * ch : -1;
+    }
     auto fetch = [&](int y0) {
 #pragma unroll
         for (int u = 0; u < NL; ++u) {
-            const int q = lane + 64 * u;
-            const int r = q / NQ, ch = q - r * NQ;
-            const int yy = y0 - P + r, xx = x0 - 8 + 8 * ch;
+            const int yy = y0 + (srow[u] >> 4);
             st[u] = make_uint4(0, 0, 0, 0);
-            if (q < NR * NQ && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-                st[u] = *reinterpret_cast<const uint4*>(xp + (long long)yy * a.W + xx);
+            if ((unsigned)yy < (unsigned)a.H)
+                st[u] = *reinterpret_cast<const uint4*>(xp + (long long)yy * a.W + x0 - 8 + 8 * (srow[u] & 15));
         }
     };
     auto put = [&]() {
 #pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int q = lane + 64 * u;
-            const int r = q / NQ, ch = q - r * NQ;
-            if (q < NR * NQ) *reinterpret_cast<uint4*>(img + r * RS + 16 * ch) = st[u];
-        }
+        for (int u = 0; u < NL; ++u)
+            if (slds[u] >= 0) *reinterpret_cast<uint4*>(img + slds[u]) = st[u];
     };
     const int yb0 = ybg * a.rb;
     const int nblk = min(a.rb, (a.H + 15) / 16 - yb0);
