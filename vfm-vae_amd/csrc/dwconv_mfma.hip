@@ -26,6 +26,7 @@
 #include "vfm_common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -93,7 +94,10 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     // per staging slot u (loop-invariant): its row r - P relative to y0 (or a large negative value when
     // the slot is unused or its columns lie outside the plane), its 16-B chunk and its LDS offset
     // (srow packed with the chunk index: srow * 16 + ch, two registers per slot with slds)
-    uint4 st[NL];
+    // D staging register sets: the non-GS forms (the data gradient) keep two row blocks' loads in flight
+    // (108 -> ~124 VGPRs, still 4 waves per SIMD); the GS form one (128 VGPRs)
+    constexpr int D = GS ? 1 : 2;
+    uint4 st[D][NL];
     int srow[NL], slds[NL];
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
@@ -104,23 +108,30 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
         srow[u] = (ok ? r - P : -(1 << 24)) * 16 + ch;
         slds[u] = q < NR * NQ ? r * RS + 16 * ch : -1;
     }
-    auto fetch = [&](int y0) {
+    auto fetch = [&](auto bc, int y0) {
+        constexpr int BF = decltype(bc)::value;
 #pragma unroll
         for (int u = 0; u < NL; ++u) {
             const int yy = y0 + (srow[u] >> 4);
-            st[u] = make_uint4(0, 0, 0, 0);
+            st[BF][u] = make_uint4(0, 0, 0, 0);
             if ((unsigned)yy < (unsigned)a.H)
-                st[u] = *reinterpret_cast<const uint4*>(xp + (long long)yy * a.W + x0 - 8 + 8 * (srow[u] & 15));
+                st[BF][u] = *reinterpret_cast<const uint4*>(xp + (long long)yy * a.W + x0 - 8 + 8 * (srow[u] & 15));
         }
     };
-    auto put = [&]() {
+    auto put = [&](auto bc) {
+        constexpr int BF = decltype(bc)::value;
 #pragma unroll
         for (int u = 0; u < NL; ++u)
-            if (slds[u] >= 0) *reinterpret_cast<uint4*>(img + slds[u]) = st[u];
+            if (slds[u] >= 0) *reinterpret_cast<uint4*>(img + slds[u]) = st[BF][u];
     };
+    constexpr std::integral_constant<int, 0> buf0{};
+    constexpr std::integral_constant<int, D - 1> buf1{};
     const int yb0 = ybg * a.rb;
     const int nblk = min(a.rb, (a.H + 15) / 16 - yb0);
-    fetch(16 * yb0);
+    fetch(buf0, 16 * yb0);
+    if constexpr (D == 2) {
+        if (nblk > 1) fetch(buf1, 16 * (yb0 + 1));
+    }
 
     // the channel's taps through LDS as zero-padded rows: tp[ky][kx + TOFF] (one global load per lane
     // instead of 8 K), so a lane's 8 band values of a kernel row are 8 consecutive entries, read without
@@ -151,10 +162,10 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
     float ndot = 0.f;
     float g_sh = 0.f, g_s1 = 0.f, g_s2 = 0.f, g_n = 0.f;    // GroupNorm statistics (GS: a.gstat)
 
-    for (int kb = 0; kb < nblk; ++kb) {
+    auto body = [&](auto bc, int kb) {
         const int y0 = 16 * (yb0 + kb);
-        put();                                              // after the previous block's fragment reads
-        if (kb + 1 < nblk) fetch(y0 + 16);
+        put(bc);                                            // after the previous block's fragment reads
+        if (kb + D < nblk) fetch(bc, y0 + 16 * D);
         __builtin_amdgcn_wave_barrier();
         const int oy = y0 + n;
         __hip_bfloat16* yp = a.y + plane + (long long)oy * a.W + x0 + 4 * g;
@@ -206,6 +217,12 @@ __global__ __launch_bounds__(64 * WAVES) void dwm_fwd(DwmArgs a) {
                     ndot = fmaf(__uint_as_float(xv.y & 0xffff0000u), pl.w, ndot);
                 }
             }
+        }
+    };
+    for (int kb = 0; kb < nblk; kb += D) {
+        body(buf0, kb);
+        if constexpr (D == 2) {
+            if (kb + 1 < nblk) body(buf1, kb + 1);
         }
     }
     if (a.npart) {
