@@ -281,6 +281,17 @@ int vfm_shuffle_blur_bwd(const void* dout, void* dx, const float* taps, int K, i
 int vfm_residual_layer_norm(const float* h, const void* delta, float* h_out, const float* w, const float* b,
                             void* y, int dtype_delta, int dtype_out, int rows, int D, float eps, void* stream);
 
+/* LayerNorm with a backward, for a tower whose parameters are frozen but whose input needs a gradient
+ * (the DINOv2 discriminator backbone in the G phase; reference HF Dinov2Layer norm1 / norm2, replaces
+ * torch's layer_norm / layer_norm_backward there). x fp32 [rows, D], D a multiple of 128, at most 1024
+ * (else VFM_NO_KERNEL); y [rows, D] (dtype_out); mean / rstd fp32 [rows] saved for the backward.
+ * Backward: dx fp32 = rstd (g - mean(g) - xhat mean(g xhat)), g = dy w (dy in dtype_dy); no gradient for
+ * w / b. Pointers 8-B aligned. */
+int vfm_layer_norm_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                       int dtype_out, int rows, int D, float eps, void* stream);
+int vfm_layer_norm_bwd(const float* x, const void* dy, const float* w, const float* mean, const float* rstd,
+                       float* dx, int dtype_dy, int rows, int D, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Frozen ViT towers: fused multi-head self-attention forward (flash-style).
  * Replaces `F.scaled_dot_product_attention(q, k, v)` of HF SiglipAttention under bf16

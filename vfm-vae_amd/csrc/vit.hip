@@ -132,7 +132,162 @@ int ln_dispatch(LnArgs& a, hipStream_t st) {
     return launch_status();
 }
 
+// ---- LayerNorm with autograd (the DINOv2 discriminator backbone: frozen parameters, gradient to the input;
+// reference HF Dinov2Layer norm1 / norm2 through networks/discriminator.py's DINO feature network) --------
+// One wave per row, D = 128 NV (NV float2 per lane: D = 384 for ViT-S, which the float4 form above does not
+// take). Forward: exact two-pass mean / variance from registers, y in the compute dtype, mean / rstd saved.
+// Backward (dx only): g = dy w, dx = rstd (g - mean(g) - xhat mean(g xhat)).
+template <class TO, int NV>
+__global__ __launch_bounds__(256) void ln2_fwd(const float* __restrict__ x, const float* __restrict__ w,
+                                               const float* __restrict__ b, TO* __restrict__ y, float* mean_out,
+                                               float* rstd_out, int rows, int D, float eps) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const long long off = (long long)row * D;
+    float v[NV][2];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const float2 t = *reinterpret_cast<const float2*>(x + off + (j * 64 + lane) * 2);
+        v[j][0] = t.x; v[j][1] = t.y;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s += v[j][0] + v[j][1];
+    const float mean = wsum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const float d0 = v[j][0] - mean, d1 = v[j][1] - mean;
+        q = fmaf(d0, d0, fmaf(d1, d1, q));
+    }
+    const float rstd = rsqrtf(wsum(q) / (float)D + eps);
+    if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int c0 = (j * 64 + lane) * 2;
+        const float2 wv = w ? *reinterpret_cast<const float2*>(w + c0) : make_float2(1.f, 1.f);
+        const float2 bv = b ? *reinterpret_cast<const float2*>(b + c0) : make_float2(0.f, 0.f);
+        const float o0 = fmaf((v[j][0] - mean) * rstd, wv.x, bv.x);
+        const float o1 = fmaf((v[j][1] - mean) * rstd, wv.y, bv.y);
+        if constexpr (sizeof(TO) == 4) {
+            *reinterpret_cast<float2*>(y + off + c0) = make_float2(o0, o1);
+        } else {
+            TO t[2];
+            st(&t[0], o0);
+            st(&t[1], o1);
+            *reinterpret_cast<uint32_t*>(y + off + c0) = *reinterpret_cast<const uint32_t*>(t);
+        }
+    }
+}
+
+template <class TG, int NV>
+__global__ __launch_bounds__(256) void ln2_bwd(const float* __restrict__ x, const TG* __restrict__ dy,
+                                               const float* __restrict__ w, const float* __restrict__ mean_in,
+                                               const float* __restrict__ rstd_in, float* __restrict__ dx, int rows,
+                                               int D) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const long long off = (long long)row * D;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NV][2], g[NV][2];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int c0 = (j * 64 + lane) * 2;
+        const float2 t = *reinterpret_cast<const float2*>(x + off + c0);
+        const float2 wv = w ? *reinterpret_cast<const float2*>(w + c0) : make_float2(1.f, 1.f);
+        float d0, d1;
+        if constexpr (sizeof(TG) == 4) {
+            const float2 u = *reinterpret_cast<const float2*>(dy + off + c0);
+            d0 = u.x; d1 = u.y;
+        } else {
+            d0 = ld(dy + off + c0);
+            d1 = ld(dy + off + c0 + 1);
+        }
+        xh[j][0] = (t.x - mean) * rstd;
+        xh[j][1] = (t.y - mean) * rstd;
+        g[j][0] = d0 * wv.x;
+        g[j][1] = d1 * wv.y;
+        sg += g[j][0] + g[j][1];
+        sgx = fmaf(g[j][0], xh[j][0], fmaf(g[j][1], xh[j][1], sgx));
+    }
+    const float mg = wsum(sg) / (float)D, mgx = wsum(sgx) / (float)D;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int c0 = (j * 64 + lane) * 2;
+        *reinterpret_cast<float2*>(dx + off + c0) =
+            make_float2(rstd * (g[j][0] - mg - xh[j][0] * mgx), rstd * (g[j][1] - mg - xh[j][1] * mgx));
+    }
+}
+
+#define LN2_NV(M)                                                   \
+    switch (D / 128) {                                              \
+    case 1: M(1) break;                                             \
+    case 2: M(2) break;                                             \
+    case 3: M(3) break;                                             \
+    case 4: M(4) break;                                             \
+    case 5: M(5) break;                                             \
+    case 6: M(6) break;                                             \
+    case 7: M(7) break;                                             \
+    case 8: M(8) break;                                             \
+    default: return VFM_NO_KERNEL;                                  \
+    }
+
+template <class TO>
+int ln2_fwd_launch(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, int rows,
+                   int D, float eps, hipStream_t st) {
+    const dim3 grid((unsigned)((rows + 3) / 4)), blk(256);
+#define LN2F(NV) VFM_LAUNCH((ln2_fwd<TO, NV>), grid, blk, 0, st, x, w, b, (TO*)y, mean, rstd, rows, D, eps);
+    LN2_NV(LN2F)
+#undef LN2F
+    return launch_status();
+}
+
+template <class TG>
+int ln2_bwd_launch(const float* x, const void* dy, const float* w, const float* mean, const float* rstd, float* dx,
+                   int rows, int D, hipStream_t st) {
+    const dim3 grid((unsigned)((rows + 3) / 4)), blk(256);
+#define LN2B(NV) VFM_LAUNCH((ln2_bwd<TG, NV>), grid, blk, 0, st, x, (const TG*)dy, w, mean, rstd, dx, rows, D);
+    LN2_NV(LN2B)
+#undef LN2B
+    return launch_status();
+}
+
 }  // namespace
+
+extern "C" int vfm_layer_norm_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                                  int dtype_out, int rows, int D, float eps, void* stream) {
+    if (!x || !y || !mean || !rstd || rows < 0 || D <= 0) return VFM_ERR_ARGS;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(w) |
+         reinterpret_cast<uintptr_t>(b)) % 8)
+        return VFM_ERR_ARGS;
+    if (D % 128 || D > 1024) return VFM_NO_KERNEL;
+    if (rows == 0) return VFM_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (dtype_out == VFM_F32) return ln2_fwd_launch<float>(x, w, b, y, mean, rstd, rows, D, eps, st);
+    if (dtype_out == VFM_BF16) return ln2_fwd_launch<__hip_bfloat16>(x, w, b, y, mean, rstd, rows, D, eps, st);
+    if (dtype_out == VFM_F16) return ln2_fwd_launch<__half>(x, w, b, y, mean, rstd, rows, D, eps, st);
+    return VFM_ERR_ARGS;
+}
+
+extern "C" int vfm_layer_norm_bwd(const float* x, const void* dy, const float* w, const float* mean,
+                                  const float* rstd, float* dx, int dtype_dy, int rows, int D, void* stream) {
+    if (!x || !dy || !mean || !rstd || !dx || rows < 0 || D <= 0) return VFM_ERR_ARGS;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(w)) % 8)
+        return VFM_ERR_ARGS;
+    if (D % 128 || D > 1024) return VFM_NO_KERNEL;
+    if (rows == 0) return VFM_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (dtype_dy == VFM_F32) return ln2_bwd_launch<float>(x, dy, w, mean, rstd, dx, rows, D, st);
+    if (dtype_dy == VFM_BF16) return ln2_bwd_launch<__hip_bfloat16>(x, dy, w, mean, rstd, dx, rows, D, st);
+    if (dtype_dy == VFM_F16) return ln2_bwd_launch<__half>(x, dy, w, mean, rstd, dx, rows, D, st);
+    return VFM_ERR_ARGS;
+}
 
 extern "C" int vfm_residual_layer_norm(const float* h, const void* delta, float* h_out, const float* w,
                                        const float* b, void* y, int dtype_delta, int dtype_out, int rows, int D,

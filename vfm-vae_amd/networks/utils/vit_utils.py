@@ -64,8 +64,18 @@ class Block(nn.Module):
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
     def forward(self, x):
-        x = x + self.attn(self.norm1(x))
-        return x + self.mlp(self.norm2(x))
+        x = x + self.attn(_norm(self.norm1, x))
+        return x + self.mlp(_norm(self.norm2, x))
+
+
+def _norm(ln, x):
+    """nn.LayerNorm(x); on ROCm fp32 with frozen parameters (the DINO discriminator backbone) the native
+    LayerNorm with an input gradient (csrc/vit.hip ln2_fwd / ln2_bwd) instead of torch's two kernels."""
+    if x.is_cuda and x.dtype == torch.float32:
+        from torch_utils.ops import vit_hip
+        if vit_hip.LN_GRAD and vit_hip.layer_norm_grad_supported(x, ln):
+            return vit_hip.layer_norm_grad(x, ln, torch.float32)
+    return ln(x)
 
 
 class VisionTransformer(nn.Module):

@@ -56,6 +56,8 @@ SIGNATURES = {
     "vfm_shuffle_blur_bwd": [c_vp, c_vp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "vfm_codebook_argmax": [c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp, c_vp],
     "vfm_residual_layer_norm": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_vp],
+    "vfm_layer_norm_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp],
+    "vfm_layer_norm_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
     "vfm_pw_gemm_gelu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
                          c_vp],
     "vfm_pw_gemm_gelu_tiles": [c_int],

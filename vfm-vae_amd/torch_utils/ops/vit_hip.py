@@ -1,9 +1,12 @@
 """gfx950 row kernels of the frozen ViT towers (csrc/vit.hip, C ABI in include/vfmvae.h).
 
-Forward only: the SigLIP2 encoder is frozen and runs under no_grad
-(reference networks/utils/vfms/siglip2_utils.py:114-137). Loading the library
+The residual LayerNorm is forward only: the SigLIP2 encoder is frozen and runs under no_grad
+(reference networks/utils/vfms/siglip2_utils.py:114-137). `layer_norm_grad` is the LayerNorm with a
+backward to its input for the frozen DINOv2 discriminator backbone in the G phase. Loading the library
 raises if it is missing (no silent fallback on ROCm tensors).
 """
+import os
+
 import torch
 
 from .. import custom_ops
@@ -47,3 +50,62 @@ def residual_layer_norm(h, delta, ln, out_dtype, write_h=True):
                                           custom_ops.stream_ptr(h.device))
     custom_ops.check(rc, "vfm_residual_layer_norm")
     return (h_out if h_out is not None else h), y
+
+
+_DN = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16"}
+# Routing switch (vit_utils.Block / vit_ops.layer_norm): off by default. The kernels replace torch's
+# LayerNorm kernels in the DINO discriminator (2.1 -> 0.8 ms/step of kernel time) but the bench measured
+# 94.5 / 93.6 img/s with them against 95.6 without (profiles/r5_bp_ln_grad_ab.txt): the autograd.Function
+# costs more host time per call than torch's native LayerNorm, and the DINO passes are host-bound.
+LN_GRAD = os.environ.get("VFM_LN_GRAD", "0") == "1"
+
+
+def layer_norm_grad_supported(h, ln):
+    """fp32 [.., D] input needing a gradient, frozen (or absent) affine parameters, D % 128 == 0, D <= 1024."""
+    D = h.shape[-1]
+    return (h.is_cuda and h.dtype == torch.float32 and D % 128 == 0 and D <= 1024 and h.numel() > 0
+            and not (ln.weight is not None and ln.weight.requires_grad)
+            and not (ln.bias is not None and ln.bias.requires_grad))
+
+
+class _LayerNorm(custom_ops.FastFunction):
+    """LayerNorm(x) * w + b in out_dtype with fp32 statistics; gradient to x only (frozen w / b)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps, out_dtype):
+        x = x.contiguous()
+        D = x.shape[-1]
+        rows = x.numel() // D
+        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+        mean = torch.empty([rows], dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        with kernel_timer.region(f'layer_norm_fwd<{_DN[y.dtype]}>', rows * D * (4 + y.element_size())):
+            custom_ops.check(_lib.vfm_layer_norm_fwd(x.data_ptr(), custom_ops.ptr(w), custom_ops.ptr(b), y.data_ptr(),
+                                                     mean.data_ptr(), rstd.data_ptr(), custom_ops.dtype_code(y), rows,
+                                                     D, float(eps), custom_ops.stream_ptr(x.device)),
+                             "vfm_layer_norm_fwd")
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        D = x.shape[-1]
+        rows = x.numel() // D
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        with kernel_timer.region(f'layer_norm_bwd<{_DN[dy.dtype]}>', rows * D * (8 + dy.element_size())):
+            custom_ops.check(_lib.vfm_layer_norm_bwd(x.data_ptr(), dy.data_ptr(), custom_ops.ptr(w), mean.data_ptr(),
+                                                     rstd.data_ptr(), dx.data_ptr(), custom_ops.dtype_code(dy), rows,
+                                                     D, custom_ops.stream_ptr(x.device)), "vfm_layer_norm_bwd")
+        return dx, None, None, None, None
+
+
+def layer_norm_grad(h, ln, out_dtype):
+    """LayerNorm of an fp32 stream that needs a gradient, through frozen parameters (DINOv2 discriminator)."""
+    w = ln.weight.detach().float().contiguous() if ln.weight is not None else None
+    b = ln.bias.detach().float().contiguous() if ln.bias is not None else None
+    w = w.clone() if w is not None and w.data_ptr() % 8 else w
+    b = b.clone() if b is not None and b.data_ptr() % 8 else b
+    return _LayerNorm.apply(h, w, b, float(ln.eps), out_dtype)

@@ -119,6 +119,12 @@ def layer_norm(h, ln, out_dtype):
         from . import vit_hip
         if vit_hip.supported(h):
             return vit_hip.residual_layer_norm(h, None, ln, out_dtype)[1]
+        if h.dtype == torch.float32 and h.shape[-1] % 128 == 0 and h.shape[-1] <= 1024 and vit_hip.LN_GRAD:
+            return vit_hip.layer_norm_grad(h, ln, out_dtype)    # D = 384 (DINOv2 ViT-S) without a graph
+    elif torch.is_grad_enabled() and h.is_cuda:
+        from . import vit_hip
+        if vit_hip.LN_GRAD and vit_hip.layer_norm_grad_supported(h, ln):   # frozen backbone, input gradient
+            return vit_hip.layer_norm_grad(h, ln, out_dtype)
     return F.layer_norm(h.float(), (h.shape[-1],), ln.weight.float(), ln.bias.float(), ln.eps).to(out_dtype)
 
 
