@@ -354,8 +354,13 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None, steps=
                              "ms_total": round(vr["total_ms"], 3), "launches": vr["launches"],
                              "avg_us": round(vr["total_ms"] * 1e3 / vr["launches"], 2)}
         out["vendor_gemm_ms_total"] = round(sum(v["total_ms"] for v in vend.values()), 3)
-    out["all_kernels"] = {k: {"ms": round(v["total_ms"], 3), "launches": v["launches"],
-                              "GBps": round(v["bytes"] / max(v["total_ms"], 1e-9) / 1e6, 1),
-                              "TFps": round(v["flops"] / max(v["total_ms"], 1e-9) / 1e9, 1)}
-                          for k, v in sorted(s.items(), key=lambda kv: -kv[1]["total_ms"])}
+    out["all_kernels"] = {}
+    for k, v in sorted(s.items(), key=lambda kv: -kv[1]["total_ms"]):
+        gbps = v["bytes"] / max(v["total_ms"], 1e-9) / 1e6
+        row = {"ms": round(v["total_ms"], 3), "launches": v["launches"], "GBps": round(gbps, 1),
+               "TFps": round(v["flops"] / max(v["total_ms"], 1e-9) / 1e9, 1)}
+        if gbps > hbm_peak_gbs:
+            # algorithmic bytes faster than HBM can deliver: operands (partly) served from L2 / MALL
+            row["cache_served"] = True
+        out["all_kernels"][k] = row
     return out
