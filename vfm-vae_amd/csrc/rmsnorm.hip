@@ -10,7 +10,8 @@
 //   dgamma[c]  = scale * sum_{b, p} dy x / n
 //
 // Block = 16 columns (consecutive p) x 64 channel groups; a thread sums every 64th channel of its
-// column (1024 threads: the 8^2-32^2 planes give only 128-2048 blocks), the 64 partial sums meet in LDS, then the same threads write their channels. The gamma
+// column (1024 threads: the 8^2-32^2 planes give only 128-2048 blocks), the 64 partial sums meet in
+// LDS, then the same threads write their channels. The gamma
 // gradient: each block reduces dy x / n over its 16 columns per channel into one partial (channel-major
 // [C][blocks]), and a second kernel sums every channel's partials in a fixed order (deterministic).
 #include "vfm_common.h"
