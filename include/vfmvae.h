@@ -387,6 +387,25 @@ int vfm_gemm_fold(const void* A, const void* B, void* C, const float* bias, int 
                   int lgp, int K, int batch, int a_kcont, long long lda, long long ldb, long long sB, long long ldc,
                   long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 
+/* Exact-fp32 form of the vfm_gemm contract on the fp32-input MFMA (csrc/sgemm.hip, v_mfma_f32_32x32x2_f32: one
+ * fmaf-chain product per multiply-add, no operand split): C[z] = epi(alpha A[z] B[z] + beta C[z]), fp32 A / B / C,
+ * bias (1 per column, 2 per row) then act (1 gelu tanh, 2 gelu erf). Replaces the reference's fp32 products with
+ * TF32 off (training/training_loop.py:504-505) that the bf16-piece kernels serve badly: the D heads' batch-folded
+ * SpectralConv1d k = 1 / 9 products (reference networks/discriminator.py:39-42, :116-142), the decoder's narrow
+ * 1x1 convolutions and GigaGAN projections of the 4^2 .. 8^2 blocks (networks/utils/convnext_utils.py:36-57,
+ * :135-138, gigagan_utils.py:53-185), the adapter's 64-wide linears (ldm_utils.py:55-166) and the small FC layers
+ * (networks/utils/shared.py FullyConnectedLayer). Layouts as vfm_gemm; contiguous extents and leading dims
+ * multiples of 4 floats and 16-B aligned A / B (else VFM_NO_KERNEL). lgp > 0: the vfm_gemm_fold batch folding
+ * (B[z] MN-contiguous [K][2^lgp], C[z] [M][2^lgp], N = batch 2^lgp). splits > 1 and / or reduce_batch (C = epi(
+ * alpha sum_z A[z] B[z]), [M, N]): the virtual K-tiles (of every batch item when reduce_batch) cut into `splits`
+ * chunks of fp32 partials in `workspace` (vfm_sgemm_workspace_floats), summed in a fixed order. tile: 0 128x128,
+ * 1 128x64, 2 64x128, 3 64x64, < 0 chosen from the shape. */
+int vfm_sgemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int batch,
+              int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB, long long ldc,
+              long long sC, float alpha, float beta, int bias_mode, int act, int lgp, float* workspace, int splits,
+              int reduce_batch, int tile, void* stream);
+long long vfm_sgemm_workspace_floats(int M, int N, int batch, int splits, int reduce_batch);
+
 /* Large-tile form (csrc/gemm8.hip: 256 x 256 tiles, 4-phase LDS-DMA pipeline) of the same contract,
  * K % 64 == 0 (else VFM_NO_KERNEL). precision VFM_BF16: A / B are bf16 matrices as above. precision
  * VFM_F32 / VFM_F32X3: A / B hold the bf16 pieces of fp32 operands from vfm_split_f32 (3 pieces:

@@ -327,3 +327,20 @@ def test_gemm9_f32x6_batched_split(M, N, K, z, b_kc):
     vend = torch.matmul(A, Bt.transpose(1, 2))
     assert _rel(out, ref) <= 2 * _rel(vend, ref) + 1e-7
     assert torch.equal(out, again)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(64, 512, 256), (512, 48, 128), (40, 40, 4096), (64, 1024, 32768), (24, 96, 2048)])
+@pytest.mark.parametrize("a_kc", [True, False])
+def test_gemm9_narrow_routes(M, N, K, a_kc):
+    """bf16 products narrower than a 128-wide output through try_gemm(auto=True): gemm9 unsplit, or its K split
+    (few output tiles over a deep K: `_plan` -> "g9r"); fp32 output within the fp32 accumulation order."""
+    if M % 8 and not a_kc:
+        pytest.skip("M-contiguous A needs M % 8 == 0 (16-B DMA chunks)")
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    A = _rnd(M, K, g=g)
+    Bt = _rnd(N, K, g=g)
+    a = A if a_kc else _operand(A, False)
+    out = gemm_hip.try_gemm(a, Bt.t(), auto=True, out_dtype=torch.float32)
+    assert out is not None and out.shape == (M, N)
+    assert _rel(out, A.float() @ Bt.float().t()) < 2e-5

@@ -102,17 +102,18 @@ def test_im2col1d_matches_torch(B, C, L, k, p, circ):
 @pytest.mark.parametrize("B,C,O,L,k,p,circ,bias", [(32, 384, 384, 196, 9, 4, True, True), (8, 384, 384, 196, 1, 0, False, True),
                                                    (8, 384, 64, 196, 1, 0, False, False), (3, 8, 5, 10, 3, 1, False, True),
                                                    (2, 16, 7, 5, 5, 2, True, False)])
-@pytest.mark.parametrize("own", [False, True], ids=["hipblaslt", "f32x6"])
+@pytest.mark.parametrize("own", ["sgemm", "torch", "hip"], ids=["sgemm", "hipblaslt", "f32x6"])
 def test_conv1d_folded_matches_conv1d(B, C, O, L, k, p, circ, bias, own, monkeypatch):
     """The D heads' Conv1d as batch-folded GEMMs (patchgan_hip.conv1d_folded: cols [C k, B Lo] from
-    vfm_im2col1d_cbl_f32, exact-fp32 vendor GEMMs -- or, opt-in, our f32x6 GEMM -- folded col2im) vs F.conv1d (circular padding through
+    vfm_im2col1d_cbl_f32, the exact-fp32 MFMA GEMM (csrc/sgemm.hip, default) -- or, for A/B, hipBLASLt's exact
+    fp32 / our f32x6 GEMM -- folded col2im) vs F.conv1d (circular padding through
     F.pad) in fp32 and in fp64: output and every gradient within 1e-5 of max |ref| (exact fp32 products
     in another summation order: the k = 9 input gradient sums 3456 products; measured 3.2e-6 against
     F.conv1d's fp32 and 3.0e-6 against fp64, where MIOpen's own fp32 is 6e-7 from fp64), and within
     5e-6 of the fp64 result; the folded gather bit-identical to the per-sample one transposed."""
     from torch_utils.ops import patchgan_hip
     import torch.nn.functional as F
-    monkeypatch.setattr(patchgan_hip, "_DHEAD_OWN", own)
+    monkeypatch.setattr(patchgan_hip, "_DHEAD", own)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
     g0 = torch.Generator().manual_seed(B * O + k)

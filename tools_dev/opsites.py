@@ -36,6 +36,11 @@ def _repo_frames(frames, n=3):
     return " < ".join(reversed(out[-n:]))
 
 
+# OPSITES_OPS=mm,bmm,addmm,convolution: only aten ops whose name contains one of these (the library GEMM /
+# convolution call sites), printed with their shapes
+ONLY = [o for o in os.environ.get("OPSITES_OPS", "").split(",") if o]
+
+
 class Sites(TorchDispatchMode):
     def __init__(self):
         super().__init__()
@@ -53,7 +58,7 @@ class Sites(TorchDispatchMode):
         out = func(*args, **(kwargs or {}))
         if ev is not None:
             ev[1].record()
-        if name in SKIP:
+        if name in SKIP or (ONLY and not any(o in name for o in ONLY)):
             return out
         t = out[0] if isinstance(out, (tuple, list)) and out else out
         if not (isinstance(t, torch.Tensor) and (t.is_cuda or os.environ.get("OPSITES_CPU"))):
@@ -70,6 +75,9 @@ class Sites(TorchDispatchMode):
             where = f"bwd {node.name()}{' @ ' + here if here else ''} < " + " < ".join(reversed(sites[-2:]))
         else:
             where = "fwd " + _repo_frames(traceback.extract_stack())
+        if ONLY:
+            where += "  " + " ".join(str(tuple(a.shape)) + ("" if a.is_contiguous() else "nc")
+                                     for a in args if isinstance(a, torch.Tensor)) + f" {t.dtype}"
         self.count[(name, where)] += 1
         if ev is not None:
             self.events[(name, where)].append(ev)

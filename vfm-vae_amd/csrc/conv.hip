@@ -298,11 +298,12 @@ __global__ __launch_bounds__(2 * BM, (BM == 256 || (NP == 3 && BN == 128)) ? 1 :
 template <int BM, int BN, int NP>
 int launch(const ConvArgs& a, hipStream_t st) {
     const size_t lds = 2 * NP * (BM + BN) * ROWB;
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)conv3x3_kernel<BM, BN, NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-        attr = true;
+        attr[dv_attr] = true;
     }
     const long long tiles = (long long)((a.M + BM - 1) / BM) * (a.Cout / BN);
     if (tiles > 0x7fffffff) return VFM_ERR_ARGS;
@@ -430,11 +431,12 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_small(const float* __restri
 template <int C>
 int launch_dgrad(const float* dz, const float* w, float* dx, int B, int H, int W, int K, hipStream_t st) {
     const size_t lds = (3 * (DG_PX + 2) * (size_t)(K + 4) + 9 * (size_t)C * K) * 4;
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)conv3x3_dgrad_small<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (3 * (DG_PX + 2) * (128 + 4) + 9 * 4 * 128) * 4);
-        attr = true;
+        attr[dv_attr] = true;
     }
     VFM_LAUNCH((conv3x3_dgrad_small<C>), dim3((W + DG_PX - 1) / DG_PX, H, B), dim3(256), lds, st, dz, w, dx, H, W,
                        K);

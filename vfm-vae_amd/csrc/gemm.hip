@@ -303,11 +303,12 @@ template <bool AK, bool BKC, int NP, bool OUTF32, int NW>
 int launch_nw(const GemmArgs& a, int batch, hipStream_t st) {
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const size_t lds = 2 * NP * IMG;
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)gemm_kernel<AK, BKC, NP, OUTF32, NW>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+        attr[dv_attr] = true;
     }
     VFM_LAUNCH((gemm_kernel<AK, BKC, NP, OUTF32, NW>), dim3(tiles, batch * a.splits), dim3(64 * NW), lds, st, a);
     return launch_status();

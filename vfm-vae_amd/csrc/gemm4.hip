@@ -329,11 +329,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm4_kernel(G4Args a) {
 
 template <bool AK, bool BKC, bool OUTF32>
 void launch4(const G4Args& a, int batch, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)gemm4_kernel<AK, BKC, OUTF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * STAGE);
-        attr = true;
+        attr[dv_attr] = true;
     }
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     VFM_LAUNCH((gemm4_kernel<AK, BKC, OUTF32>), dim3(nwg, batch), dim3(THREADS), 2 * STAGE, st, a);

@@ -620,11 +620,12 @@ int g_deep = 0;                  // K-tile staging: 1 = two K-tiles ahead, 0 = o
 
 template <bool AK, bool BKC, bool OUTF32, bool DEEP, int EPI>
 void launch8d(const G8Args& a, int nwg, int ny, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)gemm8_kernel<AK, BKC, OUTF32, DEEP, EPI>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
-        attr = true;
+        attr[dv_attr] = true;
     }
     VFM_LAUNCH((gemm8_kernel<AK, BKC, OUTF32, DEEP, EPI>), dim3(nwg, ny), dim3(THREADS), 2 * BUF, st, a);
 }

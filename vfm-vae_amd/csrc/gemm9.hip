@@ -957,22 +957,18 @@ __global__ __launch_bounds__(256) void gemm9_reduce_batched(const float* __restr
 
 int g_persistent = 1;            // vfm_gemm9_set_mode: 1 persistent (default), 0 one workgroup per tile
 
+
 // fp32-equivalent (NP = 3) products: fp32 C, plain or bias epilogue, persistent form
 template <bool AK, bool BKC>
 void launch9_pieces(const G9Args& a, int batch, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, true, 0, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
         (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, true, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
-        attr = true;
+        attr[dv_attr] = true;
     }
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
+    const int cus = device_cus(cur_dev());
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const long long total = (long long)nwg * batch;
     const int grid = (int)std::min<long long>(total, cus);
@@ -985,30 +981,26 @@ void launch9_pieces(const G9Args& a, int batch, hipStream_t st) {
 
 template <bool AK, bool BKC, bool OUTF32>
 void launch9(const G9Args& a, int batch, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)gemm9_kernel<AK, BKC, OUTF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * STAGE);
-        attr = true;
+        attr[dv_attr] = true;
     }
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const bool plain = a.beta == 0.f && a.bias_mode == 0 && a.act == 0 && a.alpha == 1.f;
     if (g_persistent && a.beta == 0.f) {
-        static bool attrp = false;
-        if (!attrp) {
+        static bool attrp[MAXDEV] = {};
+        const int dv_attrp = cur_dev();
+        if (!attrp[dv_attrp]) {
             (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
             (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
             (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
             (void)hipFuncSetAttribute((const void*)gemm9p_kernel<AK, BKC, OUTF32, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
-            attrp = true;
+            attrp[dv_attrp] = true;
         }
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (cus <= 0) cus = 256;
-        }
+        const int cus = device_cus(cur_dev());
         const long long total = (long long)nwg * (a.reduce ? a.S : batch);
         const int grid = (int)std::min<long long>(total, cus);
         if (plain)
@@ -1177,19 +1169,14 @@ extern "C" int vfm_gemm9_gelu(const void* W, const void* X, void* C, void* C2, c
     a.spanB = span9(0, N, K, ldb, sB, batch);
     a.spanC = ((long long)(M - 1) * ldc + N + (long long)(batch - 1) * sC) * 2;
     hipStream_t st = (hipStream_t)stream;
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)gemm9p_kernel<true, false, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
         (void)hipFuncSetAttribute((const void*)gemm9p_kernel<true, false, false, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS9P);
-        attr = true;
+        attr[dv_attr] = true;
     }
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
+    const int cus = device_cus(cur_dev());
     const long long total = nwg * batch;
     const int grid = (int)std::min<long long>(total, cus);
     if (mode == 1)

@@ -276,11 +276,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void pw_gemm_gelu(PwArgs a) {
 template <int MODE, int K>
 int launch(const PwArgs& a, int B, hipStream_t st) {
     const size_t lds = (size_t)K * 256 + 8 * (size_t)a.M;
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)pw_gemm_gelu<MODE, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   K * 256 + 8 * 2048);
-        attr = true;
+        attr[dv_attr] = true;
     }
     VFM_LAUNCH((pw_gemm_gelu<MODE, K>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
     return launch_status();
@@ -488,10 +489,11 @@ __global__ __launch_bounds__(64 * WAVES, 2) void mlp_fwd(MlpArgs a) {
 }
 template <int C, bool SAVE>
 void launch_mlp(const MlpArgs& a, int B, size_t lds, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[MAXDEV] = {};
+    const int dv_attr = cur_dev();
+    if (!attr[dv_attr]) {
         (void)hipFuncSetAttribute((const void*)mlp_fwd<C, SAVE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+        attr[dv_attr] = true;
     }
     VFM_LAUNCH((mlp_fwd<C, SAVE>), dim3(a.N / NT, B), dim3(64 * WAVES), lds, st, a);
 }

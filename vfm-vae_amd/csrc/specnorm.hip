@@ -110,7 +110,7 @@ __global__ __launch_bounds__(THREADS) void sn_wv(const float* __restrict__ W, co
 __global__ __launch_bounds__(THREADS) void sn_scale(const float* __restrict__ W, const float* __restrict__ r,
                                                     const float* __restrict__ rpart, int nrp, float* __restrict__ u,
                                                     float* __restrict__ u_copy, float* __restrict__ sigma,
-                                                    float* __restrict__ Wsn, int O, long long n, float eps) {
+                                                    float* __restrict__ Wsn, int O, long long n, float eps, int vec) {
     __shared__ float sh[4];
     const float rr = sum_parts(rpart, nrp, sh);
     const float inv = 1.f / fmaxf(sqrtf(rr), eps);
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(THREADS) void sn_scale(const float* __restrict__ W,
         if (threadIdx.x == 0) sigma[0] = sg;
     }
     const float is = 1.f / sg;
-    if ((n & 3) == 0) {                              // float4 per thread (the grid covers n / 4 in one pass)
+    if (vec) {                                       // float4 per thread (n % 4 == 0, 16-B aligned W / Wsn)
         const long long n4 = n >> 2;
         for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n4; e += (long long)gridDim.x * THREADS) {
             float4 w = reinterpret_cast<const float4*>(W)[e];
@@ -138,10 +138,10 @@ __global__ __launch_bounds__(THREADS) void sn_scale(const float* __restrict__ W,
 }
 
 __global__ __launch_bounds__(THREADS) void sn_gw(const float* __restrict__ g, const float* __restrict__ W,
-                                                 float* __restrict__ part, long long n) {
+                                                 float* __restrict__ part, long long n, int vec) {
     __shared__ float sh[4];
     float s = 0.f;
-    if ((n & 3) == 0) {
+    if (vec) {                                       // n % 4 == 0, 16-B aligned g / W
         const long long n4 = n >> 2;
         for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n4; e += (long long)gridDim.x * THREADS) {
             const float4 a = reinterpret_cast<const float4*>(g)[e], b = reinterpret_cast<const float4*>(W)[e];
@@ -158,12 +158,12 @@ __global__ __launch_bounds__(THREADS) void sn_gw(const float* __restrict__ g, co
 __global__ __launch_bounds__(THREADS) void sn_dw(const float* __restrict__ g, const float* __restrict__ u,
                                                  const float* __restrict__ v, const float* __restrict__ sigma,
                                                  const float* __restrict__ part, int np, float* __restrict__ dW,
-                                                 int I, long long n) {
+                                                 int I, long long n, int vec) {
     __shared__ float sh[4];
     const float S = sum_parts(part, np, sh);
     const float sg = sigma[0];
     const float is = 1.f / sg, c = S / (sg * sg);
-    if ((I & 3) == 0) {                              // float4 per thread: the 4 elements share a row
+    if (vec) {                                       // float4 per thread (I % 4 == 0, 16-B aligned g / v / dW)
         const long long n4 = n >> 2;
         const int I4 = I >> 2;
         for (long long e = (long long)blockIdx.x * THREADS + threadIdx.x; e < n4; e += (long long)gridDim.x * THREADS) {
@@ -208,9 +208,11 @@ extern "C" int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_cop
     VFM_LAUNCH(sn_wtu, dim3(tb), dim3(THREADS), 0, st, W, u, t, tpart, O, I);
     VFM_LAUNCH(sn_wv, dim3(rb), dim3(THREADS), 0, st, W, t, tpart, tb, v, v_copy, r, rpart, O, I, eps);
     const long long n = (long long)O * I;
-    const long long work = (n & 3) ? n : n / 4;       // threads' items (float4 when n % 4 == 0)
+    // float4 only on 16-B aligned views (a weight view with a storage offset takes the scalar loop)
+    const int vec = (n & 3) == 0 && (((uintptr_t)W | (uintptr_t)Wsn) & 15) == 0;
+    const long long work = vec ? n / 4 : n;           // threads' items
     const int sb = (int)std::min<long long>(4096, (work + THREADS - 1) / THREADS);
-    VFM_LAUNCH(sn_scale, dim3(sb), dim3(THREADS), 0, st, W, r, rpart, rb, u, u_copy, sigma, Wsn, O, n, eps);
+    VFM_LAUNCH(sn_scale, dim3(sb), dim3(THREADS), 0, st, W, r, rpart, rb, u, u_copy, sigma, Wsn, O, n, eps, vec);
     return launch_status();
 }
 
@@ -221,7 +223,9 @@ extern "C" int vfm_specnorm_bwd(const float* g, const float* W, const float* u, 
     const long long n = (long long)O * I;
     const int nb = (int)std::min<long long>(SCALE_BLOCKS, (n + THREADS - 1) / THREADS);
     hipStream_t st = (hipStream_t)stream;
-    VFM_LAUNCH(sn_gw, dim3(nb), dim3(THREADS), 0, st, g, W, ws, n);
-    VFM_LAUNCH(sn_dw, dim3(nb), dim3(THREADS), 0, st, g, u, v, sigma, ws, nb, dW, I, n);
+    const int vg = (n & 3) == 0 && (((uintptr_t)g | (uintptr_t)W) & 15) == 0;
+    const int vd = (I & 3) == 0 && (((uintptr_t)g | (uintptr_t)v | (uintptr_t)dW) & 15) == 0;
+    VFM_LAUNCH(sn_gw, dim3(nb), dim3(THREADS), 0, st, g, W, ws, n, vg);
+    VFM_LAUNCH(sn_dw, dim3(nb), dim3(THREADS), 0, st, g, u, v, sigma, ws, nb, dW, I, n, vd);
     return launch_status();
 }

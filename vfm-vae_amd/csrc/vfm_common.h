@@ -138,6 +138,24 @@ struct TimerArm {
 };
 TimerArm& timer_arm();
 
+// Per-device launch state (a process may drive several GPUs): the current device's index, its CU count, and
+// (at the call sites) one "dynamic LDS attribute set" flag per device for each kernel instantiation.
+constexpr int MAXDEV = 64;
+inline int cur_dev() {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    return (d < 0 || d >= MAXDEV) ? 0 : d;
+}
+inline int device_cus(int d) {
+    static int cus[MAXDEV] = {};
+    if (!cus[d]) {
+        int c = 0;
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d);
+        cus[d] = c > 0 ? c : 256;
+    }
+    return cus[d];
+}
+
 inline int launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? VFM_OK : (int)e;

@@ -15,9 +15,10 @@ import torch.nn.functional as F
 
 from torch_utils import distributed as dist
 from torch_utils.ops import vit_ops
-from torch_utils.ops.linear import Linear, linear
+from torch_utils.ops.linear import Linear, linear, bmm
 from networks.utils import kl_utils
 from networks.utils.kl_utils import DiagonalGaussianDistribution
+from networks.utils.shared import Conv1x1
 from networks.utils.quant_utils import VectorQuantizerM
 from networks.utils.dataclasses import EncodeOutput
 
@@ -251,7 +252,7 @@ class LDMAdapter(nn.Module):
 
         if use_vf_loss:
             vf_dim = patch_in_dimensions[patch_from_layers.index(-1)]
-            self.linear_proj = nn.Conv2d(in_ch, vf_dim, 1, bias=False)
+            self.linear_proj = Conv1x1(in_ch, vf_dim, 1, bias=False)   # nn.Conv2d keys; 1x1 on our GEMMs
             init_weights(self.linear_proj, conv_std_or_gain=-0.5)
             self.distmat_margin = distmat_margin
             self.cos_margin = cos_margin
@@ -265,8 +266,8 @@ class LDMAdapter(nn.Module):
         B, C = z.shape[:2]
         zn = F.normalize(z.reshape(B, C, -1), dim=1)
         an = F.normalize(aux.reshape(B, aux.shape[1], -1), dim=1)
-        z_cos = torch.bmm(zn.transpose(1, 2), zn)
-        a_cos = torch.bmm(an.transpose(1, 2), an)
+        z_cos = bmm(zn.transpose(1, 2), zn)
+        a_cos = bmm(an.transpose(1, 2), an)
         l1 = F.relu((z_cos - a_cos).abs() - self.distmat_margin).mean()
         l2 = F.relu(1 - self.cos_margin - F.cosine_similarity(aux, z)).mean()
         return l1 * self.distmat_weight + l2 * self.cos_weight

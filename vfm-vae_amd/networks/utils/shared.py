@@ -44,9 +44,16 @@ class FullyConnectedLayer(nn.Module):
     def forward(self, x):
         w = self.weight.to(x.dtype) * self.weight_gain
         b = self.bias.to(x.dtype) * self.bias_gain if self.bias is not None else None
-        if self.activation == 'linear':
+        if x.is_cuda and x.dtype == torch.float32:
+            # the product (and its gradients) on our exact-fp32 GEMM (torch_utils/ops/linear.py -> csrc/sgemm.hip)
+            from torch_utils.ops.linear import linear
+            if self.activation == 'linear':
+                return linear(x, w, b)
+            y = linear(x, w, None)
+        elif self.activation == 'linear':
             return torch.addmm(b.unsqueeze(0), x, w.t()) if b is not None else x.matmul(w.t())
-        y = x.matmul(w.t())
+        else:
+            y = x.matmul(w.t())
         if self.activation in ('relu', 'lrelu') and y.is_cuda:
             # bias + activation in one HIP bias_act pass (gain 1: F.relu / F.leaky_relu(0.2) semantics)
             from torch_utils.ops import bias_act

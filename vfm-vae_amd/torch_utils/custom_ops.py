@@ -152,6 +152,9 @@ SIGNATURES = {
                          c_ll, c_ll, c_ll, c_float, c_int, c_vp, c_int, c_int, c_vp],
     "vfm_gemm9": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
                   c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
+    "vfm_sgemm": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll, c_ll, c_ll,
+                  c_float, c_float, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
+    "vfm_sgemm_workspace_floats": [c_int, c_int, c_int, c_int, c_int],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,
                       c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_timer_arm": [c_vp, c_vp],
@@ -241,6 +244,7 @@ def get_native():
             lib.vfm_version.restype = ctypes.c_char_p
             lib.vfm_bnl_workspace_floats.restype = c_ll
             lib.vfm_gemm9_workspace_floats.restype = c_ll
+            lib.vfm_sgemm_workspace_floats.restype = c_ll
             lib.vfm_channel_rms_norm_rows.restype = c_ll
             lib.vfm_specnorm_workspace_floats.restype = c_ll
             lib.vfm_dwconv2d_fwd_mfma_units.restype = c_ll

@@ -12,6 +12,7 @@ report the dominant kernel's roofline.
 """
 import ctypes
 import os
+import threading
 import weakref
 
 import torch
@@ -322,18 +323,24 @@ DW_MFMA = os.environ.get("VFM_DW_MFMA", "1") == "1"      # A/B switch for the ba
 
 
 GN_STATS = os.environ.get("VFM_GN_STATS", "1") == "1"      # A/B switch: GroupNorm statistics from the dwconv
-_gn_stats = None        # (weakref of y, data_ptr, version, shape, partials, units per plane) of the last dwconv
+# The handoff is per thread (threading.local) and keyed on the output tensor itself (weakref), its device, storage
+# pointer, shape and version. Contract: nothing writes y in place between the dwconv and the GroupNorm that consumes
+# it -- the one consumer is the next op of ConvNeXtSynthesisLayer.forward (networks/utils/convnext_utils.py), and a
+# torch in-place write bumps y._version, which voids the handoff; a raw-pointer write by a native kernel would not,
+# and none exists on that edge.
+_gn_tls = threading.local()     # .e = (weakref of y, device, data_ptr, version, shape, partials, units per plane)
 
 
 def _gn_stats_for(x):
     """The dwconv's GroupNorm partials when x is that dwconv's unchanged output (one consumer)."""
-    global _gn_stats
-    e, _gn_stats = _gn_stats, None
+    e = getattr(_gn_tls, "e", None)
+    _gn_tls.e = None
     if e is None:
         return None
-    yref, ptr, ver, shape, part, upc = e
+    yref, dev, ptr, ver, shape, part, upc = e
     y = yref()
-    if y is None or x.data_ptr() != ptr or x.shape != shape or x._version != ver or y._version != ver:
+    if (y is None or x.data_ptr() != ptr or x.shape != shape or x.device != dev or x._version != ver
+            or y._version != ver):
         return None
     return part, upc
 
@@ -345,7 +352,6 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None, gs
     (b, c, y, x) as a 0-d fp32 tensor -- from per-wave partials of the MFMA kernel when it runs, else
     by torch -- i.e. (y, dot). gstat: the MFMA kernel also writes y's GroupNorm partials, which the
     GroupNorm that consumes y picks up (_gn_stats_for) instead of its own statistics pass."""
-    global _gn_stats
     B, C, H, W = x.shape
     K = w3.shape[-1]
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
@@ -365,7 +371,7 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None, gs
                                                        y.data_ptr(), gs.data_ptr(), B, C, H, W, K, pad, _stream())
                 if rc != custom_ops.VFM_NO_KERNEL:
                     _check(rc, name)
-                    _gn_stats = (weakref.ref(y), y.data_ptr(), y._version, y.shape, gs, units // (B * C))
+                    _gn_tls.e = (weakref.ref(y), y.device, y.data_ptr(), y._version, y.shape, gs, units // (B * C))
                     return y
         part = None
         if nplane is not None and Ho == H and Wo == W:

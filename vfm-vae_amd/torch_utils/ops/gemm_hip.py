@@ -142,9 +142,11 @@ def _workspace(n, dev):
 
 def preferred(A, M, N, reduce_batch=False):
     """Where this kernel family is routed (tools_dev/gemmbench.py, tools_dev/g4bench.py, MI355X): fp32
-    operands (the fp32-equivalent split at >= 128-wide tiles, and the batch-reduced weight gradients at
-    any width); bf16 operands on the LDS-DMA one-wave-per-SIMD kernel (csrc/gemm9.hip) at >= 128-wide
-    outputs (VFM_BF16_GEMM=torch: hipBLASLt, for A/B)."""
+    operands on the bf16-piece kernels (the fp32-equivalent split) at >= 128-wide outputs and for the
+    batch-reduced weight gradients at any width -- narrower fp32 products go to the exact-fp32 kernel
+    (`sgemm`, csrc/sgemm.hip); bf16 operands of any width on the LDS-DMA one-wave-per-SIMD kernel
+    (csrc/gemm9.hip; single products with few output tiles over a deep K run split, `_plan`), or
+    hipBLASLt under VFM_BF16_GEMM=torch (A/B)."""
     if A.dtype == torch.bfloat16:
         return BF16_OWN
     if A.dtype != torch.float32:
@@ -169,6 +171,11 @@ def _plan(dtype, M, N, K, z, reduce_batch, splits, auto):
             tiles = -(-M // 256) * -(-N // 256)
             return "g9r", max(1, min(-(-512 // tiles), z * (K // 64) // 4))
         if splits <= 1:
+            tiles = -(-M // 256) * -(-N // 256) * z
+            if z == 1 and tiles < 128 and K >= 2048:
+                # few output tiles over a deep reduction (e.g. a bf16 linear's weight gradient dy^T x, K =
+                # tokens): K splits on gemm9 so the grid covers the CUs (unsplit it ran on `tiles` workgroups)
+                return "g9r", max(1, min(-(-256 // tiles), K // 64 // 4))
             return "g9", 0
     if not FAST or K % 64:
         return "g128", splits
@@ -294,6 +301,9 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
         if out is not None:
             return out
     if auto and not preferred(A, M, N, reduce_batch):
+        if SGEMM and A.dtype == torch.float32 and (out_dtype or A.dtype) == torch.float32:
+            return sgemm(a3, b3, out=out, bias=bias, bias_dim=bias_dim, act=act, alpha=alpha, beta=beta,
+                         reduce_batch=reduce_batch, batched_out=(A.dim() == 3 or B.dim() == 3))
         return None
     g9f = None                                  # f32x6 on gemm9: K splits of the product (see _splits9f)
     if (auto and route is None and G9_F32 and A.dtype == torch.float32 and beta == 0.0 and act is None
@@ -536,4 +546,112 @@ def gemm(A, B, **kw):
     if out is None:
         raise custom_ops.NativeError(f"vfm_gemm does not cover A {tuple(A.shape)} {A.stride()} / "
                                      f"B {tuple(B.shape)} {B.stride()} {A.dtype}")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Exact-fp32 products on the fp32-input MFMA (csrc/sgemm.hip): the narrow fp32 products (outputs under 128 wide:
+# the 4^2 / 8^2 decoder blocks' 1x1s and GigaGAN projections, the adapter's 64-wide linears, the mapping / style
+# FC layers) that `preferred` keeps off the bf16-piece kernels, and the D heads' 1-D convolutions
+# (patchgan_hip.conv1d_folded). VFM_SGEMM=0: those products go back to the library (torch / hipBLASLt) for A/B.
+SGEMM = __import__("os").environ.get("VFM_SGEMM", "1") == "1"
+SG_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))      # tile codes 0-3; +4: two wave groups (KW = 2)
+
+
+def _sg_plan(M, N, K, zt, vt):
+    """(tile code, K splits) of an exact-fp32 product with zt independent output planes and vt virtual K-tiles
+    (32 deep) per output: 128 x 128 tiles when they alone give >= 1024 workgroups (4096^2: 130 TF/s), else
+    64 x 64 tiles, split along K until >= ~512 workgroups cover the 256 CUs, each chunk >= 8 K-tiles
+    (tools_dev/sgemmbench.py sweeps, profiles/r6_sgemmbench.txt: the D heads' 1-D convs 60-109 TF/s against
+    hipBLASLt's 50-100, the 4^2 decoder 1x1s 1.1-1.4x hipBLASLt, the weight gradients 1.2-2.3x)."""
+    if -(-M // 128) * -(-N // 128) * zt >= 1024:
+        return 0, 1
+    tiles = -(-M // 64) * -(-N // 64) * zt
+    if tiles >= 480:
+        return 3, 1
+    return 3, max(1, min(-(-512 // tiles), vt // 8))
+
+
+def _sg_layouts(t3, outer, kdim):
+    """Candidate (k_contiguous, leading dim) layouts of a [z, ., .] fp32 view whose dims `outer` / `kdim` are the
+    outer (m or n) and reduction indices, K-contiguous first; extents of 1 take any stride."""
+    so, sk = t3.stride(outer), t3.stride(kdim)
+    no, nk = t3.shape[outer], t3.shape[kdim]
+    out = []
+    if sk == 1 or nk == 1:
+        out.append((True, so if no > 1 else -(-nk // 4) * 4))
+    if so == 1 or no == 1:
+        out.append((False, sk if nk > 1 else -(-no // 4) * 4))
+    return out
+
+
+def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=0.0, reduce_batch=False,
+          splits=None, tile=None, batched_out=None):
+    """Exact-fp32 C = epi(alpha A @ B + beta C) on csrc/sgemm.hip for fp32 views A [z|1, M, K] / [M, K],
+    B [z|1, K, N] / [K, N]; returns C ([z, M, N], or [M, N] for 2-D operands or reduce_batch) or None when the
+    layouts are not covered (a contiguous extent or leading dim not a multiple of 4 floats, unaligned base)."""
+    if a3.dtype != torch.float32 or b3.dtype != torch.float32 or not a3.is_cuda:
+        return None
+    if batched_out is None:
+        batched_out = a3.dim() == 3 or b3.dim() == 3
+    a3 = a3 if a3.dim() == 3 else a3.unsqueeze(0)
+    b3 = b3 if b3.dim() == 3 else b3.unsqueeze(0)
+    z = max(a3.shape[0], b3.shape[0])
+    M, K, N = a3.shape[1], a3.shape[2], b3.shape[2]
+    if b3.shape[1] != K:
+        raise RuntimeError(f"sgemm: inner dims differ ({K} vs {b3.shape[1]})")
+    if a3.data_ptr() % 16 or b3.data_ptr() % 16 or min(M, N, K) <= 0:
+        return None
+    sA = a3.stride(0) if a3.shape[0] > 1 else 0
+    sB = b3.stride(0) if b3.shape[0] > 1 else 0
+    if sA % 4 or sB % 4:
+        return None
+    la = [(kc, ld) for kc, ld in _sg_layouts(a3, 1, 2) if ld % 4 == 0 and (K if kc else M) % 4 == 0]
+    lb = [(kc, ld) for kc, ld in _sg_layouts(b3, 2, 1) if ld % 4 == 0 and (K if kc else N) % 4 == 0]
+    if not la or not lb:
+        return None
+    (a_kc, lda), (b_kc, ldb) = la[0], lb[0]
+    zc = 1 if reduce_batch else z
+    if out is None:
+        if beta != 0.0:
+            raise RuntimeError("sgemm: beta != 0 needs `out`")
+        out = torch.empty((zc, M, N) if batched_out and not reduce_batch else (M, N), dtype=torch.float32,
+                          device=a3.device)
+    o3 = out if out.dim() == 3 else out.unsqueeze(0)
+    if o3.dtype != torch.float32 or o3.stride(2) != 1:
+        raise RuntimeError("sgemm: output must be row-major fp32")
+    ldc, sC = o3.stride(1), (o3.stride(0) if o3.shape[0] > 1 else 0)
+    bias_mode = 0
+    if bias is not None:
+        bias = bias.detach().float().contiguous()
+        bias_mode = 1 if bias_dim in (None, 1) else 2
+    # batch folding: per-sample planes narrower than a 64-wide tile (the 4 x 4 block's P = 16) as one product
+    lgp = 0
+    if (not reduce_batch and z > 1 and a3.shape[0] == 1 and b3.shape[0] == z and not b_kc and N < 64
+            and N >= 4 and (N & (N - 1)) == 0 and ldb >= N and ldc == N and sC == M * N and splits in (None, 1)):
+        lgp = N.bit_length() - 1
+    zt = 1 if (reduce_batch or lgp) else z
+    Ne = z * N if lgp else N
+    vt = (z if reduce_batch else 1) * -(-K // 32)
+    ptile, psplit = _sg_plan(M, Ne, K, zt, vt)
+    tile = ptile if tile is None else tile
+    splits = (1 if lgp else psplit) if splits is None else splits
+    bm, bn = SG_TILES[tile & 3]
+    ws = None
+    if splits > 1 or reduce_batch:
+        n = _lib.vfm_sgemm_workspace_floats(M, N, z, splits, int(reduce_batch))
+        ws = _workspace(max(n, 1), a3.device)
+    tb = lambda v: "true" if v else "false"
+    region = f"sgemm<{tb(a_kc)},{tb(b_kc)},{bm},{bn}>"
+    if kernel_timer.SHAPES:
+        region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
+    with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, torch.float32, reduce_batch),
+                             2.0 * z * M * N * K, "mfma"):
+        rc = _lib.vfm_sgemm(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), M, Ne, K, z,
+                            int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, sC, float(alpha), float(beta), bias_mode,
+                            ACTS[act], lgp, custom_ops.ptr(ws), int(splits), int(reduce_batch), int(tile),
+                            custom_ops.stream_ptr(a3.device))
+    if rc == custom_ops.VFM_NO_KERNEL:
+        return None
+    custom_ops.check(rc, "vfm_sgemm")
     return out

@@ -73,6 +73,42 @@ class _LinearFn(custom_ops.FastFunction):
         return dx, dw, db
 
 
+class _BmmFn(custom_ops.FastFunction):
+    """C[z] = A[z] @ B[z] (fp32 / bf16 ROCm views) on our GEMMs, both gradients on them too."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        _edges(ctx, a, b)
+        out = _gemm().try_gemm(a, b, auto=True)
+        if out is None:
+            out = torch.bmm(a, b)
+        ctx.save_for_backward(a, b)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dc):
+        a, b = ctx.saved_tensors
+        da = db = None
+        if ctx.needs_input_grad[0] and _wanted(ctx, 0):
+            da = _gemm().try_gemm(dc, b.transpose(1, 2), auto=True)
+            if da is None:
+                da = torch.bmm(dc, b.transpose(1, 2))
+        if ctx.needs_input_grad[1] and _wanted(ctx, 1):
+            db = _gemm().try_gemm(a.transpose(1, 2), dc, auto=True)
+            if db is None:
+                db = torch.bmm(a.transpose(1, 2), dc)
+        return da, db
+
+
+def bmm(a, b):
+    """torch.bmm with its forward and backward products on the HIP GEMMs for ROCm fp32 / bf16 operands (the
+    adapter's VF-loss cosine Gram matrices, reference networks/utils/ldm_utils.py:385-395)."""
+    if a.is_cuda and a.dtype == b.dtype and a.dtype in (torch.float32, torch.bfloat16):
+        return _BmmFn.apply(a, b)
+    return torch.bmm(a, b)
+
+
 def linear(x, weight, bias=None):
     if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16):
         return _LinearFn.apply(x, weight, bias)

@@ -40,11 +40,16 @@ def _gemm(A, B, **kw):
 
 
 def _gemm_or_mm(A, B, bias=None, **kw):
-    """fp32 A @ B (+ bias[:, None]): our f32x6 GEMM under VFM_DHEAD_GEMM=hip (falling back to the library
-    product for a K or N that is not a multiple of 4 fp32 elements: 1-channel logits, ragged token counts),
-    else hipBLASLt's exact-fp32 product (the default), timed as a vendor region."""
-    if _DHEAD_OWN:
-        from . import gemm_hip
+    """fp32 A @ B (+ bias[:, None]) for the D heads' 1-D convs: the exact-fp32 MFMA GEMM (csrc/sgemm.hip, the
+    default: the reference's precision with TF32 off, no operand split), VFM_DHEAD_GEMM=hip our f32x6 GEMM,
+    VFM_DHEAD_GEMM=torch hipBLASLt's exact fp32 (A/B); a layout neither kernel takes falls back to the library
+    product, timed as a vendor region."""
+    from . import gemm_hip
+    if _DHEAD == "sgemm":
+        out = gemm_hip.sgemm(A, B, bias=bias, bias_dim=None if bias is None else 0)
+        if out is not None:
+            return out
+    elif _DHEAD == "hip":
         out = gemm_hip.try_gemm(A, B, out_dtype=torch.float32, bias=bias, bias_dim=None if bias is None else 0, **kw)
         if out is not None:
             return out
@@ -327,12 +332,12 @@ def im2col1d(x, k, p, circular):
 #   forward   y [O, B Lo] = W [O, C k] cols (+ bias), one [B, O, Lo] transpose copy of the small output;
 #   backward  dW = dY [O, B Lo] cols^T  (the batch inside the reduction: no per-sample [O, C k] products
 #             and no batch sum), dcols = W^T dY, dx = the folded col2im; db = row sums of dY.
-# The products: hipBLASLt's exact fp32 by default -- the reference's precision with TF32 off, which matters
-# here: the heads' BatchNormLocal over virtual batches of 8 samples amplifies GEMM rounding into the input
-# gradient. VFM_DHEAD_GEMM=hip puts them on our f32x6 GEMM (three exact bf16 pieces per operand, six piece
-# products; parity-green, tests/test_patchgan_gpu.py), which measured 13.7 ms/step SLOWER in the bench
-# (r5o: 91.0 vs 94.7 img/s with the narrow decoder 1x1s, profiles/r5_o_f32small_ab.txt).
-_DHEAD_OWN = os.environ.get("VFM_DHEAD_GEMM", "torch") == "hip"
+# The products: the exact-fp32 MFMA GEMM (csrc/sgemm.hip) by default -- the reference's precision with TF32
+# off, which matters here: the heads' BatchNormLocal over virtual batches of 8 samples amplifies GEMM rounding into
+# the input gradient. VFM_DHEAD_GEMM=hip puts them on our f32x6 GEMM (three exact bf16 pieces per operand, six piece
+# products; measured 13.7 ms/step slower than hipBLASLt in round 5, r5o), VFM_DHEAD_GEMM=torch on hipBLASLt's exact
+# fp32 (round 5's default).
+_DHEAD = os.environ.get("VFM_DHEAD_GEMM", "sgemm")
 
 
 class _Conv1dFolded(custom_ops.FastFunction):

@@ -77,6 +77,10 @@ def patch_embed(pixels, weight, bias, patch, compute_dtype):
         from . import gemm_hip
         y = gemm_hip.try_gemm(x.reshape(-1, x.shape[-1]), w.t(), auto=True)
         y = None if y is None else y.reshape(B, gh * gw, w.shape[0])
+    if y is None and x.is_cuda and OWN_GEMM and x.dtype in (torch.float32, torch.bfloat16):
+        # input gradient wanted (the D's patch projection in the G phase): forward and data gradient on our GEMMs
+        from .linear import linear as _lin
+        y = _lin(x, w)
     if y is None:
         with _vg(x, w, "vit_patch"):
             y = torch.matmul(x, w.t())
@@ -115,7 +119,7 @@ def linear_gelu_tanh(x, w, b=None):
 
 def layer_norm(h, ln, out_dtype):
     """LayerNorm of the fp32 residual stream, emitted in the GEMM compute dtype."""
-    if _frozen(h):
+    if _frozen(h, ln.weight, ln.bias):            # no autograd graph at all (a trainable norm takes the torch path)
         from . import vit_hip
         if vit_hip.supported(h):
             return vit_hip.residual_layer_norm(h, None, ln, out_dtype)[1]
