@@ -167,3 +167,22 @@ def test_sgemm_routes_narrow_fp32_products():
     out = gemm_hip.try_gemm(xs, wl.t(), auto=True)
     assert out is not None
     _check(out, xs, wl.t())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 3, 9, 36])
+@pytest.mark.parametrize("splits", [1, 2])
+def test_sgemm_ragged_planes(P, splits):
+    """Per-sample planes whose width is not a multiple of 4 floats (the equivariance decodes' 1 x 1 .. 6 x 6 maps:
+    scalar-load staging) forward and transposed, K splits over them (the split combine over N % 4 != 0)."""
+    g = torch.Generator().manual_seed(P + splits)
+    z, M, K = 8, 512, 520
+    W = _rnd(M, K, g=g)
+    x = _rnd(z, K, P, g=g)
+    out = gemm_hip.sgemm(W, x, splits=splits)
+    _check(out, W.expand(z, M, K), x)
+    dy = _rnd(z, M, P, g=g)
+    out = gemm_hip.sgemm(W.t(), dy, splits=splits)
+    _check(out, W.t().expand(z, K, M), dy)
+    out = gemm_hip.sgemm(dy, x.transpose(1, 2), reduce_batch=True, splits=splits)
+    _check(out, dy, x.transpose(1, 2), reduce=True)

@@ -55,6 +55,7 @@ struct SgArgs {
     int tiles_m, tiles_n;
     float alpha, beta;
     int bias_mode, act;        // bias 0 none / 1 per column / 2 per row; act 0 none / 1 gelu tanh / 2 gelu erf
+    int va, vb;                // operand staged with 16-B loads (contiguous extent, leading dims, base: 16-B units)
 };
 
 __device__ __forceinline__ float gelu_tanh_f(float x) {
@@ -101,20 +102,36 @@ struct Stage {
     // base: the operand of this batch item; outer0 / k0: tile origin; bounds outer_n / K.
     // Folded (lgp): outer index o -> item o >> lgp at stride sb, column o & (2^lgp - 1) (MN-contiguous only).
     __device__ __forceinline__ void load(const float* base, long long ld, int outer0, int k0, int outer_n, int K,
-                                         int tid, int lgp, long long sb) {
+                                         int tid, int lgp, long long sb, int vec) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             int row, kk;
             chunk(tid + NTH * u, row, kk);
             const int o = outer0 + row, k = k0 + kk;
-            long long off;
-            if (KCONT) off = (long long)o * ld + k;
-            else if (lgp) off = (long long)(o >> lgp) * sb + (long long)k * ld + (o & ((1 << lgp) - 1));
-            else off = (long long)k * ld + o;
-            // branch-free bounds: an out-of-range chunk loads the operand's first chunk and is zeroed
-            const bool ok = o < outer_n && k < K;
-            const float4 v = *reinterpret_cast<const float4*>(base + (ok ? off : 0LL));
-            r[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (vec) {
+                long long off;
+                if (KCONT) off = (long long)o * ld + k;
+                else if (lgp) off = (long long)(o >> lgp) * sb + (long long)k * ld + (o & ((1 << lgp) - 1));
+                else off = (long long)k * ld + o;
+                // branch-free bounds: an out-of-range chunk loads the operand's first chunk and is zeroed
+                const bool ok = o < outer_n && k < K;
+                const float4 v = *reinterpret_cast<const float4*>(base + (ok ? off : 0LL));
+                r[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                // contiguous extent / leading dim not in 16-B units (the equivariance decodes' 3 x 3 planes):
+                // four bounds-checked scalar loads
+                float e[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int oi = KCONT ? o : o + i, ki = KCONT ? k + i : k;
+                    long long off;
+                    if (KCONT) off = (long long)oi * ld + ki;
+                    else if (lgp) off = (long long)(oi >> lgp) * sb + (long long)ki * ld + (oi & ((1 << lgp) - 1));
+                    else off = (long long)ki * ld + oi;
+                    e[i] = (oi < outer_n && ki < K) ? base[off] : 0.f;
+                }
+                r[u] = make_float4(e[0], e[1], e[2], e[3]);
+            }
         }
     }
 
@@ -189,8 +206,8 @@ __global__ __launch_bounds__(NT * KW, 2 / KW) void sgemm_kernel(SgArgs a) {
     auto load = [&](int t, SA& ra, SB& rb) {
         int z, k0;
         vtile(a, zfix, t, z, k0);
-        ra.load(a.A + z * a.sA, a.lda, m0, k0, a.M, a.K, tid, 0, 0);
-        rb.load(a.B + z * sBb, a.ldb, n0, k0, a.N, a.K, tid, a.lgp, a.sB);
+        ra.load(a.A + z * a.sA, a.lda, m0, k0, a.M, a.K, tid, 0, 0, a.va);
+        rb.load(a.B + z * sBb, a.ldb, n0, k0, a.N, a.K, tid, a.lgp, a.sB, a.vb);
     };
     const int ao = (BM / WM) * wm, bo = (BN / WN) * wn, qb = kg * QG;
     // the MFMAs of one K-tile from an LDS stage, fragments one quad of k-steps ahead (the b128 reads of quad
@@ -316,29 +333,23 @@ __global__ void sgemm_reduce(SgArgs a, int J) {
     const int zc = blockIdx.y;
     if (q >= MN) return;
     const float* w = a.ws + (long long)zc * J * MN + q;
-    const int m = (int)(q / a.N), n = (int)(q - (long long)m * a.N);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    const bool vec = (a.N & 3) == 0;
-    const int cnt = vec ? 4 : 1;
-    if (vec) {
+    const int cnt = (int)min(4LL, MN - q);
+    if ((a.N & 3) == 0) {                      // rows of whole float4s (q is a multiple of 4)
         for (int j = 0; j < J; ++j) {
             const float4 v = *reinterpret_cast<const float4*>(w + (long long)j * MN);
             s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
         }
+    } else {
+        for (int j = 0; j < J; ++j)
+            for (int c = 0; c < cnt; ++c) s[c] += w[(long long)j * MN + c];
     }
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < cnt; ++c) {
         const long long qi = q + c;
-        if (qi >= MN) break;
         const int mi = (int)(qi / a.N), ni = (int)(qi - (long long)mi * a.N);
-        float v = s[c];
-        if (c >= cnt) {
-            v = 0.f;
-            for (int j = 0; j < J; ++j) v += w[(long long)j * MN + c];
-        }
         float* cp = a.C + (long long)zc * a.sC + (long long)mi * a.ldc + ni;
-        *cp = epilogue(a, v, mi, ni, a.beta != 0.f ? *cp : 0.f);
+        *cp = epilogue(a, s[c], mi, ni, a.beta != 0.f ? *cp : 0.f);
     }
-    (void)m; (void)n;
 }
 
 template <bool AK, bool BKC, int BM, int BN, int KW>
@@ -391,10 +402,11 @@ extern "C" int vfm_sgemm(const float* A, const float* B, float* C, const float* 
     if (splits < 1) splits = 1;
     if (lgp && (b_kcont || reduce_batch || lgp < 2 || lgp > 20)) return VFM_ERR_ARGS;
     const int P = lgp ? (1 << lgp) : N;
-    // 16-B chunks along every contiguous dimension, 16-B aligned bases
+    // 16-B loads where every contiguous extent, leading dim and batch stride is in 16-B units and the base is
+    // 16-B aligned; otherwise bounds-checked scalar loads
     const int a_c = a_kcont ? K : M, b_c = b_kcont ? K : P;
-    if (a_c % 4 || b_c % 4 || lda % 4 || ldb % 4 || sA % 4 || sB % 4) return VFM_NO_KERNEL;
-    if (((uintptr_t)A | (uintptr_t)B) % 16) return VFM_NO_KERNEL;
+    const int va = !(a_c % 4 || lda % 4 || sA % 4 || ((uintptr_t)A % 16));
+    const int vb = !(b_c % 4 || ldb % 4 || sB % 4 || ((uintptr_t)B % 16));
     if (lda < a_c || ldb < b_c || ldc < P) return VFM_ERR_ARGS;
     const long long Nf = lgp ? (long long)batch * P : N;
     if (lgp && (Nf != N)) return VFM_ERR_ARGS;
@@ -412,6 +424,7 @@ extern "C" int vfm_sgemm(const float* A, const float* B, float* C, const float* 
     a.splits = (vt + a.tpc - 1) / a.tpc;           // no empty chunk
     a.alpha = alpha; a.beta = beta; a.bias_mode = bias_mode; a.act = act;
     a.ws = use_ws ? workspace : nullptr;
+    a.va = va; a.vb = vb;
     const int zgrid = (reduce_batch || lgp) ? 1 : batch;
     if ((long long)zgrid * a.splits > 65535) return VFM_ERR_ARGS;
     if (tile < 0 || tile > 7) tile = pick_tile(M, N, zgrid * a.splits);

@@ -280,8 +280,21 @@ def try_gemm(A, B, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta
     """C = epi(alpha * A @ B + beta * out). A: [M, K] or [z, M, K]; B: [K, N] or [z, K, N]
     (any strides with one unit-stride dim each). bias: fp32 [N] (bias_dim=1) or [M]
     (bias_dim=0). Returns C ([M, N] / [z, M, N], or [M, N] when reduce_batch sums over z),
-    or None when the kernel does not cover the shapes/strides. `route` forces a plan
-    (("g8", kchunk) / ("g128", splits): microbenchmarks)."""
+    or None when no kernel covers the shapes/strides. `route` forces a plan
+    (("g8", kchunk) / ("g128", splits): microbenchmarks). An fp32 product the bf16-piece kernels do not
+    take (contiguous extents that are not 16-B multiples: the equivariance decodes' 1 x 1 / 3 x 3 planes)
+    runs on the exact-fp32 kernel (`sgemm`) instead of returning None."""
+    res = _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, reduce_batch, cache_a, cache_b,
+                    auto, route)
+    if (res is None and SGEMM and route is None and A.dtype == torch.float32 and B.dtype == torch.float32
+            and A.is_cuda and (out_dtype or A.dtype) == torch.float32):
+        res = sgemm(A, B, out=out, bias=bias, bias_dim=bias_dim, act=act, alpha=alpha, beta=beta,
+                    reduce_batch=reduce_batch)
+    return res
+
+
+def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, reduce_batch, cache_a, cache_b, auto,
+              route):
     if A.dtype != B.dtype or A.dtype not in _CODES or not A.is_cuda:
         return None
     a3 = A if A.dim() == 3 else A.unsqueeze(0)
@@ -600,14 +613,15 @@ def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=
     M, K, N = a3.shape[1], a3.shape[2], b3.shape[2]
     if b3.shape[1] != K:
         raise RuntimeError(f"sgemm: inner dims differ ({K} vs {b3.shape[1]})")
-    if a3.data_ptr() % 16 or b3.data_ptr() % 16 or min(M, N, K) <= 0:
+    if min(M, N, K) <= 0:
         return None
     sA = a3.stride(0) if a3.shape[0] > 1 else 0
     sB = b3.stride(0) if b3.shape[0] > 1 else 0
-    if sA % 4 or sB % 4:
-        return None
-    la = [(kc, ld) for kc, ld in _sg_layouts(a3, 1, 2) if ld % 4 == 0 and (K if kc else M) % 4 == 0]
-    lb = [(kc, ld) for kc, ld in _sg_layouts(b3, 2, 1) if ld % 4 == 0 and (K if kc else N) % 4 == 0]
+    # a layout whose contiguous extent and leading dim are in 16-B units first (the kernel's 16-B loads), else
+    # any (bounds-checked scalar loads: the equivariance decodes' 3 x 3 / 6 x 6 planes)
+    vec = lambda kc, ld, n_out: ld % 4 == 0 and (K if kc else n_out) % 4 == 0
+    la = sorted(_sg_layouts(a3, 1, 2), key=lambda c: not vec(c[0], c[1], M))
+    lb = sorted(_sg_layouts(b3, 2, 1), key=lambda c: not vec(c[0], c[1], N))
     if not la or not lb:
         return None
     (a_kc, lda), (b_kc, ldb) = la[0], lb[0]
@@ -654,4 +668,33 @@ def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=
     if rc == custom_ops.VFM_NO_KERNEL:
         return None
     custom_ops.check(rc, "vfm_sgemm")
+    if _SG_CHECK:
+        _check_sg(a3, b3, out, bias, bias_dim, act, alpha, beta, reduce_batch,
+                  dict(tile=tile, splits=splits, lgp=lgp, a_kc=a_kc, lda=lda, sA=sA, b_kc=b_kc, ldb=ldb, sB=sB, ldc=ldc,
+                       sC=sC))
     return out
+
+
+_SG_CHECK = __import__("os").environ.get("VFM_SGEMM_CHECK") == "1"
+
+
+def _check_sg(a3, b3, out, bias, bias_dim, act, alpha, beta, reduce_batch, info):
+    """Debug (VFM_SGEMM_CHECK=1, beta == 0 products): an sgemm product against fp64 torch; prints the ones off by
+    more than 1e-5 of |A||B|."""
+    if beta != 0.0 or act is not None:
+        return
+    A64, B64 = a3.double(), b3.double()
+    ref, bnd = alpha * torch.matmul(A64, B64), abs(alpha) * torch.matmul(A64.abs(), B64.abs())
+    if reduce_batch:
+        ref, bnd = ref.sum(0), bnd.sum(0)
+    if bias is not None:
+        bb = bias.double()[:, None] if bias_dim == 0 else bias.double()
+        ref, bnd = ref + bb, bnd + bb.abs()
+    o = out.double().reshape(ref.shape) if out.numel() == ref.numel() else None
+    if o is None:
+        print(f"[sgemm check] shape mismatch out {tuple(out.shape)} ref {tuple(ref.shape)} {info}", flush=True)
+        return
+    e = float(((o - ref).abs() / (bnd + 1e-30)).max())
+    if e > 1e-5:
+        print(f"[sgemm check] err {e:.2e} A{tuple(a3.shape)}{a3.stride()} B{tuple(b3.shape)}{b3.stride()} "
+              f"out{tuple(out.shape)}{out.stride()} bias_dim={bias_dim} red={reduce_batch} {info}", flush=True)
