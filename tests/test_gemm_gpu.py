@@ -158,10 +158,15 @@ def test_gemm_f32x3_opt_in(monkeypatch):
         assert _rel(out, exact) < F32X3_TOL
 
 
-def test_gemm_unsupported_shape_returns_none():
+def test_gemm_unsupported_shape_routes_exact_fp32(monkeypatch):
+    """K = 7 (not a multiple of 4 fp32 elements): none of the bf16-piece kernels takes it; try_gemm hands it to the
+    exact-fp32 kernel (csrc/sgemm.hip, scalar-load staging), and returns None only with that route off."""
     from torch_utils.ops import gemm_hip
-    A = torch.randn(10, 7, device=DEV)         # K = 7: not a multiple of 4 fp32 elements
+    A = torch.randn(10, 7, device=DEV)
     B = torch.randn(7, 12, device=DEV)
+    out = gemm_hip.try_gemm(A, B)
+    assert out is not None and _rel(out, A.double() @ B.double()) < 1e-6
+    monkeypatch.setattr(gemm_hip, "SGEMM", False)
     assert gemm_hip.try_gemm(A, B) is None
 
 

@@ -71,3 +71,24 @@ def test_vit_ops_layer_norm_routes_grad_inputs(monkeypatch):
     vit_ops.layer_norm(h, ln, torch.float32)
     assert not any(k.startswith("layer_norm_fwd") for k in kt.summary())
     kt.enable(False)
+
+
+def test_vit_ops_layer_norm_frozen_input_trainable_affine(monkeypatch):
+    """An input that needs no gradient through a TRAINABLE LayerNorm (grad enabled) keeps torch's LayerNorm, so the
+    weight and bias gradients exist (the native ops' affine parameters are frozen)."""
+    from torch_utils.ops import kernel_timer as kt, vit_hip, vit_ops
+    monkeypatch.setattr(vit_hip, "LN_GRAD", True)
+    torch.manual_seed(1)
+    ln = torch.nn.LayerNorm(384, eps=1e-6).to(DEV)
+    h = torch.randn(2, 197, 384, device=DEV)
+    kt.enable(True)
+    y = vit_ops.layer_norm(h, ln, torch.float32)
+    y.square().sum().backward()
+    torch.cuda.synchronize()
+    names = set(kt.summary())
+    kt.enable(False)
+    assert not any(k.startswith("layer_norm_fwd") or k.startswith("residual_layer_norm") for k in names), names
+    assert ln.weight.grad is not None and ln.bias.grad is not None
+    w = ln.weight.detach().double().requires_grad_(True)
+    torch.nn.functional.layer_norm(h.double(), (384,), w, ln.bias.double(), 1e-6).square().sum().backward()
+    assert _rel(ln.weight.grad, w.grad) < 1e-4

@@ -80,7 +80,7 @@ class CLIPAttention(nn.Module):
 
     def forward(self, x):
         return mha(x, self.q_proj.weight, self.q_proj.bias, self.k_proj.weight, self.k_proj.bias,
-                   self.v_proj.weight, self.v_proj.bias, self.out_proj.weight, self.out_proj.bias, self.heads)
+                   self.v_proj.weight, self.v_proj.bias, self.out_proj.weight, self.out_proj.bias, self.heads, owner=self)
 
 
 class CLIPMLP(nn.Module):

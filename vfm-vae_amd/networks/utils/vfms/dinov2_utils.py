@@ -98,7 +98,7 @@ class Dinov2Attention(nn.Module):
     def forward(self, x):
         a, o = self.attention, self.output.dense
         return mha(x, a.query.weight, a.query.bias, a.key.weight, a.key.bias, a.value.weight, a.value.bias,
-                   o.weight, o.bias, self.heads)
+                   o.weight, o.bias, self.heads, owner=self)
 
 
 class Dinov2LayerScale(nn.Module):
@@ -114,7 +114,8 @@ class Dinov2MLP(nn.Module):
         self.fc2 = Linear(cfg["intermediate_size"], cfg["hidden_size"])
 
     def forward(self, x):
-        return self.fc2(F.gelu(self.fc1(x)))
+        # fc1 + erf-GELU in one GEMM epilogue on ROCm (vit_ops.linear_gelu), fc2
+        return self.fc2(vit_ops.linear_gelu(x, vit_ops.frozen_weight(self.fc1.weight, x.dtype), self.fc1.bias))
 
 
 class Dinov2Layer(nn.Module):

@@ -56,12 +56,27 @@ def resample_positions(pos, gh, gw):
     return torch.cat([cls, grid], 0)[None]
 
 
-def mha(x, wq, bq, wk, bk, wv, bv, wo, bo, heads):
-    """Self-attention of the compute-dtype tokens x [B, N, D] -> [B, N, D] (compute dtype):
-    fused qkv GEMM, SDPA, output projection."""
-    B, N, D = x.shape
-    w = torch.cat([wq, wk, wv], 0).to(x.dtype)
+def fused_qkv(owner, wq, bq, wk, bk, wv, bv, dtype):
+    """The concatenated [3D, D] qkv weight in the compute dtype and the [3D] bias, cached on `owner` (the frozen
+    tower's attention module) until a tensor's storage or version moves: built once, not at every forward."""
+    ts = (wq, wk, wv, bq, bk, bv)
+    key = (dtype,) + tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)
+    capturing = wq.is_cuda and torch.cuda.is_current_stream_capturing()
+    hit = getattr(owner, "_vfm_qkv", None) if owner is not None else None
+    if hit is not None and hit[0] == key and not capturing:
+        return hit[1]
+    w = torch.cat([wq, wk, wv], 0).to(dtype)
     b = torch.cat([bq, bk, bv], 0) if bq is not None else None
+    if owner is not None and not torch.is_grad_enabled() and not capturing:
+        owner._vfm_qkv = (key, (w, b))
+    return w, b
+
+
+def mha(x, wq, bq, wk, bk, wv, bv, wo, bo, heads, owner=None):
+    """Self-attention of the compute-dtype tokens x [B, N, D] -> [B, N, D] (compute dtype):
+    fused qkv GEMM (weights concatenated once per version, `fused_qkv`), SDPA, output projection."""
+    B, N, D = x.shape
+    w, b = fused_qkv(owner, wq, bq, wk, bk, wv, bv, x.dtype)
     qkv = vit_ops.linear(x, w, b)
     o = vit_ops.attention_packed(qkv, heads)
     return vit_ops.linear(o, vit_ops.frozen_weight(wo, x.dtype), bo)

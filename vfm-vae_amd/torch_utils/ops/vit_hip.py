@@ -53,11 +53,11 @@ def residual_layer_norm(h, delta, ln, out_dtype, write_h=True):
 
 
 _DN = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16"}
-# Routing switch (vit_utils.Block / vit_ops.layer_norm): off by default. The kernels replace torch's
-# LayerNorm kernels in the DINO discriminator (2.1 -> 0.8 ms/step of kernel time) but the bench measured
-# 94.5 / 93.6 img/s with them against 95.6 without (profiles/r5_bp_ln_grad_ab.txt): the autograd.Function
-# costs more host time per call than torch's native LayerNorm, and the DINO passes are host-bound.
-LN_GRAD = os.environ.get("VFM_LN_GRAD", "0") == "1"
+# Routing switch (vit_utils.Block / vit_ops.layer_norm): on by default since round 6. The kernels replace
+# torch's LayerNorm kernels in the DINO discriminator (2.1 -> 0.8 ms/step of kernel time); round 5 measured
+# them 1-2 % slower in the bench (profiles/r5_bp_ln_grad_ab.txt: per-call host work), since then the frozen
+# affine parameters are cached on the module (`_frozen_affine`). VFM_LN_GRAD=0: torch's LayerNorm (A/B).
+LN_GRAD = os.environ.get("VFM_LN_GRAD", "1") == "1"
 
 
 def layer_norm_grad_supported(h, ln):
@@ -102,10 +102,23 @@ class _LayerNorm(custom_ops.FastFunction):
         return dx, None, None, None, None
 
 
+def _frozen_affine(ln):
+    """fp32, contiguous, 8-B aligned (w, b) of a frozen LayerNorm, cached on the module until a parameter's
+    version or storage moves (the per-call detach / cast / alignment checks were most of this op's host time)."""
+    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in (ln.weight, ln.bias))
+    hit = getattr(ln, "_vfm_affine", None)
+    if hit is not None and hit[0] == key and not torch.cuda.is_current_stream_capturing():
+        return hit[1]
+    out = []
+    for t in (ln.weight, ln.bias):
+        t = t.detach().float().contiguous() if t is not None else None
+        out.append(t.clone() if t is not None and t.data_ptr() % 8 else t)
+    if not torch.cuda.is_current_stream_capturing():
+        ln._vfm_affine = (key, tuple(out))
+    return tuple(out)
+
+
 def layer_norm_grad(h, ln, out_dtype):
     """LayerNorm of an fp32 stream that needs a gradient, through frozen parameters (DINOv2 discriminator)."""
-    w = ln.weight.detach().float().contiguous() if ln.weight is not None else None
-    b = ln.bias.detach().float().contiguous() if ln.bias is not None else None
-    w = w.clone() if w is not None and w.data_ptr() % 8 else w
-    b = b.clone() if b is not None and b.data_ptr() % 8 else b
+    w, b = _frozen_affine(ln)
     return _LayerNorm.apply(h, w, b, float(ln.eps), out_dtype)

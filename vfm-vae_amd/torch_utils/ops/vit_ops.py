@@ -105,6 +105,16 @@ def linear(x, w, b=None):
         return torch.matmul(x, w.t())
 
 
+def linear_gelu(x, w, b=None):
+    """gelu(x @ w^T + b), erf form (DINOv2 / HF "gelu"): the bf16 GEMM with the erf-GELU epilogue on ROCm frozen
+    towers (one rounding of GELU(acc + b) instead of a bf16 product, a bf16 GELU pass and its HBM round trip)."""
+    if b is not None and x.dtype != torch.float32 and _frozen(x, w, b):
+        y = _own_linear(x, w, b, act="gelu")
+        if y is not None:
+            return y
+    return F.gelu(linear(x, w, b))
+
+
 def linear_gelu_tanh(x, w, b=None):
     """gelu_tanh(x @ w^T + b): GEMM with the GELU_BIAS epilogue on ROCm (frozen towers)."""
     if b is not None and x.dtype != torch.float32 and _frozen(x, w, b):
