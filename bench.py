@@ -52,14 +52,20 @@ def parse_args(argv=None):
     ap.add_argument("--no-gc-freeze", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="A/B: no per-launch HIP events in the timed region (no roofline object)")
-    ap.add_argument("--timer-steps", type=int, default=4,
-                    help="kernel timing in every n-th timed step only (1 = all timed steps). Default 4: steps "
-                         "0, 4, 8, 12, 16 of the fixed-seed sequence; timing 1/4 of the launches of every step "
-                         "cost 2.2 %% of the step rate (r5p: 93.4 vs 95.5 img/s with the timer off)")
-    ap.add_argument("--timer-every", type=int, default=4,
-                    help="per-launch HIP events on a pseudo-random 1/n of each kernel region's launches. Not every "
-                         "launch of whole steps: back-to-back event-bound launches run serialised, which timed the "
-                         "LPIPS conv 27 %% below its rocprof duration (profiles/r4_am_bench.json)")
+    ap.add_argument("--timer-steps", type=int, default=1,
+                    help="kernel timing in every n-th timed step only (1 = all timed steps, the default). The timed "
+                         "steps draw different equivariance outcomes (decode scales), so a region's launches differ in "
+                         "shape from step to step: timing only steps 0, 4, 8, 12, 16 (round 5's default) averaged those "
+                         "steps' draws and read the decoder kernels 20-30 %% below their rocprof average over all 20 "
+                         "steps (gpurun_out r6o, profiles/r6_timer_vs_rocprof_*.txt)")
+    ap.add_argument("--timer-every", type=int, default=20,
+                    help="per-launch HIP events on 1/n of each kernel region's launches, stratified by launch "
+                         "position within a step: position j of the k-th timed step is timed when (j + k) %% n == 0, "
+                         "so with n = 20 over the 20 timed steps every position of a step's launch sequence is timed "
+                         "exactly once, in a different step for each position (every step's draw enters). The same "
+                         "number of timed launches as 1/4 of every 4th step. Not every launch of whole steps: "
+                         "back-to-back event-bound launches run serialised, which timed the LPIPS conv 27 %% below its "
+                         "rocprof duration (profiles/r4_am_bench.json)")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", nargs="?", const="on", default="off", choices=["auto", "on", "off"],
                     help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5). Default off: "
@@ -269,11 +275,12 @@ def main(argv=None):
     venc = step.G.vfm_encoder
     every = max(1, args.timer_every)
     kernel_timer.enable(on_gpu and not args.no_kernel_timer, every)
+    calib_us = kernel_timer.calibrate() * 1e3 if (on_gpu and not args.no_kernel_timer) else None
     t0 = time.perf_counter()
     tsteps = max(1, args.timer_steps)
     for i in range(args.steps):
         h0 = getattr(venc, "reuse_hits", 0)
-        kernel_timer.set_active(i % tsteps == 0)
+        kernel_timer.new_step(i % tsteps == 0)
         one(args.warmup + i, cur)
         hits.append(getattr(venc, "reuse_hits", 0) - h0)
         cur += args.batch * world
@@ -310,7 +317,9 @@ def main(argv=None):
         n_t = len(range(0, args.steps, tsteps))
         where = (f"all {args.steps} timed steps" if tsteps == 1 else
                  f"{n_t} of the {args.steps} timed steps (every {tsteps}th)")
-        roof["timer_sampling"] = ((f"1/{every} of each kernel region's launches (pseudo-random by launch index) in "
+        roof["timer_calibration_us"] = round(calib_us, 2) if calib_us is not None else None
+        roof["timer_sampling"] = ((f"1/{every} of each kernel region's launches, stratified by launch position within "
+                                   f"a step (position j of the k-th timed step when (j + k) % {every} == 0) in "
                                    if every > 1 else "every launch in ") + where + ", all launches counted")
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value) if args.config == CONFIG else None
     cpu = None

@@ -59,6 +59,15 @@ const char* vfm_version(void);
  * previous arming (0: the events were not recorded). Events come from vfm_event_create.
  */
 int vfm_timer_arm(void* start, void* stop);
+/* Start-event binding of the armed timer: 1 (default) = the end of an empty probe kernel launched right before
+ * each timed kernel (the interval excludes the previous kernel's tail the timed one waits behind); 0 = the
+ * timed kernel's own dispatch (hipExtLaunchKernelGGL start event). Returns the previous mode. */
+int vfm_timer_mode(int mode);
+/* One empty kernel launch through the library's launch path (timed when armed): calibration of the fixed
+ * interval every timed launch carries (dispatch gap + an empty one-wave kernel). */
+int vfm_timer_null_launch(void* stream);
+/* vfm_timer_arm timing only the FIRST launch of the call (a GEMM's main kernel, not its split-K combine pass). */
+int vfm_timer_arm_first(void* start, void* stop);
 int vfm_event_create(void** ev);
 int vfm_event_destroy(void* ev);
 int vfm_event_elapsed(void* start, void* stop, float* ms);

@@ -8,7 +8,17 @@ TimerArm& timer_arm() {
     static thread_local TimerArm t;
     return t;
 }
+int g_timer_mode = 1;
+__global__ void timer_probe_kernel(int) {}
 }  // namespace vfm
+
+// Start-event binding of the kernel timer (see TimerArm): 1 = end of a probe kernel before the timed launch
+// (default), 0 = the timed kernel's own dispatch. Returns the previous mode.
+extern "C" int vfm_timer_mode(int mode) {
+    const int prev = vfm::g_timer_mode;
+    if (mode == 0 || mode == 1) vfm::g_timer_mode = mode;
+    return prev;
+}
 
 // Arm (start, stop) for the following launches of this thread (both null: disarm). See TimerArm.
 // Returns the number of launches made under the previous arming.
@@ -18,7 +28,22 @@ extern "C" int vfm_timer_arm(void* start, void* stop) {
     t.start = (hipEvent_t)start;
     t.stop = (hipEvent_t)stop;
     t.launches = 0;
+    t.first_only = false;
     return n;
+}
+
+// vfm_timer_arm for the first launch only: later launches of the call go untimed (see TimerArm).
+extern "C" int vfm_timer_arm_first(void* start, void* stop) {
+    const int n = vfm_timer_arm(start, stop);
+    vfm::timer_arm().first_only = start != nullptr;
+    return n;
+}
+
+// One empty one-wave kernel through VFM_LAUNCH (timed like any other launch when the timer is armed): the
+// kernel timer's calibration of the fixed per-timed-launch interval (dispatch gap + an empty kernel).
+extern "C" int vfm_timer_null_launch(void* stream) {
+    VFM_LAUNCH(vfm::timer_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, 0);
+    return vfm::launch_status();
 }
 
 extern "C" int vfm_event_create(void** ev) {

@@ -135,8 +135,18 @@ __device__ __forceinline__ GeluParts gelu_parts(float z) {
 struct TimerArm {
     hipEvent_t start = nullptr, stop = nullptr;
     int launches = 0;
+    bool first_only = false;   // vfm_timer_arm_first: only the region's first launch is timed (a GEMM's main
+                               // kernel without its split-K combine pass, which is a kernel of its own)
 };
 TimerArm& timer_arm();
+// Probe mode (vfm_timer_mode(1), the default): the start event is bound to the END of an empty one-wave probe
+// kernel launched right before the timed kernel, not to the timed kernel's own start: a dispatch-bound start
+// event reads from the moment the command processor takes the packet, i.e. it includes the tail of the
+// previous kernel the timed one waits behind (+10-50 % on the decoder's short kernels against rocprofv3's
+// kernel trace, gpurun_out r6p). The probe ends when the previous kernel has drained, so the interval is the
+// timed kernel's own execution plus one dispatch gap.
+extern int g_timer_mode;
+__global__ void timer_probe_kernel(int);
 
 // Per-device launch state (a process may drive several GPUs): the current device's index, its CU count, and
 // (at the call sites) one "dynamic LDS attribute set" flag per device for each kernel instantiation.
@@ -178,9 +188,15 @@ inline int launch_status() {
     do {                                                                                                    \
         ::vfm::TimerArm& vfm_ta_ = ::vfm::timer_arm();                                                      \
         if (vfm_ta_.stop) {                                                                                 \
+            if (vfm_ta_.start && ::vfm::g_timer_mode == 1) {                                                \
+                hipExtLaunchKernelGGL(::vfm::timer_probe_kernel, dim3(1), dim3(64), 0, stream, nullptr,     \
+                                      vfm_ta_.start, 0, 0);                                                 \
+                vfm_ta_.start = nullptr;                                                                    \
+            }                                                                                               \
             hipExtLaunchKernelGGL(kern, grid, block, shm, stream, vfm_ta_.start, vfm_ta_.stop, 0, __VA_ARGS__); \
             vfm_ta_.start = nullptr;                                                                        \
             ++vfm_ta_.launches;                                                                             \
+            if (vfm_ta_.first_only) vfm_ta_.stop = nullptr;                                                 \
         } else {                                                                                            \
             hipLaunchKernelGGL(kern, grid, block, shm, stream, __VA_ARGS__);                               \
         }                                                                                                   \

@@ -371,10 +371,10 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
         n = _lib.vfm_gemm9_workspace_floats(M, N, K, z, S, int(reduce_batch))
         if n > 0 and (reduce_batch or z == 1) and beta == 0.0 and bias is None and act is None:
             ws = _workspace(n, A.device)
-            region = f"gemm9<bf16,{tb(a_kc)},{tb(b_kc)},true>r"
+            region = f"gemm9<bf16,{tb(a_kc)},{tb(b_kc)},true>"
             if kernel_timer.SHAPES:
                 region += f"[{M}x{N}x{K}x{z}s{S}]"
-            with kernel_timer.region(region, nbytes, flops, "mfma"):
+            with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
                 rc = _lib.vfm_gemm9_ex(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), _CODES[out_dtype], M, N, K, z,
                                        int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, float(alpha), ws.data_ptr(), S,
                                        int(reduce_batch), stream)
@@ -387,7 +387,7 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
         region = f"gemm9<bf16,{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
         if kernel_timer.SHAPES:
             region += f"[{M}x{N}x{K}x{z}]"
-        with kernel_timer.region(region, nbytes, flops, "mfma"):
+        with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
             rc = _lib.vfm_gemm9(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype],
                                 M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, sC, float(alpha), float(beta),
                                 bias_mode, ACTS[act], stream)
@@ -400,7 +400,7 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
         region = f"gemm4<bf16,{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
         if kernel_timer.SHAPES:
             region += f"[{M}x{N}x{K}x{z}]"
-        with kernel_timer.region(region, nbytes, flops, "mfma"):
+        with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
             rc = _lib.vfm_gemm4(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype],
                                 M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, sC, float(alpha), float(beta),
                                 bias_mode, ACTS[act], stream)
@@ -442,10 +442,10 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
             if S9 > 1 or reduce_batch:
                 n9 = _lib.vfm_gemm9_workspace_floats(M, N, K, z, S9, int(reduce_batch))
                 ws9 = _workspace(max(n9, 1), A.device)
-            region = f"gemm9<f32x6,{tb(fa_kc)},{tb(fb_kc)},true>{'r' if ws9 is not None else ''}"
+            region = f"gemm9<f32x6,{tb(fa_kc)},{tb(fb_kc)},true>"
             if kernel_timer.SHAPES:
                 region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % S9 if S9 > 1 else ''}]"
-            with kernel_timer.region(region, nbytes, flops, "mfma"):
+            with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
                 rc = _lib.vfm_gemm9_pieces(Ak.data_ptr() + 2 * a_off, Bk.data_ptr() + 2 * b_off, out.data_ptr(),
                                            custom_ops.ptr(bias), M, N, K, z, int(fa_kc), flda, fsA, psA, int(fb_kc),
                                            fldb, fsB, psB, ldc, sC, float(alpha), bias_mode, custom_ops.ptr(ws9),
@@ -467,7 +467,7 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
             region = f"gemm8<{tag},{tb(fa_kc)},{tb(fb_kc)},{tb(out_dtype == torch.float32)}>"
             if kernel_timer.SHAPES:
                 region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'k%d' % kchunk if kchunk else ''}]"
-            with kernel_timer.region(region, nbytes, flops, "mfma"):
+            with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
                 rc = _lib.vfm_gemm8_pieces(Ak.data_ptr() + 2 * a_off, Bk.data_ptr() + 2 * b_off, out.data_ptr(),
                                            custom_ops.ptr(bias), prec, _CODES[out_dtype], M, N, K, z, int(fa_kc), flda,
                                            fsA, psA, int(fb_kc), fldb, fsB, psB, ldc, sC, float(alpha), float(beta),
@@ -488,11 +488,10 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
         in_code, _, tag = custom_ops.f32_precision()
     # one region per gemm_kernel<AK, BK, NP, OUTF32> instantiation; split-K / batch-reduced
     # launches (kernel + gemm_reduce_kernel) are their own region
-    kname = "gemm_ws" if ws is not None else "gemm"
-    region = f"{kname}<{tag},{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
+    region = f"gemm<{tag},{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
     if kernel_timer.SHAPES:
         region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
-    with kernel_timer.region(region, nbytes, flops, "mfma"):
+    with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
         rc = _lib.vfm_gemm(A.data_ptr(), B.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), custom_ops.ptr(ws),
                            in_code, _CODES[out_dtype], M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB,
                            ldc, sC, float(alpha), float(beta), bias_mode, ACTS[act], int(splits), int(reduce_batch),
@@ -534,7 +533,7 @@ def _try_fold(a3, b3, M, N, K, z, out, bias, bias_dim, act, alpha, beta, out_dty
     region = f"gemm_fold<{tag},{tb(a_kc)},{tb(out_dtype == torch.float32)}>"
     if kernel_timer.SHAPES:
         region += f"[{M}x{N}x{K}x{z}]"
-    with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype), 2.0 * z * M * N * K, "mfma"):
+    with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, out_dtype), 2.0 * z * M * N * K, "mfma", first_only=True):
         rc = _lib.vfm_gemm_fold(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), prec,
                                 _CODES[out_dtype], M, lgp, K, z, int(a_kc), lda, b3.stride(1), b3.stride(0),
                                 out.stride(1), out.stride(0), float(alpha), float(beta), bias_mode, ACTS[act],
@@ -656,11 +655,11 @@ def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=
         n = _lib.vfm_sgemm_workspace_floats(M, N, z, splits, int(reduce_batch))
         ws = _workspace(max(n, 1), a3.device)
     tb = lambda v: "true" if v else "false"
-    region = f"sgemm<{tb(a_kc)},{tb(b_kc)},{bm},{bn}>"
+    region = f"sgemm<{tb(a_kc)},{tb(b_kc)},{bm},{bn},{1 + (tile >> 2)}>"
     if kernel_timer.SHAPES:
         region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
     with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, torch.float32, reduce_batch),
-                             2.0 * z * M * N * K, "mfma"):
+                             2.0 * z * M * N * K, "mfma", first_only=True):
         rc = _lib.vfm_sgemm(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), M, Ne, K, z,
                             int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, sC, float(alpha), float(beta), bias_mode,
                             ACTS[act], lgp, custom_ops.ptr(ws), int(splits), int(reduce_batch), int(tile),

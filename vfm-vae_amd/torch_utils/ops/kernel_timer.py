@@ -34,17 +34,52 @@ _every = 1         # time ~1/n of each region's launches (the events cost host t
 
 
 _active = True     # launches are timed only while active (bench.py: every launch of every n-th timed step)
+_pos = {}          # name -> launch position within the current step (new_step resets it)
+_phase = -1        # index of the current active step (new_step), -1: stepless (launch-index sampling)
 
 
 def enable(flag: bool, every: int = 1):
-    global _enabled, _every, _active
+    """Timing on / off. The start event is bound to the timed kernel's own dispatch; VFM_TIMER_PROBE=1 binds it
+    to the end of an empty probe kernel launched before it instead (vfm_timer_mode, include/vfmvae.h): both read
+    the same averages once the fixed per-launch interval is calibrated out (gpurun_out r6q / r6q0), and the
+    probe is one more launch per timed launch."""
+    if flag:
+        _native().vfm_timer_mode(1 if os.environ.get("VFM_TIMER_PROBE", "0") == "1" else 0)
+    _enable(flag, every)
+
+
+def _enable(flag: bool, every: int = 1):
+    global _enabled, _every, _active, _phase
     _enabled = bool(flag)
     _active = True
+    _phase = -1
+    _pos.clear()
+    _per_step.clear()
     if flag:
         _records.clear()
         _counts.clear()
         _flops_all.clear()
         _every = max(1, int(every))
+
+
+_per_step = {}     # name -> launches in the previous stepped step (sets the region's sampling rate)
+MIN_SAMPLES = 2    # target timed launches per step and region: rate 1 / clamp(n // MIN_SAMPLES, 1, every)
+
+
+def new_step(active: bool):
+    """Start of one step of the timed loop (bench.py). While stepped, a region's launch at position j of the
+    k-th active step is timed when (j + k) % every == 0: STRATIFIED over the launch positions of a step, so
+    every position of the step's launch sequence (a region's launches differ in shape: the LPIPS VGG conv's
+    13 layers, the decoder's blocks) is timed equally often over `every` active steps. The pseudo-random
+    launch-index sample of round 5 carried the shape mix's sampling error: the VGG conv read 426 us by events
+    against 619 us in rocprof on the same box (What's weak 6)."""
+    global _active, _phase
+    _active = bool(active)
+    for k, n in _pos.items():
+        _per_step[k] = n
+    _pos.clear()
+    if active:
+        _phase += 1
 
 
 def set_active(flag: bool):
@@ -129,17 +164,18 @@ class _Timed:
     """One sampled launch: native regions arm the kernel library's dispatch events around the launch,
     library regions record torch events on the current stream. A plain context-manager class (a
     generator-based one costs a few microseconds of host time per timed launch)."""
-    __slots__ = ("name", "nbytes", "flops", "bound", "native", "pair")
+    __slots__ = ("name", "nbytes", "flops", "bound", "native", "pair", "first")
 
-    def __init__(self, name, nbytes, flops, bound, native):
+    def __init__(self, name, nbytes, flops, bound, native, first=False):
         # nbytes may be lazy (decoder_hip._LazyBytes): evaluated for sampled launches only
         self.name, self.nbytes, self.flops, self.bound, self.native = name, int(nbytes), flops, bound, native
+        self.first = first
 
     def __enter__(self):
         if self.native:
             lib = _native()
             self.pair = _KernelPair(lib)
-            lib.vfm_timer_arm(self.pair.s, self.pair.e)
+            (lib.vfm_timer_arm_first if self.first else lib.vfm_timer_arm)(self.pair.s, self.pair.e)
         else:
             self.pair = _TorchPair()
             self.pair.s.record(torch.cuda.current_stream())
@@ -177,19 +213,33 @@ def _sampled(c):
     return ((c * 40503) & 0xFFFF) < 65536 // _every
 
 
-def region(name, nbytes=0, flops=0, bound="hbm", native=True):
+def region(name, nbytes=0, flops=0, bound="hbm", native=True, first_only=False):
     """Context manager around one launch (native = our kernel library, timed by the kernel dispatch;
     otherwise events around the call); a shared no-op object when timing is off or the launch is not
-    sampled (this is on every launch's host path)."""
+    sampled (this is on every launch's host path). first_only: only the call's first kernel is timed (a GEMM
+    whose split-K combine pass follows as a kernel of its own: the region then covers exactly the launches of
+    the GEMM kernel instantiation rocprofv3 names)."""
     if not _enabled:
         return _NULL
     c = _counts.get(name, 0)
     _counts[name] = c + 1
     if flops:
         _flops_all[name] = _flops_all.get(name, 0.0) + flops
-    if not _active or (_every > 1 and not _sampled(c)):
+    if not _active:
         return _NULL
-    return _Timed(name, nbytes, flops, bound, native)
+    if _every > 1:
+        if _phase >= 0:
+            j = _pos.get(name, 0)
+            _pos[name] = j + 1
+            # a region with few launches per step is sampled more densely (all of them below 2 x MIN_SAMPLES):
+            # the decoder's b5 MLP runs 5 times a step, in shapes that follow each step's equivariance draw, and
+            # 1/20 of them over 20 steps were 5 samples from 5 particular steps
+            ev = max(1, min(_every, _per_step.get(name, _every * MIN_SAMPLES) // MIN_SAMPLES))
+            if (j + _phase) % ev:
+                return _NULL
+        elif not _sampled(c):
+            return _NULL
+    return _Timed(name, nbytes, flops, bound, native, first_only)
 
 
 def vendor_gemm(tag, M, N, K, z=1, esize=2):
@@ -202,12 +252,39 @@ def vendor_gemm(tag, M, N, K, z=1, esize=2):
                   native=False)
 
 
+_calib_ms = 0.0    # fixed interval of one timed launch of an empty kernel (calibrate()), subtracted per launch
+
+
+def calibrate(n=64):
+    """Median interval of `n` timed empty-kernel launches on the current stream (vfm_timer_null_launch): the
+    dispatch gap and empty-kernel time every timed native launch carries (round 6: +5-12 us on the decoder's
+    10-40 us kernels against rocprofv3's trace of the same run, gpurun_out r6r). summary() subtracts it from
+    each timed native launch. Call with the GPU idle (before the timed steps)."""
+    global _calib_ms
+    lib = _native()
+    from torch_utils import custom_ops
+    st = custom_ops.stream_ptr()
+    pairs = []
+    torch.cuda.synchronize()
+    for _ in range(n):
+        pair = _KernelPair(lib)
+        lib.vfm_timer_arm(pair.s, pair.e)
+        custom_ops.check(lib.vfm_timer_null_launch(st), "vfm_timer_null_launch")
+        pair.launched = lib.vfm_timer_arm(None, None) > 0
+        pairs.append(pair)
+    vals = sorted(v for v in (p.ms() for p in pairs) if v is not None)
+    _calib_ms = vals[len(vals) // 2] if vals else 0.0
+    return _calib_ms
+
+
 def summary():
     torch.cuda.synchronize()
     out = {}
     for name, recs in _records.items():
         timed = [(p.ms(), b, f, bd) for p, b, f, bd in recs]
         timed = [t for t in timed if t[0] is not None]      # a region that launched nothing has no time
+        if _calib_ms and recs and isinstance(recs[0][0], _KernelPair):
+            timed = [(max(t[0] - _calib_ms, 0.0),) + t[1:] for t in timed]
         if not timed:
             continue
         ms = sum(t[0] for t in timed)
@@ -239,6 +316,14 @@ _NP = {"f32x6": 3, "f32x3": 2, "bf16": 1}
 _TNAME = {"f32": "float", "bf16": "__hip_bfloat16", "f16": "__half", "f64": "double"}
 
 
+def roc_match(pattern, kernel_name):
+    """A rocprof kernel name (anonymous namespace / `void` / call arguments stripped or not) against a
+    rocprof_name() pattern: a prefix, '*' matching any run of characters."""
+    import fnmatch
+    n = kernel_name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return fnmatch.fnmatchcase(n, pattern + "*")
+
+
 def rocprof_name(region):
     """'scale_bias_gelu_bwd<bf16>' -> 'gelu_bwd<__hip_bfloat16>' (a prefix of the rocprof name)."""
     region = region.split("[", 1)[0]
@@ -246,8 +331,9 @@ def rocprof_name(region):
     args = args.rstrip(">").split(",") if args else []
     if base == "gemm8" and len(args) == 4:                     # <tag, AK, BK, OUTF32> (default schedule, EPI 0)
         return f"gemm8_kernel<{args[1]}, {args[2]}, {args[3]}, false, 0>"
-    if base == "gemm9" and len(args) == 4:                     # persistent gemm9p_kernel<AK, BK, OUTF32, EPI>
-        return f"gemm9p_kernel<{args[1]}, {args[2]}, {args[3]}, "
+    if base == "gemm9" and len(args) == 4:                     # persistent gemm9p_kernel<AK, BK, OUTF32, EPI, NP>
+        # EPI 0-3 (plain / bias / GELU epilogues); 4 and 5 are the ConvNeXt-MLP forms of the gemm9_gelu regions
+        return f"gemm9p_kernel<{args[1]}, {args[2]}, {args[3]}, [0-3], {_NP.get(args[0], 1)}>"
     if base == "gemm9_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2: EPI 4 / 5)
         return f"gemm9p_kernel<true, false, false, {3 + int(args[0])}>"
     if base == "gemm8_gelu" and len(args) == 1:                # GELU epilogue forms (mode 1 / 2)
@@ -256,6 +342,8 @@ def rocprof_name(region):
         np_ = _NP.get(args[0], 1)
         nw = 8 if (np_ == 3 and os.environ.get("VFM_GEMM128_WAVES", "8") != "4") else 4
         return f"gemm_kernel<{args[1]}, false, {np_}, {args[2]}, {nw}>"
+    if base == "sgemm" and len(args) == 5:                     # exact-fp32 sgemm_kernel<AK, BK, BM, BN, KW>
+        return f"sgemm_kernel<{args[0]}, {args[1]}, {args[2]}, {args[3]}, {args[4]}>"
     if base == "gemm4" and len(args) == 4:                     # gemm4_kernel<AK, BK, OUTF32>
         return f"gemm4_kernel<{args[1]}, {args[2]}, {args[3]}>"
     if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32, NW>
@@ -298,7 +386,7 @@ def _roof(name, r, hbm_peak_gbs, mfma_peak_tflops):
         elif "f32x3" in name:
             peak = round(mfma_peak_tflops / 3, 1)
             note = "achieved = fp32 FLOPs of the op / time; peak = dense bf16 MFMA peak / 3 (opt-in f32x3 split)"
-        elif "<f32" in name:
+        elif "<f32" in name or name.startswith("sgemm<"):
             peak = 157.3
             note = "exact fp32 MFMA peak"
     else:
@@ -324,7 +412,7 @@ def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None, steps=
         traffic = None
         if traffic_table and roc:
             hits = [(v["dispatches_fetch_pass"], v["traffic_bytes_per_launch"]) for k, v in traffic_table.items()
-                    if k.startswith(roc) and v.get("traffic_bytes_per_launch")]
+                    if roc_match(roc, k) and v.get("traffic_bytes_per_launch")]
             n = sum(h[0] for h in hits)
             if n:
                 traffic = int(sum(c * t for c, t in hits) / n)
