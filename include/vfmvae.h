@@ -396,6 +396,17 @@ int vfm_gemm_fold(const void* A, const void* B, void* C, const float* bias, int 
                   int lgp, int K, int batch, int a_kcont, long long lda, long long ldb, long long sB, long long ldc,
                   long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 
+/* im2col of a 2-D convolution (kernel kh x kw, stride (sy, sx), zero padding (py, px), dilation 1) over an NCHW
+ * fp32 x [B, C, H, W] into cols [B, C kh kw, Ho Wo] (Ho = (H + 2 py - kh) / sy + 1, likewise Wo), and its adjoint
+ * (col2im: x = the sum of the cols entries that read each element, a gather: deterministic, overwrites x).
+ * With vfm_sgemm they form the convolution of reference torch_utils/ops/conv2d_resample.py:46-141
+ * (conv2d_gradfix.conv2d / conv_transpose2d, conv2d_gradfix.py:37-58) and generator.py:46-103's grouped
+ * modulated_conv2d (torch_utils/ops/conv2d_hip.py). */
+int vfm_im2col2d_f32(const float* x, float* cols, int B, int C, int H, int W, int kh, int kw, int sy, int sx, int py,
+                     int px, int Ho, int Wo, void* stream);
+int vfm_col2im2d_f32(const float* cols, float* x, int B, int C, int H, int W, int kh, int kw, int sy, int sx, int py,
+                     int px, int Ho, int Wo, void* stream);
+
 /* Exact-fp32 form of the vfm_gemm contract on the fp32-input MFMA (csrc/sgemm.hip, v_mfma_f32_32x32x2_f32: one
  * fmaf-chain product per multiply-add, no operand split): C[z] = epi(alpha A[z] B[z] + beta C[z]), fp32 A / B / C,
  * bias (1 per column, 2 per row) then act (1 gelu tanh, 2 gelu erf). Replaces the reference's fp32 products with

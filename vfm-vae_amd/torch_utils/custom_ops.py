@@ -156,6 +156,10 @@ SIGNATURES = {
                   c_float, c_float, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
     "vfm_sgemm_workspace_floats": [c_int, c_int, c_int, c_int, c_int],
     "vfm_timer_mode": [c_int],
+    "vfm_im2col2d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_vp],
+    "vfm_col2im2d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_vp],
     "vfm_timer_null_launch": [c_vp],
     "vfm_timer_arm_first": [c_vp, c_vp],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,

@@ -1,9 +1,12 @@
 """2-D convolution with integrated FIR up/downsampling.
 
 Drop-in for reference `torch_utils/ops/conv2d_resample.py:46-141`. The
-resampling steps run on the HIP `upfirdn2d` kernels; the convolution itself is
-a library conv (MIOpen through `torch.nn.functional`), as in the reference
-(cuDNN). Padding is applied once, before any resampling.
+resampling steps run on the HIP `upfirdn2d` kernels; on ROCm tensors the
+convolution itself (plain, strided, transposed, grouped -- modulated_conv2d's
+per-sample groups) runs on our kernels too: im2col / col2im (csrc/im2col2d.hip)
+around the exact-fp32 GEMM (csrc/sgemm.hip), conv2d_hip. CPU tensors take
+conv2d_gradfix (torch.nn.functional), as the reference does. Padding is applied
+once, before any resampling.
 """
 import torch
 
@@ -18,6 +21,11 @@ def _conv(x, w, stride=1, padding=0, groups=1, transpose=False, flip_weight=True
     # conv2d correlates; flip_weight=False requests true convolution.
     if not flip_weight and (kh > 1 or kw > 1):
         w = w.flip([2, 3])
+    from . import conv2d_hip
+    if conv2d_hip.supported(x, w):
+        if transpose:
+            return conv2d_hip.conv_transpose2d(x, w, stride=stride, padding=padding, groups=groups)
+        return conv2d_hip.conv2d(x, w, stride=stride, padding=padding, groups=groups)
     if transpose:
         return conv2d_gradfix.conv_transpose2d(x, w, stride=stride, padding=padding, groups=groups)
     return conv2d_gradfix.conv2d(x, w, stride=stride, padding=padding, groups=groups)

@@ -113,9 +113,9 @@ def _planar(t3, stream):
 
 
 BF16_OWN = __import__("os").environ.get("VFM_BF16_GEMM", "hip") == "hip"
-# fp32 products narrower than 128 (the 8^2 / 16^2 decoder blocks' 1x1s): hipBLASLt's exact-fp32 GEMM by
-# default; VFM_F32_SMALL=hip routes them to the f32x6 128-tile kernel, which measured slower at these
-# shapes (r5o bench, profiles/r5_o_f32small_ab.txt)
+# fp32 products narrower than 128 (the 8^2 / 16^2 decoder blocks' 1x1s): the exact-fp32 GEMM (`sgemm`,
+# csrc/sgemm.hip) by default; VFM_F32_SMALL=hip routes them to the f32x6 128-tile kernel, which measured slower
+# at these shapes (r5o bench, profiles/r5_o_f32small_ab.txt)
 F32_SMALL_OWN = __import__("os").environ.get("VFM_F32_SMALL", "torch") == "hip"
 # bf16 products on gemm9 (csrc/gemm9.hip); False: gemm8's 256-tile pipeline (tests, A/B)
 G9 = __import__("os").environ.get("VFM_GEMM9", "1") == "1"
@@ -570,18 +570,38 @@ SGEMM = __import__("os").environ.get("VFM_SGEMM", "1") == "1"
 SG_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))      # tile codes 0-3; +4: two wave groups (KW = 2)
 
 
+# relative time of one 32-deep K-tile per tile shape (64 x 64 = 1; the larger tiles reuse operands better:
+# 4096^2 runs 130 TF/s on 128 x 128 against ~100 on 64 x 64), a workgroup's fixed prologue + epilogue in K-tiles,
+# one 64 x 64 K-tile in us with two workgroups per CU, and the workgroup slots of the chip (256 CUs x 2)
+_SG_KT = (4.0, 2.1, 2.1, 1.0)
+_SG_FIXED, _SG_KT_US, _SG_SLOTS = 3.0, 1.14, 512
+
+
 def _sg_plan(M, N, K, zt, vt):
     """(tile code, K splits) of an exact-fp32 product with zt independent output planes and vt virtual K-tiles
-    (32 deep) per output: 128 x 128 tiles when they alone give >= 1024 workgroups (4096^2: 130 TF/s), else
-    64 x 64 tiles, split along K until >= ~512 workgroups cover the 256 CUs, each chunk >= 8 K-tiles
-    (tools_dev/sgemmbench.py sweeps, profiles/r6_sgemmbench.txt: the D heads' 1-D convs 60-109 TF/s against
-    hipBLASLt's 50-100, the 4^2 decoder 1x1s 1.1-1.4x hipBLASLt, the weight gradients 1.2-2.3x)."""
-    if -(-M // 128) * -(-N // 128) * zt >= 1024:
+    (32 deep) per output: the candidate with the least modelled time -- whole rounds of workgroups over the
+    chip's 512 slots (wave quantization: the D heads' 588 64 x 64 tiles are 1.15 rounds unsplit, 3.4 split
+    three ways), each round as long as one workgroup's K chunk plus its fixed cost, plus the split's partial-sum
+    traffic and reduce launch; 64 x 64 first, a larger tile only when modelled >= 3 % faster (a lone workgroup
+    per CU does not get the two-per-CU rate the model assumes, which favours the small tile in practice). The
+    model reproduces the sweeps of tools_dev/sgemmbench.py within ~10 % (profiles/r6_sgemmbench.txt: e.g.
+    D-head k9 forward 247 us unsplit, 171 us in three). Deep products with >= 1024 128 x 128 tiles take
+    128 x 128 unsplit (4096^2: 130 TF/s; at K <= 384 64 x 64 stays faster)."""
+    if -(-M // 128) * -(-N // 128) * zt >= 1024 and vt >= 32:
         return 0, 1
-    tiles = -(-M // 64) * -(-N // 64) * zt
-    if tiles >= 480:
-        return 3, 1
-    return 3, max(1, min(-(-512 // tiles), vt // 8))
+    best = None
+    for tile in (3, 1, 2, 0):
+        kt = _SG_KT[tile]
+        bm, bn = SG_TILES[tile]
+        tiles = -(-M // bm) * -(-N // bn) * zt
+        for s in range(1, max(1, min(16, vt // 4)) + 1):
+            rounds = -(-tiles * s // _SG_SLOTS)
+            t = rounds * (-(-vt // s) + _SG_FIXED) * kt * _SG_KT_US
+            if s > 1:
+                t += 4.0 + s * zt * M * N * 8 / 5e6            # partials written + read at ~5 TB/s, the reduce launch
+            if best is None or t < best[0] * 0.97:             # prefer the earlier (larger-tile, less-split) plan on ties
+                best = (t, tile, s)
+    return best[1], best[2]
 
 
 def _sg_layouts(t3, outer, kdim):
