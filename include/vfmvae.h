@@ -165,6 +165,16 @@ int vfm_style_demod_bwd(const float* w, long long ldw, const float* A, const flo
                         const float* s, const float* d, const float* ds_in, const float* dd, float wg, float bg,
                         int B, int C, int WD, int O, float* ws, float* dW1, float* dA, float* dab, float* dw,
                         void* stream);
+/* The style path of every ConvNeXt layer of a synthesis network in one launch per phase (forward launches 0, 1;
+ * backward 2, 4, 3, 5, in that order; torch_utils/ops/style_group.py): vfm_style_group_pack writes launch `launch`'s
+ * layer table and block offsets for n layers into host memory (vfm_style_group_bytes(n) bytes; per layer 16 pointer
+ * slots w, A, ab, W1, m, s, d, ds_in, dd, ws, dW1, dA, dab, dw, ldw, lddw (dw's row stride), dims B, C, WD, O and
+ * gains wg, bg, eps, as the single-layer calls above take them) and returns its total blocks; the caller uploads
+ * the bytes and vfm_style_group_launch runs them. Same arithmetic per layer as the single-layer calls. */
+long long vfm_style_group_bytes(int n);
+long long vfm_style_group_pack(int launch, int n, const long long* ptrs, const int* dims, const float* gains,
+                               void* host_out);
+int vfm_style_group_launch(int launch, const void* dev_packed, int n, long long total_blocks, void* stream);
 
 /* Spectral normalisation in training mode (torch.nn.utils.spectral_norm, one power iteration, dim 0: the
  * projected discriminator heads' SpectralConv1d, reference networks/discriminator.py): for fp32 W [O, I],
@@ -407,6 +417,17 @@ int vfm_im2col2d_f32(const float* x, float* cols, int B, int C, int H, int W, in
 int vfm_col2im2d_f32(const float* cols, float* x, int B, int C, int H, int W, int kh, int kw, int sy, int sx, int py,
                      int px, int Ho, int Wo, void* stream);
 
+/* One launch for a phase's optimizer step (csrc/adam.hip): Adam (torch.optim.Adam's fused arithmetic, ORIGINAL
+ * weight decay) over every tensor of the device table `tensors` (ntensors 64-B records {p, g, m, v, ema or null, n,
+ * vec, 0}) through the chunk list `chunks` (nchunks int pairs (tensor, chunk) of vfm_adam_chunk_elems() elements),
+ * and for records with an EMA copy the G_ema lerp ema <- ema + ema_w (p - ema) on the stepped p. bc1 =
+ * 1 - beta1^step, bc2_sqrt = sqrt(1 - beta2^step). Replaces the reference's opt.step() + G_ema lerp (reference
+ * training/training_loop.py:722-742; host side training_loop.fast_adam_step / torch_utils/ops/adam_hip.py). */
+int vfm_adam_chunk_elems(void);
+int vfm_adam_ema_step(const void* tensors, int ntensors, const void* chunks, int nchunks, double lr, double beta1,
+                      double beta2, double weight_decay, double eps, double bc1, double bc2_sqrt, float ema_w,
+                      void* stream);
+
 /* Exact-fp32 form of the vfm_gemm contract on the fp32-input MFMA (csrc/sgemm.hip, v_mfma_f32_32x32x2_f32: one
  * fmaf-chain product per multiply-add, no operand split): C[z] = epi(alpha A[z] B[z] + beta C[z]), fp32 A / B / C,
  * bias (1 per column, 2 per row) then act (1 gelu tanh, 2 gelu erf). Replaces the reference's fp32 products with
@@ -454,15 +475,6 @@ int vfm_gemm8_pieces(const void* A, const void* B, void* C, const float* bias, i
                      void* stream);
 int vfm_gemm8_workspace_floats(int precision, int M, int N, int K, int batch, int kchunk,
                                int reduce_batch);  /* -1: too large */
-/* bf16 form of the same contract with one wave per SIMD (csrc/gemm4.hip: 256 x 256 tiles, 4 waves of
- * 128 x 128, register-staged operand tiles, C stored from the accumulators): the frozen SigLIP2
- * tower's linears (reference networks/utils/vfms/siglip2_utils.py:120-121, HF SiglipMLP /
- * SiglipAttention projections under bf16 autocast) and the decoder's bf16 1x1 convolutions
- * (reference networks/utils/convnext_utils.py:135-138 pwconv1 / pwconv2 under autocast).
- * bf16 A / B only; K % 64 == 0 (else VFM_NO_KERNEL); no split-K. */
-int vfm_gemm4(const void* A, const void* B, void* C, const float* bias, int out_dtype, int M, int N, int K,
-              int batch, int a_kcont, long long lda, long long sA, int b_kcont, long long ldb, long long sB,
-              long long ldc, long long sC, float alpha, float beta, int bias_mode, int act, void* stream);
 /* bf16 form of the same contract on the LDS-DMA one-wave-per-SIMD kernel (csrc/gemm9.hip: 256 x 256 tiles,
  * 4 waves of 128 x 128, both operand tiles moved global -> LDS by LDS-DMA two K-tiles ahead, two barriers
  * per K-tile, accumulators pinned to AGPRs, C stored from the accumulators): the frozen SigLIP2 tower's

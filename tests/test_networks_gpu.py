@@ -70,6 +70,8 @@ def test_generator_forward_backward_gpu(vfm_dir, precision):
     for m in (G.synthesis, G.mapping, G.ldm_adapter):
         m.requires_grad_(True)
     img = torch.from_numpy(_arr("G/img")).to(DEV)
+    with torch.no_grad():                           # first forward: records the grouped style plan, so the
+        G(img, ['x'] * 2, validation=True)          # checked one runs csrc/style.hip's grouped launches
     torch.manual_seed(123)                          # posterior noise: CPU RNG, as the reference
     kt.enable(True)
     out = G(img, ['x'] * 2, validation=True)
@@ -85,7 +87,7 @@ def test_generator_forward_backward_gpu(vfm_dir, precision):
     loss.backward()
     torch.cuda.synchronize()
     _native_ran(kt, "dwconv2d_fwd", "dwconv2d_bwd_data", "dwconv2d_bwd_weight", "group_norm_fwd",
-                "group_norm_bwd", "shuffle_blur_fwd", "shuffle_blur_bwd")
+                "group_norm_bwd", "shuffle_blur_fwd", "shuffle_blur_bwd", "style_group_fwd", "style_group_bwd")
     kt.enable(False)
     _check_grads("G", G, norm_tol=tol["norm"], full_tol=tol["full"], sum_tol=tol["sums"])
 

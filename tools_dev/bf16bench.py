@@ -1,7 +1,7 @@
 """Microbench of the decoder's bf16 1x1 convolutions at batch 32 (blocks 3-4, the ConvNeXt MLP widths):
 forward W . x[b], data gradient W^T . dy[b] and the batch-reduced weight gradient sum_b dy[b] x[b]^T,
 on hipBLASLt (torch.bmm; the weight gradient as bmm + sum(0) in fp32, what decoder_hip does) and on our
-kernels (gemm8 batched / batch-reduced split-K, gemm4)."""
+kernels (gemm8 batched / batch-reduced split-K)."""
 import os
 import sys
 
@@ -58,11 +58,9 @@ for name, O, I, P in SHAPES:
         line(f"dW  {name}", fl, vs)
         continue
     line(f"fwd {name}", fl, [("blas", lambda: torch.bmm(W.expand(Bn, O, I), x)),
-                             ("g8", lambda: gemm_hip.try_gemm(W, x, route=("g8", 0))),
-                             ("g4", lambda: gemm_hip.try_gemm(W, x, route=("g4", 0)))])
+                             ("g8", lambda: gemm_hip.try_gemm(W, x, route=("g8", 0)))])
     line(f"dx  {name}", fl, [("blas", lambda: torch.bmm(W.t().expand(Bn, I, O), dy)),
-                             ("g8", lambda: gemm_hip.try_gemm(W.t(), dy, route=("g8", 0))),
-                             ("g4", lambda: gemm_hip.try_gemm(W.t(), dy, route=("g4", 0)))])
+                             ("g8", lambda: gemm_hip.try_gemm(W.t(), dy, route=("g8", 0)))])
     V = Bn * (P // 64)
     vs = [("blas", lambda: torch.bmm(dy, x.transpose(1, 2), out_dtype=torch.float32).sum(0))]
     for S in (8, 16, 32, 64):

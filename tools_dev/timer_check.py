@@ -15,12 +15,12 @@ W = torch.randn(3072, 1024, device="cuda")
 Ab, Wb = A.bfloat16(), W.bfloat16()
 for _ in range(3):
     gemm_hip.try_gemm(A, W.t(), route=("g8", 0), cache_b=True)
-    gemm_hip.try_gemm(Ab, Wb.t(), route=("g4", 0))
+    gemm_hip.try_gemm(Ab, Wb.t(), route=("g9", 0))
 torch.cuda.synchronize()
 kernel_timer.enable(True, 1)
 for i in range(20):
     gemm_hip.try_gemm(A, W.t(), route=("g8", 0), cache_b=True)
-    gemm_hip.try_gemm(Ab, Wb.t(), route=("g4", 0))
+    gemm_hip.try_gemm(Ab, Wb.t(), route=("g9", 0))
     if i % 5 == 0:
         torch.cuda.synchronize()          # idle gaps in front of some launches: the events must not see them
 kernel_timer.enable(False)

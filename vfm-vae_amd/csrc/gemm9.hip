@@ -6,7 +6,7 @@
 // these shapes is a 256-thread workgroup whose 4 waves each own a 128 x 128 block, with both operand
 // tiles moved global -> LDS by LDS-DMA, two K-tiles in flight and two barriers per 64-deep K-tile
 // (its code object's name and instruction mix: DirectToLds A/B, prefetch depth 2, wave tile 8 x 8 of
-// v_mfma_f32_16x16x32_bf16). gemm4 (register staging) lost its K-loop to the compiler serialising the
+// v_mfma_f32_16x16x32_bf16). gemm4 (register staging, removed in round 6) lost its K-loop to the compiler serialising the
 // staged loads behind the MFMA chain; gemm8 (8 waves of 128 x 64) spends twice the fragment reads per
 // MFMA and 8 barriers per K-tile. Here, per K-tile and wave: 128 MFMAs, 32 fragment reads (one per
 // MFMA in the two read phases), 16 LDS-DMA issues (one per ~5 MFMAs), 2 barriers:

@@ -61,7 +61,8 @@ struct StyleArgs {
     float* dW1;                           // [O, C] or null
     float* dA;                            // [3C, WD] or null
     float* dab;                           // [3C] or null
-    float* dw;                            // [B, WD] or null
+    float* dw;                            // [B, WD] (row stride lddw) or null
+    long long lddw;
     int blocks0;                          // blocks of the launch's first job
     int tpb;                              // tiles per block of the forward's tile jobs (1 or WAVES)
     int ks;                               // K chunks of the column-sum job
@@ -250,11 +251,10 @@ __device__ __forceinline__ void store4(float* p, long long ld, int r, int rows, 
 // LAUNCH 3: dA + dab (outer tiles, blocks0) | dw partials (column sums over A)
 // LAUNCH 4: ds = ds_in + 2 s sum(partials)          LAUNCH 5: dw = wg sum(partials)
 template <int LAUNCH>
-__global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
-    __shared__ __attribute__((aligned(16))) float smem[OT_B * OT_R + OT_B * OT_C];
+__device__ __forceinline__ void style_body(const StyleArgs& a, int bid, float* smem) {
     float* red = smem;
-    const bool second = (int)blockIdx.x >= a.blocks0;
-    const int blk = second ? blockIdx.x - a.blocks0 : blockIdx.x;
+    const bool second = bid >= a.blocks0;
+    const int blk = second ? bid - a.blocks0 : bid;
     const int C = a.C, C3 = 3 * a.C, WD = a.WD, O = a.O, B = a.B;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     // forward tile jobs: one tile per block (tpb = 1) or per wave (tpb = 4); the result sits in lane
@@ -390,17 +390,35 @@ __global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
                 [&](int k, int n) { return a.A[(long long)k * WD + n]; }, a.part, smem);
         }
     } else if (LAUNCH == 4) {     // ds = ds_in + 2 s sum_ks part (fixed order)
-        const long long i = (long long)blockIdx.x * THREADS + t;
+        const long long i = (long long)bid * THREADS + t;
         if (i >= (long long)B * C) return;
         const float acc = sum_parts(a.part + i, (long long)B * C, a.ks);
         a.ds[i] = (a.dsin ? a.dsin[i] : 0.f) + 2.f * a.s[i] * acc;
     } else {                      // dw = wg sum_ks part (fixed order)
-        const long long i = (long long)blockIdx.x * THREADS + t;
+        const long long i = (long long)bid * THREADS + t;
         if (i >= (long long)B * WD) return;
         const float acc = sum_parts(a.part + i, (long long)B * WD, a.ks);
         const long long b = i / WD, n = i - b * WD;
-        a.dw[b * WD + n] = a.wg * acc;
+        a.dw[b * a.lddw + n] = a.wg * acc;
     }
+}
+
+template <int LAUNCH>
+__global__ __launch_bounds__(THREADS) void style_kernel(StyleArgs a) {
+    __shared__ __attribute__((aligned(16))) float smem[OT_B * OT_R + OT_B * OT_C];
+    style_body<LAUNCH>(a, blockIdx.x, smem);
+}
+
+// The same launch over a group of layers (every ConvNeXt layer of the synthesis network in one launch): the
+// layer table tab[n] and the block offsets off[n + 1] (layer l owns blocks off[l] .. off[l + 1] - 1).
+template <int LAUNCH>
+__global__ __launch_bounds__(THREADS) void style_group_kernel(const StyleArgs* __restrict__ tab,
+                                                              const int* __restrict__ off, int n) {
+    __shared__ __attribute__((aligned(16))) float smem[OT_B * OT_R + OT_B * OT_C];
+    int l = 0;
+    while (l + 1 < n && (int)blockIdx.x >= off[l + 1]) ++l;
+    const StyleArgs a = tab[l];
+    style_body<LAUNCH>(a, (int)blockIdx.x - off[l], smem);
 }
 
 template <int L>
@@ -495,4 +513,119 @@ extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A
     if (rc || !dw) return rc;
     a.blocks0 = 0;
     return launch<5>(a, cdiv_i((long long)B * WD, THREADS), st);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Grouped form: one launch per phase of the style path for all layers of a network (torch_utils/ops/style_group.py).
+// The host packs each launch's layer table + block offsets (vfm_style_group_pack, host memory only), uploads the
+// packed bytes, and launches vfm_style_group_launch with the device copy.
+namespace {
+constexpr int GP = 16;           // per-layer pointer slots of the pack call
+}
+
+// Bytes of one packed launch section for n layers (table + offsets, 16-B multiple).
+extern "C" long long vfm_style_group_bytes(int n) {
+    if (n <= 0) return -1;
+    const long long b = (long long)n * sizeof(StyleArgs) + (long long)(n + 1) * 4;
+    return (b + 15) / 16 * 16;
+}
+
+// Pack launch `launch` (0, 1: forward m / s, d; 2, 4, 3, 5: backward, in that order) for n layers into host_out
+// (vfm_style_group_bytes(n) bytes). Per layer l: ptrs[GP l ..] = w, A, ab, W1, m, s, d, ds_in, dd, ws (workspace of
+// vfm_style_demod_bwd_workspace_floats), dW1, dA, dab, dw, ldw, lddw (null / 0 where absent, as the single-layer
+// entry points take them); dims[4 l ..] = B, C, WD, O; gains[3 l ..] = wg, bg, eps. Layers with nothing to do in
+// this launch, or whose w slot is null (left out), get no blocks. Returns the launch's total blocks (0: nothing to launch) or an error code < 0.
+extern "C" long long vfm_style_group_pack(int launch, int n, const long long* ptrs, const int* dims, const float* gains,
+                                          void* host_out) {
+    if (n <= 0 || !ptrs || !dims || !gains || !host_out) return VFM_ERR_ARGS;
+    StyleArgs* tab = reinterpret_cast<StyleArgs*>(host_out);
+    int* off = reinterpret_cast<int*>(reinterpret_cast<char*>(host_out) + (size_t)n * sizeof(StyleArgs));
+    long long total = 0;
+    for (int l = 0; l < n; ++l) {
+        const long long* p = ptrs + (long long)GP * l;
+        if (!p[0]) {                 // a layer left out of this call (no gradient reached it): no blocks
+            tab[l] = StyleArgs{};
+            off[l] = (int)total;
+            continue;
+        }
+        const int B = dims[4 * l], C = dims[4 * l + 1], WD = dims[4 * l + 2], O = dims[4 * l + 3];
+        if (!sizes_ok(B, C, WD, O) || !p[0] || !p[1] || !p[4] || !p[5]) return VFM_ERR_ARGS;
+        StyleArgs a{};
+        a.w = (const float*)p[0]; a.A = (const float*)p[1]; a.ab = (const float*)p[2]; a.W1 = (const float*)p[3];
+        a.m = (float*)p[4]; a.s = (float*)p[5]; a.d = (float*)p[6];
+        a.dsin = (const float*)p[7]; a.dd = (const float*)p[8];
+        float* ws = (float*)p[9];
+        a.dW1 = (float*)p[10]; a.dA = (float*)p[11]; a.dab = (float*)p[12]; a.dw = (float*)p[13];
+        a.ldw = p[14]; a.lddw = p[15];
+        a.wg = gains[3 * l]; a.bg = gains[3 * l + 1]; a.eps = gains[3 * l + 2];
+        a.B = B; a.C = C; a.WD = WD; a.O = O;
+        if (a.ldw < WD) return VFM_ERR_ARGS;
+        const long long nbg = cdiv_i(B, RB);
+        const bool demod = a.dd != nullptr;
+        long long blocks = 0;
+        if (launch == 0) {
+            a.tpb = tiles_per_block(WD);
+            a.blocks0 = cdiv_i(nbg * cdiv_i(C, 4), a.tpb);
+            blocks = a.blocks0;
+        } else if (launch == 1) {
+            if (a.W1) {
+                if (!a.d || O <= 0) return VFM_ERR_ARGS;
+                a.tpb = tiles_per_block(C);
+                a.blocks0 = cdiv_i(nbg * cdiv_i(O, 8), a.tpb);
+                blocks = a.blocks0;
+            }
+        } else if (launch == 2 || launch == 4 || launch == 3 || launch == 5) {
+            if (demod && (!a.W1 || !a.d || O <= 0 || !ws)) return VFM_ERR_ARGS;
+            if (!demod && a.dW1) return VFM_ERR_ARGS;
+            a.ds = ws;
+            a.part = ws ? ws + (long long)B * C : nullptr;
+            a.dsv = demod ? a.ds : a.dsin;
+            const bool any_out = demod || a.dsin;
+            if (launch == 2 && demod) {
+                a.ks = ks_ds(O);
+                a.blocks0 = cdiv_i(C, 64) * a.ks;
+                blocks = a.blocks0 + (a.dW1 ? (long long)cdiv_i(O, OT_R) * cdiv_i(C, OT_C) : 0);
+            } else if (launch == 4 && demod) {
+                a.blocks0 = 0;
+                blocks = cdiv_i((long long)B * C, THREADS);
+            } else if (launch == 3 && any_out && (a.dA || a.dab || a.dw)) {
+                if (!ws) return VFM_ERR_ARGS;
+                a.ks = ks_dw(C);
+                a.blocks0 = (a.dA || a.dab) ? cdiv_i(3LL * C, OT_R) * cdiv_i(WD, OT_C) : 0;
+                blocks = a.blocks0 + (a.dw ? (long long)cdiv_i(WD, 64) * a.ks : 0);
+            } else if (launch == 5 && any_out && a.dw) {
+                a.ks = ks_dw(C);
+                a.blocks0 = 0;
+                blocks = cdiv_i((long long)B * WD, THREADS);
+            }
+        } else {
+            return VFM_ERR_ARGS;
+        }
+        tab[l] = a;
+        off[l] = (int)total;
+        total += blocks;
+        if (total > 0x7fffffffLL) return VFM_ERR_ARGS;
+    }
+    off[n] = (int)total;
+    return total;
+}
+
+// Launch a packed section (device copy `dev_packed` of vfm_style_group_pack's output for the same launch / n).
+extern "C" int vfm_style_group_launch(int launch, const void* dev_packed, int n, long long total_blocks, void* stream) {
+    if (!dev_packed || n <= 0 || total_blocks < 0 || total_blocks > 0x7fffffffLL) return VFM_ERR_ARGS;
+    if (total_blocks == 0) return 0;
+    const StyleArgs* tab = reinterpret_cast<const StyleArgs*>(dev_packed);
+    const int* off = reinterpret_cast<const int*>(reinterpret_cast<const char*>(dev_packed) + (size_t)n * sizeof(StyleArgs));
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)total_blocks), block(THREADS);
+    switch (launch) {
+    case 0: VFM_LAUNCH(style_group_kernel<0>, grid, block, 0, st, tab, off, n); break;
+    case 1: VFM_LAUNCH(style_group_kernel<1>, grid, block, 0, st, tab, off, n); break;
+    case 2: VFM_LAUNCH(style_group_kernel<2>, grid, block, 0, st, tab, off, n); break;
+    case 3: VFM_LAUNCH(style_group_kernel<3>, grid, block, 0, st, tab, off, n); break;
+    case 4: VFM_LAUNCH(style_group_kernel<4>, grid, block, 0, st, tab, off, n); break;
+    case 5: VFM_LAUNCH(style_group_kernel<5>, grid, block, 0, st, tab, off, n); break;
+    default: return VFM_ERR_ARGS;
+    }
+    return launch_status();
 }

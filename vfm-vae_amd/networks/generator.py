@@ -30,7 +30,7 @@ from torch.nn.parameter import Parameter
 
 from torch_utils import misc
 from torch_utils import distributed as dist
-from torch_utils.ops import upfirdn2d, conv2d_resample, bias_act, fma
+from torch_utils.ops import upfirdn2d, conv2d_resample, bias_act, fma, style_group
 from networks.utils.shared import FullyConnectedLayer, MLP, GroupNorm32, StyleSplit, ScaleAdaptiveAvgPool2d
 from networks.utils.shared import DepthwiseConv2d, Conv1x1, LeakyReLU
 from networks.utils.ldm_utils import LDMAdapter, EquivarianceTransform
@@ -507,6 +507,14 @@ class SynthesisNetwork(nn.Module):
                 w_idx += b.num_conv + b.num_torgb
         x = x_sum = img = None
         multiscale = []
+        # every layer's style (+ demodulation) in one grouped launch per phase on ROCm (torch_utils/ops/style_group.py)
+        with style_group.StyleGroup(self, ws):
+            img, multiscale = self._blocks(z, block_ws, text, text_mask, **block_kwargs)
+        return img, multiscale[::-1]
+
+    def _blocks(self, z, block_ws, text, text_mask, **block_kwargs):
+        x = x_sum = img = None
+        multiscale = []
         for idx, cur_ws in enumerate(block_ws):
             block = self.blocks[f"{idx:01d}"]
             if idx in self.concat_z_block_indices:
@@ -517,7 +525,7 @@ class SynthesisNetwork(nn.Module):
             x, x_sum, img = block(x, x_sum, img, cur_ws, text, text_mask, **block_kwargs)
             if not block.is_last:
                 multiscale.append(img)
-        return img, multiscale[::-1]
+        return img, multiscale
 
     def extra_repr(self):
         return (f'w_dim={self.w_dim:d}, num_ws={self.num_ws:d}, img_resolution={self.img_resolution:d}, '

@@ -148,7 +148,9 @@ class ConvNeXtToRGBLayer(nn.Module):
 
     def forward(self, x, w):
         B, C, H, W = x.shape
-        style = self.affine(w) * self.weight_gain                              # [B, C]
+        from torch_utils.ops import style_group
+        r = style_group.lookup(self.affine, w)                                 # grouped launch (style_group.py)
+        style = (r[0] if r is not None else self.affine(w)) * self.weight_gain  # [B, C]
         if self.kernel_size == 1:
             return decoder_ops.torgb(x, self.weight.reshape(self.out_channels, C), style, self.bias)
         else:

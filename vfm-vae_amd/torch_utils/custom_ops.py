@@ -139,8 +139,6 @@ SIGNATURES = {
                              c_vp],
     "vfm_attention_f32_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_llp, c_llp, c_llp,
                               c_llp, c_float, c_int, c_vp],
-    "vfm_gemm4": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll, c_ll,
-                  c_ll, c_ll, c_float, c_float, c_int, c_int, c_vp],
     "vfm_gemm9_set_mode": [c_int],
     "vfm_gemm9_gelu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_ll,
                        c_ll, c_ll, c_ll, c_ll, c_vp],
@@ -161,6 +159,12 @@ SIGNATURES = {
     "vfm_col2im2d_f32": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_vp],
     "vfm_timer_null_launch": [c_vp],
+    "vfm_adam_chunk_elems": [],
+    "vfm_style_group_bytes": [c_int],
+    "vfm_style_group_pack": [c_int, c_int, c_vp, c_vp, c_vp, c_vp],
+    "vfm_style_group_launch": [c_int, c_vp, c_int, c_ll, c_vp],
+    "vfm_adam_ema_step": [c_vp, c_int, c_vp, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                          ctypes.c_double, ctypes.c_double, ctypes.c_double, c_float, c_vp],
     "vfm_timer_arm_first": [c_vp, c_vp],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,
                       c_ll, c_float, c_float, c_int, c_int, c_vp],
@@ -252,6 +256,8 @@ def get_native():
             lib.vfm_bnl_workspace_floats.restype = c_ll
             lib.vfm_gemm9_workspace_floats.restype = c_ll
             lib.vfm_sgemm_workspace_floats.restype = c_ll
+            lib.vfm_style_group_bytes.restype = c_ll
+            lib.vfm_style_group_pack.restype = c_ll
             lib.vfm_channel_rms_norm_rows.restype = c_ll
             lib.vfm_specnorm_workspace_floats.restype = c_ll
             lib.vfm_dwconv2d_fwd_mfma_units.restype = c_ll

@@ -204,6 +204,10 @@ def style_and_demod(affine, w, w1=None, eps=1e-8):
     affine(w) (a StyleSplit over a linear FullyConnectedLayer, reference networks/utils/shared.py),
     dcoef = demod_coefficients(w1, style) when w1 is given. ROCm fp32: csrc/style.hip (two launches
     each way); elsewhere the torch formulation."""
+    from . import style_group
+    r = style_group.lookup(affine, w, w1, eps)            # the network's grouped launch (style_group.StyleGroup)
+    if r is not None:
+        return r
     fc = affine.proj
     if (STYLE_HIP and w.is_cuda and not _FORCE_REF and w.dtype == torch.float32 and w.dim() == 2 and fc.activation == 'linear'
             and fc.bias is not None and fc.weight.dtype == torch.float32

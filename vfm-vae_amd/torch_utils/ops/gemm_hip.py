@@ -395,19 +395,6 @@ def _try_gemm(A, B, out, bias, bias_dim, act, alpha, beta, out_dtype, splits, re
             custom_ops.check(rc, "vfm_gemm9")
             return out
         kern, arg = "g8", 0
-    if kern == "g4" and A.dtype == torch.bfloat16 and not reduce_batch:
-        # one wave per SIMD, 128 x 128 per wave (csrc/gemm4.hip)
-        region = f"gemm4<bf16,{tb(a_kc)},{tb(b_kc)},{tb(out_dtype == torch.float32)}>"
-        if kernel_timer.SHAPES:
-            region += f"[{M}x{N}x{K}x{z}]"
-        with kernel_timer.region(region, nbytes, flops, "mfma", first_only=True):
-            rc = _lib.vfm_gemm4(a3.data_ptr(), b3.data_ptr(), out.data_ptr(), custom_ops.ptr(bias), _CODES[out_dtype],
-                                M, N, K, z, int(a_kc), lda, sA, int(b_kc), ldb, sB, ldc, sC, float(alpha), float(beta),
-                                bias_mode, ACTS[act], stream)
-        if rc != custom_ops.VFM_NO_KERNEL:
-            custom_ops.check(rc, "vfm_gemm4")
-            return out
-        kern, arg = "g8", 0
     if kern == "g8":
         # 256 tiles + LDS-DMA pipeline (csrc/gemm8.hip); fp32 operands as their bf16 pieces along
         # K, the kernel accumulating the piece products of every K-tile

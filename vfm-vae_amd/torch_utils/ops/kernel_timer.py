@@ -344,8 +344,6 @@ def rocprof_name(region):
         return f"gemm_kernel<{args[1]}, false, {np_}, {args[2]}, {nw}>"
     if base == "sgemm" and len(args) == 5:                     # exact-fp32 sgemm_kernel<AK, BK, BM, BN, KW>
         return f"sgemm_kernel<{args[0]}, {args[1]}, {args[2]}, {args[3]}, {args[4]}>"
-    if base == "gemm4" and len(args) == 4:                     # gemm4_kernel<AK, BK, OUTF32>
-        return f"gemm4_kernel<{args[1]}, {args[2]}, {args[3]}>"
     if base == "gemm" and len(args) == 4:                      # gemm_kernel<AK, BK, NP, OUTF32, NW>
         np_ = _NP.get(args[0], 1)
         nw = 8 if (np_ == 3 and os.environ.get("VFM_GEMM128_WAVES", "8") != "4") else 4

@@ -242,14 +242,20 @@ class FlatGradSync:
                 p.grad = None
 
 
-def fast_adam_step(phase):
+HIP_ADAM = os.environ.get("VFM_ADAM", "hip") == "hip"      # VFM_ADAM=torch: torch's fused Adam + foreach lerp (A/B)
+
+
+def fast_adam_step(phase, ema=None):
     """torch.optim.Adam(fused=True).step() without its per-step Python bookkeeping: after one regular
     step has created the state, the tensor lists of the parameters that have gradients are cached per
-    parameter set and handed to the same two calls torch's fused path makes (`_foreach_add_` on the
-    step counters, `_fused_adam_`): identical arithmetic. Falls back (returns False) for anything but
-    a single fp32 CUDA group of plain fused Adam with float hyper-parameters. The regular step loops
-    over every parameter checking grads, state and dtypes: ~2-4 ms of host time per phase with the GPU
-    idle (r4k gap profile)."""
+    parameter set. On ROCm the step is one launch of csrc/adam.hip over device tables built once per set
+    (torch_utils/ops/adam_hip.py: torch's fused arithmetic), which also applies the G_ema lerp to the
+    parameters `ema` = (pairs, weight) maps (pairs: {id(p): p_ema}); elsewhere (or VFM_ADAM=torch) the same
+    two calls torch's fused path makes (`_foreach_add_` on the step counters, `_fused_adam_`). Returns False
+    (nothing done: the caller runs opt.step()) for anything but a single fp32 group of plain fused Adam with
+    float hyper-parameters, or on the first step of a parameter set (the regular path creates state); else
+    the set of ids of the parameters whose EMA it applied. The regular step loops over every parameter
+    checking grads, state and dtypes: ~2-4 ms of host time per phase with the GPU idle (r4k gap profile)."""
     opt = phase.opt
     if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1:
         return False
@@ -263,14 +269,16 @@ def fast_adam_step(phase):
     if plist is None:
         plist = phase.adam_params = list(g['params'])
     now = [p.grad for p in plist]                       # the one Python pass over the parameters
+    pairs = ema[0] if ema is not None else None
     cache = phase.__dict__.get('adam_cache')
-    if cache is not None and all(map(operator.is_, now, cache[0])):
-        _, params, grads, m1, m2, steps = cache         # same grad tensors as last time (flat-buffer views)
+    st = opt.state
+    if (cache is not None and cache[6] is pairs and all(map(operator.is_, now, cache[0]))
+            and st[cache[1][0]]['exp_avg'] is cache[3][0] and st[cache[1][-1]]['exp_avg_sq'] is cache[4][-1]):
+        _, params, grads, m1, m2, steps, _, plan = cache  # same grad tensors as last time (flat-buffer views)
     else:
         with_grad = [p for p, gr in zip(plist, now) if gr is not None]
         if not with_grad:
-            return True
-        st = opt.state
+            return set()
         dev = with_grad[0].device
         if any(p not in st or p.dtype != torch.float32 or p.device != dev or p.grad.dtype != torch.float32
                for p in with_grad):
@@ -279,14 +287,27 @@ def fast_adam_step(phase):
         params, grads = with_grad, [p.grad for p in with_grad]
         m1, m2 = [st[p]['exp_avg'] for p in with_grad], [st[p]['exp_avg_sq'] for p in with_grad]
         steps = [st[p]['step'] for p in with_grad]
-        phase.adam_cache = (now, params, grads, m1, m2, steps)
+        plan = None
+        if HIP_ADAM and dev.type == 'cuda':
+            counts = torch.stack([s.reshape(()) for s in steps]).cpu()
+            if bool((counts == counts[0]).all()):
+                from torch_utils.ops import adam_hip
+                emas = [pairs.get(id(p)) if pairs is not None else None for p in with_grad]
+                plan = [adam_hip.AdamEmaPlan(params, grads, m1, m2, emas), float(counts[0]),
+                        {id(p) for p, e in zip(with_grad, emas) if e is not None}]
+        phase.adam_cache = (now, params, grads, m1, m2, steps, pairs, plan)
     beta1, beta2 = g['betas']
     with torch.no_grad():
         torch._foreach_add_(steps, 1)
+        if plan is not None:
+            plan[1] += 1.0
+            plan[0].step(g['lr'], beta1, beta2, g['weight_decay'], g['eps'], plan[1],
+                         ema[1] if ema is not None else 0.0)
+            return plan[2]
         torch._fused_adam_(params, grads, m1, m2, [], steps, amsgrad=False, lr=g['lr'], beta1=beta1, beta2=beta2,
                            weight_decay=g['weight_decay'], eps=g['eps'], maximize=False, grad_scale=None,
                            found_inf=None)
-    return True
+    return set()
 
 
 class TrainingIteration:
@@ -333,7 +354,10 @@ class TrainingIteration:
                 p.requires_grad_(f)
         phase.active_flags = flags
 
-    def run_phase(self, phase, real_imgs, real_cs, cur_nimg):
+    def run_phase(self, phase, real_imgs, real_cs, cur_nimg, ema=None):
+        """One phase (reference :708-732); `ema` = (pairs, weight) hands the G_ema update of the phase's
+        parameters to the fused optimizer step (fast_adam_step). Returns the ids of the parameters whose EMA
+        was applied."""
         self._apply_freeze(phase)
         phase.sync.prepare()
         enc = getattr(self.G, 'vfm_encoder', None)
@@ -354,16 +378,36 @@ class TrainingIteration:
                 p.requires_grad_(False)
         if phase.sync.params or any(p.grad is not None for p, _ in flags):
             phase.sync.finish(gain=self.n_batch_acc)
-        if not fast_adam_step(phase):
+        done = fast_adam_step(phase, ema)
+        if done is False:
             phase.opt.step()
+            done = set()
         phase.opt.zero_grad(set_to_none=True)
+        return done
 
-    @torch.no_grad()
-    def update_ema(self, cur_nimg):
+    def _phase_ema(self, phase, cur_nimg):
+        """(pairs, lerp weight) for the G phase's fused optimizer step, None otherwise: the EMA of G's stepped
+        parameters then rides on that step (the D phase does not change G, so after the G phase's update the
+        parameters are the values the reference's end-of-iteration lerp reads)."""
+        if phase.name != 'G' or not HIP_ADAM:
+            return None
+        return self._ema_pair_map(), 1.0 - self._ema_beta(cur_nimg)
+
+    def _ema_beta(self, cur_nimg):
         ema_nimg = self.ema_kimg * 1000
         if self.ema_rampup is not None:
             ema_nimg = min(ema_nimg, cur_nimg * self.ema_rampup)
-        beta = 0.5 ** (self.batch_size / max(ema_nimg, 1e-8))
+        return 0.5 ** (self.batch_size / max(ema_nimg, 1e-8))
+
+    def _ema_pair_map(self):
+        """{id(p): p_ema} of the current EMA pair list (the same dict object while the list is unchanged)."""
+        pairs = self._current_ema_pairs()
+        if self.__dict__.get('_ema_map_src') is not pairs:
+            self._ema_map = {id(p): pe for pe, p in zip(pairs[1], pairs[2])}
+            self._ema_map_src = pairs
+        return self._ema_map
+
+    def _current_ema_pairs(self):
         # frozen tensors equal in G and G_ema are left out of the lerp; the pair list is rebuilt when the
         # trainable set changes or any left-out tensor was written since (a checkpoint loaded into one
         # side bumps its version counter), so a frozen tensor that comes to differ is averaged again
@@ -382,7 +426,17 @@ class TrainingIteration:
                 else:
                     same.append((pe, p, pe._version, p._version))
             pairs = self._ema_pairs = (tuple(names), dst, src, same)
-        _, dst, src, _ = pairs
+        return pairs
+
+    @torch.no_grad()
+    def update_ema(self, cur_nimg, done=()):
+        """G_ema <- lerp toward G (reference :734-742) for the pairs not in `done` (ids of G parameters whose
+        EMA the fused G-phase optimizer step already applied), then the changed buffers."""
+        beta = self._ema_beta(cur_nimg)
+        _, dst, src, _ = self._current_ema_pairs()
+        if done:
+            keep = [(d, s_) for d, s_ in zip(dst, src) if id(s_) not in done]
+            dst, src = [d for d, _ in keep], [s_ for _, s_ in keep]
         if dst:
             # p_ema <- p.lerp(p_ema, beta) == p_ema + (1 - beta) * (p - p_ema)
             torch._foreach_lerp_(dst, src, 1.0 - beta)
@@ -407,9 +461,10 @@ class TrainingIteration:
 
     def __call__(self, phase_real_img, phase_real_c, cur_nimg):
         if self.trace is None:
+            done = set()
             for phase in self.phases:
-                self.run_phase(phase, phase_real_img, phase_real_c, cur_nimg)
-            self.update_ema(cur_nimg)
+                done |= self.run_phase(phase, phase_real_img, phase_real_c, cur_nimg, ema=self._phase_ema(phase, cur_nimg))
+            self.update_ema(cur_nimg, done)
             return
         import time
         for phase in self.phases:
