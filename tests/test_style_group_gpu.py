@@ -32,8 +32,7 @@ class _Net(torch.nn.Module):
             if O:
                 outs += list(decoder_ops.style_and_demod(aff, w, w1.reshape(O, C)))
             else:
-                r = style_group.lookup(aff, w)
-                outs.append(r[0] if r is not None else aff(w))
+                outs.append(decoder_ops.style_and_demod(aff, w, None)[0])
         return outs
 
 
@@ -70,18 +69,16 @@ def test_style_group_matches_per_layer_and_torch():
     assert ctx.record is not None and len(ctx.record) == len(LAYERS)
     grp_out, grp_grads, ctx = _run(net, ws, True, dys)                 # grouped launches
     assert ctx.record is None and not ctx.results, "every layer took its grouped outputs"
-    # ConvNeXt layers: the same kernels' arithmetic, bit-identical; the ToRGB style (per-layer path: the torch
-    # StyleSplit over the exact-fp32 GEMM) and the gradients it feeds: one fp32 summation order apart
-    k = 0
-    for C, O, j in LAYERS:
-        if O:
-            assert torch.equal(grp_out[k], ref_out[k]) and torch.equal(grp_out[k + 1], ref_out[k + 1])
-            k += 2
-        else:
-            assert _rel(grp_out[k], ref_out[k]) <= 2e-6
-            k += 1
-    for a, b in zip(grp_grads, ref_grads):
-        assert (a is None and b is None) or _rel(a, b) <= 2e-6
+    # the same kernels' per-layer arithmetic: bit-identical outputs and gradients
+    for a, b in zip(grp_out, ref_out):
+        assert torch.equal(a, b)
+    names = ["ws"] + [n for n, _ in net.named_parameters()]
+    bad = [(n, _rel(a, b)) for n, a, b in zip(names, grp_grads, ref_grads)
+           if not ((a is None and b is None) or torch.equal(a, b))]
+    if bad:
+        cols = [(j, _rel(grp_grads[0][:, j], ref_grads[0][:, j])) for j in range(NW)]
+        print("differing gradients:", bad, "ws columns:", cols, flush=True)
+    assert not bad, bad
     # the torch formulation in fp64
     ws64 = ws.double().requires_grad_(True)
     outs = []

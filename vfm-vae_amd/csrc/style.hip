@@ -490,7 +490,7 @@ extern "C" int vfm_style_demod_bwd(const float* w, long long ldw, const float* A
     a.w = w; a.ldw = ldw; a.A = A; a.W1 = W1; a.wg = wg; a.bg = bg;
     a.B = B; a.C = C; a.WD = WD; a.O = O; a.m = const_cast<float*>(m); a.s = const_cast<float*>(s);
     a.d = const_cast<float*>(d); a.dsin = ds_in; a.dd = dd; a.ds = ws; a.part = ws + (long long)B * C;
-    a.dW1 = dW1; a.dA = dA; a.dab = dab; a.dw = dw;
+    a.dW1 = dW1; a.dA = dA; a.dab = dab; a.dw = dw; a.lddw = WD;
     hipStream_t st = (hipStream_t)stream;
     if (demod) {
         a.ks = ks_ds(O);
@@ -586,6 +586,7 @@ extern "C" long long vfm_style_group_pack(int launch, int n, const long long* pt
                 a.blocks0 = cdiv_i(C, 64) * a.ks;
                 blocks = a.blocks0 + (a.dW1 ? (long long)cdiv_i(O, OT_R) * cdiv_i(C, OT_C) : 0);
             } else if (launch == 4 && demod) {
+                a.ks = ks_ds(O);                 // the partials launch 2 wrote
                 a.blocks0 = 0;
                 blocks = cdiv_i((long long)B * C, THREADS);
             } else if (launch == 3 && any_out && (a.dA || a.dab || a.dw)) {

@@ -148,9 +148,9 @@ class ConvNeXtToRGBLayer(nn.Module):
 
     def forward(self, x, w):
         B, C, H, W = x.shape
-        from torch_utils.ops import style_group
-        r = style_group.lookup(self.affine, w)                                 # grouped launch (style_group.py)
-        style = (r[0] if r is not None else self.affine(w)) * self.weight_gain  # [B, C]
+        # the network's grouped launch, else the same style kernel for this layer alone (csrc/style.hip), so
+        # the grouped and per-layer results are bit-identical (a captured HIP graph replays the per-layer form)
+        style = decoder_ops.style_and_demod(self.affine, w, None)[0] * self.weight_gain    # [B, C]
         if self.kernel_size == 1:
             return decoder_ops.torgb(x, self.weight.reshape(self.out_channels, C), style, self.bias)
         else:

@@ -564,6 +564,7 @@ _SG_KT = (4.0, 2.1, 2.1, 1.0)
 _SG_FIXED, _SG_KT_US, _SG_SLOTS = 3.0, 1.14, 512
 
 
+@__import__('functools').lru_cache(maxsize=4096)
 def _sg_plan(M, N, K, zt, vt):
     """(tile code, K splits) of an exact-fp32 product with zt independent output planes and vt virtual K-tiles
     (32 deep) per output: the candidate with the least modelled time -- whole rounds of workgroups over the

@@ -265,17 +265,18 @@ def fast_adam_step(phase, ema=None):
             isinstance(g['lr'], torch.Tensor) or \
             any(isinstance(b, torch.Tensor) for b in g['betas']):
         return False
-    plist = phase.__dict__.get('adam_params')
+    plist = getattr(phase, 'adam_params', None)     # (phases are EasyDicts: attributes are items)
     if plist is None:
         plist = phase.adam_params = list(g['params'])
     now = [p.grad for p in plist]                       # the one Python pass over the parameters
     pairs = ema[0] if ema is not None else None
-    cache = phase.__dict__.get('adam_cache')
+    cache = getattr(phase, 'adam_cache', None)
     st = opt.state
     if (cache is not None and cache[6] is pairs and all(map(operator.is_, now, cache[0]))
             and st[cache[1][0]]['exp_avg'] is cache[3][0] and st[cache[1][-1]]['exp_avg_sq'] is cache[4][-1]):
         _, params, grads, m1, m2, steps, _, plan = cache  # same grad tensors as last time (flat-buffer views)
     else:
+        phase.adam_rebuilds = getattr(phase, 'adam_rebuilds', 0) + 1       # (tools_dev/adam_cache_debug.py)
         with_grad = [p for p, gr in zip(plist, now) if gr is not None]
         if not with_grad:
             return set()
