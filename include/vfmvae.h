@@ -186,6 +186,15 @@ int vfm_specnorm_fwd(const float* W, float* u, float* v, float* u_copy, float* v
                      float* ws, int O, int I, float eps, void* stream);
 int vfm_specnorm_bwd(const float* g, const float* W, const float* u, const float* v, const float* sigma, float* dW,
                      float* ws, int O, int I, void* stream);
+/* Grouped spectral norm: every weight of the discriminator heads in one launch per phase (forward phases 0-2,
+ * backward 3-4; torch_utils/ops/specnorm_group.py). vfm_specnorm_group_pack writes phase `phase`'s table for n
+ * weights into host memory (vfm_specnorm_group_bytes(n) bytes; per weight 10 pointer slots W, u, v, u_copy, v_copy,
+ * sigma, Wsn, ws, g, dW, dims O, I and eps) and returns its total blocks; the caller uploads the bytes and
+ * vfm_specnorm_group_launch runs them. Same arithmetic per weight as vfm_specnorm_fwd / _bwd. */
+long long vfm_specnorm_group_bytes(int n);
+long long vfm_specnorm_group_pack(int phase, int n, const long long* ptrs, const int* dims, const float* eps,
+                                  void* host_out);
+int vfm_specnorm_group_launch(int phase, const void* dev_packed, int n, long long total_blocks, void* stream);
 
 /* im2col of a 1-D conv with zero / circular padding and its adjoint, fp32 (the D heads' k = 9
  * SpectralConv1d, padding_mode='circular', reference networks/discriminator.py make_block):

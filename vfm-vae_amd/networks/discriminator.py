@@ -389,7 +389,9 @@ class ProjectedDiscriminator(nn.Module):
             x = F.interpolate(x, res, mode=self.interpolation, align_corners=False, antialias=True)
         x = (x - self._norm_mean) / self._norm_std
         feats = self.dino(x)
-        logits = [head(feats[k], c_enc).view(x.size(0), -1) for k, head in self.heads.items()]
+        from torch_utils.ops import specnorm_group
+        with specnorm_group.SpecNormGroup(self.heads):   # every head weight's spectral norm in one launch per phase
+            logits = [head(feats[k], c_enc).view(x.size(0), -1) for k, head in self.heads.items()]
         return torch.cat(logits, dim=1)
 
     def patchgan_forward(self, x):

@@ -161,6 +161,9 @@ SIGNATURES = {
     "vfm_timer_null_launch": [c_vp],
     "vfm_adam_chunk_elems": [],
     "vfm_style_group_bytes": [c_int],
+    "vfm_specnorm_group_bytes": [c_int],
+    "vfm_specnorm_group_pack": [c_int, c_int, c_vp, c_vp, c_vp, c_vp],
+    "vfm_specnorm_group_launch": [c_int, c_vp, c_int, c_ll, c_vp],
     "vfm_style_group_pack": [c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     "vfm_style_group_launch": [c_int, c_vp, c_int, c_ll, c_vp],
     "vfm_adam_ema_step": [c_vp, c_int, c_vp, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
@@ -257,6 +260,8 @@ def get_native():
             lib.vfm_gemm9_workspace_floats.restype = c_ll
             lib.vfm_sgemm_workspace_floats.restype = c_ll
             lib.vfm_style_group_bytes.restype = c_ll
+            lib.vfm_specnorm_group_bytes.restype = c_ll
+            lib.vfm_specnorm_group_pack.restype = c_ll
             lib.vfm_style_group_pack.restype = c_ll
             lib.vfm_channel_rms_norm_rows.restype = c_ll
             lib.vfm_specnorm_workspace_floats.restype = c_ll

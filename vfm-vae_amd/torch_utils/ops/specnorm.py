@@ -17,10 +17,14 @@ class FusedSpectralNormHook:
         w = getattr(module, self.name + "_orig")
         if (module.training and w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()
                 and self.fn.n_power_iterations == 1 and self.fn.dim == 0):
-            u = getattr(module, self.name + "_u")
-            v = getattr(module, self.name + "_v")
-            from . import patchgan_hip
-            setattr(module, self.name, patchgan_hip.spectral_norm_weight(w, u, v, self.fn.eps))
+            from . import specnorm_group
+            r = specnorm_group.lookup(module, self.fn)      # the heads' grouped launch (specnorm_group.py)
+            if r is None:
+                from . import patchgan_hip
+                u = getattr(module, self.name + "_u")
+                v = getattr(module, self.name + "_v")
+                r = patchgan_hip.spectral_norm_weight(w, u, v, self.fn.eps)
+            setattr(module, self.name, r)
             return None
         return self.fn(module, inputs)
 
