@@ -635,6 +635,11 @@ int vfm_dwconv2d_fwd_mfma(const void* x, const float* w, const float* bias, cons
  * (dx = dwconv(dy, rot180(w)), pad' = K - 1 - pad) without a flipped copy of the weights. */
 int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* bias, const float* noise, void* y, int dtype,
                         int B, int C, int H, int W, int K, int pad, int flip, void* stream);
+/* vfm_dwconv2d_fwd_ex + res (a tensor of y's shape and dtype, or null) added to y in the store: the ConvNeXt
+ * layer's residual-branch gradient summed into the data gradient of the fp32 planes' dwconv (reference
+ * networks/utils/convnext_utils.py:117-142, x feeding both the dwconv and the residual). */
+int vfm_dwconv2d_fwd_res(const void* x, const float* w, const float* bias, const float* noise, const void* res,
+                         void* y, int dtype, int B, int C, int H, int W, int K, int pad, int flip, void* stream);
 int vfm_dwconv2d_fwd_mfma_ex(const void* x, const float* w, const float* bias, const float* noise, const void* res,
                              void* y, int B, int C, int H, int W, int K, int pad, int flip, void* stream);
 /* vfm_dwconv2d_fwd_mfma_ex that also writes, when npart is given (with nplane fp32 [H, W], 16-B aligned),

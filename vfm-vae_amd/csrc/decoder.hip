@@ -32,6 +32,7 @@ struct DwArgs {
     const float* w;       // [C, K, K] fp32
     const float* bias;    // [C] or null
     const float* noise;   // [Ho, Wo] or null
+    const void* res;      // [B, C, Ho, Wo] in y's dtype, added to y, or null
     void* y;
     int B, C, H, W, Ho, Wo, pad;
     int flip;             // taps read rotated by 180 degrees (the data gradient)
@@ -121,12 +122,14 @@ __global__ __launch_bounds__(NT) void dw_fwd(DwArgs a) {
         }
     }
     T* yp = reinterpret_cast<T*>(a.y) + (long long)plane * a.Ho * a.Wo + ox;
+    const T* rp = a.res ? reinterpret_cast<const T*>(a.res) + (long long)plane * a.Ho * a.Wo + ox : nullptr;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
         const int oy = oy0 + r0 + i;
         if (oy < a.Ho) {
             float v = acc[i];
             if (a.noise) v += a.noise[oy * a.Wo + ox];
+            if (rp) v += ld(rp + (long long)oy * a.Wo);
             st(yp + (long long)oy * a.Wo, v);
         }
     }
@@ -277,6 +280,7 @@ struct DwRowArgs {
     const float* w;       // [C, K, K]
     const float* bias;    // [C] or null
     const float* noise;   // [H, W] or null
+    const void* res;      // [B, C, H, W] in y's dtype, added to y, or null
     void* y;
     const void* dy;       // weight-gradient mode
     float* partial;       // [wpc, C, K*K+1]
@@ -381,6 +385,7 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
     const float bias = a.bias ? a.bias[c] : 0.f;
     const T* xp = reinterpret_cast<const T*>(a.x) + ln.poff;
     T* yp = reinterpret_cast<T*>(a.y) + ln.poff;
+    const T* rp = a.res ? reinterpret_cast<const T*>(a.res) + ln.poff : nullptr;
     const float* np = a.noise ? a.noise + 4 * q : nullptr;
 
     f2 acc2[K][2];
@@ -429,6 +434,12 @@ __global__ __launch_bounds__(NT) void dwr_fwd(DwRowArgs a) {
                     if (np) {
 #pragma unroll
                         for (int c4 = 0; c4 < 4; ++c4) o[c4] += np[oy * a.W + c4];
+                    }
+                    if (rp) {
+                        float rv[4];
+                        ld4(rp + (long long)oy * a.W, rv);
+#pragma unroll
+                        for (int c4 = 0; c4 < 4; ++c4) o[c4] += rv[c4];
                     }
                     st4(yp + (long long)oy * a.W, o);
                 }
@@ -1707,17 +1718,18 @@ extern "C" int vfm_dwconv2d_wgrad_reduce(const float* partial, float* dw, float*
     return launch_status();
 }
 
-extern "C" int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* bias, const float* noise, void* y,
-                                   int dtype, int B, int C, int H, int W, int K, int pad, int flip, void* stream) {
+extern "C" int vfm_dwconv2d_fwd_res(const void* x, const float* w, const float* bias, const float* noise,
+                                    const void* res, void* y, int dtype, int B, int C, int H, int W, int K, int pad,
+                                    int flip, void* stream) {
     if (!x || !w || !y || B <= 0 || C <= 0 || H <= 0 || W <= 0 || pad < 0) return VFM_ERR_ARGS;
     DwArgs a{};
-    a.x = x; a.w = w; a.bias = bias; a.noise = noise; a.y = y;
+    a.x = x; a.w = w; a.bias = bias; a.noise = noise; a.res = res; a.y = y;
     a.B = B; a.C = C; a.H = H; a.W = W; a.pad = pad; a.flip = flip != 0;
     a.Ho = H + 2 * pad - K + 1; a.Wo = W + 2 * pad - K + 1;
     if (a.Ho <= 0 || a.Wo <= 0) return VFM_ERR_ARGS;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     DwRowArgs r{};
-    r.x = x; r.w = w; r.bias = bias; r.noise = noise; r.y = y; r.B = B; r.C = C; r.H = H; r.W = W;
+    r.x = x; r.w = w; r.bias = bias; r.noise = noise; r.res = res; r.y = y; r.B = B; r.C = C; r.H = H; r.W = W;
     r.flip = flip != 0;
     if (dwr_plan(r, K, pad)) {
         switch (dtype) {
@@ -1734,6 +1746,11 @@ extern "C" int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* b
     case VFM_BF16: return dw_dispatch<__hip_bfloat16>(a, K, 0, nullptr, nullptr, st);
     }
     return VFM_ERR_ARGS;
+}
+
+extern "C" int vfm_dwconv2d_fwd_ex(const void* x, const float* w, const float* bias, const float* noise, void* y,
+                                   int dtype, int B, int C, int H, int W, int K, int pad, int flip, void* stream) {
+    return vfm_dwconv2d_fwd_res(x, w, bias, noise, nullptr, y, dtype, B, C, H, W, K, pad, flip, stream);
 }
 
 extern "C" int vfm_dwconv2d_fwd(const void* x, const float* w, const float* bias, const float* noise, void* y,

@@ -162,6 +162,8 @@ SIGNATURES = {
     "vfm_adam_chunk_elems": [],
     "vfm_style_group_bytes": [c_int],
     "vfm_specnorm_group_bytes": [c_int],
+    "vfm_dwconv2d_fwd_res": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                             c_int, c_vp],
     "vfm_specnorm_group_pack": [c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     "vfm_specnorm_group_launch": [c_int, c_vp, c_int, c_ll, c_vp],
     "vfm_style_group_pack": [c_int, c_int, c_vp, c_vp, c_vp, c_vp],

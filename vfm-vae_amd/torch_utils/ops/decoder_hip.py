@@ -386,10 +386,10 @@ def _dw_fwd(x, w3, bias, noise, pad, name, res=None, flip=False, nplane=None, gs
             if nplane is None:
                 return y
             return y, (part.sum() if part is not None else _plane_dot(x, nplane))
-    with kernel_timer.region(_rn(name, x, K), _nb(x, y)):
-        _check(_lib.vfm_dwconv2d_fwd_ex(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), y.data_ptr(), _code(x),
-                                        B, C, H, W, K, pad, int(flip), _stream()), name)
-    y = y if res is None else y.add_(res.to(y.dtype))
+    r = None if res is None else _c(res.to(y.dtype))       # added in the kernel's store (no torch add)
+    with kernel_timer.region(_rn(name, x, K), _nb(x, y, r)):
+        _check(_lib.vfm_dwconv2d_fwd_res(x.data_ptr(), w3.data_ptr(), _p(bias), _p(noise), _p(r), y.data_ptr(),
+                                         _code(x), B, C, H, W, K, pad, int(flip), _stream()), name)
     return y if nplane is None else (y, _plane_dot(x, nplane))
 
 
