@@ -624,14 +624,20 @@ def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=
         return None
     sA = a3.stride(0) if a3.shape[0] > 1 else 0
     sB = b3.stride(0) if b3.shape[0] > 1 else 0
-    # a layout whose contiguous extent and leading dim are in 16-B units first (the kernel's 16-B loads), else
-    # any (bounds-checked scalar loads: the equivariance decodes' 3 x 3 / 6 x 6 planes)
-    vec = lambda kc, ld, n_out: ld % 4 == 0 and (K if kc else n_out) % 4 == 0
-    la = sorted(_sg_layouts(a3, 1, 2), key=lambda c: not vec(c[0], c[1], M))
-    lb = sorted(_sg_layouts(b3, 2, 1), key=lambda c: not vec(c[0], c[1], N))
-    if not la or not lb:
+    lk = (a3.shape, a3.stride(), b3.shape, b3.stride())
+    lay = _SG_LAYOUT_CACHE.get(lk)
+    if lay is None:
+        # a layout whose contiguous extent and leading dim are in 16-B units first (the kernel's 16-B loads),
+        # else any (bounds-checked scalar loads: the equivariance decodes' 3 x 3 / 6 x 6 planes)
+        vec = lambda kc, ld, n_out: ld % 4 == 0 and (K if kc else n_out) % 4 == 0
+        la = sorted(_sg_layouts(a3, 1, 2), key=lambda c: not vec(c[0], c[1], M))
+        lb = sorted(_sg_layouts(b3, 2, 1), key=lambda c: not vec(c[0], c[1], N))
+        lay = (la[0], lb[0]) if la and lb else ()
+        if len(_SG_LAYOUT_CACHE) < 4096:
+            _SG_LAYOUT_CACHE[lk] = lay
+    if not lay:
         return None
-    (a_kc, lda), (b_kc, ldb) = la[0], lb[0]
+    (a_kc, lda), (b_kc, ldb) = lay
     zc = 1 if reduce_batch else z
     if out is None:
         if beta != 0.0:
@@ -662,8 +668,7 @@ def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=
     if splits > 1 or reduce_batch:
         n = _lib.vfm_sgemm_workspace_floats(M, N, z, splits, int(reduce_batch))
         ws = _workspace(max(n, 1), a3.device)
-    tb = lambda v: "true" if v else "false"
-    region = f"sgemm<{tb(a_kc)},{tb(b_kc)},{bm},{bn},{1 + (tile >> 2)}>"
+    region = _sg_region(a_kc, b_kc, bm, bn, 1 + (tile >> 2))
     if kernel_timer.SHAPES:
         region += f"[{M}x{N}x{K}x{z}{'r' if reduce_batch else ''}{'s%d' % splits if splits > 1 else ''}]"
     with kernel_timer.region(region, gemm_bytes(a3, b3, M, N, K, z, torch.float32, reduce_batch),
@@ -683,6 +688,13 @@ def sgemm(a3, b3, out=None, bias=None, bias_dim=None, act=None, alpha=1.0, beta=
 
 
 _SG_CHECK = __import__("os").environ.get("VFM_SGEMM_CHECK") == "1"
+_SG_LAYOUT_CACHE = {}       # (shapes, strides) -> chosen (k-contiguous, leading dim) of A and B
+
+
+@__import__('functools').lru_cache(maxsize=64)
+def _sg_region(a_kc, b_kc, bm, bn, kw):
+    tb = lambda v: "true" if v else "false"
+    return f"sgemm<{tb(a_kc)},{tb(b_kc)},{bm},{bn},{kw}>"
 
 
 def _check_sg(a3, b3, out, bias, bias_dim, act, alpha, beta, reduce_batch, info):

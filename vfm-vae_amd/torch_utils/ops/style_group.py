@@ -159,6 +159,12 @@ def _launch(sections, n, ptrs, dims, gains, dev):
     return packed, host
 
 
+def _ws_slice(wbuf, n):
+    t = wbuf[0].narrow(0, wbuf[1], max(1, n))
+    wbuf[1] += -(-max(1, n) // 4) * 4
+    return t
+
+
 class _StyleGroupFn(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, ws, plan, *params):
@@ -169,11 +175,22 @@ class _StyleGroupFn(custom_ops.FastFunction):
         f32 = dict(dtype=torch.float32, device=dev)
         ptrs = np.zeros((n, GP), dtype=np.int64)
         ms, ss, ds = [], [], []
+        # m, s, d of every layer carved from one allocation (16-B aligned slices)
+        sizes = [(B * 3 * int(C), B * int(C), B * int(O)) for _, C, _, O in dims]
+        total = sum(-(-x // 4) * 4 for t in sizes for x in t)
+        buf = torch.empty([max(1, total)], **f32)
+        off = 0
+
+        def carve(numel, shape):
+            nonlocal off
+            t = buf.narrow(0, off, numel).view(shape)
+            off += -(-numel // 4) * 4
+            return t
         for i, lay in enumerate(plan):
-            _, C, _, O = dims[i]
+            _, C, _, O = (int(v) for v in dims[i])
             fc = lay.affine.proj
-            m, s = torch.empty([B, 3 * C], **f32), torch.empty([B, C], **f32)
-            d = torch.empty([B, O], **f32) if O else None
+            m, s = carve(B * 3 * C, [B, 3 * C]), carve(B * C, [B, C])
+            d = carve(B * O, [B, O]) if O else None
             ms.append(m), ss.append(s), ds.append(d)
             ptrs[i, :7] = (ws.data_ptr() + lay.j * ws.stride(1) * 4, fc.weight.data_ptr(), fc.bias.data_ptr(),
                            lay.w1.data_ptr() if O else 0, m.data_ptr(), s.data_ptr(), d.data_ptr() if O else 0)
@@ -209,6 +226,10 @@ class _StyleGroupFn(custom_ops.FastFunction):
         ptrs = np.zeros((n, GP), dtype=np.int64)
         pgrads = []
         keep = []
+        # every layer's workspace carved from one allocation
+        wtot = sum(-(-max(1, int(lib.vfm_style_demod_bwd_workspace_floats(int(B), int(C), int(WD), int(O)))) // 4) * 4
+                   for _, C, _, O in dims)
+        wbuf = [torch.empty([max(1, wtot)], **f32), 0]
         k, pi = 0, 2
         nbytes = 0
         for i, lay in enumerate(plan):
@@ -230,7 +251,7 @@ class _StyleGroupFn(custom_ops.FastFunction):
             wsz = int(lib.vfm_style_demod_bwd_workspace_floats(int(B), int(C), int(WD), int(O)))
             if wsz < 0:
                 raise custom_ops.NativeError("vfm_style_group: workspace exceeds 2^31 floats")
-            work = torch.empty([max(1, wsz)], **f32)
+            work = _ws_slice(wbuf, wsz)
             dW1 = torch.empty([O, C], **f32) if want_W1 else None
             dA = torch.empty([3 * C, WD], **f32) if want_A else None
             dab = torch.empty([3 * C], **f32) if want_ab else None

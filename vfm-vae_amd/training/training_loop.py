@@ -351,8 +351,13 @@ class TrainingIteration:
             flags = [(p, p.requires_grad) for p in phase.module.parameters()]
             cache[key] = flags
         else:
+            # the trainable ones were switched off at the end of the phase's last run; the frozen ones only
+            # need a call when something switched them on since (attribute reads are ~10x cheaper than the call)
             for p, f in flags:
-                p.requires_grad_(f)
+                if f:
+                    p.requires_grad_(True)
+                elif p.requires_grad:
+                    p.requires_grad_(False)
         phase.active_flags = flags
 
     def run_phase(self, phase, real_imgs, real_cs, cur_nimg, ema=None):
