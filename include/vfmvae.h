@@ -254,6 +254,12 @@ int vfm_dwconv2d_bwd_weight(const void* x, const void* dy, float* partial, int d
 int vfm_group_norm_fwd(const void* x, const float* w, const float* b, const float* s, void* y,
                        float* mean, float* rstd, int dtype_in, int dtype_out,
                        int B, int C, int G, int HW, float eps, void* stream);
+/* vfm_group_norm_fwd that also writes an fp32 y's exact bf16 pieces [3][B C HW] (16-B aligned, HW % 8 == 0) for
+ * the f32x6 GEMM it feeds: the fp32 ConvNeXt layers' GN(d) * s, pwconv1's input (reference
+ * networks/utils/convnext_utils.py:117-138). */
+int vfm_group_norm_fwd_pc(const void* x, const float* w, const float* b, const float* s, void* y, void* y_pieces,
+                          float* mean, float* rstd, int dtype_in, int dtype_out, int B, int C, int G, int HW,
+                          float eps, void* stream);
 /* vfm_group_norm_fwd (bf16 x) with each group's statistics merged, in double and a fixed order,
  * from the producer's per-wave partials stats [B C upc][4] (vfm_dwconv2d_fwd_mfma_gs; upc = units
  * per (sample, channel) plane) instead of a pass over x: x is read once. */
@@ -286,6 +292,18 @@ int vfm_layer_scale_residual_fwd(const void* y, const float* bias, const float* 
 int vfm_layer_scale_residual_bwd(const void* y, const float* bias, const float* gamma, const void* dout,
                                  void* dy, float* d_gamma_rows, float* d_sum_rows,
                                  int dtype_y, int dtype_x, int B, int C, int P, void* stream);
+/* The same three kernels writing, with an fp32 output, also its exact bf16 pieces (hi, mid, lo) as the planar
+ * [3][numel] operand of the f32x6 GEMMs (`*_pieces`, 16-B aligned; bit-identical to vfm_split_f32's planar
+ * split): the fp32 ConvNeXt layers' pwconv2 input g, pwconv1's output gradient dh and pwconv2's output gradient
+ * dy (reference networks/utils/convnext_utils.py:135-142) enter their 1x1 products without a split pass. */
+int vfm_scale_bias_gelu_fwd_pc(const void* h, const float* scale, const float* bias, void* g, void* g_pieces,
+                               int dtype, int B, int O, int P, void* stream);
+int vfm_scale_bias_gelu_bwd_pc(const void* h, const void* dg, const float* scale, const float* bias, void* dh,
+                               void* dh_pieces, float* d_scale_rows, float* d_bias_rows, int dtype, int B, int O,
+                               int P, void* stream);
+int vfm_layer_scale_residual_bwd_pc(const void* y, const float* bias, const float* gamma, const void* dout, void* dy,
+                                    void* dy_pieces, float* d_gamma_rows, float* d_sum_rows, int dtype_y,
+                                    int dtype_x, int B, int C, int P, void* stream);
 
 /* PixelShuffle(r) (r = 1: none) + replicate pad ((K-1)/2 before, K/2 after) + blur
  * with the separable normalised taps[K] (K <= 8; HOST pointer, read at launch):

@@ -17,6 +17,8 @@
 //    gather-form adjoint including the replicate-padding edge folding.
 #include "vfm_common.h"
 
+#include <type_traits>
+
 namespace {
 
 using namespace vfm;
@@ -647,6 +649,7 @@ struct GnArgs {
     // sum (x - shift)^2} per producer wave, upc per (sample, channel) plane; null: computed here
     const float* stats;
     int upc;
+    __hip_bfloat16* pc;  // fp32 y only: its exact bf16 pieces [3][B C HW] (store_pieces8), or null
 };
 
 // (count, sum, sum of squares) of a (sample, group) about the shift of its first partial, merged from the
@@ -685,6 +688,17 @@ __device__ __forceinline__ void gn_merge_stats(const GnArgs& a, int bg, float& m
 // Flat forms (8 | HW, HW / 8 a power of two, at most GN_FLAT_MAX channels per group): the
 // group is walked as one run of 8-element chunks by all threads instead of channel by channel
 // (which left most threads idle on planes under 2048 elements and cost two barriers per channel).
+// the three bf16 pieces (hi, mid, lo) of 8 consecutive fp32 outputs at element offset off of a planar
+// [3][n] piece array: bit-identical to csrc/gemm8.hip split_planar_kernel<3> over the same values
+__device__ __forceinline__ void store_pieces8(__hip_bfloat16* pc, long long n, long long off, const float (&v)[8]) {
+    uint32_t q[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pieces<3>(v[2 * j], v[2 * j + 1], q[j]);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint4*>(pc + (long long)p * n + off) = make_uint4(q[0][p], q[1][p], q[2][p], q[3][p]);
+}
+
 constexpr int GN_FLAT_MAX = 128;
 
 template <class TI, class TO>
@@ -761,6 +775,8 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sc, sh);
             store8(yp + i * 8, v);
+            if (std::is_same<TO, float>::value && a.pc)
+                store_pieces8(a.pc, (long long)a.B * a.C * a.HW, (long long)bg * n + i * 8, v);
         }
         return;
     }
@@ -782,6 +798,8 @@ __global__ __launch_bounds__(NT) void gn_fwd(GnArgs a) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sc, sh);
                 store8(yc + i * 8, v);
+                if (std::is_same<TO, float>::value && a.pc)
+                    store_pieces8(a.pc, (long long)a.B * a.C * a.HW, (long long)bg * n + (long long)cl * a.HW + i * 8, v);
             }
         } else {
             for (int i = threadIdx.x; i < a.HW; i += NT) st(yc + i, fmaf(ld(xc + i), sc, sh));
@@ -1054,7 +1072,10 @@ struct RowArgs {
     float* rsum0;         // per-row partial sums [R]
     float* rsum1;         // per-row partial sums [R]
     int R, O, P;
+    __hip_bfloat16* pc;   // fp32 out0 only: its exact bf16 pieces [3][R P] (the f32x6 GEMMs' planar operand
+                          // split, split_planar_kernel's layout and arithmetic) written with it, or null
 };
+
 
 template <class T>
 __global__ __launch_bounds__(NT) void gelu_fwd(RowArgs a) {
@@ -1073,6 +1094,8 @@ __global__ __launch_bounds__(NT) void gelu_fwd(RowArgs a) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = gelu_erf(fmaf(v[k], sc, bi));
         store8(gp + i * 8, v);
+        if (std::is_same<T, float>::value && a.pc)
+            store_pieces8(a.pc, (long long)a.R * a.P, (long long)row * a.P + i * 8, v);
     }
 }
 
@@ -1102,6 +1125,8 @@ __global__ __launch_bounds__(NT) void gelu_bwd(RowArgs a) {
             d[k] = dz * sc;
         }
         store8(dp + i * 8, d);
+        if (std::is_same<T, float>::value && a.pc)
+            store_pieces8(a.pc, (long long)a.R * a.P, (long long)row * a.P + i * 8, d);
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
@@ -1159,6 +1184,8 @@ __global__ __launch_bounds__(NT) void lsr_bwd(RowArgs a) {
             d[k] = gm * g[k];
         }
         store8(dp + i * 8, d);
+        if (std::is_same<TY, float>::value && a.pc)
+            store_pieces8(a.pc, (long long)a.R * a.P, (long long)row * a.P + i * 8, d);
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
@@ -1803,11 +1830,13 @@ static int gn_fwd_launch(GnArgs& a, hipStream_t st) {
     return launch_status();
 }
 
-extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b, const float* s, void* y,
-                                  float* mean, float* rstd, int dtype_in, int dtype_out, int B, int C, int G, int HW,
-                                  float eps, void* stream) {
+extern "C" int vfm_group_norm_fwd_pc(const void* x, const float* w, const float* b, const float* s, void* y,
+                                     void* y_pieces, float* mean, float* rstd, int dtype_in, int dtype_out, int B,
+                                     int C, int G, int HW, float eps, void* stream) {
     if (!x || !y || !mean || !rstd || B <= 0 || C <= 0 || G <= 0 || C % G || HW <= 0) return VFM_ERR_ARGS;
-    GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps, nullptr, 0};
+    // pieces only on the vectorised paths (HW % 8 == 0) of an fp32 output
+    if (y_pieces && (dtype_out != VFM_F32 || HW % 8 || (uintptr_t)y_pieces % 16)) return VFM_ERR_ARGS;
+    GnArgs a{x, w, b, s, y, mean, rstd, B, C, G, HW, eps, nullptr, 0, (__hip_bfloat16*)y_pieces};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define GN_CASE(DI, TI)                                                        \
     if (dtype_in == DI) {                                                      \
@@ -1820,6 +1849,12 @@ extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b,
     GN_CASE(VFM_F16, __half)
 #undef GN_CASE
     return VFM_ERR_ARGS;
+}
+
+extern "C" int vfm_group_norm_fwd(const void* x, const float* w, const float* b, const float* s, void* y,
+                                  float* mean, float* rstd, int dtype_in, int dtype_out, int B, int C, int G, int HW,
+                                  float eps, void* stream) {
+    return vfm_group_norm_fwd_pc(x, w, b, s, y, nullptr, mean, rstd, dtype_in, dtype_out, B, C, G, HW, eps, stream);
 }
 
 // vfm_group_norm_fwd with the statistics merged from a producer's per-wave partials (vfm_dwconv2d_fwd_mfma_gs:
@@ -1873,11 +1908,13 @@ extern "C" int vfm_group_norm_bwd(const void* x, const void* dy, const float* me
     return VFM_ERR_ARGS;
 }
 
-extern "C" int vfm_scale_bias_gelu_fwd(const void* h, const float* scale, const float* bias, void* g, int dtype,
-                                       int B, int O, int P, void* stream) {
+extern "C" int vfm_scale_bias_gelu_fwd_pc(const void* h, const float* scale, const float* bias, void* g,
+                                          void* g_pieces, int dtype, int B, int O, int P, void* stream) {
     if (!h || !g || B <= 0 || O <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    if (g_pieces && (dtype != VFM_F32 || (uintptr_t)g_pieces % 16)) return VFM_ERR_ARGS;
     RowArgs a{};
     a.in0 = h; a.out0 = g; a.rscale = scale; a.cvec0 = bias; a.R = B * O; a.O = O; a.P = P;
+    a.pc = (__hip_bfloat16*)g_pieces;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid((a.R + 3) / 4);
     switch (dtype) {
@@ -1889,11 +1926,18 @@ extern "C" int vfm_scale_bias_gelu_fwd(const void* h, const float* scale, const 
     return launch_status();
 }
 
-extern "C" int vfm_scale_bias_gelu_bwd(const void* h, const void* dg, const float* scale, const float* bias, void* dh,
-                                       float* d_scale_rows, float* d_bias_rows, int dtype, int B, int O, int P,
-                                       void* stream) {
+extern "C" int vfm_scale_bias_gelu_fwd(const void* h, const float* scale, const float* bias, void* g, int dtype,
+                                       int B, int O, int P, void* stream) {
+    return vfm_scale_bias_gelu_fwd_pc(h, scale, bias, g, nullptr, dtype, B, O, P, stream);
+}
+
+extern "C" int vfm_scale_bias_gelu_bwd_pc(const void* h, const void* dg, const float* scale, const float* bias,
+                                          void* dh, void* dh_pieces, float* d_scale_rows, float* d_bias_rows,
+                                          int dtype, int B, int O, int P, void* stream) {
     if (!h || !dg || !dh || !d_bias_rows || B <= 0 || O <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    if (dh_pieces && (dtype != VFM_F32 || (uintptr_t)dh_pieces % 16)) return VFM_ERR_ARGS;
     RowArgs a{};
+    a.pc = (__hip_bfloat16*)dh_pieces;
     a.in0 = h; a.dout = dg; a.out0 = dh; a.rscale = scale; a.cvec0 = bias; a.rsum0 = d_scale_rows;
     a.rsum1 = d_bias_rows; a.R = B * O; a.O = O; a.P = P;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1905,6 +1949,13 @@ extern "C" int vfm_scale_bias_gelu_bwd(const void* h, const void* dg, const floa
     default: return VFM_ERR_ARGS;
     }
     return launch_status();
+}
+
+extern "C" int vfm_scale_bias_gelu_bwd(const void* h, const void* dg, const float* scale, const float* bias, void* dh,
+                                       float* d_scale_rows, float* d_bias_rows, int dtype, int B, int O, int P,
+                                       void* stream) {
+    return vfm_scale_bias_gelu_bwd_pc(h, dg, scale, bias, dh, nullptr, d_scale_rows, d_bias_rows, dtype, B, O, P,
+                                      stream);
 }
 
 #define LSR_DISPATCH(KERNEL)                                                                       \
@@ -1926,11 +1977,14 @@ extern "C" int vfm_layer_scale_residual_fwd(const void* y, const float* bias, co
     return launch_status();
 }
 
-extern "C" int vfm_layer_scale_residual_bwd(const void* y, const float* bias, const float* gamma, const void* dout,
-                                            void* dy, float* d_gamma_rows, float* d_sum_rows, int dtype_y, int dtype_x,
-                                            int B, int C, int P, void* stream) {
+extern "C" int vfm_layer_scale_residual_bwd_pc(const void* y, const float* bias, const float* gamma,
+                                               const void* dout, void* dy, void* dy_pieces, float* d_gamma_rows,
+                                               float* d_sum_rows, int dtype_y, int dtype_x, int B, int C, int P,
+                                               void* stream) {
     if (!y || !dout || !dy || !d_gamma_rows || !d_sum_rows || B <= 0 || C <= 0 || P <= 0 || P % 8) return VFM_ERR_ARGS;
+    if (dy_pieces && (dtype_y != VFM_F32 || (uintptr_t)dy_pieces % 16)) return VFM_ERR_ARGS;
     RowArgs a{};
+    a.pc = (__hip_bfloat16*)dy_pieces;
     a.in0 = y; a.dout = dout; a.out0 = dy; a.cvec0 = bias; a.cvec1 = gamma; a.rsum0 = d_gamma_rows;
     a.rsum1 = d_sum_rows; a.R = B * C; a.O = C; a.P = P;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1939,6 +1993,13 @@ extern "C" int vfm_layer_scale_residual_bwd(const void* y, const float* bias, co
     return launch_status();
 }
 #undef LSR_DISPATCH
+
+extern "C" int vfm_layer_scale_residual_bwd(const void* y, const float* bias, const float* gamma, const void* dout,
+                                            void* dy, float* d_gamma_rows, float* d_sum_rows, int dtype_y, int dtype_x,
+                                            int B, int C, int P, void* stream) {
+    return vfm_layer_scale_residual_bwd_pc(y, bias, gamma, dout, dy, nullptr, d_gamma_rows, d_sum_rows, dtype_y,
+                                           dtype_x, B, C, P, stream);
+}
 
 extern "C" int vfm_shuffle_blur_fwd(const void* x, void* y, const float* taps, int K, int dtype, int B, int C, int H,
                                     int W, int r, void* stream) {

@@ -162,6 +162,12 @@ SIGNATURES = {
     "vfm_adam_chunk_elems": [],
     "vfm_style_group_bytes": [c_int],
     "vfm_specnorm_group_bytes": [c_int],
+    "vfm_group_norm_fwd_pc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_float, c_vp],
+    "vfm_scale_bias_gelu_fwd_pc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_scale_bias_gelu_bwd_pc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "vfm_layer_scale_residual_bwd_pc": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                        c_int, c_vp],
     "vfm_dwconv2d_fwd_res": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_vp],
     "vfm_specnorm_group_pack": [c_int, c_int, c_vp, c_vp, c_vp, c_vp],

@@ -553,10 +553,13 @@ class _GroupNorm(custom_ops.FastFunction):
                                                      rstd.data_ptr(), st[0].data_ptr(), st[1], _code(x), _code(y), B,
                                                      C, groups, HW, float(eps), _stream()), 'vfm_group_norm_fwd_stats')
         else:
-            with kernel_timer.region(_rn('group_norm_fwd', x), _nb(x, y)):
-                _check(_lib.vfm_group_norm_fwd(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), mean.data_ptr(),
-                                               rstd.data_ptr(), _code(x), _code(y), B, C, groups, HW, float(eps),
-                                               _stream()), 'vfm_group_norm_fwd')
+            # the ConvNeXt layer's GN(d) * s (style given) feeds pwconv1's f32x6 product: pieces written here
+            yp = _pieces_for(y, HW) if (s is not None and HW % 8 == 0) else None
+            with kernel_timer.region(_rn('group_norm_fwd', x), _nb(x, y, yp)):
+                _check(_lib.vfm_group_norm_fwd_pc(x.data_ptr(), _p(w), _p(b), _p(s), y.data_ptr(), _p(yp),
+                                                  mean.data_ptr(), rstd.data_ptr(), _code(x), _code(y), B, C, groups,
+                                                  HW, float(eps), _stream()), 'vfm_group_norm_fwd')
+            _attach_pieces(y, yp)
         ctx.save_for_backward(x, w, b, s, mean, rstd)
         ctx.groups = groups
         ctx.meta = tuple(None if t is None else t.dtype for t in (weight, bias, style))
@@ -595,6 +598,29 @@ def group_norm(x, num_groups, weight, bias, eps, out_dtype, style):
 # (reference convnext_utils.py:60-66 demodulation, :129-130 bias + GELU).
 
 
+PRODUCER_PIECES = os.environ.get("VFM_PRODUCER_PIECES", "1") == "1"
+
+
+def _pieces_for(t, P):
+    """A planar [3, numel] bf16 piece buffer for the fp32 output t of a row kernel that feeds the f32x6 GEMMs
+    (planes of >= 64 pixels: narrower products go to the exact-fp32 GEMM, which takes no pieces), or None."""
+    if not (PRODUCER_PIECES and t.dtype == torch.float32 and P >= 64 and gemm_pieces_mode() == 3) or \
+            torch.cuda.is_current_stream_capturing():
+        return None
+    return torch.empty((3, t.numel()), dtype=torch.bfloat16, device=t.device)
+
+
+def gemm_pieces_mode():
+    return custom_ops.f32_precision()[1]
+
+
+def _attach_pieces(t, pieces):
+    """Hand the producer-written pieces to gemm_hip._planar's per-tensor cache (same key it computes), so the
+    products of t skip their split pass."""
+    if pieces is not None and not torch.cuda.is_current_stream_capturing():
+        t._vfm_planar = ((t.data_ptr(), t.numel(), t._version, custom_ops.f32_precision()[0]), pieces)
+
+
 class _ScaleBiasGelu(custom_ops.FastFunction):
     @staticmethod
     def forward(ctx, h, scale, bias):
@@ -604,9 +630,11 @@ class _ScaleBiasGelu(custom_ops.FastFunction):
         P = h[0, 0].numel()
         s, b = _f32(scale), _f32(bias)
         g = torch.empty_like(h)
-        with kernel_timer.region(_rn('scale_bias_gelu_fwd', h), _nb(h, g)):
-            _check(_lib.vfm_scale_bias_gelu_fwd(h.data_ptr(), _p(s), _p(b), g.data_ptr(), _code(h), B, O, P,
-                                                _stream()), 'vfm_scale_bias_gelu_fwd')
+        gp = _pieces_for(g, P)
+        with kernel_timer.region(_rn('scale_bias_gelu_fwd', h), _nb(h, g, gp)):
+            _check(_lib.vfm_scale_bias_gelu_fwd_pc(h.data_ptr(), _p(s), _p(b), g.data_ptr(), _p(gp), _code(h), B, O, P,
+                                                   _stream()), 'vfm_scale_bias_gelu_fwd')
+        _attach_pieces(g, gp)
         ctx.save_for_backward(h, s, b)
         ctx.meta = (None if scale is None else scale.dtype, None if bias is None else bias.dtype)
         return g
@@ -622,10 +650,12 @@ class _ScaleBiasGelu(custom_ops.FastFunction):
         want_s = s is not None and _wanted(ctx, 1)
         ds_rows = torch.empty([B * O], dtype=torch.float32, device=h.device) if want_s else None
         db_rows = torch.empty([B * O], dtype=torch.float32, device=h.device)
-        with kernel_timer.region(_rn('scale_bias_gelu_bwd', h), _nb(h, dg, dh)):
-            _check(_lib.vfm_scale_bias_gelu_bwd(h.data_ptr(), dg.data_ptr(), _p(s), _p(b), dh.data_ptr(),
-                                                _p(ds_rows), db_rows.data_ptr(), _code(h), B, O, P, _stream()),
+        dhp = _pieces_for(dh, P) if ctx.needs_input_grad[0] else None
+        with kernel_timer.region(_rn('scale_bias_gelu_bwd', h), _nb(h, dg, dh, dhp)):
+            _check(_lib.vfm_scale_bias_gelu_bwd_pc(h.data_ptr(), dg.data_ptr(), _p(s), _p(b), dh.data_ptr(), _p(dhp),
+                                                   _p(ds_rows), db_rows.data_ptr(), _code(h), B, O, P, _stream()),
                    'vfm_scale_bias_gelu_bwd')
+        _attach_pieces(dh, dhp)
         sdt, bdt = ctx.meta
         ds = ds_rows.view(B, O).to(sdt) if want_s else None
         db = db_rows.view(B, O).sum(0).to(bdt) if (b is not None and _wanted(ctx, 2)) else None
@@ -669,10 +699,12 @@ class _LayerScaleResidual(custom_ops.FastFunction):
         dy = torch.empty_like(y)
         r0 = torch.empty([B * C], dtype=torch.float32, device=y.device)
         r1 = torch.empty_like(r0)
-        with kernel_timer.region(_rn('layer_scale_residual_bwd', y), _nb(y, dout, dy)):
-            _check(_lib.vfm_layer_scale_residual_bwd(y.data_ptr(), _p(b), _p(g), dout.data_ptr(), dy.data_ptr(),
-                                                     r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout), B, C, P,
-                                                     _stream()), 'vfm_layer_scale_residual_bwd')
+        dyp = _pieces_for(dy, P) if ctx.needs_input_grad[0] else None
+        with kernel_timer.region(_rn('layer_scale_residual_bwd', y), _nb(y, dout, dy, dyp)):
+            _check(_lib.vfm_layer_scale_residual_bwd_pc(y.data_ptr(), _p(b), _p(g), dout.data_ptr(), dy.data_ptr(),
+                                                        _p(dyp), r0.data_ptr(), r1.data_ptr(), _code(y), _code(dout),
+                                                        B, C, P, _stream()), 'vfm_layer_scale_residual_bwd')
+        _attach_pieces(dy, dyp)
         db, dg = _colsum2(r1, r0, g, b is not None and _wanted(ctx, 1), g is not None and _wanted(ctx, 2), B, C)
         db = None if db is None else db.to(bdt)
         dg = None if dg is None else dg.to(gdt)
