@@ -129,16 +129,66 @@ def lookup(affine, w, w1=None, eps=1e-8):
     return None if ctx is None else ctx.lookup(affine, w, w1, eps)
 
 
-def _dims(plan, B, WD):
-    dims = np.zeros((len(plan), 4), dtype=np.int32)
-    gains = np.zeros((len(plan), 3), dtype=np.float32)
-    for i, lay in enumerate(plan):
-        fc = lay.affine.proj
-        C = fc.weight.shape[0] // 3
-        O = lay.w1.numel() // C if lay.w1 is not None else 0
-        dims[i] = (B, C, WD, O)
-        gains[i] = (fc.weight_gain, fc.bias_gain, lay.eps)
-    return dims, gains
+class _Layout:
+    """The call-independent part of a plan's tables at one (B, WD, NW): dims / gains, the parameters, and the
+    float offsets of every layer's m / s / d in the forward's one buffer and of its workspace and dA / dab / dW1
+    in the backward's buffers -- a call only adds its buffers' base pointers (vectorised)."""
+
+    def __init__(self, plan, B, WD, NW, ws_row_stride, lib):
+        n = len(plan)
+        self.dims = np.zeros((n, 4), dtype=np.int32)
+        self.gains = np.zeros((n, 3), dtype=np.float32)
+        C = np.array([lay.affine.proj.weight.shape[0] // 3 for lay in plan], dtype=np.int64)
+        O = np.array([(lay.w1.numel() // int(c)) if lay.w1 is not None else 0 for lay, c in zip(plan, C)],
+                     dtype=np.int64)
+        for i, lay in enumerate(plan):
+            fc = lay.affine.proj
+            self.dims[i] = (B, C[i], WD, O[i])
+            self.gains[i] = (fc.weight_gain, fc.bias_gain, lay.eps)
+        self.C, self.O, self.has_d = C, O, O > 0
+        r4 = lambda x: -(-x // 4) * 4
+        # forward buffer: per layer m [B, 3C], s [B, C], d [B, O] (16-B aligned slices)
+        sz = np.stack([B * 3 * C, B * C, B * O], 1)
+        szr = r4(sz)
+        flat = np.concatenate([[0], np.cumsum(szr.reshape(-1))])
+        self.fwd_off = flat[:-1].reshape(n, 3)
+        self.fwd_total = int(flat[-1])
+        self.split_sizes = [int(v) for v in szr.reshape(-1)]
+        self.s_shapes = [(B, int(c)) for c in C]
+        self.d_shapes = [(B, int(o)) for o in O]
+        self.ws_off = np.array([lay.j * ws_row_stride * 4 for lay in plan], dtype=np.int64)
+        self.dws_off = np.array([lay.j * WD * 4 for lay in plan], dtype=np.int64)
+        # backward buffers: workspace, and dA [3C, WD] / dab [3C] / dW1 [O, C] per layer
+        wsz = np.array([max(1, int(lib.vfm_style_demod_bwd_workspace_floats(B, int(c), WD, int(o))))
+                        for c, o in zip(C, O)], dtype=np.int64)
+        if (wsz <= 0).any():
+            raise custom_ops.NativeError("vfm_style_group: workspace exceeds 2^31 floats")
+        wflat = np.concatenate([[0], np.cumsum(r4(wsz))])
+        self.work_off, self.work_total = wflat[:-1], int(wflat[-1])
+        gsz = np.stack([3 * C * WD, 3 * C, O * C], 1)
+        gflat = np.concatenate([[0], np.cumsum(r4(gsz).reshape(-1))])
+        self.grad_off = gflat[:-1].reshape(n, 3)
+        self.grad_total = int(gflat[-1])
+        self.grad_split = [int(v) for v in r4(gsz).reshape(-1)]
+        self.fwd_bytes = int(np.sum(4 * (B * WD + 3 * C * WD + 3 * C + O * C + B * (4 * C + O))))
+        self.bwd_bytes = int(np.sum(4 * (2 * B * WD + 2 * (3 * C * WD + O * C) + B * (4 * C + 2 * O))))
+
+    def param_ptrs(self, plan):
+        ptr = np.array([(lay.affine.proj.weight.data_ptr(), lay.affine.proj.bias.data_ptr(),
+                         lay.w1.data_ptr() if lay.w1 is not None else 0) for lay in plan], dtype=np.int64)
+        return ptr
+
+
+_LAYOUTS = weakref.WeakKeyDictionary()
+
+
+def _layout(plan_owner, plan, B, WD, NW, ws_row_stride, lib):
+    d = _LAYOUTS.setdefault(plan_owner, {})
+    key = (id(plan), B, WD, NW, ws_row_stride)
+    L = d.get(key)
+    if L is None:
+        L = d[key] = _Layout(plan, B, WD, NW, ws_row_stride, lib)
+    return L
 
 
 def _launch(sections, n, ptrs, dims, gains, dev):
@@ -159,10 +209,19 @@ def _launch(sections, n, ptrs, dims, gains, dev):
     return packed, host
 
 
-def _ws_slice(wbuf, n):
-    t = wbuf[0].narrow(0, wbuf[1], max(1, n))
-    wbuf[1] += -(-max(1, n) // 4) * 4
-    return t
+class _PlanKey:
+    """Weak-referenceable owner of a plan's cached layouts (plans are lists)."""
+    __slots__ = ("__weakref__",)
+
+
+_PLAN_KEYS = {}
+
+
+def _plan_key(plan):
+    k = _PLAN_KEYS.get(id(plan))
+    if k is None or k[0] is not plan:
+        k = _PLAN_KEYS[id(plan)] = (plan, _PlanKey())
+    return k[1]
 
 
 class _StyleGroupFn(custom_ops.FastFunction):
@@ -171,70 +230,63 @@ class _StyleGroupFn(custom_ops.FastFunction):
         B, NW, WD = ws.shape
         dev = ws.device
         n = len(plan)
-        dims, gains = _dims(plan, B, WD)
-        f32 = dict(dtype=torch.float32, device=dev)
+        lib = custom_ops.get_native()
+        L = _layout(_plan_key(plan), plan, B, WD, NW, ws.stride(1), lib)
+        buf = torch.empty([max(1, L.fwd_total)], dtype=torch.float32, device=dev)
+        base = buf.data_ptr()
         ptrs = np.zeros((n, GP), dtype=np.int64)
-        ms, ss, ds = [], [], []
-        # m, s, d of every layer carved from one allocation (16-B aligned slices)
-        sizes = [(B * 3 * int(C), B * int(C), B * int(O)) for _, C, _, O in dims]
-        total = sum(-(-x // 4) * 4 for t in sizes for x in t)
-        buf = torch.empty([max(1, total)], **f32)
-        off = 0
-
-        def carve(numel, shape):
-            nonlocal off
-            t = buf.narrow(0, off, numel).view(shape)
-            off += -(-numel // 4) * 4
-            return t
-        for i, lay in enumerate(plan):
-            _, C, _, O = (int(v) for v in dims[i])
-            fc = lay.affine.proj
-            m, s = carve(B * 3 * C, [B, 3 * C]), carve(B * C, [B, C])
-            d = carve(B * O, [B, O]) if O else None
-            ms.append(m), ss.append(s), ds.append(d)
-            ptrs[i, :7] = (ws.data_ptr() + lay.j * ws.stride(1) * 4, fc.weight.data_ptr(), fc.bias.data_ptr(),
-                           lay.w1.data_ptr() if O else 0, m.data_ptr(), s.data_ptr(), d.data_ptr() if O else 0)
-            ptrs[i, 14] = ws.stride(0)
-            ptrs[i, 15] = WD
-        nbytes = sum(4 * (B * WD + 3 * C * WD + 3 * C + O * C + B * (4 * C + O)) for _, C, _, O in dims)
-        with kernel_timer.region("style_group_fwd<f32>", int(nbytes)):
-            keep = _launch((0, 1), n, ptrs, dims, gains, dev)
-        ctx.save_for_backward(ws, *[t for t in ms], *[t for t in ss], *[t for t in ds if t is not None])
-        ctx.plan, ctx.dims, ctx.gains, ctx.keep = plan, dims, gains, keep
+        ptrs[:, 0] = ws.data_ptr() + L.ws_off
+        ptrs[:, 1:4] = L.param_ptrs(plan)
+        ptrs[:, 4:7] = base + 4 * L.fwd_off
+        ptrs[~L.has_d, 6] = 0
+        ptrs[:, 14] = ws.stride(0)
+        ptrs[:, 15] = WD
+        with kernel_timer.region("style_group_fwd<f32>", L.fwd_bytes):
+            keep = _launch((0, 1), n, ptrs, L.dims, L.gains, dev)
+        pieces = buf.split(L.split_sizes)
         out = []
-        for s, d in zip(ss, ds):
-            out.append(s)
-            if d is not None:
-                out.append(d)
+        for i in range(n):
+            out.append(pieces[3 * i + 1].narrow(0, 0, B * int(L.C[i])).view(L.s_shapes[i]))
+            if L.has_d[i]:
+                out.append(pieces[3 * i + 2].narrow(0, 0, B * int(L.O[i])).view(L.d_shapes[i]))
+        ctx.save_for_backward(ws, buf)
+        ctx.plan, ctx.L, ctx.keep = plan, L, keep
         return tuple(out)
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, *grads):
-        plan, dims, gains = ctx.plan, ctx.dims, ctx.gains
-        saved = ctx.saved_tensors
+        plan, L = ctx.plan, ctx.L
+        ws, buf = ctx.saved_tensors
         n = len(plan)
-        ws, ms, ss = saved[0], saved[1:1 + n], saved[1 + n:1 + 2 * n]
-        dlist = iter(saved[1 + 2 * n:])
-        dsv = [next(dlist) if dims[i][3] else None for i in range(n)]
         B, NW, WD = ws.shape
         dev = ws.device
         f32 = dict(dtype=torch.float32, device=dev)
-        lib = custom_ops.get_native()
         want_ws = ctx.needs_input_grad[0]
         dws = torch.zeros([B, NW, WD], **f32) if want_ws else None
+        work = torch.empty([max(1, L.work_total)], **f32)
+        gbuf = torch.empty([max(1, L.grad_total)], **f32)
+        gpieces = gbuf.split(L.grad_split)
+        base, wbase, gbase = buf.data_ptr(), work.data_ptr(), gbuf.data_ptr()
         ptrs = np.zeros((n, GP), dtype=np.int64)
-        pgrads = []
-        keep = []
-        # every layer's workspace carved from one allocation
-        wtot = sum(-(-max(1, int(lib.vfm_style_demod_bwd_workspace_floats(int(B), int(C), int(WD), int(O)))) // 4) * 4
-                   for _, C, _, O in dims)
-        wbuf = [torch.empty([max(1, wtot)], **f32), 0]
+        ptrs[:, 0] = ws.data_ptr() + L.ws_off
+        ptrs[:, 1:4] = L.param_ptrs(plan)
+        ptrs[:, 4:7] = base + 4 * L.fwd_off
+        ptrs[~L.has_d, 6] = 0
+        ptrs[:, 9] = wbase + 4 * L.work_off
+        ptrs[:, 10] = gbase + 4 * L.grad_off[:, 2]
+        ptrs[:, 11] = gbase + 4 * L.grad_off[:, 0]
+        ptrs[:, 12] = gbase + 4 * L.grad_off[:, 1]
+        ptrs[~L.has_d, 10] = 0                  # no demodulated weight: no dW1
+        if want_ws:
+            ptrs[:, 13] = dws.data_ptr() + L.dws_off
+        ptrs[:, 14] = ws.stride(0)
+        ptrs[:, 15] = NW * WD
+        pgrads, keep = [], []
         k, pi = 0, 2
-        nbytes = 0
+        live = False
         for i, lay in enumerate(plan):
-            _, C, _, O = dims[i]
-            fc = lay.affine.proj
+            C, O = int(L.C[i]), int(L.O[i])
             g_s = grads[k]
             g_d = grads[k + 1] if O else None
             k += 2 if O else 1
@@ -242,29 +294,33 @@ class _StyleGroupFn(custom_ops.FastFunction):
             want_W1 = bool(O) and ctx.needs_input_grad[pi + 2]
             pi += 3 if O else 2
             if g_s is None and g_d is None:
+                ptrs[i, 0] = 0                      # left out of this call (no blocks)
                 pgrads += [None, None] + ([None] if O else [])
                 continue
+            live = True
             if O and g_d is None:
                 g_d = torch.zeros([B, O], **f32)
-            g_s = g_s.float().contiguous() if g_s is not None else (None if O else torch.zeros([B, C], **f32))
-            g_d = g_d.float().contiguous() if g_d is not None else None
-            wsz = int(lib.vfm_style_demod_bwd_workspace_floats(int(B), int(C), int(WD), int(O)))
-            if wsz < 0:
-                raise custom_ops.NativeError("vfm_style_group: workspace exceeds 2^31 floats")
-            work = _ws_slice(wbuf, wsz)
-            dW1 = torch.empty([O, C], **f32) if want_W1 else None
-            dA = torch.empty([3 * C, WD], **f32) if want_A else None
-            dab = torch.empty([3 * C], **f32) if want_ab else None
-            keep += [g_s, g_d, work]
-            ptrs[i] = (ws.data_ptr() + lay.j * ws.stride(1) * 4, fc.weight.data_ptr(), fc.bias.data_ptr(),
-                       lay.w1.data_ptr() if O else 0, ms[i].data_ptr(), ss[i].data_ptr(),
-                       dsv[i].data_ptr() if O else 0, g_s.data_ptr() if g_s is not None else 0,
-                       g_d.data_ptr() if O else 0, work.data_ptr(), dW1.data_ptr() if dW1 is not None else 0,
-                       dA.data_ptr() if dA is not None else 0, dab.data_ptr() if dab is not None else 0,
-                       dws.data_ptr() + lay.j * WD * 4 if want_ws else 0, ws.stride(0), NW * WD)
-            nbytes += 4 * (2 * B * WD + 2 * (3 * C * WD + O * C) + B * (4 * C + 2 * O))
-            pgrads += [dA, dab] + ([dW1.view(lay.w1.shape) if dW1 is not None else None] if O else [])
-        if keep:
-            with kernel_timer.region("style_group_bwd<f32>", int(nbytes)):
-                ctx.keep = _launch((2, 4, 3, 5), n, ptrs, dims, gains, dev), keep
+            if g_s is None and not O:
+                g_s = torch.zeros([B, C], **f32)
+            if g_s is not None:
+                g_s = g_s.float().contiguous()
+                keep.append(g_s)
+                ptrs[i, 7] = g_s.data_ptr()
+            if O:
+                g_d = g_d.float().contiguous()
+                keep.append(g_d)
+                ptrs[i, 8] = g_d.data_ptr()
+            if not want_W1:
+                ptrs[i, 10] = 0
+            if not want_A:
+                ptrs[i, 11] = 0
+            if not want_ab:
+                ptrs[i, 12] = 0
+            dA = gpieces[3 * i].narrow(0, 0, 3 * C * WD).view(3 * C, WD) if want_A else None
+            dab = gpieces[3 * i + 1].narrow(0, 0, 3 * C) if want_ab else None
+            dW1 = gpieces[3 * i + 2].narrow(0, 0, O * C).view(lay.w1.shape) if want_W1 else None
+            pgrads += [dA, dab] + ([dW1] if O else [])
+        if live:
+            with kernel_timer.region("style_group_bwd<f32>", L.bwd_bytes):
+                ctx.keep = _launch((2, 4, 3, 5), n, ptrs, L.dims, L.gains, dev), keep, work
         return (dws, None, *pgrads)
