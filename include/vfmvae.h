@@ -454,6 +454,13 @@ int vfm_adam_chunk_elems(void);
 int vfm_adam_ema_step(const void* tensors, int ntensors, const void* chunks, int nchunks, double lr, double beta1,
                       double beta2, double weight_decay, double eps, double bc1, double bc2_sqrt, float ema_w,
                       void* stream);
+/* The same step with the gradients read through `grads` (device array of ntensors float pointers replacing the
+ * records' g; null: the records' g) and, when clean != 0, used as nan_to_num(g * gscale) (nan 0, +inf 1e5, -inf
+ * -1e5): the gradient scaling and cleanup of FlatGradSync.finish() (reference training/training_loop.py:281-289,
+ * sync_grads' gain and nan_to_num over the flat gradient) applied as the raw per-step gradient tensors are read. */
+int vfm_adam_ema_step_raw(const void* tensors, int ntensors, const void* chunks, int nchunks, const void* grads,
+                          float gscale, int clean, double lr, double beta1, double beta2, double weight_decay,
+                          double eps, double bc1, double bc2_sqrt, float ema_w, void* stream);
 
 /* Exact-fp32 form of the vfm_gemm contract on the fp32-input MFMA (csrc/sgemm.hip, v_mfma_f32_32x32x2_f32: one
  * fmaf-chain product per multiply-add, no operand split): C[z] = epi(alpha A[z] B[z] + beta C[z]), fp32 A / B / C,

@@ -103,3 +103,69 @@ def test_fused_adam_hip_is_used():
     with Rec():
         assert fast_adam_step(phase) is not False
     assert not any("fused_adam" in n for n in Rec.names), Rec.names
+
+
+def test_direct_mode_grads_match_flat_buffer():
+    """FlatGradSync direct mode (world size 1 on a GPU: autograd's own gradient tensors, the gain and nan_to_num
+    applied inside the Adam kernel, csrc/adam.hip vfm_adam_ema_step_raw) against the flat-buffer mode (gather,
+    flat *= gain, nan_to_num over the buffer, reference training_loop.py:281-289) on twin modules: two microbatches
+    per step, gain 2, non-finite gradient entries, a parameter without a gradient on one step, the G_ema lerp;
+    bit-identical parameters, moments and EMA copies after every step."""
+    from training import training_loop as tl
+
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(33, 64), torch.nn.GELU(), torch.nn.Linear(64, 5),
+                                   torch.nn.Linear(5, 7)).to(DEV)
+
+    mods = [make(), make()]
+    phases, emas = [], []
+    for direct, m in zip((True, False), mods):
+        old = tl.DIRECT_GRADS
+        tl.DIRECT_GRADS = direct
+        try:
+            sync = tl.FlatGradSync(m, collective=False)
+            m.requires_grad_(True)
+            sync.prepare()
+        finally:
+            tl.DIRECT_GRADS = old
+        assert sync.direct == direct
+        opt = torch.optim.Adam(m.parameters(), lr=1e-2, betas=(0.5, 0.99), eps=1e-8, fused=True)
+        phases.append(dnnlib.EasyDict(opt=opt, sync=sync))
+        emas.append([p.detach().clone() for p in m.parameters()])
+    g = torch.Generator().manual_seed(3)
+    hip_steps = [0, 0]
+    # step 0 creates the state (regular opt.step), 1-4 run the native kernel (2: +-inf, 3: nan gradient entries,
+    # 4: the last layer without a gradient), 5 torch's fused Adam (the step counters differ since step 4)
+    for it in range(6):
+        xs = [torch.randn(16, 33, generator=g).to(DEV) for _ in range(2)]
+        for k, (m, phase, ema) in enumerate(zip(mods, phases, emas)):
+            phase.sync.prepare()
+            for mb, x in enumerate(xs):
+                y = m[:3](x) if it == 4 else m(x)
+                loss = (y ** 2).sum()
+                if it == 2 and mb == 1:
+                    loss = loss + m[0].bias[0] * float("inf") - m[0].bias[1] * float("inf")
+                if it == 3 and mb == 0:
+                    loss = loss + m[2].weight[0, 0] * float("nan")
+                loss.backward()
+            phase.sync.finish(gain=2)
+            pairs = {id(p): e for p, e in zip(m.parameters(), ema)}
+            done = tl.fast_adam_step(phase, (pairs, 0.25))
+            if done is False:
+                phase.opt.step()
+                done = set()
+            hip_steps[k] += bool(done)
+            rest = [(e, p) for p, e in zip(m.parameters(), ema) if id(p) not in done and p.grad is not None]
+            if rest:
+                torch._foreach_lerp_([e for e, _ in rest], [p.detach() for _, p in rest], 0.25)
+            phase.opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        for (na, pa), (_, pb), ea, eb in zip(mods[0].named_parameters(), mods[1].named_parameters(), *emas):
+            assert torch.isfinite(pa).all(), (it, na)
+            assert torch.equal(pa, pb), (it, na)
+            assert torch.equal(ea, eb), (it, na)
+            sa, sb = phases[0].opt.state[pa], phases[1].opt.state[pb]
+            assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"])
+    assert phases[0].sync.raw is None
+    assert hip_steps == [4, 4]

@@ -55,6 +55,7 @@ def _run_phase_checked(step, phase, img, labels, cur_nimg=0):
     step.loss.accumulate_gradients(phase=phase.name, real_img=img, real_c=labels, cur_nimg=cur_nimg)
     phase.module.requires_grad_(False)
     phase.sync.finish(gain=1)
+    phase.sync.materialize()             # (direct mode: gain and nan_to_num are otherwise left to the Adam kernel)
     grads = {n: p.grad for n, p in phase.module.named_parameters() if p.grad is not None}
     assert grads, f"phase {phase.name}: no gradients"
     assert set(grads) <= trainable

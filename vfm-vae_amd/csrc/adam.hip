@@ -14,6 +14,11 @@
 // store; step_size = lr / bc1 and the denominator rounded to float; the update in float; bc1 = 1 - beta1^step,
 // sqrt(1 - beta2^step) from the host in double. The lerp is torch's (|w| < 0.5: self + w (end - self), else
 // end - (end - self) (1 - w)) in float. Per element: 28 B (p, g, m, v read; p, m, v written), + 8 B with EMA.
+//
+// Raw gradients (vfm_adam_ema_step_raw): at world size 1 the phase's gradients are the tensors autograd allocated
+// this step (training_loop.FlatGradSync direct mode: no per-parameter hooks, no gather into a flat buffer), so
+// their addresses come per step in a device array, and the kernel applies what FlatGradSync.finish() applies to
+// the flat buffer -- g * gain in float, then nan_to_num(nan 0, +inf 1e5, -inf -1e5) -- as it reads them.
 #include "vfm_common.h"
 
 namespace {
@@ -37,9 +42,15 @@ struct AdamHyper {
     double lr, beta1, beta2, wd, eps, bc1, bc2_sqrt;
     float ema_w;
     int has_wd;
+    float gscale;               // raw gradients: g * gscale, then nan_to_num
+    int clean;
 };
 
 __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, const AdamHyper& h) {
+    if (h.clean) {
+        g *= h.gscale;
+        g = isnan(g) ? 0.f : isinf(g) ? (g > 0.f ? 1e5f : -1e5f) : g;
+    }
     if (h.has_wd) g = (float)((double)g + (double)p * h.wd);
     m = (float)(h.beta1 * (double)m + (1.0 - h.beta1) * (double)g);
     v = (float)(h.beta2 * (double)v + (1.0 - h.beta2) * (double)g * (double)g);
@@ -53,9 +64,13 @@ __device__ __forceinline__ float lerp1(float self, float end, float w) {
 }
 
 __global__ __launch_bounds__(THREADS) void adam_ema_kernel(const AdamT* __restrict__ T, const int2* __restrict__ chunks,
-                                                           AdamHyper h) {
+                                                           const float* const* __restrict__ graw, AdamHyper h) {
     const int2 c = chunks[blockIdx.x];
-    const AdamT t = T[c.x];
+    AdamT t = T[c.x];
+    if (graw) {                 // this step's gradient of tensor c.x (its record's vec flag covers p, m, v, e and n)
+        t.g = graw[c.x];
+        t.vec = t.vec && (reinterpret_cast<unsigned long long>(t.g) & 15) == 0;
+    }
     const long long s = (long long)c.y * CH, e = min(t.n, s + (long long)CH);
     if (t.vec) {
         for (long long i = s + 4LL * threadIdx.x; i < e; i += 4LL * THREADS) {
@@ -100,13 +115,29 @@ extern "C" int vfm_adam_chunk_elems(void) { return CH; }
 // null, n, vec flag, 0) through the chunk list `chunks` (device array of nchunks (tensor, chunk) int pairs).
 // bc1 = 1 - beta1^step, bc2_sqrt = sqrt(1 - beta2^step); ema_w: the lerp weight 1 - beta_ema (records with a
 // null ema pointer ignore it).
+extern "C" int vfm_adam_ema_step_raw(const void* tensors, int ntensors, const void* chunks, int nchunks,
+                                     const void* grads, float gscale, int clean, double lr, double beta1, double beta2,
+                                     double weight_decay, double eps, double bc1, double bc2_sqrt, float ema_w,
+                                     void* stream);
+
 extern "C" int vfm_adam_ema_step(const void* tensors, int ntensors, const void* chunks, int nchunks, double lr,
                                  double beta1, double beta2, double weight_decay, double eps, double bc1,
                                  double bc2_sqrt, float ema_w, void* stream) {
+    return vfm_adam_ema_step_raw(tensors, ntensors, chunks, nchunks, nullptr, 1.f, 0, lr, beta1, beta2, weight_decay,
+                                 eps, bc1, bc2_sqrt, ema_w, stream);
+}
+
+// vfm_adam_ema_step with the gradients read through `grads` (device array of ntensors float pointers, one per record,
+// replacing the records' g; null: use the records' g) and, when clean != 0, transformed to nan_to_num(g * gscale)
+// (nan 0, +inf 1e5, -inf -1e5) before use. Each gradient holds its tensor's n contiguous floats.
+extern "C" int vfm_adam_ema_step_raw(const void* tensors, int ntensors, const void* chunks, int nchunks,
+                                     const void* grads, float gscale, int clean, double lr, double beta1, double beta2,
+                                     double weight_decay, double eps, double bc1, double bc2_sqrt, float ema_w,
+                                     void* stream) {
     if (!tensors || !chunks || ntensors <= 0 || nchunks < 0 || !(bc1 > 0.0) || !(bc2_sqrt > 0.0)) return VFM_ERR_ARGS;
     if (nchunks == 0) return 0;
-    AdamHyper h{lr, beta1, beta2, weight_decay, eps, bc1, bc2_sqrt, ema_w, weight_decay != 0.0};
+    AdamHyper h{lr, beta1, beta2, weight_decay, eps, bc1, bc2_sqrt, ema_w, weight_decay != 0.0, gscale, clean != 0};
     VFM_LAUNCH(adam_ema_kernel, dim3((unsigned)nchunks), dim3(THREADS), 0, (hipStream_t)stream,
-               (const AdamT*)tensors, (const int2*)chunks, h);
+               (const AdamT*)tensors, (const int2*)chunks, (const float* const*)grads, h);
     return launch_status();
 }

@@ -176,6 +176,9 @@ SIGNATURES = {
     "vfm_style_group_launch": [c_int, c_vp, c_int, c_ll, c_vp],
     "vfm_adam_ema_step": [c_vp, c_int, c_vp, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                           ctypes.c_double, ctypes.c_double, ctypes.c_double, c_float, c_vp],
+    "vfm_adam_ema_step_raw": [c_vp, c_int, c_vp, c_int, c_vp, c_float, c_int, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              c_float, c_vp],
     "vfm_timer_arm_first": [c_vp, c_vp],
     "vfm_gemm_fold": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,
                       c_ll, c_float, c_float, c_int, c_int, c_vp],

@@ -6,7 +6,10 @@ The moment buffers are the optimizer's own state tensors (exp_avg / exp_avg_sq) 
 tensors are advanced as torch's fused path advances them, so `opt.state_dict()`, a later regular `opt.step()` and
 checkpoints see the same state either way. The tensor / chunk tables live on the device and are rebuilt only when
 the parameter set or a tensor's storage changes (`AdamEmaPlan`), so a step costs one launch and a multi-tensor
-add on the step counters.
+add on the step counters. A plan built without gradients (`grads=None`) takes the gradient tensors per step
+(`step(..., raw=grads, gscale=gain)`: FlatGradSync's direct mode, where autograd's own gradient tensors are used
+without a gather into a flat buffer): their addresses are uploaded with the launch, and the kernel applies the
+gain and nan_to_num that FlatGradSync.finish() applies to the flat buffer (reference training_loop.py:281-289).
 """
 import numpy as np
 import torch
@@ -22,18 +25,22 @@ class AdamEmaPlan:
 
     def __init__(self, params, grads, m1, m2, emas):
         dev = params[0].device
+        self.raw = grads is None
+        if grads is None:
+            grads = [None] * len(params)
         ch = int(_lib.vfm_adam_chunk_elems())
         rec = np.zeros((len(params), 8), dtype=np.int64)
         chunks = []
         self.nbytes = 0
         for i, (p, g, m, v, e) in enumerate(zip(params, grads, m1, m2, emas)):
-            ts = (p, g, m, v) + ((e,) if e is not None else ())
+            ts = (p,) + ((g,) if g is not None else ()) + (m, v) + ((e,) if e is not None else ())
             for t in ts:
                 if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev or t.numel() != p.numel():
                     raise custom_ops.NativeError("adam_hip: fp32 contiguous tensors of equal size on one device expected")
             n = p.numel()
             ptrs = [t.data_ptr() for t in ts]
-            rec[i, :5] = [p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), e.data_ptr() if e is not None else 0]
+            rec[i, :5] = [p.data_ptr(), g.data_ptr() if g is not None else 0, m.data_ptr(), v.data_ptr(),
+                          e.data_ptr() if e is not None else 0]
             rec[i, 5] = n
             rec[i, 6] = int(n % 4 == 0 and all(q % 16 == 0 for q in ptrs))
             chunks.extend((i, c) for c in range(-(-n // ch)))
@@ -43,12 +50,25 @@ class AdamEmaPlan:
         self.ntensors, self.nchunks = len(params), len(chunks)
         self.keep = (params, grads, m1, m2, emas)       # the tables hold raw pointers into these
 
-    def step(self, lr, beta1, beta2, weight_decay, eps, step, ema_w=0.0):
+    def step(self, lr, beta1, beta2, weight_decay, eps, step, ema_w=0.0, raw=None, gscale=1.0):
+        """raw: this step's gradient tensors (plans built with grads=None; contiguous fp32 of the parameters'
+        sizes on their device -- what autograd hands a parameter), used as nan_to_num(g * gscale)."""
         bc1 = 1.0 - beta1 ** step
         bc2_sqrt = (1.0 - beta2 ** step) ** 0.5
         dev = self.tensors.device
+        if self.raw != (raw is not None) or (raw is not None and len(raw) != self.ntensors):
+            raise custom_ops.NativeError("adam_hip: raw gradients go with plans built without gradients, one per tensor")
+        gptr = 0
+        if raw is not None:
+            # pinned staging + stream-ordered copy (the caching host allocator keeps the staging buffer until the
+            # copy has run); the device array lives until the launch below has consumed it (stream order)
+            host = torch.empty(self.ntensors, dtype=torch.int64, pin_memory=True)
+            host.numpy()[:] = [g.data_ptr() for g in raw]
+            graw = host.to(dev, non_blocking=True)
+            gptr = graw.data_ptr()
         with kernel_timer.region("adam_ema", self.nbytes):
-            custom_ops.check(_lib.vfm_adam_ema_step(self.tensors.data_ptr(), self.ntensors, self.chunks.data_ptr(),
-                                                    self.nchunks, float(lr), float(beta1), float(beta2),
-                                                    float(weight_decay), float(eps), bc1, bc2_sqrt, float(ema_w),
-                                                    custom_ops.stream_ptr(dev)), "vfm_adam_ema_step")
+            custom_ops.check(_lib.vfm_adam_ema_step_raw(self.tensors.data_ptr(), self.ntensors, self.chunks.data_ptr(),
+                                                        self.nchunks, gptr, float(gscale), int(raw is not None),
+                                                        float(lr), float(beta1), float(beta2), float(weight_decay),
+                                                        float(eps), bc1, bc2_sqrt, float(ema_w),
+                                                        custom_ops.stream_ptr(dev)), "vfm_adam_ema_step_raw")

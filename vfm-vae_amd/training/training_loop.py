@@ -10,6 +10,9 @@ with keys {G, D, G_ema, training_set_kwargs} (:782-801) and auto-resume.
 MI355X-specific execution (`TrainingIteration`, shared with bench.py):
   * gradients of each phase live in ONE flat fp32 buffer (parameter .grad are
     views), so the reduction, /world, *gain and nan_to_num are single passes;
+    on one GPU without a collective (the bench) the gradients stay the tensors
+    autograd allocated and the fused Adam kernel applies *gain and nan_to_num
+    as it reads them (FlatGradSync direct mode);
   * with world_size > 1 the buffer is all-reduced in buckets launched from
     post-accumulate-grad hooks on a dedicated stream, overlapping the backward
     (RCCL over xGMI); the math equals the reference's flat sharded all-reduce;
@@ -51,7 +54,14 @@ class FlatGradSync:
     parameters the last microbatch did not touch (tests/test_distributed.py covers two microbatches
     with parameters seen in only one of them). The rank-agreement check on the parameter set runs
     without a host sync and therefore raises one step late, at the next prepare(): by then Adam has
-    applied one step of the divergent gradients."""
+    applied one step of the divergent gradients.
+
+    Direct mode (a GPU, no collective, the native Adam: `self.direct`): no flat buffer, hooks or
+    gather -- each parameter keeps the gradient tensor autograd allocated (or accumulated into,
+    over microbatches), finish() only records the gain (`self.raw`), and fast_adam_step hands the
+    gain and nan_to_num to the Adam kernel, which applies them as it reads the gradients
+    (csrc/adam.hip vfm_adam_ema_step_raw: the same float multiply and clamp as the flat passes).
+    Whatever else steps the phase calls materialize() first, which applies them in place."""
 
     def __init__(self, module: nn.Module, bucket_mb: float = 64.0, collective: Optional[bool] = None):
         self.module = module
@@ -65,6 +75,8 @@ class FlatGradSync:
         self.key = None
         self.hooks = []
         self.comm_stream = None
+        self.direct = False
+        self.raw = None
 
     def _build(self, params):
         for h in self.hooks:
@@ -72,6 +84,10 @@ class FlatGradSync:
         self.hooks = []
         self.params = params
         self.key = tuple(id(p) for p in params)
+        self.direct = params[0].device.type == 'cuda' and not self.collective and HIP_ADAM and DIRECT_GRADS
+        if self.direct:
+            self.flat = None
+            return
         order = list(reversed(params))              # gradients of late layers arrive first
         total = sum(p.numel() for p in order)
         dev = params[0].device
@@ -119,6 +135,11 @@ class FlatGradSync:
             return
         if tuple(id(p) for p in params) != self.key:
             self._build(params)
+        self.raw = None
+        if self.direct:
+            for p in self.params:
+                p.grad = None
+            return
         self.flat.zero_()
         # grads start as None: the autograd engine then hands each parameter its gradient tensor
         # without a kernel (AccumulateGrad "steals" it), and the grads move into the flat buffer
@@ -215,8 +236,12 @@ class FlatGradSync:
             self.pending[bi] = torch.distributed.all_reduce(view, async_op=True)
 
     def finish(self, gain: Optional[float] = None):
-        """Complete the reduction: flat = nan_to_num(sum_ranks / world * gain)."""
+        """Complete the reduction: flat = nan_to_num(sum_ranks / world * gain) (direct mode: deferred to the
+        optimizer step, see materialize())."""
         if not self.params:
+            return
+        if self.direct:
+            self.raw = 1.0 if gain is None else float(gain)
             return
         if self.collective:
             for bi in range(len(self.buckets)):
@@ -241,8 +266,22 @@ class FlatGradSync:
             if id(p) not in self.seen:
                 p.grad = None
 
+    def materialize(self):
+        """Direct mode: apply the pending gain and nan_to_num to the gradients in place (for an optimizer step
+        other than the native fused one)."""
+        if self.raw is None:
+            return
+        gain, self.raw = self.raw, None
+        grads = [p.grad for p in self.params if p.grad is not None]
+        with torch.no_grad():
+            if grads and gain != 1:
+                torch._foreach_mul_(grads, gain)
+            for g in grads:
+                torch.nan_to_num_(g, nan=0, posinf=1e5, neginf=-1e5)
+
 
 HIP_ADAM = os.environ.get("VFM_ADAM", "hip") == "hip"      # VFM_ADAM=torch: torch's fused Adam + foreach lerp (A/B)
+DIRECT_GRADS = os.environ.get("VFM_DIRECT_GRADS", "1") == "1"  # 0: flat-buffer gradients at world size 1 too (A/B)
 
 
 def fast_adam_step(phase, ema=None):
@@ -255,36 +294,45 @@ def fast_adam_step(phase, ema=None):
     (nothing done: the caller runs opt.step()) for anything but a single fp32 group of plain fused Adam with
     float hyper-parameters, or on the first step of a parameter set (the regular path creates state); else
     the set of ids of the parameters whose EMA it applied. The regular step loops over every parameter
-    checking grads, state and dtypes: ~2-4 ms of host time per phase with the GPU idle (r4k gap profile)."""
+    checking grads, state and dtypes: ~2-4 ms of host time per phase with the GPU idle (r4k gap profile).
+    With the phase's FlatGradSync in direct mode (gradients pending gain / nan_to_num, `sync.raw`) the native
+    step applies them; every other outcome materializes them first (the caller's opt.step() included)."""
+    sync = getattr(phase, 'sync', None)
+    gain = getattr(sync, 'raw', None)
     opt = phase.opt
     if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1:
-        return False
+        return _materialized(sync, False)
     g = opt.param_groups[0]
     if not g.get('fused') or g.get('amsgrad') or g.get('capturable') or g.get('differentiable') or \
             g.get('maximize') or g.get('foreach') or g.get('decoupled_weight_decay') or \
             isinstance(g['lr'], torch.Tensor) or \
             any(isinstance(b, torch.Tensor) for b in g['betas']):
-        return False
+        return _materialized(sync, False)
     plist = getattr(phase, 'adam_params', None)     # (phases are EasyDicts: attributes are items)
     if plist is None:
         plist = phase.adam_params = list(g['params'])
     now = [p.grad for p in plist]                       # the one Python pass over the parameters
+    raw = gain is not None
+    # cache key: the gradient tensors themselves (flat-buffer views persist across steps), or with raw
+    # gradients (new tensors every step) which parameters have one
+    key = [gr is None for gr in now] if raw else now
     pairs = ema[0] if ema is not None else None
     cache = getattr(phase, 'adam_cache', None)
     st = opt.state
-    if (cache is not None and cache[6] is pairs and all(map(operator.is_, now, cache[0]))
+    if (cache is not None and cache[6] is pairs and cache[8] == raw
+            and (key == cache[0] if raw else all(map(operator.is_, now, cache[0])))
             and st[cache[1][0]]['exp_avg'] is cache[3][0] and st[cache[1][-1]]['exp_avg_sq'] is cache[4][-1]):
-        _, params, grads, m1, m2, steps, _, plan = cache  # same grad tensors as last time (flat-buffer views)
+        _, params, grads, m1, m2, steps, _, plan, _ = cache
     else:
         phase.adam_rebuilds = getattr(phase, 'adam_rebuilds', 0) + 1       # (tools_dev/adam_cache_debug.py)
         with_grad = [p for p, gr in zip(plist, now) if gr is not None]
         if not with_grad:
-            return set()
+            return _materialized(sync, set())
         dev = with_grad[0].device
         if any(p not in st or p.dtype != torch.float32 or p.device != dev or p.grad.dtype != torch.float32
                for p in with_grad):
             phase.adam_cache = None
-            return False                 # first step of these parameters: the regular path creates state
+            return _materialized(sync, False)   # first step of these parameters: the regular path creates state
         params, grads = with_grad, [p.grad for p in with_grad]
         m1, m2 = [st[p]['exp_avg'] for p in with_grad], [st[p]['exp_avg_sq'] for p in with_grad]
         steps = [st[p]['step'] for p in with_grad]
@@ -294,21 +342,38 @@ def fast_adam_step(phase, ema=None):
             if bool((counts == counts[0]).all()):
                 from torch_utils.ops import adam_hip
                 emas = [pairs.get(id(p)) if pairs is not None else None for p in with_grad]
-                plan = [adam_hip.AdamEmaPlan(params, grads, m1, m2, emas), float(counts[0]),
+                plan = [adam_hip.AdamEmaPlan(params, None if raw else grads, m1, m2, emas), float(counts[0]),
                         {id(p) for p, e in zip(with_grad, emas) if e is not None}]
-        phase.adam_cache = (now, params, grads, m1, m2, steps, pairs, plan)
+        phase.adam_cache = (key, params, grads, m1, m2, steps, pairs, plan, raw)
+    if raw:
+        grads = [gr for gr in now if gr is not None]
+        if plan is not None and not all(gr.is_contiguous() for gr in grads):
+            plan = None                       # (autograd hands contiguous gradients; an assigned .grad may not be)
+        if plan is None:
+            sync.materialize()
     beta1, beta2 = g['betas']
     with torch.no_grad():
         torch._foreach_add_(steps, 1)
         if plan is not None:
             plan[1] += 1.0
             plan[0].step(g['lr'], beta1, beta2, g['weight_decay'], g['eps'], plan[1],
-                         ema[1] if ema is not None else 0.0)
+                         ema[1] if ema is not None else 0.0, raw=grads if raw else None,
+                         gscale=gain if raw else 1.0)
+            if raw:
+                sync.raw = None
             return plan[2]
         torch._fused_adam_(params, grads, m1, m2, [], steps, amsgrad=False, lr=g['lr'], beta1=beta1, beta2=beta2,
                            weight_decay=g['weight_decay'], eps=g['eps'], maximize=False, grad_scale=None,
                            found_inf=None)
     return set()
+
+
+def _materialized(sync, result):
+    """fast_adam_step's exits that leave the step to something else: the pending direct-mode gain and
+    nan_to_num applied to the gradients first."""
+    if sync is not None and getattr(sync, 'raw', None) is not None:
+        sync.materialize()
+    return result
 
 
 class TrainingIteration:
