@@ -11,7 +11,7 @@ decoder block, a square latent-stem 1x1, the adapter's projections): norm and su
 transposed or permuted gradient, the projection and the stored tensors can (tests/test_fullsize_checker.py
 proves it on CPU with a deliberately transposed gradient).
 
-Stated tolerances:
+Stated tolerances (the matched-precision bf16 test at the end has its own):
   fp32 -- the product path at reference precision (decoder num_fp16_res 0, fp32 tower; our kernels
   with fp32-equivalent f32x6 products): loss terms 1e-5 relative; every parameter's gradient norm and
   projection within FP32_TOL = 2e-4 (relative to the gradient's norm, floor 1e-4 of the largest norm for
@@ -139,3 +139,63 @@ def test_generator_training_backward_full_size(vfm_dir, golden, precision):
     else:
         assert e_loss < 3e-2, e_loss
         assert all(e < 5e-2 for e in g_err.values()), g_err
+
+
+# matched precision (bf16 HIP kernels vs the reference's op sequence in torch at the same bf16 schedule), measured
+# on MI355X (r6bf): loss 4.4e-3; tensor gradients: difference median 2.0e-2, worst 3.2e-2, norm error median
+# 9.5e-4, worst 1.0e-2; the 38 scalar gradients (noise strengths: sums of many cancelling products, and the torch
+# side's reductions are not run-to-run deterministic) 1.0e-1 worst over two runs. Bounds ~2x.
+MATCHED_BF16 = dict(loss=4.4e-3, diff=3.19e-2, diff_median=1.97e-2, norm=1.00e-2, scalar=1.00e-1)
+MATCHED_LOSS_TOL = 1e-2
+MATCHED_DIFF_TOL = 6e-2
+MATCHED_DIFF_MEDIAN_TOL = 3e-2
+MATCHED_NORM_TOL = 2e-2
+MATCHED_SCALAR_TOL = 2e-1
+
+
+def test_generator_backward_bf16_matched_precision(vfm_dir, golden):
+    """The bench's precision pinned at matched precision: the bf16 Generator's training backward with the
+    decoder's HIP kernels against the same network, same init and same noise draws with every decoder op
+    on its torch restatement of the reference (decoder_ops.set_force_ref(True): torch's bf16 convolutions,
+    GroupNorm, GELU ... in the dtypes the reference's autocast gives them). Both runs share everything
+    else (tower, adapter), so the difference is the decoder kernels' own rounding: each parameter gradient
+    compared as a whole tensor, |g_hip - g_torch| / max(|g_torch|, 1e-3 max norm). A systematic error of a
+    few percent in one bf16 kernel exceeds the bound, which the fp32-golden comparison above (bf16 noise
+    against fp32 numbers: 13.5 %) cannot resolve: tensor gradients within MATCHED_DIFF_TOL = 6e-2 as a
+    difference, MATCHED_NORM_TOL = 2e-2 in norm (a systematic scale error of a few percent moves the norm
+    by as much, rounding noise moves it by ~1e-3), median difference below 3e-2; scalars within 2e-1."""
+    from torch_utils.ops import decoder_ops
+    _, meta = golden
+    G_hip, out_hip, loss_hip = _run(vfm_dir, meta, "bf16")
+    decoder_ops.set_force_ref(True)
+    try:
+        G_ref, out_ref, loss_ref = _run(vfm_dir, meta, "bf16")
+    finally:
+        decoder_ops.set_force_ref(False)
+    e_loss = _rel(loss_hip, loss_ref)
+    ph, pr = dict(G_hip.named_parameters()), dict(G_ref.named_parameters())
+    names = [n for n, p in pr.items() if p.grad is not None]
+    assert names and {n for n, p in ph.items() if p.grad is not None} == set(names)
+    floor = 1e-3 * max(float(pr[n].grad.double().norm()) for n in names)
+    rows = []            # (difference error, norm error, name, numel)
+    for n in names:
+        gh, gr = ph[n].grad.double(), pr[n].grad.double()
+        scale = max(float(gr.norm()), floor)
+        rows.append((float((gh - gr).norm()) / scale, abs(float(gh.norm()) - float(gr.norm())) / scale, n, gr.numel()))
+    e_px = float((out_hip.gen_img.double() - out_ref.gen_img.double()).abs().max())
+    print(f"matched bf16: loss rel {e_loss:.2e}, max |pixel diff| {e_px:.2e}")
+    for label, sel in (("tensors", [r for r in rows if r[3] > 1]), ("scalars", [r for r in rows if r[3] == 1])):
+        if not sel:
+            continue
+        by_diff = sorted(sel, reverse=True)
+        by_norm = sorted(sel, key=lambda r: -r[1])
+        print(f"matched bf16 {label} ({len(sel)}): difference median {by_diff[len(sel) // 2][0]:.2e}, worst "
+              + ", ".join(f"{r[2]} {r[0]:.2e}" for r in by_diff[:5]))
+        print(f"matched bf16 {label}: norm error median {by_norm[len(sel) // 2][1]:.2e}, worst "
+              + ", ".join(f"{r[2]} {r[1]:.2e}" for r in by_norm[:5]))
+    assert e_loss < MATCHED_LOSS_TOL, e_loss
+    tens = [r for r in rows if r[3] > 1]
+    bad = [(n, e, en) for e, en, n, k in rows
+           if (k > 1 and (e >= MATCHED_DIFF_TOL or en >= MATCHED_NORM_TOL)) or (k == 1 and e >= MATCHED_SCALAR_TOL)]
+    assert not bad, bad[:10]
+    assert sorted(r[0] for r in tens)[len(tens) // 2] < MATCHED_DIFF_MEDIAN_TOL
