@@ -344,3 +344,28 @@ def test_gemm9_narrow_routes(M, N, K, a_kc):
     out = gemm_hip.try_gemm(a, Bt.t(), auto=True, out_dtype=torch.float32)
     assert out is not None and out.shape == (M, N)
     assert _rel(out, A.float() @ Bt.float().t()) < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,z", [(64, 520, 128, 1), (304, 40, 192, 1), (48, 64, 4096, 1), (32, 24, 8192, 1),
+                                     (64, 1024, 256, 3), (40, 72, 2048, 2)])
+@pytest.mark.parametrize("b_kc", [True, False])
+def test_gemm9_narrow_default_route(M, N, K, z, b_kc):
+    """bf16 products with an output side of 64 or less through the default routing (preferred() sends every
+    bf16 product to gemm9; few-tile deep-K single products run K-split, `_plan` "g9r"): the narrow shapes of
+    the bf16 linears' weight gradients (dy^T x over the tokens) and of narrow heads. fp32 output against the
+    fp32 product of the same operands at 2e-5, bf16 output at one rounding (8e-3); deterministic."""
+    g = torch.Generator().manual_seed(M * 7 + N + K + z)
+    A = _rnd(z, M, K, g=g)
+    Bt = _rnd(z, N, K, g=g)
+    b = Bt.transpose(1, 2) if b_kc else Bt.transpose(1, 2).contiguous()
+    ref = torch.matmul(A.float(), Bt.float().transpose(1, 2))
+    assert gemm_hip.preferred(A, M, N)
+    out = gemm_hip.try_gemm(A, b, out_dtype=torch.float32, auto=True)
+    assert out is not None and out.shape == (z, M, N)
+    assert _rel(out, ref) < 2e-5
+    again = gemm_hip.try_gemm(A, b, out_dtype=torch.float32, auto=True)
+    assert torch.equal(out, again)
+    outb = gemm_hip.try_gemm(A, b, auto=True)
+    assert outb is not None and outb.dtype == torch.bfloat16
+    assert _rel(outb, ref) < 8e-3
