@@ -891,7 +891,8 @@ __device__ __forceinline__ void gn_bwd_flat(const GnBwdArgs& a, int bg, int bidx
     __syncthreads();
     const int seg = cpc < 64 ? cpc : 64;
     float sa = 0.f, sb = 0.f;
-    // one chunk of lookahead: the next chunk's two 16-B loads are issued before this one is used
+    // one chunk of lookahead: the next chunk's two 16-B loads are issued before this one is used (two chunks
+    // ahead measured the same: the two passes together run at ~5.7 TB/s of actual reads + writes, r6bk)
     float xv[8], gv[8];
     if (threadIdx.x < nch) {
         load8(xp + threadIdx.x * 8, xv);
@@ -949,8 +950,11 @@ __device__ __forceinline__ void gn_bwd_flat(const GnBwdArgs& a, int bg, int bidx
     const float n = (float)nch * 8.f;
     const float m1 = block_sum(cx, scratch) / n, m2 = block_sum(cxx, scratch + 4) / n;
     TX* dxp = reinterpret_cast<TX*>(a.dx) + (long long)bg * nch * 8;
+    // pass 2 walks the group backwards: its first reads are the chunks pass 1 read last, still in L2 / MALL
 #pragma unroll 4
-    for (long long i = threadIdx.x; i < nch; i += NT) {
+    for (long long base = (nch - 1) / NT * NT; base >= 0; base -= NT) {
+        const long long i = base + threadIdx.x;
+        if (i >= nch) continue;
         const float k = s_k[(int)(i >> lg)];
         float xv[8], gv[8], o[8];
         load8(xp + i * 8, xv);
