@@ -66,6 +66,12 @@ def parse_args(argv=None):
                          "number of timed launches as 1/4 of every 4th step. Not every launch of whole steps: "
                          "back-to-back event-bound launches run serialised, which timed the LPIPS conv 27 %% below its "
                          "rocprof duration (profiles/r4_am_bench.json)")
+    ap.add_argument("--timer-prepass", type=int, default=10,
+                    help="untimed steps after the warm-up in which every kernel region is timed (1/n of each region's "
+                         "launches, stratified as --timer-every) to rank the regions and fill `all_kernels`; the timed "
+                         "steps then count and time only the dominant region, so the timer's per-launch bookkeeping "
+                         "stays out of the measured wall time (~2 %% with every region timed, "
+                         "profiles/r6_bm_timer_overhead_ab.txt). 0: every region timed inside the timed steps")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", nargs="?", const="on", default="off", choices=["auto", "on", "off"],
                     help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5). Default off: "
@@ -249,6 +255,24 @@ def main(argv=None):
         _log(rank, f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t1:.2f}s")
     if not args.trace:
         step.trace = None
+    prepass, target = None, None
+    if on_gpu and not args.no_kernel_timer and args.timer_prepass > 0:
+        # rank the kernel regions over untimed steps; the timed steps below time only the dominant one
+        t1 = time.perf_counter()
+        n_pre = args.timer_prepass
+        kernel_timer.enable(True, n_pre)
+        kernel_timer.calibrate()
+        for i in range(n_pre):
+            kernel_timer.new_step(True)
+            one(args.warmup + i, cur)
+            cur += args.batch * world
+        sync()
+        pre = kernel_timer.summary()
+        kernel_timer.enable(False)
+        target = kernel_timer.dominant_name(pre)
+        prepass = (pre, args.steps / n_pre)
+        _log(rank, f"timer pre-pass ({n_pre} steps, every region): {time.perf_counter() - t1:.1f}s; "
+                   f"timed steps time {target}")
     # Long-lived objects (modules, optimiser state, autograd caches) leave the collector's
     # young generations: a full collection over them mid-step stalls the launch stream
     # for ~100 ms. training_loop.py does the same after its first iteration.
@@ -276,6 +300,7 @@ def main(argv=None):
     every = max(1, args.timer_every)
     kernel_timer.enable(on_gpu and not args.no_kernel_timer, every)
     calib_us = kernel_timer.calibrate() * 1e3 if (on_gpu and not args.no_kernel_timer) else None
+    kernel_timer.set_target(target)
     t0 = time.perf_counter()
     tsteps = max(1, args.timer_steps)
     for i in range(args.steps):
@@ -311,7 +336,8 @@ def main(argv=None):
     traffic_table = None
     if os.path.exists(PMC_TRAFFIC):       # committed PMC passes of this workload (tools_dev/pmc_traffic.py)
         traffic_table = json.load(open(PMC_TRAFFIC)).get("kernels")
-    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table) if on_gpu else None
+    roof = kernel_timer.dominant_roofline(HBM_PEAK_GBS, BF16_PEAK_TFLOPS, traffic_table, prepass=prepass) \
+        if on_gpu else None
     if roof is not None:
         roof["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) if roof.get("traffic") else None
         n_t = len(range(0, args.steps, tsteps))
@@ -320,7 +346,11 @@ def main(argv=None):
         roof["timer_calibration_us"] = round(calib_us, 2) if calib_us is not None else None
         roof["timer_sampling"] = ((f"1/{every} of each kernel region's launches, stratified by launch position within "
                                    f"a step (position j of the k-th timed step when (j + k) % {every} == 0) in "
-                                   if every > 1 else "every launch in ") + where + ", all launches counted")
+                                   if every > 1 else "every launch in ") + where + ", all launches counted"
+                                  + (f"; only the roofline kernel's region is timed in the timed steps, the ranking, "
+                                     f"runner_up and all_kernels come from {args.timer_prepass} untimed pre-pass steps "
+                                     f"(1/{args.timer_prepass} of every region's launches, stratified) with totals "
+                                     f"scaled to {args.steps} steps" if prepass is not None else ""))
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value) if args.config == CONFIG else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -34,6 +34,7 @@ _every = 1         # time ~1/n of each region's launches (the events cost host t
 
 
 _active = True     # launches are timed only while active (bench.py: every launch of every n-th timed step)
+_target = None     # set_target(): the one region counted and timed (bench.py's timed steps); None: all regions
 _pos = {}          # name -> launch position within the current step (new_step resets it)
 _phase = -1        # index of the current active step (new_step), -1: stepless (launch-index sampling)
 
@@ -49,10 +50,11 @@ def enable(flag: bool, every: int = 1):
 
 
 def _enable(flag: bool, every: int = 1):
-    global _enabled, _every, _active, _phase
+    global _enabled, _every, _active, _phase, _target
     _enabled = bool(flag)
     _active = True
     _phase = -1
+    _target = None
     _pos.clear()
     _per_step.clear()
     if flag:
@@ -93,6 +95,21 @@ def set_active(flag: bool):
 
 def is_enabled():
     return _enabled
+
+
+def set_target(name):
+    """Count and time only region `name` (None: every region) until the next enable(). bench.py ranks the regions
+    in untimed pre-pass steps and then times only the dominant one over its timed steps: the per-launch
+    bookkeeping of every region (counts, sampling, HIP events on 1/n of ~6 k launches a step) cost ~2 % of the
+    step's wall time (profiles/r6_bm_timer_overhead_ab.txt), and a bypassed region costs one string compare."""
+    global _target
+    _target = name
+
+
+def dominant_name(s):
+    """The region with the largest total time among our kernels (not library GEMMs) of a summary() dict."""
+    own = [(v["total_ms"], k) for k, v in s.items() if not k.startswith("vendor_gemm<")]
+    return max(own)[1] if own else None
 
 
 class _Null:
@@ -219,7 +236,7 @@ def region(name, nbytes=0, flops=0, bound="hbm", native=True, first_only=False):
     sampled (this is on every launch's host path). first_only: only the call's first kernel is timed (a GEMM
     whose split-K combine pass follows as a kernel of its own: the region then covers exactly the launches of
     the GEMM kernel instantiation rocprofv3 names)."""
-    if not _enabled:
+    if not _enabled or (_target is not None and name != _target):
         return _NULL
     c = _counts.get(name, 0)
     _counts[name] = c + 1
@@ -393,16 +410,28 @@ def _roof(name, r, hbm_peak_gbs, mfma_peak_tflops):
     return achieved, peak, unit, note
 
 
-def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None, steps=None):
+def dominant_roofline(hbm_peak_gbs, mfma_peak_tflops, traffic_table=None, steps=None, prepass=None):
     """The roofline object of the bench line: our kernel (timer region) with the largest total
     time, plus `vendor_top`, the library GEMM region with the largest total time (ranked the same
-    way; hipBLASLt kernels are not ours, so they never become the roofline kernel itself)."""
+    way; hipBLASLt kernels are not ours, so they never become the roofline kernel itself).
+    prepass = (summary of untimed pre-pass steps, scale): the current records hold only the target region
+    (set_target); the ranking, runner-up, vendor_top and all_kernels come from the pre-pass summary, its
+    totals multiplied by `scale` (timed steps / pre-pass steps)."""
     s = summary()
     if not s:
         return None
+    timed = s
+    if prepass is not None:
+        pre, scale = prepass
+        s = {k: dict(v, total_ms=v["total_ms"] * scale, bytes=v["bytes"] * scale, flops=v["flops"] * scale,
+                     launches=max(1, round(v["launches"] * scale))) for k, v in pre.items()}
+        s.update(timed)
     own = {k: v for k, v in s.items() if not k.startswith("vendor_gemm<")}
     vend = {k: v for k, v in s.items() if k.startswith("vendor_gemm<")}
     ranked = sorted(own.items(), key=lambda kv: -kv[1]["total_ms"])
+    if prepass is not None:
+        # the timed region's own record leads (it was the pre-pass's dominant region)
+        ranked = [kv for kv in ranked if kv[0] in timed] + [kv for kv in ranked if kv[0] not in timed]
 
     def entry(name, r):
         achieved, peak, unit, note = _roof(name, r, hbm_peak_gbs, mfma_peak_tflops)
