@@ -380,6 +380,8 @@ def main(argv=None):
             "roofline": roof,
             "step_mfma": step_mfma,
             "cpu_baseline": cpu,
+            # A/B switches set for this run (empty: every default, the tested product path)
+            "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("VFM_")},
         }
         print(json.dumps(line), flush=True)
     if tunable and tunable["mode"] == "tune":
