@@ -66,12 +66,14 @@ def parse_args(argv=None):
                          "number of timed launches as 1/4 of every 4th step. Not every launch of whole steps: "
                          "back-to-back event-bound launches run serialised, which timed the LPIPS conv 27 %% below its "
                          "rocprof duration (profiles/r4_am_bench.json)")
-    ap.add_argument("--timer-prepass", type=int, default=10,
-                    help="untimed steps after the warm-up in which every kernel region is timed (1/n of each region's "
-                         "launches, stratified as --timer-every) to rank the regions and fill `all_kernels`; the timed "
-                         "steps then count and time only the dominant region, so the timer's per-launch bookkeeping "
-                         "stays out of the measured wall time (~2 %% with every region timed, "
-                         "profiles/r6_bm_timer_overhead_ab.txt). 0: every region timed inside the timed steps")
+    ap.add_argument("--timer-prepass", type=int, default=-1,
+                    help="untimed steps after the warm-up in which every kernel region is timed (stratified as "
+                         "--timer-every) to rank the regions and fill `all_kernels`; they draw the timed steps' own "
+                         "seeded sequence of equivariance outcomes, so with the default (-1: as many as --steps) they "
+                         "run the timed steps' shape mix. The timed steps then count and time only the dominant "
+                         "region, so the timer's per-launch bookkeeping stays out of the measured wall time (~2 %% "
+                         "with every region timed, profiles/r6_bm_timer_overhead_ab.txt). 0: every region timed "
+                         "inside the timed steps")
     ap.add_argument("--trace", action="store_true", help="per-phase wall times during warmup (stderr)")
     ap.add_argument("--graphs", nargs="?", const="on", default="off", choices=["auto", "on", "off"],
                     help="replay the D phase's no-grad generator forward from HIP graphs (DESIGN.md §5). Default off: "
@@ -256,11 +258,16 @@ def main(argv=None):
     if not args.trace:
         step.trace = None
     prepass, target = None, None
-    if on_gpu and not args.no_kernel_timer and args.timer_prepass > 0:
-        # rank the kernel regions over untimed steps; the timed steps below time only the dominant one
+    n_pre = args.steps if args.timer_prepass < 0 else args.timer_prepass
+    if on_gpu and not args.no_kernel_timer and n_pre > 0:
+        # rank the kernel regions over untimed steps; the timed steps below time only the dominant one. The
+        # pre-pass draws the timed steps' seeded outcome sequence (same shapes, same stratified sampling)
         t1 = time.perf_counter()
-        n_pre = args.timer_prepass
-        kernel_timer.enable(True, n_pre)
+        pseed = TIMED_SEED + 1000 * rank
+        random.seed(pseed)
+        np.random.seed(pseed % 2**32)
+        torch.manual_seed(pseed)
+        kernel_timer.enable(True, max(1, args.timer_every))
         kernel_timer.calibrate()
         for i in range(n_pre):
             kernel_timer.new_step(True)
@@ -348,9 +355,9 @@ def main(argv=None):
                                    f"a step (position j of the k-th timed step when (j + k) % {every} == 0) in "
                                    if every > 1 else "every launch in ") + where + ", all launches counted"
                                   + (f"; only the roofline kernel's region is timed in the timed steps, the ranking, "
-                                     f"runner_up and all_kernels come from {args.timer_prepass} untimed pre-pass steps "
-                                     f"(1/{args.timer_prepass} of every region's launches, stratified) with totals "
-                                     f"scaled to {args.steps} steps" if prepass is not None else ""))
+                                     f"runner_up and all_kernels come from {n_pre} untimed pre-pass steps drawing the "
+                                     f"timed steps' seeded outcome sequence (every region, the same stratified 1/{every}) "
+                                     f"with totals scaled to {args.steps} steps" if prepass is not None else ""))
     step_mfma = step_flops(draws, hits, args.batch, args.steps, value) if args.config == CONFIG else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
