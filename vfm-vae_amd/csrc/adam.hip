@@ -35,7 +35,7 @@ struct AdamT {                  // 64 B, the host writes it as 8 int64 (torch_ut
     float* e;                   // EMA copy (null: none)
     long long n;
     long long vec;              // every pointer 16-B aligned and n % 4 == 0
-    long long pad;
+    float* step;                // the optimizer's fp32 step counter of this tensor (null: the host advances it)
 };
 
 struct AdamHyper {
@@ -67,6 +67,7 @@ __global__ __launch_bounds__(THREADS) void adam_ema_kernel(const AdamT* __restri
                                                            const float* const* __restrict__ graw, AdamHyper h) {
     const int2 c = chunks[blockIdx.x];
     AdamT t = T[c.x];
+    if (t.step && c.y == 0 && threadIdx.x == 0) *t.step += 1.f;     // torch's _foreach_add_(steps, 1)
     if (graw) {                 // this step's gradient of tensor c.x (its record's vec flag covers p, m, v, e and n)
         t.g = graw[c.x];
         t.vec = t.vec && (reinterpret_cast<unsigned long long>(t.g) & 15) == 0;
@@ -108,7 +109,9 @@ __global__ __launch_bounds__(THREADS) void adam_ema_kernel(const AdamT* __restri
 
 }  // namespace
 
-// Elements per chunk of the work list (the host splits every tensor into ceil(n / CH) chunks).
+// Elements per chunk of the work list (the host splits every tensor into ceil(n / CH) chunks). A record's step
+// pointer (its last 8 B; null: none) names the optimizer's fp32 step counter of that tensor, advanced by 1 in the
+// launch (the host's bc1 / bc2_sqrt are for the advanced count).
 extern "C" int vfm_adam_chunk_elems(void) { return CH; }
 
 // One Adam (+ EMA) step over the tensors of `tensors` (device array of ntensors 64-B records: p, g, m, v, ema or

@@ -23,7 +23,9 @@ _lib = custom_ops.get_native()
 class AdamEmaPlan:
     """Device tables of one parameter set: records (p, g, m, v, ema, n, vec) and the (tensor, chunk) list."""
 
-    def __init__(self, params, grads, m1, m2, emas):
+    def __init__(self, params, grads, m1, m2, emas, steps=None):
+        """steps: the optimizer's per-parameter step tensors (fp32 scalars on the device), advanced by 1 inside
+        each launch (else the caller advances them)."""
         dev = params[0].device
         self.raw = grads is None
         if grads is None:
@@ -43,12 +45,18 @@ class AdamEmaPlan:
                           e.data_ptr() if e is not None else 0]
             rec[i, 5] = n
             rec[i, 6] = int(n % 4 == 0 and all(q % 16 == 0 for q in ptrs))
+            if steps is not None:
+                s_ = steps[i]
+                if s_.dtype != torch.float32 or s_.device != dev or s_.numel() != 1:
+                    raise custom_ops.NativeError("adam_hip: fp32 device step counters expected")
+                rec[i, 7] = s_.data_ptr()
             chunks.extend((i, c) for c in range(-(-n // ch)))
             self.nbytes += n * (28 + (8 if e is not None else 0))
         self.tensors = torch.from_numpy(rec.view(np.uint8).reshape(-1)).to(dev)
         self.chunks = torch.from_numpy(np.asarray(chunks, dtype=np.int32).reshape(-1)).to(dev)
         self.ntensors, self.nchunks = len(params), len(chunks)
-        self.keep = (params, grads, m1, m2, emas)       # the tables hold raw pointers into these
+        self.keep = (params, grads, m1, m2, emas, steps)   # the tables hold raw pointers into these
+        self.owns_steps = steps is not None
 
     def step(self, lr, beta1, beta2, weight_decay, eps, step, ema_w=0.0, raw=None, gscale=1.0):
         """raw: this step's gradient tensors (plans built with grads=None; contiguous fp32 of the parameters'

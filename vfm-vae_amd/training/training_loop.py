@@ -342,19 +342,20 @@ def fast_adam_step(phase, ema=None):
             if bool((counts == counts[0]).all()):
                 from torch_utils.ops import adam_hip
                 emas = [pairs.get(id(p)) if pairs is not None else None for p in with_grad]
-                plan = [adam_hip.AdamEmaPlan(params, None if raw else grads, m1, m2, emas), float(counts[0]),
+                plan = [adam_hip.AdamEmaPlan(params, None if raw else grads, m1, m2, emas, steps), float(counts[0]),
                         {id(p) for p, e in zip(with_grad, emas) if e is not None}]
         phase.adam_cache = (key, params, grads, m1, m2, steps, pairs, plan, raw)
     if raw:
         grads = [gr for gr in now if gr is not None]
-        if plan is not None and not all(gr.is_contiguous() for gr in grads):
+        if plan is not None and not all(map(torch.Tensor.is_contiguous, grads)):
             plan = None                       # (autograd hands contiguous gradients; an assigned .grad may not be)
         if plan is None:
             sync.materialize()
     beta1, beta2 = g['betas']
     with torch.no_grad():
-        torch._foreach_add_(steps, 1)
-        if plan is not None:
+        if plan is None or not plan[0].owns_steps:
+            torch._foreach_add_(steps, 1)
+        if plan is not None:                      # (the launch advances the step counters it owns)
             plan[1] += 1.0
             plan[0].step(g['lr'], beta1, beta2, g['weight_decay'], g['eps'], plan[1],
                          ema[1] if ema is not None else 0.0, raw=grads if raw else None,
@@ -441,18 +442,18 @@ class TrainingIteration:
             self.loss.accumulate_gradients(phase=phase.name, real_img=img, real_c=c, cur_nimg=cur_nimg)
         if reuse and phase.name == 'G':
             enc.clear_features()                 # entries the G phase did not take (other draws) freed
-        # requires_grad_(False) over the flag list of _apply_freeze (a module walk costs ms of host
-        # time at the point where the GPU queue is shortest)
         flags = phase.active_flags
-        for p, f in flags:
-            if f:
-                p.requires_grad_(False)
         if phase.sync.params or any(p.grad is not None for p, _ in flags):
             phase.sync.finish(gain=self.n_batch_acc)
         done = fast_adam_step(phase, ema)
         if done is False:
             phase.opt.step()
             done = set()
+        # requires_grad_(False) over the flag list of _apply_freeze (a module walk costs ms of host time at the
+        # point where the GPU queue is shortest), after the optimizer launch so that it overlaps it
+        for p, f in flags:
+            if f:
+                p.requires_grad_(False)
         phase.opt.zero_grad(set_to_none=True)
         return done
 
