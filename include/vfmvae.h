@@ -446,7 +446,8 @@ int vfm_col2im2d_f32(const float* cols, float* x, int B, int C, int H, int W, in
 
 /* One launch for a phase's optimizer step (csrc/adam.hip): Adam (torch.optim.Adam's fused arithmetic, ORIGINAL
  * weight decay) over every tensor of the device table `tensors` (ntensors 64-B records {p, g, m, v, ema or null, n,
- * vec, 0}) through the chunk list `chunks` (nchunks int pairs (tensor, chunk) of vfm_adam_chunk_elems() elements),
+ * vec, fp32 step counter or null: advanced by 1 in the launch}) through the chunk list `chunks` (nchunks int pairs
+ * (tensor, chunk) of vfm_adam_chunk_elems() elements),
  * and for records with an EMA copy the G_ema lerp ema <- ema + ema_w (p - ema) on the stepped p. bc1 =
  * 1 - beta1^step, bc2_sqrt = sqrt(1 - beta2^step). Replaces the reference's opt.step() + G_ema lerp (reference
  * training/training_loop.py:722-742; host side training_loop.fast_adam_step / torch_utils/ops/adam_hip.py). */
