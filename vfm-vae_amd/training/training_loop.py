@@ -280,6 +280,7 @@ class FlatGradSync:
                 torch.nan_to_num_(g, nan=0, posinf=1e5, neginf=-1e5)
 
 
+_VERSION = operator.attrgetter('_version')
 HIP_ADAM = os.environ.get("VFM_ADAM", "hip") == "hip"      # VFM_ADAM=torch: torch's fused Adam + foreach lerp (A/B)
 DIRECT_GRADS = os.environ.get("VFM_DIRECT_GRADS", "1") == "1"  # 0: flat-buffer gradients at world size 1 too (A/B)
 
@@ -484,8 +485,9 @@ class TrainingIteration:
         # trainable set changes or any left-out tensor was written since (a checkpoint loaded into one
         # side bumps its version counter), so a frozen tensor that comes to differ is averaged again
         pairs = self._ema_pairs
+        # (the version check runs twice a step over the ~400 left-out tensors: one C-level map, not a generator)
         if pairs is not None and (pairs[0] != tuple(self.G.trainable_layers)
-                                  or any(pe._version != ve or p._version != vp for pe, p, ve, vp in pairs[3])):
+                                  or list(map(_VERSION, pairs[4])) != pairs[5]):
             pairs = None
         if pairs is None:
             names = self.G.trainable_layers
@@ -497,7 +499,8 @@ class TrainingIteration:
                     src.append(p)
                 else:
                     same.append((pe, p, pe._version, p._version))
-            pairs = self._ema_pairs = (tuple(names), dst, src, same)
+            flat = [t for pe, p, _, _ in same for t in (pe, p)]
+            pairs = self._ema_pairs = (tuple(names), dst, src, same, flat, list(map(_VERSION, flat)))
         return pairs
 
     @torch.no_grad()
@@ -505,7 +508,7 @@ class TrainingIteration:
         """G_ema <- lerp toward G (reference :734-742) for the pairs not in `done` (ids of G parameters whose
         EMA the fused G-phase optimizer step already applied), then the changed buffers."""
         beta = self._ema_beta(cur_nimg)
-        _, dst, src, _ = self._current_ema_pairs()
+        _, dst, src = self._current_ema_pairs()[:3]
         if done:
             keep = [(d, s_) for d, s_ in zip(dst, src) if id(s_) not in done]
             dst, src = [d for d, _ in keep], [s_ for _, s_ in keep]
