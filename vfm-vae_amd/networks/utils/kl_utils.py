@@ -75,6 +75,10 @@ class DiagonalGaussianDistribution(object):
 def _draw_eps(shape, device, dtype):
     """The noise DiagonalGaussianDistribution.sample() draws (same source, shape and order)."""
     eps = _noise_source(tuple(shape)) if _noise_source is not None else torch.randn(shape)
+    if torch.device(device).type == 'cuda' and eps.device.type == 'cpu':
+        # through pinned memory, asynchronously: a pageable host-to-device copy blocks the host until the GPU
+        # has drained its queue (tools_dev/sync_probe.py); the staging block is kept until the copy has run
+        return eps.to(dtype=dtype).pin_memory().to(device=device, non_blocking=True)
     return eps.to(device=device, dtype=dtype)
 
 

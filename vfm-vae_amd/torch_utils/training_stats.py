@@ -43,7 +43,8 @@ class StatsRegistry:
         if x.numel() == 0:
             return
         x = x.detach().reshape(-1).float()
-        acc = torch.stack([x.new_tensor(float(x.numel())), x.sum(), (x * x).sum()]).double()
+        # (new_full: a fill kernel; new_tensor(python number) would be a blocking host-to-device copy on a GPU)
+        acc = torch.stack([x.new_full((), float(x.numel())), x.sum(), (x * x).sum()]).double()
         cur = slots.get(acc.device)
         if cur is None:
             slots[acc.device] = acc

@@ -98,12 +98,17 @@ def rand_cutout(x, ratio=0.2):
     ch, cw = int(H * ratio + 0.5), int(W * ratio + 0.5)
     ox = torch.randint(0, H + (1 - ch % 2), size=[B, 1, 1], device=x.device)
     oy = torch.randint(0, W + (1 - cw % 2), size=[B, 1, 1], device=x.device)
-    gb, gx, gy = torch.meshgrid(torch.arange(B, device=x.device), torch.arange(ch, device=x.device),
-                                torch.arange(cw, device=x.device), indexing='ij')
-    gx = torch.clamp(gx + ox - ch // 2, min=0, max=H - 1)
-    gy = torch.clamp(gy + oy - cw // 2, min=0, max=W - 1)
-    mask = torch.ones(B, H, W, dtype=x.dtype, device=x.device)
-    mask[gb, gx, gy] = 0
+    # the reference scatters zeros at the clamped grid clamp(offset - c // 2 + [0, c), 0, H - 1): a contiguous row
+    # (column) range, the window's rows (columns) clamped to the plane. Built by comparisons instead: the scatter
+    # (index_put_ with device indices) synchronised the host with the GPU on every call (tools_dev/sync_probe.py)
+    r0 = torch.clamp(ox - ch // 2, min=0, max=H - 1)
+    r1 = torch.clamp(ox - ch // 2 + ch - 1, min=0, max=H - 1)
+    c0 = torch.clamp(oy - cw // 2, min=0, max=W - 1)
+    c1 = torch.clamp(oy - cw // 2 + cw - 1, min=0, max=W - 1)
+    rows = torch.arange(H, device=x.device).view(1, H, 1)
+    cols = torch.arange(W, device=x.device).view(1, 1, W)
+    hole = (rows >= r0) & (rows <= r1) & (cols >= c0) & (cols <= c1)        # [B, H, W]
+    mask = (~hole).to(x.dtype)
     return x * mask.unsqueeze(1)
 
 

@@ -303,12 +303,12 @@ class TotalLoss:
     def calculate_patchgan_disc_loss(self, logits, type):
         assert type in ['real', 'fake']
         if len(logits) == 0:
-            return torch.tensor(0.0, device=self.device)
+            return torch.zeros((), device=self.device)
         return sum(self._patch_loss(s[-1], type == 'real') for s in logits) / len(logits)
 
     def calculate_patchgan_gen_loss(self, logits):
         if len(logits) == 0:
-            return torch.tensor(0.0, device=self.device)
+            return torch.zeros((), device=self.device)
         loss = 0.
         for s in logits:
             pred = s[-1]
@@ -440,7 +440,7 @@ class TotalLoss:
     def accumulate_gradients(self, phase, real_img, real_c, cur_nimg):
         self.set_blur_sigma(cur_nimg)
         is_text_cond = isinstance(real_c, list) and len(real_c) > 0 and isinstance(real_c[0], str)
-        zero = lambda: torch.tensor(0.0, device=self.device)
+        zero = lambda: torch.zeros((), device=self.device)      # (a fill kernel, not a blocking host copy)
         check_now = cur_nimg > (self.resume_kimg * 1e3 + self.safe_loss_checking_start_nimg)
 
         if phase == 'D':
