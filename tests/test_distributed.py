@@ -340,3 +340,23 @@ def test_bench_main_two_ranks_gloo(tmp_path):
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2" and line["steps"] == 2
     assert line["config"]["global_batch"] == 2 and line["value"] > 0
     assert abs(line["value"] - 2 * 2 / (line["ms_per_step"] * 2 / 1e3)) / line["value"] < 1e-2
+
+
+def _safety_worker(rank, world):
+    """TotalLoss._sync_safety at world 2: a rank's unsafe mark reaches every rank when the check ran
+    (checked=True); with checked=False (no rank ran it) each rank keeps its own values with no collective."""
+    from training.loss import TotalLoss
+    obj = TotalLoss.__new__(TotalLoss)
+    obj.device = torch.device("cpu")
+    marks = [1, 1, 1]
+    mine = [1, 0, 1] if rank == 1 else marks
+    skip, got = obj._sync_safety(rank == 1, mine, checked=True)
+    skip2, got2 = obj._sync_safety(False, marks, checked=False)
+    return {"skip": skip, "marks": got, "skip2": skip2, "marks2": got2}
+
+
+def test_sync_safety_agrees_only_when_checked():
+    res = _spawn("_safety_worker", 2)
+    for r in range(2):
+        assert res[r]["skip"] is True and res[r]["marks"] == [1, 0, 1]
+        assert res[r]["skip2"] is False and res[r]["marks2"] == [1, 1, 1]

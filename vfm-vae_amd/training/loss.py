@@ -343,9 +343,11 @@ class TotalLoss:
         self.kl_loss_weight = self.vq_loss_weight = self.vf_loss_weight = 0.0
         dist.print0("[Reconstruction & Quantization Losses] Off perceptual, SSIM, multiscale pixel, pixel, KL, VQ, and VF losses.")
 
-    def _sync_safety(self, skip_local: bool, marks: list):
-        """One collective: returns (skip_any_rank, marks_min_over_ranks)."""
-        if not dist.is_initialized() or dist.get_world_size() == 1:
+    def _sync_safety(self, skip_local: bool, marks: list, checked: bool = True):
+        """One collective: returns (skip_any_rank, marks_min_over_ranks). checked=False: no rank ran the check this
+        step (a condition every rank evaluates alike: cur_nimg and whether a previous step exists), so every rank
+        holds (False, all safe) and there is nothing to agree on -- no collective and no host round trip."""
+        if not checked or not dist.is_initialized() or dist.get_world_size() == 1:
             return skip_local, list(marks)                 # nothing to agree on: no device round trip
         vec = torch.tensor([int(skip_local)] + [-int(m) for m in marks], dtype=torch.int32, device=self.device)
         if dist.is_initialized():
@@ -508,7 +510,7 @@ class TotalLoss:
                     if on and (not math.isfinite(v) or abs(v) > 1e4):
                         marks[i] = UNSAFE_MARK
                         skip = True
-            skip, marks = self._sync_safety(skip, marks)
+            skip, marks = self._sync_safety(skip, marks, checked=check_now)
             if skip:
                 d_loss = torch.nan_to_num(d_loss, nan=0.0, posinf=0.0, neginf=0.0) * 0.0
             training_stats.report('Loss/D/skipped', 1.0 if skip else 0.0)
@@ -626,7 +628,7 @@ class TotalLoss:
                 if bad:
                     marks[i] = UNSAFE_MARK
                     skip = True
-        skip, marks = self._sync_safety(skip, marks)
+        skip, marks = self._sync_safety(skip, marks, checked=check_now and self.prev_loss_dict is not None)
 
         if self.compression_mode == 'continuous':
             g_loss = (rec + self.stylegan_t_discriminator_loss_weight * st_gen
