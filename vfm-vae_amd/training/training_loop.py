@@ -349,7 +349,10 @@ def fast_adam_step(phase, ema=None):
     if raw:
         grads = [gr for gr in now if gr is not None]
         if plan is not None and not all(map(torch.Tensor.is_contiguous, grads)):
-            plan = None                       # (autograd hands contiguous gradients; an assigned .grad may not be)
+            # (autograd hands contiguous gradients; an assigned .grad may not be): torch's step this time, and the
+            # cached plan dropped -- its host step count would fall behind the counters torch advances
+            plan = None
+            phase.adam_cache = None
         if plan is None:
             sync.materialize()
     beta1, beta2 = g['betas']
