@@ -9,11 +9,14 @@
 //   dx         = k dy / n - x (sum_c k dy x) / n^3   where the norm is not clamped,   k dy / n  where it is
 //   dgamma[c]  = scale * sum_{b, p} dy x / n
 //
-// Block = 16 columns (consecutive p) x 64 channel groups; a thread sums every 64th channel of its
-// column (1024 threads: the 8^2-32^2 planes give only 128-2048 blocks), the 64 partial sums meet in
-// LDS, then the same threads write their channels. The gamma
-// gradient: each block reduces dy x / n over its 16 columns per channel into one partial (channel-major
-// [C][blocks]), and a second kernel sums every channel's partials in a fixed order (deterministic).
+// Block = 32 columns (consecutive p) x 32 channel groups; a thread sums every 32nd channel of its
+// column (1024 threads), the 32 partial sums meet in LDS, then the same threads write their channels. A
+// wave's loads are two 128-B rows (32 consecutive fp32 of two channels): whole cache lines, where the
+// 16-column form read 64-B halves whose other halves belonged to the neighbouring block (forward at 32^2 x
+// 512: 48 -> 30 us, 64^2 x 256: 82 -> 51 us; backward 64^2: 194 -> 128-154 us, profiles/r6_by_crms_tiling.txt).
+// The gamma gradient: each block reduces dy x / n over its columns per channel into one partial
+// (channel-major [C][blocks]), and a second kernel sums every channel's partials in a fixed order
+// (deterministic).
 #include "vfm_common.h"
 
 namespace {
@@ -21,9 +24,12 @@ namespace {
 using namespace vfm;
 
 #ifndef CRMS_GROUPS
-#define CRMS_GROUPS 64
+#define CRMS_GROUPS 32
 #endif
-constexpr int COLS = 16, GROUPS = CRMS_GROUPS, THREADS = COLS * GROUPS;
+#ifndef CRMS_COLS
+#define CRMS_COLS 32
+#endif
+constexpr int COLS = CRMS_COLS, GROUPS = CRMS_GROUPS, THREADS = COLS * GROUPS;
 constexpr float NORM_EPS = 1e-12f;
 
 __global__ __launch_bounds__(THREADS) void crms_fwd(const float* __restrict__ x, const float* __restrict__ gamma,
@@ -103,9 +109,11 @@ __global__ __launch_bounds__(THREADS) void crms_bwd(const float* __restrict__ x,
             gx = d * xv * r;
         }
         if (gpart) {
-            // sum over the block's 16 columns: lanes col = 0..15 of one channel group are 16 consecutive lanes
+            // sum over the block's COLS columns: lanes col = 0..COLS-1 of one channel group are COLS consecutive
+            // lanes of one wave (COLS divides 64)
+            static_assert(COLS <= 64 && 64 % COLS == 0, "a channel group's columns must lie in one wave");
 #pragma unroll
-            for (int o = 8; o >= 1; o >>= 1) gx += __shfl_xor(gx, o, 16);
+            for (int o = COLS / 2; o >= 1; o >>= 1) gx += __shfl_xor(gx, o, COLS);
             if (col == 0) gpart[(long long)c * gridDim.x + blockIdx.x] = gx;     // channel-major: [C][rows]
         }
     }
