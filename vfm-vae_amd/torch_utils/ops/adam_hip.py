@@ -57,6 +57,7 @@ class AdamEmaPlan:
         self.ntensors, self.nchunks = len(params), len(chunks)
         self.keep = (params, grads, m1, m2, emas, steps)   # the tables hold raw pointers into these
         self.owns_steps = steps is not None
+        self._raw_ptrs, self._graw = None, None       # last uploaded raw-gradient addresses and their device array
 
     def step(self, lr, beta1, beta2, weight_decay, eps, step, ema_w=0.0, raw=None, gscale=1.0):
         """raw: this step's gradient tensors (plans built with grads=None; contiguous fp32 of the parameters'
@@ -68,12 +69,16 @@ class AdamEmaPlan:
             raise custom_ops.NativeError("adam_hip: raw gradients go with plans built without gradients, one per tensor")
         gptr = 0
         if raw is not None:
-            # pinned staging + stream-ordered copy (the caching host allocator keeps the staging buffer until the
-            # copy has run); the device array lives until the launch below has consumed it (stream order)
-            host = torch.empty(self.ntensors, dtype=torch.int64, pin_memory=True)
-            host.numpy()[:] = [g.data_ptr() for g in raw]
-            graw = host.to(dev, non_blocking=True)
-            gptr = graw.data_ptr()
+            ptrs = list(map(torch.Tensor.data_ptr, raw))
+            if ptrs != self._raw_ptrs:
+                # pinned staging + stream-ordered copy (the caching host allocator keeps the staging buffer until
+                # the copy has run); the device array is kept for later steps whose gradients land at the same
+                # addresses (the caching allocator's usual pattern), which then skip the upload
+                host = torch.empty(self.ntensors, dtype=torch.int64, pin_memory=True)
+                host.numpy()[:] = ptrs
+                self._graw = host.to(dev, non_blocking=True)
+                self._raw_ptrs = ptrs
+            gptr = self._graw.data_ptr()
         with kernel_timer.region("adam_ema", self.nbytes):
             custom_ops.check(_lib.vfm_adam_ema_step_raw(self.tensors.data_ptr(), self.ntensors, self.chunks.data_ptr(),
                                                         self.nchunks, gptr, float(gscale), int(raw is not None),
